@@ -1,0 +1,255 @@
+"""bench.py -- GPAD inner-loop throughput on MI355X (BASELINE.json metric).
+
+Workload (default, ``--workload c4``): the C4 shard -- 8192 independent MPC QP instances per GPU
+(weak scaling), horizon N = 50 with n_u = 4 (n = 200 primal variables), m = 200 constraints,
+shared ML/G (one plant) and per-instance M/g (seeded synthetic generator of SURVEY.md §8d),
+solved to eps = 1e-4 with Algorithm 1 (check every 10 iterations, at most 5000 iterations).
+One step = reset z, y -> one gpad_run over the local shard -> RCCL gather of (z*, y*, iters) to
+rank 0.  ``value`` = GPAD iterations/s (instance-iterations actually executed, summed over all
+ranks) / max-over-ranks step time.
+
+Also reported on rank 0: QP-solves/s, the C2 single-instance iteration rate, the roofline of
+the dominant kernel (HIP events on the solve stream) and the reference's own CPU GPAD timed on
+this host (cpu_baseline).
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
+        torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gpu-dualgradient-mpc_amd"))
+
+FP32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 (VALU = f32 MFMA rate), MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0
+
+
+def flops_per_iter(n, m):
+    """F = 4nm + 5m + 4n per instance-iteration."""
+    return 4 * n * m + 5 * m + 4 * n
+
+
+def bytes_per_iter_shared(n, m, batch):
+    """shared ML/G: 4 (2nm + B (4m + 3n)) per batch-iteration."""
+    return 4 * (2 * n * m + batch * (4 * m + 3 * n))
+
+
+def make_shard(n, m, batch, start, seed=0):
+    """Shared (ML, G, L) from ``seed``; instance i (global index) draws q, b from seed + 1 + i."""
+    from gpad_mpc import problems
+    base = problems.synthetic_qp(n, m, batch=1, seed=seed)
+    G, H = base.G, base.H
+    Hinv = np.linalg.inv(H)
+    Q = np.empty((batch, n))
+    Bv = np.empty((batch, m))
+    for j in range(batch):
+        rng = np.random.default_rng(seed + 1 + start + j)
+        zf = rng.uniform(-0.5, 0.5, size=n)
+        Bv[j] = G @ zf + rng.uniform(0.1, 1.0, size=m)
+        Q[j] = rng.normal(0.0, 1.0, size=n)
+    M = Q @ Hinv.T
+    return base.ML, G, base.L, M, Bv
+
+
+def cpu_baseline(n, m, ML, G, L, M, g, iters_per_instance, budget_s=12.0):
+    """The reference's own seq_functions.cpp (oracle/_ref, -O3 -march=x86-64-v3) in main.cu
+    loop order on this host: instance-iterations/s over a bounded sample, all host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    O = pyoracle.Oracle()
+    kind = "reference"
+    path = pyoracle.REF_O3 if os.path.exists(pyoracle.REF_O3) else pyoracle.REF
+    if os.path.exists(path):
+        R = pyoracle.RefSeq(path)
+    else:
+        R, kind = None, "port"
+    ML32, G32, L32 = ML.astype(np.float32), G.astype(np.float32), np.float32(L)
+    MGneg, GL, _ = O.scale(ML32, G32, g[0].astype(np.float32), L32)
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    cores = max(1, min(cores, 16))
+    N = max(1, int(round(iters_per_instance)))
+    th, be = O.schedule_f32(N)
+
+    def run(count, threads):
+        GP = M[:count].astype(np.float32)
+        PD = O.scale_vec(g[:count], L32)
+        Z = np.zeros((count, n), np.float32)
+        Y = np.zeros((count, m), np.float32)
+        t0 = time.perf_counter()
+        if R is not None:
+            R.solve_batch_c(Z, Y, MGneg, GP, GL, PD, th, be, N, shared=True, threads=threads)
+        else:
+            O.solve_batch_f32(Z, Y, MGneg, GP, GL, PD, N, L32, 0.0, threads=threads)
+        return time.perf_counter() - t0
+
+    probe = run(cores, cores)  # one instance per core, to size the sample
+    count = int(max(cores, min(len(M), cores * max(1, int(budget_s / max(probe, 1e-6))))))
+    count = (count // cores) * cores
+    dt = run(count, cores)
+    t1 = run(1, 1)
+    return {"value": count * N / dt, "unit": "GPAD iterations/s", "cores": cores, "kind": kind,
+            "sample": f"{count} C4 instances x {N} iterations (fixed, = mean GPU iterations to "
+                      f"eps), shared ML/G, fp32, OpenMP over instances",
+            "single_thread_value": N / t1, "seconds": round(dt, 2)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=8192, help="instances per GPU")
+    ap.add_argument("--horizon", type=int, default=50)
+    ap.add_argument("--nu", type=int, default=4)
+    ap.add_argument("--m", type=int, default=200)
+    ap.add_argument("--tol", type=float, default=1e-4)
+    ap.add_argument("--max-iters", type=int, default=5000)
+    ap.add_argument("--kernel", default="auto", choices=["auto", "stream", "resident", "panel"])
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import gpad_mpc
+    from gpad_mpc import _lib
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    stream = torch.cuda.current_stream(dev)
+
+    n, m, B = args.nu * args.horizon, args.m, args.batch
+    ML, G, L, M, g = make_shard(n, m, B, rank * B)
+    f32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)  # noqa: E731
+    dML, dG, dM, dg = f32(ML), f32(G), f32(M), f32(g)
+    z = torch.zeros(B, n, device=dev)
+    y = torch.zeros(B, m, device=dev)
+    kern = {"auto": _lib.KERNEL_AUTO, "stream": _lib.KERNEL_STREAM, "resident": _lib.KERNEL_RESIDENT,
+            "panel": _lib.KERNEL_PANEL}[args.kernel]
+    solver = gpad_mpc.GpadSolver(local, stream=stream.cuda_stream)
+    L32 = float(np.float32(L))
+    solver.setup(dML, dG, L32, n=n, m=m, batch=B, shared=True, check_every=10, kernel=kern)
+    packed = torch.empty(B, n + m + 1, device=dev)
+    gathered = [torch.empty_like(packed) for _ in range(world)] if (world > 1 and rank == 0) else None
+
+    def step():
+        z.zero_()
+        y.zero_()
+        solver.run(z, y, dM, dg, args.max_iters, args.tol, stats=False)
+        if world > 1:
+            packed[:, :n] = z
+            packed[:, n:n + m] = y
+            dist.gather(packed, gathered, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    st0 = solver.last_stats()
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    kern_ms = 0.0
+    total_iters = 0
+    for _ in range(args.steps):
+        step()
+        st = solver.last_stats()      # syncs the solve stream; events bracket the kernel only
+        kern_ms += st["kernel_ms"]
+        total_iters += st["total_iterations"]
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    # max time over ranks, sum of work over ranks
+    stats = torch.tensor([dt, float(total_iters), kern_ms, float(st["converged"])], dtype=torch.float64,
+                         device=dev)
+    if world > 1:
+        tmax = stats[0:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        work = stats[1:4].clone()
+        dist.all_reduce(work, op=dist.ReduceOp.SUM)
+        dt = float(tmax.item())
+        total_iters_all = float(work[0].item())
+        converged_all = float(work[2].item())
+    else:
+        total_iters_all = float(total_iters)
+        converged_all = float(st["converged"])
+
+    if rank == 0:
+        ms_per_step = dt / args.steps * 1e3
+        value = total_iters_all / dt
+        solves = B * world * args.steps / dt
+        avg_kernel_s = kern_ms / args.steps / 1e3
+        iters_per_launch = total_iters / args.steps
+        F = flops_per_iter(n, m)
+        achieved_tf = iters_per_launch * F / avg_kernel_s / 1e12
+        mean_iters = iters_per_launch / B
+        # C2 single instance (config 1): latency kernel, fixed 1000 iterations
+        one = dict()
+        with gpad_mpc.GpadSolver(local, stream=stream.cuda_stream) as s1:
+            s1.setup(dML, dG, L32, n=n, m=m, batch=1)
+            z1 = torch.zeros(1, n, device=dev)
+            y1 = torch.zeros(1, m, device=dev)
+            s1.run(z1, y1, dM[:1], dg[:1], 1000, 0.0)
+            t = []
+            for _ in range(3):
+                st1 = s1.run(z1.zero_(), y1.zero_(), dM[:1], dg[:1], 1000, 0.0)
+                t.append(st1["kernel_ms"])
+            one = {"config": "C2 single instance n=200 m=200", "kernel": st1["kernel"],
+                   "iters_per_s": 1000 / (min(t) / 1e3)}
+        cpu = None
+        if not args.no_cpu and world == 1:
+            cpu = cpu_baseline(n, m, ML, G, L, M, g, mean_iters)
+        out = {
+            "metric": "GPAD iterations/s (instance-iterations, solve to eps=1e-4)",
+            "value": value,
+            "unit": "GPAD iterations/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded SURVEY.md §8d generator; shared ML/G, per-instance q/b)",
+            "config": {"workload": f"C4 shard: {B} instances/GPU, N={args.horizon} (n={n}), m={m}, "
+                                   f"shared ML/G, Algorithm 1 eps={args.tol}, K=10",
+                       "batch_per_gpu": B, "global_batch": B * world, "n": n, "m": m,
+                       "parallelism": f"instance-sharded x{world}, RCCL gather"},
+            "qp_solves_per_s": solves,
+            "mean_iters_to_eps": mean_iters,
+            "converged": int(converged_all),
+            "kernel": st["kernel"],
+            "single_instance": one,
+            "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP32_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": achieved_tf / FP32_PEAK_TFLOPS, "traffic": None,
+                         "kernel_ms": avg_kernel_s * 1e3,
+                         "note": "fp32 FMA-bound (matrices stay on chip); F = 4nm+5m+4n per "
+                                 "instance-iteration"},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    solver.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

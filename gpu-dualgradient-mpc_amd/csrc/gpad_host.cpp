@@ -1,0 +1,544 @@
+// gpad_host.cpp -- host runtime behind the C-ABI of include/gpad.h.
+//
+// Owns, per handle: the packed device copies of the constant matrices (k-major -ML and G/L,
+// and the MFMA fragment image for shared-matrix batches), the theta/beta table, per-instance
+// workspaces for host-memory callers, per-instance iteration/convergence counters and the
+// HIP events that time the solve launch.  Replaces the host driver of the reference
+// (main.cu:79-203: file read, 9 cudaMallocs, H2D copies, 100 x (6 launches + 3 syncs), D2H).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/gpad.h"
+#include "gpad_internal.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t _e = (expr);                                                              \
+        if (_e != hipSuccess) {                                                              \
+            return fail(_e == hipErrorOutOfMemory ? GPAD_ERR_NOMEM : GPAD_ERR_HIP,           \
+                        std::string(#expr) + ": " + hipGetErrorString(_e));                   \
+        }                                                                                    \
+    } while (0)
+
+size_t esize(int dtype) { return dtype == GPAD_DTYPE_F64 ? sizeof(double) : sizeof(float); }
+int round4(int x) { return (x + 3) & ~3; }
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int ensure(size_t want) {
+        if (want <= bytes && p) return GPAD_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        if (want == 0) return GPAD_OK;
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return fail(e == hipErrorOutOfMemory ? GPAD_ERR_NOMEM : GPAD_ERR_HIP,
+                        std::string("hipMalloc: ") + hipGetErrorString(e));
+        }
+        bytes = want;
+        return GPAD_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
+void host_schedule(int N, int kind, double* theta, double* beta) {
+    // acceldualgrad.m:18,27,55-56 (MATLAB: beta lagged one iteration) / paper eq. (8e)
+    double th = 1.0, thm1 = 1.0, b = 0.0;
+    for (int v = 0; v < N; ++v) {
+        const double thn = (std::sqrt(std::pow(th, 4.0) + 4.0 * std::pow(th, 2.0)) - std::pow(th, 2.0)) / 2.0;
+        theta[v] = th;
+        if (kind == GPAD_SCHEDULE_PAPER) {
+            beta[v] = th * (1.0 / thm1 - 1.0);
+        } else {
+            beta[v] = b;
+            b = th * (1.0 / thm1 - 1.0);
+        }
+        thm1 = th;
+        th = thn;
+    }
+}
+
+}  // namespace
+
+struct gpad_handle_s {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    bool ready = false;
+    gpad_dims_t dims{};
+    double L = 1.0;
+    bool scaled = false;
+    int ldn = 0, ldm = 0;
+    DevBuf MGt, GLt, frag, stage;
+    DevBuf theta, beta;
+    int sched_len = 0, sched_kind = -1, sched_dtype = -1;
+    DevBuf work, counters;
+    std::vector<int> h_iters, h_conv;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int last_kernel = 0, last_batch = 0;
+    bool timed = false;
+};
+
+extern "C" {
+
+const char* gpad_version(void) { return "gpad-mi355x 0.1 (gfx950)"; }
+
+const char* gpad_strerror(int status) {
+    switch (status) {
+        case GPAD_OK: return "ok";
+        case GPAD_ERR_INVALID: return "invalid argument";
+        case GPAD_ERR_HIP: return "HIP runtime error";
+        case GPAD_ERR_NOMEM: return "device out of memory";
+        case GPAD_ERR_UNSUPPORTED: return "unsupported shape/kernel combination";
+        case GPAD_ERR_NOT_SETUP: return "gpad_run before gpad_setup";
+        case GPAD_ERR_NO_DEVICE: return "no HIP device";
+        default: return "unknown status";
+    }
+}
+
+const char* gpad_last_error(void) { return g_last_error.c_str(); }
+
+int gpad_create(gpad_handle_t* out, int device, void* stream) {
+    if (!out) return fail(GPAD_ERR_INVALID, "gpad_create: null handle pointer");
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+        return fail(GPAD_ERR_NO_DEVICE, "gpad_create: no HIP device visible");
+    if (device < 0 || device >= count) return fail(GPAD_ERR_INVALID, "gpad_create: bad device index");
+    HIP_TRY(hipSetDevice(device));
+    auto h = std::make_unique<gpad_handle_s>();
+    h->device = device;
+    if (stream) {
+        h->stream = static_cast<hipStream_t>(stream);
+    } else {
+        HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+        h->own_stream = true;
+    }
+    HIP_TRY(hipEventCreate(&h->ev0));
+    HIP_TRY(hipEventCreate(&h->ev1));
+    *out = h.release();
+    return GPAD_OK;
+}
+
+int gpad_destroy(gpad_handle_t h) {
+    if (!h) return GPAD_OK;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    h->MGt.release();
+    h->GLt.release();
+    h->frag.release();
+    h->stage.release();
+    h->theta.release();
+    h->beta.release();
+    h->work.release();
+    h->counters.release();
+    if (h->ev0) (void)hipEventDestroy(h->ev0);
+    if (h->ev1) (void)hipEventDestroy(h->ev1);
+    if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return GPAD_OK;
+}
+
+int gpad_set_stream(gpad_handle_t h, void* stream) {
+    if (!h) return fail(GPAD_ERR_INVALID, "gpad_set_stream: null handle");
+    (void)hipSetDevice(h->device);
+    if (h->own_stream && h->stream) {
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        HIP_TRY(hipStreamDestroy(h->stream));
+        h->own_stream = false;
+        h->stream = nullptr;
+    }
+    if (stream) {
+        h->stream = static_cast<hipStream_t>(stream);
+    } else {
+        HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+        h->own_stream = true;
+    }
+    return GPAD_OK;
+}
+
+int gpad_sync(gpad_handle_t h) {
+    if (!h) return fail(GPAD_ERR_INVALID, "gpad_sync: null handle");
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return GPAD_OK;
+}
+
+int gpad_schedule(int N, int kind, double* theta, double* beta) {
+    if (N < 0 || !theta || !beta) return fail(GPAD_ERR_INVALID, "gpad_schedule: bad arguments");
+    host_schedule(N, kind, theta, beta);
+    return GPAD_OK;
+}
+
+static int validate_dims(const gpad_dims_t* d) {
+    if (!d) return fail(GPAD_ERR_INVALID, "null dims");
+    if (d->n <= 0 || d->m <= 0 || d->batch <= 0)
+        return fail(GPAD_ERR_INVALID, "dims: n, m, batch must be positive");
+    if (d->dtype != GPAD_DTYPE_F32 && d->dtype != GPAD_DTYPE_F64)
+        return fail(GPAD_ERR_INVALID, "dims: bad dtype");
+    if (d->memory != GPAD_MEM_HOST && d->memory != GPAD_MEM_DEVICE)
+        return fail(GPAD_ERR_INVALID, "dims: bad memory kind");
+    if (d->schedule != GPAD_SCHEDULE_MATLAB && d->schedule != GPAD_SCHEDULE_PAPER)
+        return fail(GPAD_ERR_INVALID, "dims: bad schedule");
+    if (d->kernel < GPAD_KERNEL_AUTO || d->kernel > GPAD_KERNEL_PANEL)
+        return fail(GPAD_ERR_INVALID, "dims: bad kernel");
+    return GPAD_OK;
+}
+
+static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, const void* B, double L,
+                      bool scaled) {
+    if (!h) return fail(GPAD_ERR_INVALID, "gpad_setup: null handle");
+    int rc = validate_dims(d);
+    if (rc) return rc;
+    if (!A || !B) return fail(GPAD_ERR_INVALID, "gpad_setup: null matrix");
+    if (!(L > 0.0) || !std::isfinite(L)) return fail(GPAD_ERR_INVALID, "gpad_setup: L must be > 0");
+    HIP_TRY(hipSetDevice(h->device));
+    h->ready = false;
+    h->dims = *d;
+    if (h->dims.check_every <= 0) h->dims.check_every = 10;
+    h->L = L;
+    h->scaled = scaled;
+    const int n = d->n, m = d->m;
+    h->ldn = round4(n);
+    h->ldm = round4(m);
+    const size_t es = esize(d->dtype);
+    const int nmats = d->shared ? 1 : d->batch;
+    const size_t a_elems = (size_t)m * h->ldn, b_elems = (size_t)n * h->ldm;
+    if ((rc = h->MGt.ensure(es * a_elems * nmats))) return rc;
+    if ((rc = h->GLt.ensure(es * b_elems * nmats))) return rc;
+    const size_t raw = (size_t)n * m * nmats * es;
+    const void* dA = A;
+    const void* dB = B;
+    if (d->memory == GPAD_MEM_HOST) {
+        if ((rc = h->stage.ensure(2 * raw))) return rc;
+        HIP_TRY(hipMemcpyAsync(h->stage.p, A, raw, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipMemcpyAsync((char*)h->stage.p + raw, B, raw, hipMemcpyHostToDevice, h->stream));
+        dA = h->stage.p;
+        dB = (char*)h->stage.p + raw;
+    }
+    // -ML -> k-major [m][ldn];  G/L -> k-major [n][ldm]   (acceldualgrad.m:20,22)
+    const double sa = scaled ? 1.0 : -1.0;
+    const double sb = scaled ? 1.0 : 1.0 / L;
+    const long long in_stride = d->shared ? 0 : (long long)n * m;
+    if (d->dtype == GPAD_DTYPE_F32) {
+        HIP_TRY(gpad::launch_pack_kmajor<float>((const float*)dA, (float*)h->MGt.p, n, m, h->ldn, sa,
+                                                nmats, in_stride, (long long)a_elems, h->stream));
+        HIP_TRY(gpad::launch_pack_kmajor<float>((const float*)dB, (float*)h->GLt.p, m, n, h->ldm, sb,
+                                                nmats, in_stride, (long long)b_elems, h->stream));
+    } else {
+        HIP_TRY(gpad::launch_pack_kmajor<double>((const double*)dA, (double*)h->MGt.p, n, m, h->ldn, sa,
+                                                 nmats, in_stride, (long long)a_elems, h->stream));
+        HIP_TRY(gpad::launch_pack_kmajor<double>((const double*)dB, (double*)h->GLt.p, m, n, h->ldm, sb,
+                                                 nmats, in_stride, (long long)b_elems, h->stream));
+    }
+    // fragment image for the MFMA panel kernel (shared f32 matrices only)
+    h->frag.release();
+    if (d->shared && d->dtype == GPAD_DTYPE_F32) {
+        const size_t fb = gpad::panel_frag_bytes(n, m);
+        if (fb > 0) {
+            if ((rc = h->frag.ensure(fb))) return rc;
+            HIP_TRY(gpad::launch_pack_panel((const float*)dA, (const float*)dB, n, m,
+                                            (float)sa, sb, h->frag.p, h->stream));
+        }
+    }
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    if (d->memory == GPAD_MEM_HOST) h->stage.release();
+    h->ready = true;
+    return GPAD_OK;
+}
+
+int gpad_setup(gpad_handle_t h, const gpad_dims_t* d, const void* ML, const void* G, double L) {
+    return setup_impl(h, d, ML, G, L, false);
+}
+
+int gpad_setup_scaled(gpad_handle_t h, const gpad_dims_t* d, const void* MGneg, const void* GL,
+                      double L) {
+    return setup_impl(h, d, MGneg, GL, L, true);
+}
+
+static int ensure_schedule(gpad_handle_t h, int N, const void* theta_in, const void* beta_in) {
+    const int dt = h->dims.dtype;
+    const size_t es = esize(dt);
+    const bool custom = theta_in != nullptr || beta_in != nullptr;
+    if (!custom && h->sched_len >= N + 1 && h->sched_kind == h->dims.schedule && h->sched_dtype == dt)
+        return GPAD_OK;
+    const int len = std::max(N + 1, 1);
+    std::vector<double> th(len, 0.0), be(len, 0.0);
+    host_schedule(N, h->dims.schedule, th.data(), be.data());
+    if (custom) {
+        if (!theta_in || !beta_in) return fail(GPAD_ERR_INVALID, "run_scaled: give both theta and beta");
+        for (int v = 0; v < N; ++v) {
+            th[v] = dt == GPAD_DTYPE_F64 ? ((const double*)theta_in)[v] : ((const float*)theta_in)[v];
+            be[v] = dt == GPAD_DTYPE_F64 ? ((const double*)beta_in)[v] : ((const float*)beta_in)[v];
+        }
+    }
+    be[N] = 0.0;  // w for a non-existent iteration N: computed, never used
+    int rc;
+    if ((rc = h->theta.ensure(es * len))) return rc;
+    if ((rc = h->beta.ensure(es * len))) return rc;
+    if (dt == GPAD_DTYPE_F64) {
+        HIP_TRY(hipMemcpyAsync(h->theta.p, th.data(), es * len, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipMemcpyAsync(h->beta.p, be.data(), es * len, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+    } else {
+        std::vector<float> tf(len), bf(len);
+        for (int i = 0; i < len; ++i) {
+            tf[i] = (float)th[i];
+            bf[i] = (float)be[i];
+        }
+        HIP_TRY(hipMemcpyAsync(h->theta.p, tf.data(), es * len, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipMemcpyAsync(h->beta.p, bf.data(), es * len, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+    }
+    h->sched_len = custom ? 0 : len;  // custom tables are never reused
+    h->sched_kind = h->dims.schedule;
+    h->sched_dtype = dt;
+    return GPAD_OK;
+}
+
+static int collect_stats(gpad_handle_t h, gpad_stats_t* st) {
+    const int batch = h->last_batch;
+    h->h_iters.resize(batch);
+    h->h_conv.resize(batch);
+    int* dI = (int*)h->counters.p;
+    int* dC = dI + batch;
+    HIP_TRY(hipMemcpyAsync(h->h_iters.data(), dI, sizeof(int) * batch, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemcpyAsync(h->h_conv.data(), dC, sizeof(int) * batch, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    st->iterations = 0;
+    st->converged = 0;
+    st->total_iterations = 0;
+    for (int b = 0; b < batch; ++b) {
+        st->iterations = std::max(st->iterations, h->h_iters[b]);
+        st->converged += h->h_conv[b] != 0;
+        st->total_iterations += h->h_iters[b];
+        if (st->iters) st->iters[b] = h->h_iters[b];
+    }
+    st->kernel = h->last_kernel;
+    float ms = 0.0f;
+    st->kernel_ms = 0.0;
+    if (h->timed && hipEventElapsedTime(&ms, h->ev0, h->ev1) == hipSuccess) st->kernel_ms = ms;
+    return GPAD_OK;
+}
+
+int gpad_last_stats(gpad_handle_t h, gpad_stats_t* st) {
+    if (!h || !st) return fail(GPAD_ERR_INVALID, "gpad_last_stats: null argument");
+    if (h->last_batch <= 0) return fail(GPAD_ERR_NOT_SETUP, "gpad_last_stats: no run yet");
+    HIP_TRY(hipSetDevice(h->device));
+    return collect_stats(h, st);
+}
+
+}  // extern "C"
+
+template <typename T>
+static int run_typed(gpad_handle_t h, T* z, T* y, const T* M, const T* g, int N, double tol,
+                     const void* theta_in, const void* beta_in, bool scaled_vec, gpad_stats_t* st) {
+    const gpad_dims_t& d = h->dims;
+    const int n = d.n, m = d.m, batch = d.batch;
+    int rc = ensure_schedule(h, N, theta_in, beta_in);
+    if (rc) return rc;
+    if ((rc = h->counters.ensure(sizeof(int) * 2 * (size_t)batch))) return rc;
+    T *dz = z, *dy = y;
+    const T *dM = M, *dg = g;
+    const size_t zb = sizeof(T) * (size_t)batch * n, yb = sizeof(T) * (size_t)batch * m;
+    if (d.memory == GPAD_MEM_HOST) {
+        if ((rc = h->work.ensure(2 * zb + 2 * yb))) return rc;
+        char* base = (char*)h->work.p;
+        dz = (T*)base;
+        dy = (T*)(base + zb);
+        T* wM = (T*)(base + zb + yb);
+        T* wg = (T*)(base + 2 * zb + yb);
+        HIP_TRY(hipMemcpyAsync(dz, z, zb, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipMemcpyAsync(dy, y, yb, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipMemcpyAsync(wM, M, zb, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipMemcpyAsync(wg, g, yb, hipMemcpyHostToDevice, h->stream));
+        dM = wM;
+        dg = wg;
+    }
+    gpad::SolveArgs<T> a{};
+    a.MGt = (const T*)h->MGt.p;
+    a.GLt = (const T*)h->GLt.p;
+    a.strideA = d.shared ? 0 : (long long)m * h->ldn;
+    a.strideB = d.shared ? 0 : (long long)n * h->ldm;
+    a.frag = h->frag.p;
+    a.gP = dM;
+    a.g = dg;
+    a.ld_gP = n;
+    a.ld_g = m;
+    a.gscale = scaled_vec ? 1.0 : -1.0 / h->L;
+    a.z = dz;
+    a.y = dy;
+    a.n = n;
+    a.m = m;
+    a.ldn = h->ldn;
+    a.ldm = h->ldm;
+    a.batch = batch;
+    a.N = N;
+    a.check_every = d.check_every;
+    a.tol = tol;
+    a.L = h->L;
+    a.theta = (const T*)h->theta.p;
+    a.beta = (const T*)h->beta.p;
+    a.iters = (int*)h->counters.p;
+    a.conv = a.iters + batch;
+    int kernel = d.kernel;
+    HIP_TRY(hipEventRecord(h->ev0, h->stream));
+    hipError_t e = hipSuccess;
+    bool ok = false;
+    if constexpr (sizeof(T) == sizeof(float)) {
+        if (kernel == GPAD_KERNEL_PANEL || (kernel == GPAD_KERNEL_AUTO && d.shared && batch >= 64)) {
+            e = gpad::launch_panel(a, h->stream, &ok);
+            if (e != hipSuccess) return fail(GPAD_ERR_HIP, std::string("panel: ") + hipGetErrorString(e));
+            if (ok) kernel = GPAD_KERNEL_PANEL;
+            else if (kernel == GPAD_KERNEL_PANEL)
+                return fail(GPAD_ERR_UNSUPPORTED, "panel kernel: needs shared f32 matrices");
+        }
+        if (!ok && (kernel == GPAD_KERNEL_RESIDENT || kernel == GPAD_KERNEL_AUTO)) {
+            e = gpad::launch_resident(a, h->stream, &ok);
+            if (e != hipSuccess) return fail(GPAD_ERR_HIP, std::string("resident: ") + hipGetErrorString(e));
+            if (ok) kernel = GPAD_KERNEL_RESIDENT;
+            else if (kernel == GPAD_KERNEL_RESIDENT)
+                return fail(GPAD_ERR_UNSUPPORTED, "resident kernel: needs n, m <= 208");
+        }
+    } else {
+        if (kernel == GPAD_KERNEL_PANEL || kernel == GPAD_KERNEL_RESIDENT)
+            return fail(GPAD_ERR_UNSUPPORTED, "f64 runs on the stream kernel only");
+    }
+    if (!ok) {
+        kernel = GPAD_KERNEL_STREAM;
+        e = gpad::launch_stream<T>(a, h->stream);
+        if (e != hipSuccess)
+            return fail(e == hipErrorInvalidValue ? GPAD_ERR_UNSUPPORTED : GPAD_ERR_HIP,
+                        std::string("stream kernel: ") + hipGetErrorString(e) +
+                            " (n+m beyond the LDS budget?)");
+    }
+    HIP_TRY(hipEventRecord(h->ev1, h->stream));
+    h->timed = true;
+    h->last_kernel = kernel;
+    h->last_batch = batch;
+    if (d.memory == GPAD_MEM_HOST) {
+        HIP_TRY(hipMemcpyAsync(z, dz, zb, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipMemcpyAsync(y, dy, yb, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+    }
+    if (st) return collect_stats(h, st);
+    return GPAD_OK;
+}
+
+extern "C" {
+
+static int run_impl(gpad_handle_t h, void* z0, void* y0, const void* M, const void* g, int N,
+                    double tol, const void* theta, const void* beta, bool scaled_vec,
+                    gpad_stats_t* st) {
+    if (!h) return fail(GPAD_ERR_INVALID, "gpad_run: null handle");
+    if (!h->ready) return fail(GPAD_ERR_NOT_SETUP, "gpad_run: call gpad_setup first");
+    if (!z0 || !y0 || !M || !g) return fail(GPAD_ERR_INVALID, "gpad_run: null vector");
+    if (N < 0) return fail(GPAD_ERR_INVALID, "gpad_run: N < 0");
+    if (!(tol <= 0.0) && !std::isfinite(tol)) return fail(GPAD_ERR_INVALID, "gpad_run: bad tol");
+    HIP_TRY(hipSetDevice(h->device));
+    if (h->dims.dtype == GPAD_DTYPE_F64)
+        return run_typed<double>(h, (double*)z0, (double*)y0, (const double*)M, (const double*)g, N,
+                                 tol, theta, beta, scaled_vec, st);
+    return run_typed<float>(h, (float*)z0, (float*)y0, (const float*)M, (const float*)g, N, tol, theta,
+                            beta, scaled_vec, st);
+}
+
+int gpad_run(gpad_handle_t h, void* z0, void* y0, const void* M, const void* g, int N, double tol,
+             gpad_stats_t* st) {
+    return run_impl(h, z0, y0, M, g, N, tol, nullptr, nullptr, false, st);
+}
+
+int gpad_run_scaled(gpad_handle_t h, void* z0, void* y0, const void* gP, const void* pD, int N,
+                    double tol, const void* theta, const void* beta, gpad_stats_t* st) {
+    return run_impl(h, z0, y0, gP, pD, N, tol, theta, beta, true, st);
+}
+
+int gpad_solve(void* z0, void* y0, const void* ML, const void* M, const void* G, const void* g, int N,
+               double L, double tol, const gpad_dims_t* dims, gpad_stats_t* st) {
+    struct Cache {
+        gpad_handle_t h = nullptr;
+        int device = -1;
+        ~Cache() {
+            if (h) gpad_destroy(h);
+        }
+    };
+    thread_local Cache cache;
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    if (!cache.h || cache.device != dev) {
+        if (cache.h) gpad_destroy(cache.h);
+        cache.h = nullptr;
+        int rc = gpad_create(&cache.h, dev, nullptr);
+        if (rc) return rc;
+        cache.device = dev;
+    }
+    int rc = gpad_setup(cache.h, dims, ML, G, L);
+    if (rc) return rc;
+    gpad_stats_t local{};
+    rc = gpad_run(cache.h, z0, y0, M, g, N, tol, st ? st : &local);
+    if (rc) return rc;
+    return gpad_sync(cache.h);
+}
+
+// ---- per-step entry points ---------------------------------------------------------------
+int gpad_step1_extrapolate(gpad_handle_t h, const float* y, const float* ym1, float* w, float beta,
+                           int m) {
+    if (!h || !y || !ym1 || !w || m < 0) return fail(GPAD_ERR_INVALID, "gpad_step1: bad arguments");
+    if (m == 0) return GPAD_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(gpad::launch_step1(y, ym1, w, beta, m, h->stream));
+    return GPAD_OK;
+}
+
+int gpad_step2_primal(gpad_handle_t h, const float* MGneg, const float* w, const float* gP,
+                      float* zhat, int n, int m) {
+    if (!h || !MGneg || !w || !gP || !zhat || n <= 0 || m <= 0)
+        return fail(GPAD_ERR_INVALID, "gpad_step2: bad arguments");
+    if ((size_t)m * sizeof(float) > 64 * 1024) return fail(GPAD_ERR_UNSUPPORTED, "gpad_step2: m too large");
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(gpad::launch_step2(MGneg, w, gP, zhat, n, m, h->stream));
+    return GPAD_OK;
+}
+
+int gpad_step3_average(gpad_handle_t h, float theta, const float* zm1, const float* zhat, float* z,
+                       int n) {
+    if (!h || !zm1 || !zhat || !z || n < 0) return fail(GPAD_ERR_INVALID, "gpad_step3: bad arguments");
+    if (n == 0) return GPAD_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(gpad::launch_step3(theta, zm1, zhat, z, n, h->stream));
+    return GPAD_OK;
+}
+
+int gpad_step4_project(gpad_handle_t h, const float* GL, float* yp1, const float* w,
+                       const float* pD, const float* zhat, int n, int m) {
+    if (!h || !GL || !yp1 || !w || !pD || !zhat || n <= 0 || m <= 0)
+        return fail(GPAD_ERR_INVALID, "gpad_step4: bad arguments");
+    if ((size_t)n * sizeof(float) > 64 * 1024) return fail(GPAD_ERR_UNSUPPORTED, "gpad_step4: n too large");
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(gpad::launch_step4(GL, yp1, w, pD, zhat, n, m, h->stream));
+    return GPAD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,57 @@
+// gpad_internal.h -- device-side argument blocks and kernel launchers shared by the
+// HIP kernels (gpad_kernels.hip, gpad_panel.hip) and the host runtime (gpad_host.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace gpad {
+
+// Arguments of a fused solve launch (all kernel families).  Every instance b of the batch
+// reads its matrices at MGt + b*strideA / GLt + b*strideB (stride 0 = shared).
+template <typename T>
+struct SolveArgs {
+    const T* MGt;          // -ML, k-major: [m][ldn]   (column k of -ML is contiguous)
+    const T* GLt;          // G/L, k-major: [n][ldm]
+    long long strideA;     // elements between consecutive instances' -ML images (0 = shared)
+    long long strideB;     // elements between consecutive instances' G/L images (0 = shared)
+    const void* frag;      // panel kernel: fragment-packed matrices (see gpad_panel.hip)
+    const T* gP;           // per-instance H^-1 q, [batch][ld_gP]
+    const T* g;            // per-instance rhs,    [batch][ld_g]
+    long long ld_gP, ld_g;
+    double gscale;         // pD = (T)(gscale * g): -1/L, or 1 when g already holds p_D
+    T* z;                  // [batch][n]  in z_{-1}, out z*
+    T* y;                  // [batch][m]  in y0,     out y*
+    int n, m, ldn, ldm;    // ldn = round_up(n,4), ldm = round_up(m,4)
+    int batch, N, check_every;
+    double tol, L;         // Algorithm 1: stop when L*viol <= tol (tol <= 0: fixed N)
+    const T* theta;        // [N+1] theta_v
+    const T* beta;         // [N+1] beta_v  (beta[N] = 0 pad)
+    int* iters;            // [batch] iterations executed
+    int* conv;             // [batch] 1 if the tolerance test passed
+};
+
+// launchers (return hipError_t of the launch)
+template <typename T>
+hipError_t launch_stream(const SolveArgs<T>& a, hipStream_t s);
+hipError_t launch_resident(const SolveArgs<float>& a, hipStream_t s, bool* supported);
+hipError_t launch_panel(const SolveArgs<float>& a, hipStream_t s, bool* supported);
+size_t panel_frag_bytes(int n, int m);
+hipError_t launch_pack_panel(const float* ML, const float* G, int n, int m, float mg_sign,
+                             double g_scale, void* frag, hipStream_t s);
+
+// layout: out[k*ld + i] = (T)(scale * in[i*cols + k]) for i < rows, k < cols; zero pad i >= rows
+template <typename T>
+hipError_t launch_pack_kmajor(const T* in, T* out, int rows, int cols, int ld, double scale,
+                              int batch, long long in_stride, long long out_stride, hipStream_t s);
+
+hipError_t launch_step1(const float* y, const float* ym1, float* w, float beta, int m, hipStream_t s);
+hipError_t launch_step2(const float* MGneg, const float* w, const float* gP, float* zhat, int n,
+                        int m, hipStream_t s);
+hipError_t launch_step3(float theta, const float* zm1, const float* zhat, float* z, int n,
+                        hipStream_t s);
+hipError_t launch_step4(const float* GL, float* yp1, const float* w, const float* pD,
+                        const float* zhat, int n, int m, hipStream_t s);
+
+}  // namespace gpad

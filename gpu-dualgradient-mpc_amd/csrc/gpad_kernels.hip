@@ -1,0 +1,577 @@
+// gpad_kernels.hip -- GPAD inner-loop kernels for MI355X (gfx950, CDNA4, wave64).
+//
+// Two fused, persistent solve kernels (the whole iteration loop of main.cu:160-175 lives
+// inside ONE launch: no per-iteration launches, host syncs or y-copy kernels):
+//
+//   gpad_stream_kernel<T>   generic family (f32 / f64, any n, m up to the LDS budget).
+//                           One workgroup per instance; -ML and G/L are read every
+//                           iteration from HBM/L2 in k-major layout, 4 rows per lane
+//                           (one 16-B/32-B load per lane per k -> 1 KiB per wave-instruction,
+//                           fully coalesced), 8 k-steps in flight per lane.
+//   gpad_resident_kernel<K> latency family (f32, n, m <= 208).  One workgroup per
+//                           instance; each lane holds ONE matrix row in VGPRs for the
+//                           whole solve (loaded once), so an iteration touches no memory but
+//                           LDS.  Waves [0,nA) own the rows of -ML, waves [nA,nA+nB) the rows
+//                           of G/L; w and zhat are broadcast through LDS (ds_read_b128).
+//
+// Numerics (bit-exact with the reference CPU path, see oracle/gpad_oracle.h): every dot
+// product is ONE sequential fmaf chain per output row, k = 0..K-1 from +0 -- exactly what
+// seq_functions.cpp:61,82 compute under FMA contraction and what the reference's
+// one-thread-per-row CUDA kernels compute (kernel_functions.cu:46-61,176-191).  The file is
+// compiled with -ffp-contract=off; every fused multiply-add is an explicit __builtin_fma.
+//
+// Per-step kernels mirroring kernel_functions.h one-for-one are at the end of this file.
+
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+
+#include "gpad_internal.h"
+
+namespace gpad {
+
+__device__ __forceinline__ float fmad(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ double fmad(double a, double b, double c) { return __builtin_fma(a, b, c); }
+__device__ __forceinline__ float absd(float a) { return __builtin_fabsf(a); }
+__device__ __forceinline__ double absd(double a) { return __builtin_fabs(a); }
+template <typename T> __device__ __forceinline__ T neg_inf();
+template <> __device__ __forceinline__ float neg_inf<float>() { return -INFINITY; }
+template <> __device__ __forceinline__ double neg_inf<double>() { return -INFINITY; }
+
+template <typename T> struct V4;
+template <> struct V4<float> { using type = float4; };
+template <> struct V4<double> { using type = double4; };
+
+// ---- wave64 reductions (DPP/permute lowered by the compiler) ---------------------------
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_min(T v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Per-wave partials of the Algorithm-1 test -> LDS slot of the wave.
+struct CheckSlot {
+    double violz, violh, wmin, gap;
+};
+
+template <typename T>
+__device__ __forceinline__ void check_publish(CheckSlot* slots, T violz, T violh, T wmin,
+                                              double gap) {
+    const T a = wave_max(violz), b = wave_max(violh), c = wave_min(wmin);
+    const double d = wave_sum(gap);
+    if ((threadIdx.x & 63) == 0) {
+        CheckSlot& s = slots[threadIdx.x >> 6];
+        s.violz = (double)a;
+        s.violh = (double)b;
+        s.wmin = (double)c;
+        s.gap = d;
+    }
+}
+
+// Every thread evaluates the decision from the same LDS words -> uniform, no extra barrier.
+// 1: (A) L*max(G_L z + pD) <= tol              -> z certified
+// 2: (B) L*max(G_L zhat + pD) <= tol, w >= 0, -L w't <= tol -> zhat certified (returned as z*)
+__device__ __forceinline__ int check_decide(const CheckSlot* slots, int nwaves, double L,
+                                            double tol) {
+    double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gap = 0.0;
+    for (int i = 0; i < nwaves; ++i) {
+        vz = fmax(vz, slots[i].violz);
+        vh = fmax(vh, slots[i].violh);
+        wm = fmin(wm, slots[i].wmin);
+        gap += slots[i].gap;
+    }
+    if (vz * L <= tol) return 1;
+    return ((vh * L <= tol) && (wm >= 0.0) && (gap * L <= tol)) ? 2 : 0;
+}
+
+// =========================================================================================
+// gpad_stream_kernel
+// =========================================================================================
+constexpr int kStreamBlock = 256;
+constexpr int kUnrollK = 8;
+
+template <typename T>
+struct StreamLds {
+    T *w, *zh, *zs, *ys, *gp, *pd;
+    CheckSlot* slots;
+};
+
+template <typename T>
+__device__ __forceinline__ StreamLds<T> stream_lds(unsigned char* smem, int ldn, int ldm) {
+    StreamLds<T> s;
+    s.w = reinterpret_cast<T*>(smem);   // [ldm] current w (read by every lane in phase 1)
+    s.zh = s.w + ldm;                   // [ldn] zhat (read by every lane in phase 2)
+    s.zs = s.zh + ldn;                  // [ldn] z (averaged primal)
+    s.ys = s.zs + ldn;                  // [ldm] y
+    s.gp = s.ys + ldm;                  // [ldn] g_P
+    s.pd = s.gp + ldn;                  // [ldm] p_D
+    s.slots = reinterpret_cast<CheckSlot*>(s.pd + ldm);
+    return s;
+}
+
+// acc[r] = sum_k Mt[k*ld + r0 + r] * v[k], sequential in k, 4 rows per lane.
+template <typename T>
+__device__ __forceinline__ void chain4(const T* __restrict__ Mt, int ld, int r0, const T* v, int K,
+                                       T (&acc)[4]) {
+    using V = typename V4<T>::type;
+    const T* col = Mt + r0;
+    int k = 0;
+    for (; k + kUnrollK <= K; k += kUnrollK) {
+        V a[kUnrollK];
+#pragma unroll
+        for (int u = 0; u < kUnrollK; ++u) a[u] = *reinterpret_cast<const V*>(col + (size_t)(k + u) * ld);
+#pragma unroll
+        for (int u = 0; u < kUnrollK; ++u) {
+            const T vk = v[k + u];
+            acc[0] = fmad(a[u].x, vk, acc[0]);
+            acc[1] = fmad(a[u].y, vk, acc[1]);
+            acc[2] = fmad(a[u].z, vk, acc[2]);
+            acc[3] = fmad(a[u].w, vk, acc[3]);
+        }
+    }
+    for (; k < K; ++k) {
+        const V a = *reinterpret_cast<const V*>(col + (size_t)k * ld);
+        const T vk = v[k];
+        acc[0] = fmad(a.x, vk, acc[0]);
+        acc[1] = fmad(a.y, vk, acc[1]);
+        acc[2] = fmad(a.z, vk, acc[2]);
+        acc[3] = fmad(a.w, vk, acc[3]);
+    }
+}
+
+// Two chains sharing the matrix stream (zhat and z for the termination test).
+template <typename T>
+__device__ __forceinline__ void chain4x2(const T* __restrict__ Mt, int ld, int r0, const T* v,
+                                         const T* u2, int K, T (&acc)[4], T (&acc2)[4]) {
+    using V = typename V4<T>::type;
+    const T* col = Mt + r0;
+    int k = 0;
+    for (; k + kUnrollK <= K; k += kUnrollK) {
+        V a[kUnrollK];
+#pragma unroll
+        for (int u = 0; u < kUnrollK; ++u) a[u] = *reinterpret_cast<const V*>(col + (size_t)(k + u) * ld);
+#pragma unroll
+        for (int u = 0; u < kUnrollK; ++u) {
+            const T vk = v[k + u], zk = u2[k + u];
+            acc[0] = fmad(a[u].x, vk, acc[0]);
+            acc[1] = fmad(a[u].y, vk, acc[1]);
+            acc[2] = fmad(a[u].z, vk, acc[2]);
+            acc[3] = fmad(a[u].w, vk, acc[3]);
+            acc2[0] = fmad(a[u].x, zk, acc2[0]);
+            acc2[1] = fmad(a[u].y, zk, acc2[1]);
+            acc2[2] = fmad(a[u].z, zk, acc2[2]);
+            acc2[3] = fmad(a[u].w, zk, acc2[3]);
+        }
+    }
+    for (; k < K; ++k) {
+        const V a = *reinterpret_cast<const V*>(col + (size_t)k * ld);
+        const T vk = v[k], zk = u2[k];
+        acc[0] = fmad(a.x, vk, acc[0]);
+        acc[1] = fmad(a.y, vk, acc[1]);
+        acc[2] = fmad(a.z, vk, acc[2]);
+        acc[3] = fmad(a.w, vk, acc[3]);
+        acc2[0] = fmad(a.x, zk, acc2[0]);
+        acc2[1] = fmad(a.y, zk, acc2[1]);
+        acc2[2] = fmad(a.z, zk, acc2[2]);
+        acc2[3] = fmad(a.w, zk, acc2[3]);
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kStreamBlock) void gpad_stream_kernel(SolveArgs<T> a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x;
+    const int b = blockIdx.x;
+    const int n = a.n, m = a.m, ldn = a.ldn, ldm = a.ldm;
+    const StreamLds<T> s = stream_lds<T>(smem, ldn, ldm);
+    const T* __restrict__ MGt = a.MGt + (size_t)b * a.strideA;
+    const T* __restrict__ GLt = a.GLt + (size_t)b * a.strideB;
+    T* zg = a.z + (size_t)b * n;
+    T* yg = a.y + (size_t)b * m;
+    const T* gPg = a.gP + (size_t)b * a.ld_gP;
+    const T* gg = a.g + (size_t)b * a.ld_g;
+    const T beta0 = a.beta[0];
+
+    for (int i = tid; i < ldn; i += kStreamBlock) {
+        s.zs[i] = i < n ? zg[i] : T(0);
+        s.gp[i] = i < n ? gPg[i] : T(0);
+        s.zh[i] = T(0);
+    }
+    for (int i = tid; i < ldm; i += kStreamBlock) {
+        const T yv = i < m ? yg[i] : T(0);
+        s.ys[i] = yv;
+        s.pd[i] = i < m ? (T)(a.gscale * (double)gg[i]) : T(0);
+        s.w[i] = fmad(beta0, yv - yv, yv);  // 8a with y_0 = y_{-1} (acceldualgrad.m:16,43)
+    }
+    __syncthreads();
+
+    const int nwaves = kStreamBlock / 64;
+    int it = 0;
+    int done = 0;
+    for (int v = 0; v < a.N; ++v) {
+        const T th = a.theta[v];
+        const T omt = T(1) - th;
+        const T bnext = a.beta[v + 1];
+        // ---- phase 1: 8b + 8c, rows of -ML ----------------------------------------------
+        for (int r0 = 4 * tid; r0 < n; r0 += 4 * kStreamBlock) {
+            T acc[4] = {T(0), T(0), T(0), T(0)};
+            chain4<T>(MGt, ldn, r0, s.w, m, acc);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = r0 + r;
+                if (i < n) {
+                    const T zhv = acc[r] - s.gp[i];                 // seq_functions.cpp:63
+                    s.zh[i] = zhv;
+                    s.zs[i] = fmad(omt, s.zs[i], th * zhv);         // seq_functions.cpp:70
+                }
+            }
+        }
+        __syncthreads();
+        // ---- phase 2: 8d + next 8a, rows of G/L ------------------------------------------
+        const bool chk = a.tol > 0.0 && ((v + 1) % a.check_every) == 0;
+        T violz = neg_inf<T>(), violh = neg_inf<T>(), wmin = -neg_inf<T>();
+        double gap = 0.0;
+        for (int r0 = 4 * tid; r0 < m; r0 += 4 * kStreamBlock) {
+            T c[4] = {T(0), T(0), T(0), T(0)};
+            T cz[4] = {T(0), T(0), T(0), T(0)};
+            if (chk)
+                chain4x2<T>(GLt, ldm, r0, s.zh, s.zs, n, c, cz);
+            else
+                chain4<T>(GLt, ldm, r0, s.zh, n, c);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = r0 + r;
+                if (i < m) {
+                    const T wi = s.w[i], pdi = s.pd[i], yi = s.ys[i];
+                    const T sv = (wi + pdi) + c[r];                 // seq_functions.cpp:84
+                    const T yp = (absd(sv) + sv) * T(0.5);          // seq_functions.cpp:85
+                    if (chk) {
+                        const T t = c[r] + pdi;
+                        violh = fmax(violh, t);
+                        wmin = fmin(wmin, wi);
+                        gap -= (double)wi * (double)t;
+                        violz = fmax(violz, cz[r] + pdi);
+                    }
+                    s.w[i] = fmad(bnext, yp - yi, yp);               // next 8a
+                    s.ys[i] = yp;
+                }
+            }
+        }
+        if (chk) check_publish<T>(s.slots, violz, violh, wmin, gap);
+        __syncthreads();
+        it = v + 1;
+        if (chk) done = check_decide(s.slots, nwaves, a.L, a.tol);
+        if (done) break;
+    }
+    const T* zout = done == 2 ? s.zh : s.zs;  // test (B) certifies zhat
+    for (int i = tid; i < n; i += kStreamBlock) zg[i] = zout[i];
+    for (int i = tid; i < m; i += kStreamBlock) yg[i] = s.ys[i];
+    if (tid == 0) {
+        a.iters[b] = it;
+        a.conv[b] = done;
+    }
+}
+
+template <typename T>
+hipError_t launch_stream(const SolveArgs<T>& a, hipStream_t st) {
+    const size_t lds = sizeof(T) * (size_t)(3 * a.ldn + 3 * a.ldm) +
+                       sizeof(CheckSlot) * (kStreamBlock / 64);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)gpad_stream_kernel<T>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(gpad_stream_kernel<T>, dim3(a.batch), dim3(kStreamBlock), lds, st, a);
+    return hipGetLastError();
+}
+template hipError_t launch_stream<float>(const SolveArgs<float>&, hipStream_t);
+template hipError_t launch_stream<double>(const SolveArgs<double>&, hipStream_t);
+
+// =========================================================================================
+// gpad_resident_kernel: one matrix row per lane, held in VGPRs for the whole solve.
+// =========================================================================================
+// K = row-register capacity (multiple of 16, >= max(m, n)).  A lane owning primal row i
+// keeps -ML[i][0..m); a lane owning constraint row i keeps G_L[i][0..n).  Both roles use the
+// same register array r[] (they live in different waves).
+//
+// The broadcast vector is read 8 floats (two ds_read_b128) one group ahead and a
+// sched_barrier closes every group: without it the scheduler hoists all K/4 LDS reads to
+// the top of the chain and the live vector copy spills r[] to scratch.
+constexpr int kResGroup = 8;
+
+template <int K>
+__device__ __forceinline__ float chain_regs(const float (&r)[K], const float* v, int len) {
+    static_assert(K % kResGroup == 0, "K must be a multiple of the group");
+    float acc = 0.0f;
+    float4 c0 = *reinterpret_cast<const float4*>(v);
+    float4 c1 = *reinterpret_cast<const float4*>(v + 4);
+#pragma unroll
+    for (int k = 0; k < K; k += kResGroup) {
+        // wave-uniform skip (a constant trip count keeps r[] in VGPRs); r[] and v[] are
+        // zero-padded to K, so the tail of the last live group adds +0 products
+        if (k < len) {
+            float4 n0 = c0, n1 = c1;
+            if (k + kResGroup < K) {
+                n0 = *reinterpret_cast<const float4*>(v + k + kResGroup);
+                n1 = *reinterpret_cast<const float4*>(v + k + kResGroup + 4);
+            }
+            acc = __builtin_fmaf(r[k + 0], c0.x, acc);
+            acc = __builtin_fmaf(r[k + 1], c0.y, acc);
+            acc = __builtin_fmaf(r[k + 2], c0.z, acc);
+            acc = __builtin_fmaf(r[k + 3], c0.w, acc);
+            acc = __builtin_fmaf(r[k + 4], c1.x, acc);
+            acc = __builtin_fmaf(r[k + 5], c1.y, acc);
+            acc = __builtin_fmaf(r[k + 6], c1.z, acc);
+            acc = __builtin_fmaf(r[k + 7], c1.w, acc);
+            c0 = n0;
+            c1 = n1;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    return acc;
+}
+
+constexpr int kResidentMaxThreads = 512;
+constexpr int kResidentMaxRow = 208;
+
+template <int K>
+__global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(SolveArgs<float> a) {
+    __shared__ __attribute__((aligned(16))) float w_l[K];   // w, broadcast to -ML rows
+    __shared__ __attribute__((aligned(16))) float zh_l[K];  // zhat, broadcast to G/L rows
+    __shared__ __attribute__((aligned(16))) float z_l[K];   // z, for the termination test
+    __shared__ CheckSlot slots[kResidentMaxThreads / 64];
+
+    const int tid = threadIdx.x;
+    const int b = blockIdx.x;
+    const int n = a.n, m = a.m;
+    const int nA = (n + 63) >> 6;
+    const int nwaves = blockDim.x >> 6;
+    const bool isA = (tid >> 6) < nA;               // wave-uniform role
+    const int row = isA ? tid : tid - 64 * nA;
+    const bool live = isA ? row < n : row < m;
+    const int len = isA ? m : n;                     // chain length of this lane's row
+    const float* __restrict__ Mt = isA ? a.MGt + (size_t)b * a.strideA
+                                       : a.GLt + (size_t)b * a.strideB;
+    const int ld = isA ? a.ldn : a.ldm;
+
+    // preload the row (k-major layout: consecutive lanes read consecutive words)
+    float r[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) r[k] = (live && k < len) ? Mt[(size_t)k * ld + row] : 0.0f;
+
+    float* zg = a.z + (size_t)b * n;
+    float* yg = a.y + (size_t)b * m;
+    float zi = 0.0f, gpi = 0.0f, yi = 0.0f, pdi = 0.0f, wi = 0.0f;
+    if (isA) {
+        if (live) {
+            zi = zg[row];
+            gpi = a.gP[(size_t)b * a.ld_gP + row];
+        }
+    } else if (live) {
+        yi = yg[row];
+        pdi = (float)(a.gscale * (double)a.g[(size_t)b * a.ld_g + row]);
+        wi = __builtin_fmaf(a.beta[0], yi - yi, yi);
+    }
+    for (int i = tid; i < K; i += blockDim.x) {
+        w_l[i] = 0.0f;
+        zh_l[i] = 0.0f;
+        z_l[i] = 0.0f;
+    }
+    __syncthreads();
+    if (!isA && live) w_l[row] = wi;
+    __syncthreads();
+
+    int it = 0;
+    int done = 0;
+    float zhi = 0.0f;
+    for (int v = 0; v < a.N; ++v) {
+        const bool chk = a.tol > 0.0 && ((v + 1) % a.check_every) == 0;
+        if (isA) {  // ---- 8b + 8c --------------------------------------------------------
+            const float acc = chain_regs<K>(r, w_l, m);
+            if (live) {
+                const float th = a.theta[v];
+                const float zhv = acc - gpi;
+                zi = __builtin_fmaf(1.0f - th, zi, th * zhv);
+                zh_l[row] = zhv;
+                zhi = zhv;
+                if (chk) z_l[row] = zi;
+            }
+        }
+        __syncthreads();
+        float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY;
+        double gap = 0.0;
+        if (!isA) {  // ---- 8d + next 8a ------------------------------------------------
+            const float c = chain_regs<K>(r, zh_l, n);
+            const float cz = chk ? chain_regs<K>(r, z_l, n) : 0.0f;
+            if (live) {
+                const float sv = (wi + pdi) + c;
+                const float yp = (__builtin_fabsf(sv) + sv) * 0.5f;
+                if (chk) {
+                    const float t = c + pdi;
+                    violh = t;
+                    wmin = wi;
+                    gap = -((double)wi * (double)t);
+                    violz = cz + pdi;
+                }
+                wi = __builtin_fmaf(a.beta[v + 1], yp - yi, yp);
+                yi = yp;
+                w_l[row] = wi;
+            }
+        }
+        if (chk) check_publish<float>(slots, violz, violh, wmin, gap);
+        __syncthreads();
+        it = v + 1;
+        if (chk) done = check_decide(slots, nwaves, a.L, a.tol);
+        if (done) break;
+    }
+    if (live) {
+        if (isA)
+            zg[row] = done == 2 ? zhi : zi;  // test (B) certifies zhat
+        else
+            yg[row] = yi;
+    }
+    if (tid == 0) {
+        a.iters[b] = it;
+        a.conv[b] = done;
+    }
+}
+
+hipError_t launch_resident(const SolveArgs<float>& a, hipStream_t st, bool* supported) {
+    const int mx = a.n > a.m ? a.n : a.m;
+    const int threads = 64 * (((a.n + 63) >> 6) + ((a.m + 63) >> 6));
+    *supported = mx <= kResidentMaxRow && threads <= kResidentMaxThreads && a.n > 0 && a.m > 0;
+    if (!*supported) return hipSuccess;
+    const dim3 grid(a.batch), block(threads);
+    if (mx <= 64)
+        hipLaunchKernelGGL(gpad_resident_kernel<64>, grid, block, 0, st, a);
+    else if (mx <= 128)
+        hipLaunchKernelGGL(gpad_resident_kernel<128>, grid, block, 0, st, a);
+    else if (mx <= 192)
+        hipLaunchKernelGGL(gpad_resident_kernel<192>, grid, block, 0, st, a);
+    else
+        hipLaunchKernelGGL(gpad_resident_kernel<kResidentMaxRow>, grid, block, 0, st, a);
+    return hipGetLastError();
+}
+
+// =========================================================================================
+// layout kernels
+// =========================================================================================
+// out[k*ld + i] = (T)(scale * in[i*cols + k]); 32x32 tiles through LDS so both the read of
+// the row-major input and the write of the k-major output are coalesced.
+template <typename T>
+__global__ __launch_bounds__(256) void pack_kmajor_kernel(const T* __restrict__ in, T* __restrict__ out,
+                                                          int rows, int cols, int ld, double scale,
+                                                          long long in_stride, long long out_stride) {
+    __shared__ T tile[32][33];
+    const T* src = in + (size_t)blockIdx.z * in_stride;
+    T* dst = out + (size_t)blockIdx.z * out_stride;
+    const int i0 = blockIdx.y * 32, k0 = blockIdx.x * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+    for (int r = ty; r < 32; r += 8) {
+        const int i = i0 + r, k = k0 + tx;
+        tile[r][tx] = (i < rows && k < cols) ? (T)(scale * (double)src[(size_t)i * cols + k]) : T(0);
+    }
+    __syncthreads();
+    for (int r = ty; r < 32; r += 8) {
+        const int k = k0 + r, i = i0 + tx;
+        if (k < cols && i < ld) dst[(size_t)k * ld + i] = tile[tx][r];
+    }
+}
+
+template <typename T>
+hipError_t launch_pack_kmajor(const T* in, T* out, int rows, int cols, int ld, double scale,
+                              int batch, long long in_stride, long long out_stride, hipStream_t s) {
+    const dim3 grid((cols + 31) / 32, (ld + 31) / 32, batch);
+    hipLaunchKernelGGL(pack_kmajor_kernel<T>, grid, dim3(256), 0, s, in, out, rows, cols, ld, scale,
+                       in_stride, out_stride);
+    return hipGetLastError();
+}
+template hipError_t launch_pack_kmajor<float>(const float*, float*, int, int, int, double, int,
+                                              long long, long long, hipStream_t);
+template hipError_t launch_pack_kmajor<double>(const double*, double*, int, int, int, double, int,
+                                               long long, long long, hipStream_t);
+
+// =========================================================================================
+// per-step kernels (kernel_functions.h:9-41 one for one; seq_functions.cpp semantics)
+// =========================================================================================
+__global__ void step1_kernel(const float* __restrict__ y, const float* __restrict__ ym1,
+                             float* __restrict__ w, float beta, int m) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x)
+        w[i] = __builtin_fmaf(beta, y[i] - ym1[i], y[i]);
+}
+
+// One lane per output row, sequential chain over the row (bit-exact with the CPU step);
+// the vector is staged in LDS (as StepTwoGPADKernel's w_vs, kernel_functions.cu:37-42).
+__global__ __launch_bounds__(256) void step_gemv_kernel(const float* __restrict__ A,
+                                                        const float* __restrict__ x, int rows, int cols,
+                                                        const float* __restrict__ bias, float bsign,
+                                                        const float* __restrict__ addv,
+                                                        float* __restrict__ out, int relu) {
+    extern __shared__ __attribute__((aligned(16))) float xs[];
+    for (int k = threadIdx.x; k < cols; k += blockDim.x) xs[k] = x[k];
+    __syncthreads();
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rows) return;
+    const float* row = A + (size_t)i * cols;
+    float acc = 0.0f;
+    for (int k = 0; k < cols; ++k) acc = __builtin_fmaf(row[k], xs[k], acc);
+    if (!relu) {
+        out[i] = acc - bias[i];  // 8b: zhat = MGneg w - gP
+    } else {
+        const float s = (addv[i] + bias[i]) + acc;  // 8d: (w + pD) + sum
+        out[i] = (__builtin_fabsf(s) + s) * 0.5f;
+    }
+    (void)bsign;
+}
+
+__global__ void step3_kernel(float theta, const float* zm1, const float* __restrict__ zhat, float* z,
+                             int n) {
+    const float omt = 1.0f - theta;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        z[i] = __builtin_fmaf(omt, zm1[i], theta * zhat[i]);
+}
+
+static dim3 grid1d(int n) {
+    int g = (n + 255) / 256;
+    if (g < 1) g = 1;
+    if (g > 2048) g = 2048;
+    return dim3(g);
+}
+
+hipError_t launch_step1(const float* y, const float* ym1, float* w, float beta, int m, hipStream_t s) {
+    hipLaunchKernelGGL(step1_kernel, grid1d(m), dim3(256), 0, s, y, ym1, w, beta, m);
+    return hipGetLastError();
+}
+hipError_t launch_step2(const float* MGneg, const float* w, const float* gP, float* zhat, int n,
+                        int m, hipStream_t s) {
+    hipLaunchKernelGGL(step_gemv_kernel, dim3((n + 255) / 256), dim3(256), sizeof(float) * (size_t)m, s,
+                       MGneg, w, n, m, gP, -1.0f, (const float*)nullptr, zhat, 0);
+    return hipGetLastError();
+}
+hipError_t launch_step3(float theta, const float* zm1, const float* zhat, float* z, int n,
+                        hipStream_t s) {
+    hipLaunchKernelGGL(step3_kernel, grid1d(n), dim3(256), 0, s, theta, zm1, zhat, z, n);
+    return hipGetLastError();
+}
+hipError_t launch_step4(const float* GL, float* yp1, const float* w, const float* pD,
+                        const float* zhat, int n, int m, hipStream_t s) {
+    hipLaunchKernelGGL(step_gemv_kernel, dim3((m + 255) / 256), dim3(256), sizeof(float) * (size_t)n, s,
+                       GL, zhat, m, n, pD, 1.0f, w, yp1, 1);
+    return hipGetLastError();
+}
+
+}  // namespace gpad

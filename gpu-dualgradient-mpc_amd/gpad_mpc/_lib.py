@@ -1,0 +1,98 @@
+"""ctypes binding of libgpad.so (include/gpad.h).
+
+The shared library is built in-tree (``make -C gpu-dualgradient-mpc_amd``) next to this file
+so it travels with the repository.  There is no fallback: if the library is missing or does
+not load, every entry point raises -- the product path never silently drops to Python.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgpad.so")
+
+GPAD_OK = 0
+ERR_INVALID, ERR_HIP, ERR_NOMEM, ERR_UNSUPPORTED, ERR_NOT_SETUP, ERR_NO_DEVICE = -1, -2, -3, -4, -5, -6
+SCHEDULE_MATLAB, SCHEDULE_PAPER = 0, 1
+MEM_HOST, MEM_DEVICE = 0, 1
+DTYPE_F32, DTYPE_F64 = 0, 1
+KERNEL_AUTO, KERNEL_STREAM, KERNEL_RESIDENT, KERNEL_PANEL = 0, 1, 2, 3
+KERNEL_NAMES = {KERNEL_AUTO: "auto", KERNEL_STREAM: "stream", KERNEL_RESIDENT: "resident",
+                KERNEL_PANEL: "panel"}
+
+# every symbol include/gpad.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "gpad_version", "gpad_strerror", "gpad_last_error", "gpad_create", "gpad_destroy",
+    "gpad_set_stream", "gpad_setup", "gpad_setup_scaled", "gpad_run", "gpad_run_scaled",
+    "gpad_last_stats", "gpad_solve", "gpad_step1_extrapolate", "gpad_step2_primal",
+    "gpad_step3_average", "gpad_step4_project", "gpad_schedule", "gpad_sync",
+]
+
+
+class Dims(C.Structure):
+    _fields_ = [("n", C.c_int), ("m", C.c_int), ("batch", C.c_int), ("shared", C.c_int),
+                ("dtype", C.c_int), ("memory", C.c_int), ("schedule", C.c_int),
+                ("check_every", C.c_int), ("kernel", C.c_int)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("iterations", C.c_int), ("converged", C.c_int),
+                ("total_iterations", C.c_longlong), ("kernel", C.c_int),
+                ("kernel_ms", C.c_double), ("iters", C.POINTER(C.c_int))]
+
+
+class GpadError(RuntimeError):
+    def __init__(self, code: int, where: str, detail: str = ""):
+        self.code = code
+        super().__init__(f"{where}: status {code}" + (f" ({detail})" if detail else ""))
+
+
+_LIB = None
+
+
+def load(path: str = LIB_PATH) -> C.CDLL:
+    """Load libgpad.so once.  Raises (loudly) when the HIP library is absent."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise ImportError(f"libgpad.so not built at {path}: run `make -C gpu-dualgradient-mpc_amd` "
+                          "(or __graft_entry__.build()); there is no CPU fallback")
+    L = C.CDLL(path)
+    vp, cvp, i, d = C.c_void_p, C.c_void_p, C.c_int, C.c_double
+    L.gpad_version.restype = C.c_char_p
+    L.gpad_strerror.restype = C.c_char_p
+    L.gpad_strerror.argtypes = [i]
+    L.gpad_last_error.restype = C.c_char_p
+    L.gpad_create.argtypes = [C.POINTER(vp), i, vp]
+    L.gpad_destroy.argtypes = [vp]
+    L.gpad_set_stream.argtypes = [vp, vp]
+    L.gpad_sync.argtypes = [vp]
+    L.gpad_setup.argtypes = [vp, C.POINTER(Dims), cvp, cvp, d]
+    L.gpad_setup_scaled.argtypes = [vp, C.POINTER(Dims), cvp, cvp, d]
+    L.gpad_run.argtypes = [vp, vp, vp, cvp, cvp, i, d, C.POINTER(Stats)]
+    L.gpad_run_scaled.argtypes = [vp, vp, vp, cvp, cvp, i, d, cvp, cvp, C.POINTER(Stats)]
+    L.gpad_last_stats.argtypes = [vp, C.POINTER(Stats)]
+    L.gpad_solve.argtypes = [vp, vp, cvp, cvp, cvp, cvp, i, d, d, C.POINTER(Dims), C.POINTER(Stats)]
+    f = C.POINTER(C.c_float)
+    L.gpad_step1_extrapolate.argtypes = [vp, vp, vp, vp, C.c_float, i]
+    L.gpad_step2_primal.argtypes = [vp, vp, vp, vp, vp, i, i]
+    L.gpad_step3_average.argtypes = [vp, C.c_float, vp, vp, vp, i]
+    L.gpad_step4_project.argtypes = [vp, vp, vp, vp, vp, vp, i, i]
+    L.gpad_schedule.argtypes = [i, i, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    del f
+    for name in ["gpad_create", "gpad_destroy", "gpad_set_stream", "gpad_sync", "gpad_setup",
+                 "gpad_setup_scaled", "gpad_run", "gpad_run_scaled", "gpad_last_stats",
+                 "gpad_solve", "gpad_step1_extrapolate", "gpad_step2_primal",
+                 "gpad_step3_average", "gpad_step4_project", "gpad_schedule"]:
+        getattr(L, name).restype = i
+    _LIB = L
+    return L
+
+
+def check(code: int, where: str) -> None:
+    if code != GPAD_OK:
+        L = load()
+        detail = (L.gpad_last_error() or b"").decode(errors="replace")
+        raise GpadError(code, where, detail or L.gpad_strerror(code).decode())

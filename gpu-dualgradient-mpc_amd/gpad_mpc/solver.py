@@ -1,0 +1,213 @@
+"""Host-side mirror of the reference's GPAD interfaces, on top of libgpad.so.
+
+* ``solve(z0, y0, ML, M, G, g, N, L, tol)`` -- the north-star entry surface (BASELINE.json),
+  numpy in / numpy out (host memory) or torch device tensors (device memory, in place).
+* ``acceldualgrad(H, f, A_i, b_i, Qx, Qu, n_u)`` -- the reference MATLAB function
+  (Code/MATLAB/acceldualgrad.m:1) with the same arguments and return ``u = z(1:n_u)``;
+  precompute as acceldualgrad.m:11,20-23, the 100-iteration loop on the GPU.
+* ``GpadSolver`` -- a handle: ``setup`` once per plant (constant ML/G), ``run`` per state.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import Dims, Stats, check
+
+
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch")
+
+
+def _dtype_code(x) -> int:
+    if _is_torch(x):
+        import torch
+        if x.dtype == torch.float64:
+            return _lib.DTYPE_F64
+        if x.dtype == torch.float32:
+            return _lib.DTYPE_F32
+        raise TypeError(f"unsupported torch dtype {x.dtype}")
+    if x.dtype == np.float64:
+        return _lib.DTYPE_F64
+    if x.dtype == np.float32:
+        return _lib.DTYPE_F32
+    raise TypeError(f"unsupported dtype {x.dtype}")
+
+
+def _ptr(x):
+    if _is_torch(x):
+        if not x.is_contiguous():
+            raise ValueError("device tensors must be contiguous")
+        return C.c_void_p(x.data_ptr())
+    if not x.flags["C_CONTIGUOUS"]:
+        raise ValueError("host arrays must be C-contiguous")
+    return C.c_void_p(x.ctypes.data)
+
+
+class GpadSolver:
+    """One libgpad handle (device + HIP stream + packed matrices + workspaces)."""
+
+    def __init__(self, device: int = 0, stream=None):
+        self.lib = _lib.load()
+        self.h = C.c_void_p()
+        if stream is None and self._torch_device_ready():
+            import torch
+            stream = torch.cuda.current_stream(device).cuda_stream
+        check(self.lib.gpad_create(C.byref(self.h), device, C.c_void_p(stream or 0)), "gpad_create")
+        self.dims = None
+
+    @staticmethod
+    def _torch_device_ready() -> bool:
+        try:
+            import torch
+            return torch.cuda.is_available()
+        except Exception:  # noqa: BLE001 - torch is optional for host-memory use
+            return False
+
+    def close(self):
+        if self.h:
+            self.lib.gpad_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_stream(self, stream) -> None:
+        check(self.lib.gpad_set_stream(self.h, C.c_void_p(stream or 0)), "gpad_set_stream")
+
+    def setup(self, ML, G, L: float, *, n: int, m: int, batch: int = 1, shared: bool = True,
+              schedule: int = _lib.SCHEDULE_MATLAB, check_every: int = 10,
+              kernel: int = _lib.KERNEL_AUTO, scaled: bool = False) -> None:
+        """Bind (ML, G, L) -- or (MGneg, GL, L) with ``scaled`` (reference data-file form)."""
+        mem = _lib.MEM_DEVICE if _is_torch(ML) else _lib.MEM_HOST
+        if _is_torch(ML) and not ML.is_cuda:
+            raise ValueError("torch inputs must live on the GPU (use numpy for host memory)")
+        self.dims = Dims(n=n, m=m, batch=batch, shared=int(bool(shared)), dtype=_dtype_code(ML),
+                         memory=mem, schedule=schedule, check_every=check_every, kernel=kernel)
+        fn = self.lib.gpad_setup_scaled if scaled else self.lib.gpad_setup
+        check(fn(self.h, C.byref(self.dims), _ptr(ML), _ptr(G), float(L)), "gpad_setup")
+
+    def run(self, z, y, M, g, N: int, tol: float = 0.0, *, stats: bool = True, iters=None,
+            scaled: bool = False, theta=None, beta=None):
+        """Run GPAD in place on z [batch][n] / y [batch][m].  Returns a dict of stats, or None
+        when ``stats`` is False and the inputs are device tensors (asynchronous launch)."""
+        st = Stats()
+        it_arr = None
+        if iters is not None:
+            it_arr = iters
+            st.iters = it_arr.ctypes.data_as(C.POINTER(C.c_int))
+        want = stats or not _is_torch(z)
+        if scaled:
+            rc = self.lib.gpad_run_scaled(self.h, _ptr(z), _ptr(y), _ptr(M), _ptr(g), int(N),
+                                          float(tol), _ptr(theta) if theta is not None else None,
+                                          _ptr(beta) if beta is not None else None,
+                                          C.byref(st) if want else None)
+        else:
+            rc = self.lib.gpad_run(self.h, _ptr(z), _ptr(y), _ptr(M), _ptr(g), int(N), float(tol),
+                                   C.byref(st) if want else None)
+        check(rc, "gpad_run")
+        if not want:
+            return None
+        return self._stats_dict(st)
+
+    def last_stats(self, iters=None) -> dict:
+        st = Stats()
+        if iters is not None:
+            st.iters = iters.ctypes.data_as(C.POINTER(C.c_int))
+        check(self.lib.gpad_last_stats(self.h, C.byref(st)), "gpad_last_stats")
+        return self._stats_dict(st)
+
+    @staticmethod
+    def _stats_dict(st: Stats) -> dict:
+        return dict(iterations=st.iterations, converged=st.converged,
+                    total_iterations=st.total_iterations, kernel=_lib.KERNEL_NAMES.get(st.kernel),
+                    kernel_ms=st.kernel_ms)
+
+    def sync(self) -> None:
+        check(self.lib.gpad_sync(self.h), "gpad_sync")
+
+    # ---- per-step entry points (device tensors; kernel_functions.h one-for-one) ----------
+    def step1(self, y, ym1, w, beta: float):
+        check(self.lib.gpad_step1_extrapolate(self.h, _ptr(y), _ptr(ym1), _ptr(w), float(beta),
+                                              y.numel()), "gpad_step1")
+
+    def step2(self, MGneg, w, gP, zhat):
+        n, m = MGneg.shape
+        check(self.lib.gpad_step2_primal(self.h, _ptr(MGneg), _ptr(w), _ptr(gP), _ptr(zhat), n, m),
+              "gpad_step2")
+
+    def step3(self, theta: float, zm1, zhat, z):
+        check(self.lib.gpad_step3_average(self.h, float(theta), _ptr(zm1), _ptr(zhat), _ptr(z),
+                                          z.numel()), "gpad_step3")
+
+    def step4(self, GL, yp1, w, pD, zhat):
+        m, n = GL.shape
+        check(self.lib.gpad_step4_project(self.h, _ptr(GL), _ptr(yp1), _ptr(w), _ptr(pD),
+                                          _ptr(zhat), n, m), "gpad_step4")
+
+
+def schedule(N: int, kind: int = _lib.SCHEDULE_MATLAB):
+    """theta[v], beta[v] (acceldualgrad.m:18,27,55-56) from the library's host routine."""
+    lib = _lib.load()
+    th = np.empty(max(N, 1), np.float64)
+    be = np.empty(max(N, 1), np.float64)
+    check(lib.gpad_schedule(N, kind, th.ctypes.data_as(C.POINTER(C.c_double)),
+                            be.ctypes.data_as(C.POINTER(C.c_double))), "gpad_schedule")
+    return th[:N], be[:N]
+
+
+def solve(z0, y0, ML, M, G, g, N: int, L: float, tol: float = 0.0, *, shared: bool = True,
+          schedule: int = _lib.SCHEDULE_MATLAB, check_every: int = 10,
+          kernel: int = _lib.KERNEL_AUTO, device: int = 0):
+    """solve(z0, y0, ML, M, G, g, N, L, tol) -> (z*, y*, stats).
+
+    Shapes: z0 (n,) or (batch, n); y0 (m,) or (batch, m); ML (n, m) or (batch, n, m); M like z0;
+    G (m, n) or (batch, m, n); g like y0.  numpy inputs are copied (host memory); torch device
+    tensors are updated in place."""
+    torch_in = _is_torch(z0)
+    if torch_in:
+        z, y = z0, y0
+    else:
+        dt = np.float64 if np.asarray(ML).dtype == np.float64 else np.float32
+        z = np.array(z0, dtype=dt, copy=True, order="C")
+        y = np.array(y0, dtype=dt, copy=True, order="C")
+        ML = np.ascontiguousarray(ML, dt)
+        G = np.ascontiguousarray(G, dt)
+        M = np.ascontiguousarray(M, dt)
+        g = np.ascontiguousarray(g, dt)
+    n, m = ML.shape[-2], ML.shape[-1]
+    batch = z.shape[0] if z.ndim == 2 else 1
+    shared = shared and ML.ndim == 2
+    with GpadSolver(device) as s:
+        s.setup(ML, G, L, n=n, m=m, batch=batch, shared=shared, schedule=schedule,
+                check_every=check_every, kernel=kernel)
+        st = s.run(z, y, M, g, N, tol)
+    return z, y, st
+
+
+def acceldualgrad(H, f, A_i, b_i, Qx=None, Qu=None, n_u: int = 1, num_iterations: int = 100,
+                  dtype=np.float64, tol: float = 0.0):
+    """Code/MATLAB/acceldualgrad.m:1 -- [u, z, y] with u = z(1:n_u) (:83).  Qx/Qu are accepted
+    and unused, as in the reference.  Precompute (:11,20-23) on the host in fp64; the GPAD
+    iterations run in libgpad on the GPU."""
+    H = np.asarray(H, np.float64)
+    A_i = np.asarray(A_i, np.float64)
+    Hinv = np.linalg.inv(H)
+    L = float(np.linalg.norm(H, "fro") ** 2)                    # acceldualgrad.m:11
+    ML = Hinv @ A_i.T                                           # :20
+    M = Hinv @ np.asarray(f, np.float64).reshape(-1)            # :21
+    n, m = ML.shape
+    z, y, _ = solve(np.zeros(n), np.zeros(m), ML.astype(dtype), M.astype(dtype), A_i.astype(dtype),
+                    np.asarray(b_i, np.float64).astype(dtype), num_iterations, L, tol)
+    return z[:n_u], z, y

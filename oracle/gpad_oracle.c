@@ -1,0 +1,243 @@
+/*
+ * gpad_oracle.c -- CPU ORACLE for the GPAD inner loop.  TEST INFRASTRUCTURE ONLY
+ * (the checker, never the thing measured or shipped).  See gpad_oracle.h for the
+ * parity pins.  Compiled with -ffp-contract=off: every fused multiply-add below is
+ * an explicit fmaf()/fma() mirroring what the reference's FMA-contracted build does.
+ */
+#include "gpad_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* 8a -- seq_functions.cpp:45-51.  g++ contracts y + beta*(y - ym1) to fma(beta, y-ym1, y). */
+void orc_step1_f32(const float* y, const float* ym1, float* w, float beta, int m) {
+    for (int i = 0; i < m; i++) w[i] = fmaf(beta, y[i] - ym1[i], y[i]);
+}
+
+/* 8b -- seq_functions.cpp:54-66.  Row-major n x m, sequential fmaf chain from +0. */
+void orc_step2_f32(const float* MGneg, const float* w, const float* gP, float* zhat, int n, int m) {
+    for (int i = 0; i < n; i++) {
+        float sum = 0.0f;
+        const float* row = MGneg + (size_t)i * m;
+        for (int j = 0; j < m; j++) sum = fmaf(row[j], w[j], sum);
+        zhat[i] = sum - gP[i];
+    }
+}
+
+/* 8c -- seq_functions.cpp:68-72 (= step3.cu:24-28).  g++ emits
+ * t = theta*zhat; z = fma(1-theta, zm1, t). */
+void orc_step3_f32(float theta, int n, const float* zm1, const float* zhat, float* z) {
+    const float omt = 1.0f - theta;
+    for (int i = 0; i < n; i++) z[i] = fmaf(omt, zm1[i], theta * zhat[i]);
+}
+
+/* 8d -- seq_functions.cpp:75-87.  s = (w + pD) + sum;  y+ = (|s| + s) / 2 (exact relu). */
+void orc_step4_f32(const float* GL, float* yp1, const float* w, const float* pD, const float* zhat,
+                   int n, int m) {
+    for (int i = 0; i < m; i++) {
+        float sum = 0.0f;
+        const float* row = GL + (size_t)i * n;
+        for (int j = 0; j < n; j++) sum = fmaf(row[j], zhat[j], sum);
+        float s = (w[i] + pD[i]) + sum;
+        yp1[i] = (fabsf(s) + s) * 0.5f;
+    }
+}
+
+/* acceldualgrad.m:20-23: M_G = inv(H)*A', G_L = (1/L)*A, p_D = (-1/L)*b.  The C path's
+ * file stores M_G sign-folded (main.cu:43-44 + seq_functions.cpp:61 compute +M_G.w), so
+ * MGneg = -ML.  The scalings are done in fp64 as MATLAB does, then rounded to fp32. */
+void orc_scale_f32(const float* ML, const float* G, const float* g, float L, int n, int m,
+                   float* MGneg, float* GL, float* pD) {
+    const double inv = 1.0 / (double)L, ninv = -1.0 / (double)L;
+    if (MGneg) for (size_t k = 0; k < (size_t)n * m; k++) MGneg[k] = -ML[k];
+    if (GL) for (size_t k = 0; k < (size_t)n * m; k++) GL[k] = (float)(inv * (double)G[k]);
+    if (pD) for (int i = 0; i < m; i++) pD[i] = (float)(ninv * (double)g[i]);
+}
+
+/* acceldualgrad.m:18,27,55-56 (MATLAB, beta lagged) or eq. (8e) of the paper. */
+void orc_schedule(int N, int kind, double* theta, double* beta) {
+    double th = 1.0, thm1 = 1.0, b = 0.0;
+    for (int v = 0; v < N; v++) {
+        const double thn = (sqrt(pow(th, 4.0) + 4.0 * pow(th, 2.0)) - pow(th, 2.0)) / 2.0;
+        if (kind == ORC_SCHEDULE_PAPER) {
+            theta[v] = th;
+            beta[v] = th * (1.0 / thm1 - 1.0);
+        } else {
+            theta[v] = th;
+            beta[v] = b;                      /* value computed in the previous iteration */
+            b = th * (1.0 / thm1 - 1.0);      /* acceldualgrad.m:56, used next iteration  */
+        }
+        thm1 = th;
+        th = thn;
+    }
+}
+
+/* Algorithm 1 test (nmpc12-gpad.pdf sec. 4.2; acceldualgrad.m:66-79 restricted to the
+ * branches computable from (ML, M, G, g, L)):
+ *   (A) max_i (G z - g)_i <= tol                                   -> stop, return z     (1)
+ *   (B) max_i (G zhat - g)_i <= tol, w >= 0, -w'(G zhat - g) <= tol -> stop, return zhat  (2)
+ * with G x - g = L (GL x + pD) evaluated as an fmaf chain + pD, then scaled in fp64.  The
+ * paper (sec. 4.2) returns whichever candidate passed; the commented MATLAB returns z_v in
+ * both branches, which for (B) hands back a point that was never certified. */
+static int orc_check_f32(const float* GL, const float* pD, const float* z, const float* zhat,
+                         const float* w, int n, int m, float L, float tol) {
+    float viol = -INFINITY;
+    for (int i = 0; i < m; i++) {
+        float sum = 0.0f;
+        const float* row = GL + (size_t)i * n;
+        for (int j = 0; j < n; j++) sum = fmaf(row[j], z[j], sum);
+        float t = sum + pD[i];
+        viol = fmaxf(viol, t);
+    }
+    if ((double)viol * (double)L <= (double)tol) return 1;
+    float violh = -INFINITY, wmin = INFINITY;
+    double gap = 0.0;
+    for (int i = 0; i < m; i++) {
+        float sum = 0.0f;
+        const float* row = GL + (size_t)i * n;
+        for (int j = 0; j < n; j++) sum = fmaf(row[j], zhat[j], sum);
+        float t = sum + pD[i];
+        violh = fmaxf(violh, t);
+        wmin = fminf(wmin, w[i]);
+        gap -= (double)w[i] * (double)t;
+    }
+    gap *= (double)L;
+    return (((double)violh * (double)L <= (double)tol) && (wmin >= 0.0f) && (gap <= (double)tol)) ? 2 : 0;
+}
+
+int orc_solve_f32(float* z, float* y, const float* MGneg, const float* gP, const float* GL,
+                  const float* pD, int n, int m, int N, float L, float tol, int check_every,
+                  const float* theta, const float* beta, int* converged) {
+    float* base = (float*)malloc(sizeof(float) * (size_t)(m > 0 ? m : 1) * 4);
+    float* ycur = base;
+    float* yprev = ycur + (m > 0 ? m : 1);
+    float* w = yprev + (m > 0 ? m : 1);
+    float* ynew = w + (m > 0 ? m : 1);
+    float* zhat = (float*)malloc(sizeof(float) * (size_t)(n > 0 ? n : 1));
+    if (check_every <= 0) check_every = 10;
+    memcpy(ycur, y, sizeof(float) * m);
+    memcpy(yprev, y, sizeof(float) * m); /* acceldualgrad.m:16: y_0 = y_{-1} */
+    int it = 0, conv = 0;
+    for (int v = 0; v < N; v++) {
+        orc_step1_f32(ycur, yprev, w, beta[v], m);          /* main.cu:163 */
+        orc_step2_f32(MGneg, w, gP, zhat, n, m);            /* main.cu:166 */
+        orc_step3_f32(theta[v], n, z, zhat, z);             /* main.cu:170 */
+        orc_step4_f32(GL, ynew, w, pD, zhat, n, m);         /* main.cu:171 */
+        float* t = yprev; yprev = ycur; ycur = ynew; ynew = t; /* main.cu:167 + MATLAB :60-64 */
+        it = v + 1;
+        if (tol > 0.0f && (it % check_every) == 0) {
+            const int c = orc_check_f32(GL, pD, z, zhat, w, n, m, L, tol);
+            if (c) {
+                if (c == 2) memcpy(z, zhat, sizeof(float) * n);
+                conv = c;
+                break;
+            }
+        }
+    }
+    memcpy(y, ycur, sizeof(float) * m);
+    free(base);
+    free(zhat);
+    if (converged) *converged = conv;
+    return it;
+}
+
+/* ---- fp64, acceldualgrad.m operation order ------------------------------------- */
+static int orc_check_f64(const double* GL, const double* pD, const double* z, const double* zhat,
+                         const double* w, int n, int m, double L, double tol) {
+    double viol = -INFINITY;
+    for (int i = 0; i < m; i++) {
+        double sum = 0.0;
+        for (int j = 0; j < n; j++) sum = fma(GL[(size_t)i * n + j], z[j], sum);
+        viol = fmax(viol, sum + pD[i]);
+    }
+    if (viol * L <= tol) return 1;
+    double violh = -INFINITY, wmin = INFINITY, gap = 0.0;
+    for (int i = 0; i < m; i++) {
+        double sum = 0.0;
+        for (int j = 0; j < n; j++) sum = fma(GL[(size_t)i * n + j], zhat[j], sum);
+        double t = sum + pD[i];
+        violh = fmax(violh, t);
+        wmin = fmin(wmin, w[i]);
+        gap -= w[i] * t;
+    }
+    return ((violh * L <= tol) && (wmin >= 0.0) && (gap * L <= tol)) ? 2 : 0;
+}
+
+int orc_solve_f64(double* z, double* y, const double* ML, const double* gP, const double* G,
+                  const double* g, int n, int m, int N, double L, double tol, int check_every,
+                  int schedule, int* converged) {
+    const size_t nm = (size_t)n * m;
+    double* GL = (double*)malloc(sizeof(double) * (nm + 1));
+    double* pD = (double*)malloc(sizeof(double) * (m + 1));
+    double* yv = (double*)malloc(sizeof(double) * (m + 1));
+    double* yvm1 = (double*)malloc(sizeof(double) * (m + 1));
+    double* w = (double*)malloc(sizeof(double) * (m + 1));
+    double* yp1 = (double*)malloc(sizeof(double) * (m + 1));
+    double* zhat = (double*)malloc(sizeof(double) * (n + 1));
+    double* th = (double*)malloc(sizeof(double) * (N + 1));
+    double* be = (double*)malloc(sizeof(double) * (N + 1));
+    const double inv = 1.0 / L, ninv = -1.0 / L;
+    for (size_t k = 0; k < nm; k++) GL[k] = inv * G[k];           /* acceldualgrad.m:22 */
+    for (int i = 0; i < m; i++) pD[i] = ninv * g[i];              /* acceldualgrad.m:23 */
+    orc_schedule(N, schedule, th, be);
+    if (check_every <= 0) check_every = 10;
+    memcpy(yv, y, sizeof(double) * m);
+    memcpy(yvm1, y, sizeof(double) * m);
+    int it = 0, conv = 0;
+    for (int v = 0; v < N; v++) {
+        for (int i = 0; i < m; i++) w[i] = yv[i] + be[v] * (yv[i] - yvm1[i]);      /* :43 */
+        for (int i = 0; i < n; i++) {                                               /* :46 */
+            double sum = 0.0;
+            for (int j = 0; j < m; j++) sum = fma(-ML[(size_t)i * m + j], w[j], sum);
+            zhat[i] = sum - gP[i];
+        }
+        for (int i = 0; i < n; i++) z[i] = (1.0 - th[v]) * z[i] + th[v] * zhat[i]; /* :49 */
+        for (int i = 0; i < m; i++) {                                               /* :52 */
+            double sum = 0.0;
+            for (int j = 0; j < n; j++) sum = fma(GL[(size_t)i * n + j], zhat[j], sum);
+            double s = (w[i] + sum) + pD[i];
+            yp1[i] = s > 0.0 ? s : 0.0;
+        }
+        double* t = yvm1; yvm1 = yv; yv = yp1; yp1 = t;                               /* :60-64 */
+        it = v + 1;
+        if (tol > 0.0 && (it % check_every) == 0) {
+            const int c = orc_check_f64(GL, pD, z, zhat, w, n, m, L, tol);
+            if (c) {
+                if (c == 2) memcpy(z, zhat, sizeof(double) * n);
+                conv = c;
+                break;
+            }
+        }
+    }
+    memcpy(y, yv, sizeof(double) * m);
+    free(GL); free(pD); free(yv); free(yvm1); free(w); free(yp1); free(zhat); free(th); free(be);
+    if (converged) *converged = conv;
+    return it;
+}
+
+long long orc_solve_batch_f32(float* z, float* y, const float* MGneg, const float* gP,
+                              const float* GL, const float* pD, int n, int m, int batch,
+                              int shared, int N, float L, float tol, int check_every,
+                              const float* theta, const float* beta, int* iters, int threads) {
+    long long total = 0;
+    const size_t nm = (size_t)n * m;
+#ifdef _OPENMP
+    if (threads <= 0) threads = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : total) num_threads(threads > 0 ? threads : omp_get_max_threads())
+#endif
+    for (int b = 0; b < batch; b++) {
+        const float* mg = shared ? MGneg : MGneg + (size_t)b * nm;
+        const float* gl = shared ? GL : GL + (size_t)b * nm;
+        int conv = 0;
+        int it = orc_solve_f32(z + (size_t)b * n, y + (size_t)b * m, mg, gP + (size_t)b * n, gl,
+                               pD + (size_t)b * m, n, m, N, L, tol, check_every, theta, beta, &conv);
+        if (iters) iters[b] = it;
+        total += it;
+    }
+    (void)threads;
+    return total;
+}

@@ -1,0 +1,255 @@
+"""ctypes front-end for the CPU ORACLE (TEST INFRASTRUCTURE ONLY).
+
+Loads ``oracle/liboracle.so`` (our C restatement, gpad_oracle.c) and, where it was built,
+``oracle/_ref/libref_seq.so`` (the reference's own seq_functions.cpp compiled in place by
+``make -C oracle ref``).  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg import this module -- it is the checker, never the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+REF = os.path.join(HERE, "_ref", "libref_seq.so")
+REF_O3 = os.path.join(HERE, "_ref", "libref_seq_o3.so")
+
+_f = C.POINTER(C.c_float)
+_d = C.POINTER(C.c_double)
+_i = C.POINTER(C.c_int)
+
+SCHEDULE_MATLAB = 0
+SCHEDULE_PAPER = 1
+
+
+def build(ref: bool | None = None) -> None:
+    """Compile liboracle.so (and _ref/ when the reference tree is present)."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    if ref is None:
+        ref = os.path.isdir("/root/reference")
+    if ref:
+        subprocess.run(["make", "-s", "-C", HERE, "ref"], check=True)
+
+
+def _fp(a):
+    return a.ctypes.data_as(_f)
+
+
+def _dp(a):
+    return a.ctypes.data_as(_d)
+
+
+class Oracle:
+    def __init__(self, path: str = LIB):
+        if not os.path.exists(path):
+            build(ref=False)
+        L = C.CDLL(path)
+        L.orc_step1_f32.argtypes = [_f, _f, _f, C.c_float, C.c_int]
+        L.orc_step2_f32.argtypes = [_f, _f, _f, _f, C.c_int, C.c_int]
+        L.orc_step3_f32.argtypes = [C.c_float, C.c_int, _f, _f, _f]
+        L.orc_step4_f32.argtypes = [_f, _f, _f, _f, _f, C.c_int, C.c_int]
+        L.orc_scale_f32.argtypes = [_f, _f, _f, C.c_float, C.c_int, C.c_int, _f, _f, _f]
+        L.orc_schedule.argtypes = [C.c_int, C.c_int, _d, _d]
+        L.orc_solve_f32.argtypes = [_f, _f, _f, _f, _f, _f, C.c_int, C.c_int, C.c_int, C.c_float,
+                                    C.c_float, C.c_int, _f, _f, _i]
+        L.orc_solve_f32.restype = C.c_int
+        L.orc_solve_f64.argtypes = [_d, _d, _d, _d, _d, _d, C.c_int, C.c_int, C.c_int, C.c_double,
+                                    C.c_double, C.c_int, C.c_int, _i]
+        L.orc_solve_f64.restype = C.c_int
+        L.orc_solve_batch_f32.argtypes = [_f, _f, _f, _f, _f, _f, C.c_int, C.c_int, C.c_int, C.c_int,
+                                          C.c_int, C.c_float, C.c_float, C.c_int, _f, _f, _i, C.c_int]
+        L.orc_solve_batch_f32.restype = C.c_longlong
+        self.lib = L
+
+    # -- steps ------------------------------------------------------------------
+    def step1(self, y, ym1, beta):
+        y = np.ascontiguousarray(y, np.float32); ym1 = np.ascontiguousarray(ym1, np.float32)
+        w = np.empty_like(y)
+        self.lib.orc_step1_f32(_fp(y), _fp(ym1), _fp(w), beta, y.size)
+        return w
+
+    def step2(self, MGneg, w, gP):
+        MGneg = np.ascontiguousarray(MGneg, np.float32); n, m = MGneg.shape
+        w = np.ascontiguousarray(w, np.float32); gP = np.ascontiguousarray(gP, np.float32)
+        zh = np.empty(n, np.float32)
+        self.lib.orc_step2_f32(_fp(MGneg), _fp(w), _fp(gP), _fp(zh), n, m)
+        return zh
+
+    def step3(self, theta, zm1, zhat):
+        zm1 = np.ascontiguousarray(zm1, np.float32); zhat = np.ascontiguousarray(zhat, np.float32)
+        z = np.empty_like(zm1)
+        self.lib.orc_step3_f32(theta, zm1.size, _fp(zm1), _fp(zhat), _fp(z))
+        return z
+
+    def step4(self, GL, w, pD, zhat):
+        GL = np.ascontiguousarray(GL, np.float32); m, n = GL.shape
+        w = np.ascontiguousarray(w, np.float32); pD = np.ascontiguousarray(pD, np.float32)
+        zhat = np.ascontiguousarray(zhat, np.float32)
+        y = np.empty(m, np.float32)
+        self.lib.orc_step4_f32(_fp(GL), _fp(y), _fp(w), _fp(pD), _fp(zhat), n, m)
+        return y
+
+    # -- inputs -----------------------------------------------------------------
+    def scale(self, ML, G, g, L):
+        ML = np.ascontiguousarray(ML, np.float32); n, m = ML.shape
+        G = np.ascontiguousarray(G, np.float32); g = np.ascontiguousarray(g, np.float32)
+        MGneg = np.empty((n, m), np.float32); GL = np.empty((m, n), np.float32)
+        pD = np.empty(m, np.float32)
+        self.lib.orc_scale_f32(_fp(ML), _fp(G), _fp(g), np.float32(L), n, m, _fp(MGneg), _fp(GL),
+                               _fp(pD))
+        return MGneg, GL, pD
+
+    def scale_vec(self, g, L):
+        """pD = fl32((-1/L)_64 * g) for a (batch, m) array."""
+        g = np.asarray(g, np.float32)
+        return ((-1.0 / np.float64(np.float32(L))) * g.astype(np.float64)).astype(np.float32)
+
+    def schedule(self, N, kind=SCHEDULE_MATLAB):
+        th = np.empty(N, np.float64); be = np.empty(N, np.float64)
+        self.lib.orc_schedule(N, kind, _dp(th), _dp(be))
+        return th, be
+
+    def schedule_f32(self, N, kind=SCHEDULE_MATLAB):
+        th, be = self.schedule(N, kind)
+        return th.astype(np.float32), be.astype(np.float32)
+
+    # -- solves -----------------------------------------------------------------
+    def solve_f32(self, z0, y0, ML, M, G, g, N, L, tol=0.0, check_every=10,
+                  schedule=SCHEDULE_MATLAB):
+        """solve(z0, y0, ML, M, G, g, N, L, tol) restated on the CPU in fp32."""
+        MGneg, GL, pD = self.scale(ML, G, g, L)
+        return self.solve_scaled_f32(z0, y0, MGneg, M, GL, pD, N, L, tol, check_every, schedule)
+
+    def solve_scaled_f32(self, z0, y0, MGneg, gP, GL, pD, N, L, tol=0.0, check_every=10,
+                         schedule=SCHEDULE_MATLAB, theta=None, beta=None):
+        n, m = MGneg.shape
+        z = np.array(z0, np.float32, copy=True).reshape(n)
+        y = np.array(y0, np.float32, copy=True).reshape(m)
+        if theta is None:
+            theta, beta = self.schedule_f32(max(N, 1), schedule)
+        theta = np.ascontiguousarray(theta, np.float32); beta = np.ascontiguousarray(beta, np.float32)
+        conv = C.c_int(0)
+        it = self.lib.orc_solve_f32(_fp(z), _fp(y), _fp(np.ascontiguousarray(MGneg, np.float32)),
+                                    _fp(np.ascontiguousarray(gP, np.float32)),
+                                    _fp(np.ascontiguousarray(GL, np.float32)),
+                                    _fp(np.ascontiguousarray(pD, np.float32)), n, m, N,
+                                    np.float32(L), np.float32(tol), check_every, _fp(theta),
+                                    _fp(beta), C.byref(conv))
+        return z, y, it, bool(conv.value)
+
+    def solve_f64(self, z0, y0, ML, M, G, g, N, L, tol=0.0, check_every=10,
+                  schedule=SCHEDULE_MATLAB):
+        ML = np.ascontiguousarray(ML, np.float64); n, m = ML.shape
+        z = np.array(z0, np.float64, copy=True).reshape(n)
+        y = np.array(y0, np.float64, copy=True).reshape(m)
+        conv = C.c_int(0)
+        it = self.lib.orc_solve_f64(_dp(z), _dp(y), _dp(ML), _dp(np.ascontiguousarray(M, np.float64)),
+                                    _dp(np.ascontiguousarray(G, np.float64)),
+                                    _dp(np.ascontiguousarray(g, np.float64)), n, m, N, float(L),
+                                    float(tol), check_every, schedule, C.byref(conv))
+        return z, y, it, bool(conv.value)
+
+    def solve_batch_f32(self, Z0, Y0, MGneg, GP, GL, PD, N, L, tol=0.0, check_every=10,
+                        shared=True, threads=1, schedule=SCHEDULE_MATLAB):
+        """Batch of instances; per-instance vectors packed [batch][n] / [batch][m]."""
+        Z = np.array(Z0, np.float32, copy=True); Y = np.array(Y0, np.float32, copy=True)
+        batch, n = Z.shape
+        m = Y.shape[1]
+        theta, beta = self.schedule_f32(max(N, 1), schedule)
+        iters = np.zeros(batch, np.int32)
+        total = self.lib.orc_solve_batch_f32(
+            _fp(Z), _fp(Y), _fp(np.ascontiguousarray(MGneg, np.float32)),
+            _fp(np.ascontiguousarray(GP, np.float32)), _fp(np.ascontiguousarray(GL, np.float32)),
+            _fp(np.ascontiguousarray(PD, np.float32)), n, m, batch, int(bool(shared)), N,
+            np.float32(L), np.float32(tol), check_every, _fp(theta), _fp(beta),
+            iters.ctypes.data_as(_i), threads)
+        return Z, Y, iters, int(total)
+
+
+class RefSeq:
+    """The reference's own seq_functions.cpp (extern "C", seq_functions.h:4-17), composed in
+    main.cu:160-175 loop order by ``solve``.  Available only where ``make -C oracle ref`` ran."""
+
+    def __init__(self, path: str = REF):
+        L = C.CDLL(path)
+        L.StepOneGPADSequential.argtypes = [_f, _f, _f, C.c_float, C.c_int]
+        L.StepTwoGPADSequential.argtypes = [_f, _f, _f, _f, C.c_int, C.c_int, C.c_int]
+        L.StepThreeGPADSequential.argtypes = [C.c_float, C.c_int, _f, _f, _f]
+        L.StepFourGPADSequential.argtypes = [_f, _f, _f, _f, _f, C.c_int, C.c_int, C.c_int]
+        L.ref_solve_f32.argtypes = [_f, _f, _f, _f, _f, _f, C.c_int, C.c_int, C.c_int, _f, _f]
+        L.ref_solve_batch_f32.argtypes = [_f, _f, _f, _f, _f, _f, C.c_int, C.c_int, C.c_int,
+                                          C.c_int, C.c_int, _f, _f, C.c_int]
+        self.lib = L
+
+    @staticmethod
+    def available(path: str = REF) -> bool:
+        return os.path.exists(path)
+
+    def step1(self, y, ym1, beta):
+        y = np.ascontiguousarray(y, np.float32); ym1 = np.ascontiguousarray(ym1, np.float32)
+        w = np.empty_like(y)
+        self.lib.StepOneGPADSequential(_fp(y), _fp(ym1), _fp(w), beta, y.size)
+        return w
+
+    def step2(self, MGneg, w, gP):
+        MGneg = np.ascontiguousarray(MGneg, np.float32); n, m = MGneg.shape
+        zh = np.empty(n, np.float32)
+        self.lib.StepTwoGPADSequential(_fp(MGneg), _fp(np.ascontiguousarray(w, np.float32)),
+                                       _fp(np.ascontiguousarray(gP, np.float32)), _fp(zh), n, 1, m)
+        return zh
+
+    def step3(self, theta, zm1, zhat):
+        zm1 = np.ascontiguousarray(zm1, np.float32)
+        z = np.empty_like(zm1)
+        self.lib.StepThreeGPADSequential(theta, zm1.size, _fp(zm1),
+                                         _fp(np.ascontiguousarray(zhat, np.float32)), _fp(z))
+        return z
+
+    def step4(self, GL, w, pD, zhat):
+        GL = np.ascontiguousarray(GL, np.float32); m, n = GL.shape
+        y = np.empty(m, np.float32)
+        self.lib.StepFourGPADSequential(_fp(GL), _fp(y), _fp(np.ascontiguousarray(w, np.float32)),
+                                        _fp(np.ascontiguousarray(pD, np.float32)),
+                                        _fp(np.ascontiguousarray(zhat, np.float32)), n, 1, m)
+        return y
+
+    def solve_c(self, z0, y0, MGneg, gP, GL, pD, theta, beta, N):
+        """Same loop as ``solve`` but driven from C (oracle/ref_driver.c)."""
+        MGneg = np.ascontiguousarray(MGneg, np.float32); n, m = MGneg.shape
+        z = np.array(z0, np.float32, copy=True); y = np.array(y0, np.float32, copy=True)
+        self.lib.ref_solve_f32(_fp(z), _fp(y), _fp(MGneg), _fp(np.ascontiguousarray(gP, np.float32)),
+                               _fp(np.ascontiguousarray(GL, np.float32)),
+                               _fp(np.ascontiguousarray(pD, np.float32)), n, m, N,
+                               _fp(np.ascontiguousarray(theta, np.float32)),
+                               _fp(np.ascontiguousarray(beta, np.float32)))
+        return z, y
+
+    def solve_batch_c(self, Z0, Y0, MGneg, GP, GL, PD, theta, beta, N, shared=True, threads=1):
+        Z = np.array(Z0, np.float32, copy=True); Y = np.array(Y0, np.float32, copy=True)
+        batch, n = Z.shape
+        m = Y.shape[1]
+        self.lib.ref_solve_batch_f32(_fp(Z), _fp(Y), _fp(np.ascontiguousarray(MGneg, np.float32)),
+                                     _fp(np.ascontiguousarray(GP, np.float32)),
+                                     _fp(np.ascontiguousarray(GL, np.float32)),
+                                     _fp(np.ascontiguousarray(PD, np.float32)), n, m, batch,
+                                     int(bool(shared)), N,
+                                     _fp(np.ascontiguousarray(theta, np.float32)),
+                                     _fp(np.ascontiguousarray(beta, np.float32)), threads)
+        return Z, Y
+
+    def solve(self, z0, y0, MGneg, gP, GL, pD, theta, beta, N):
+        """main.cu:160-175: step1 -> step2 (+copy) -> step3 -> step4, N fixed iterations."""
+        z = np.array(z0, np.float32, copy=True)
+        ycur = np.array(y0, np.float32, copy=True)
+        yprev = ycur.copy()
+        for v in range(N):
+            w = self.step1(ycur, yprev, np.float32(beta[v]))
+            zh = self.step2(MGneg, w, gP)
+            z = self.step3(np.float32(theta[v]), z, zh)
+            ynew = self.step4(GL, w, pD, zh)
+            yprev, ycur = ycur, ynew
+        return z, ycur

@@ -1,0 +1,103 @@
+"""Generate the committed golden vectors under tests/golden/ (run in the BUILD container only).
+
+Sources of truth:
+  * the reference's own CPU steps (Code/CUDA/FinalProject/src/seq_functions.cpp), compiled in
+    place by ``make -C oracle ref`` into oracle/_ref/libref_seq.so and composed in the loop order
+    of main.cu:160-175 (pyoracle.RefSeq) -> fp32 end states after K = 1, 10, 100 iterations and
+    one-step known-answer vectors;
+  * a numpy restatement of Code/MATLAB/acceldualgrad.m (tests/matlab_ref.py) -> fp64 end states;
+  * our oracle (oracle/liboracle.so) for the Algorithm-1 (tol) runs, which the reference lacks.
+
+Inputs are stored in float64; the fp32 path receives ``x.astype(np.float32)`` of them.
+Usage:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "gpu-dualgradient-mpc_amd"))
+sys.path.insert(0, os.path.dirname(HERE))
+
+import matlab_ref  # noqa: E402
+import pyoracle  # noqa: E402
+from gpad_mpc import problems  # noqa: E402
+
+STEP3_SRC = "/root/reference/Code/CUDA/FinalProject/build/step3"
+
+
+def problem_set():
+    return {
+        "battery_c1": problems.battery_mpc(4, 10, seed=0),        # config C1: n=40, m=180
+        "battery_10x4": problems.battery_mpc(10, 4),              # gpad.m:10 fixed x0, n=40, m=168
+        "synth_small": problems.synthetic_qp(48, 80, seed=7),     # generic generator, n=48, m=80
+    }
+
+
+def make(name, qp, O, R):
+    n, m = qp.n, qp.m
+    f32 = lambda a: np.asarray(a, np.float64).astype(np.float32)  # noqa: E731
+    ML, M, G, g, L = f32(qp.ML), f32(qp.M), f32(qp.G), f32(qp.g), np.float32(qp.L)
+    MGneg, GL, pD = O.scale(ML, G, g, L)
+    th, be = O.schedule_f32(100)
+    out = dict(ML=qp.ML, M=qp.M, G=qp.G, g=qp.g, L=np.float64(qp.L), H=qp.H, q=qp.q,
+               theta100=th, beta100=be)
+    z0 = np.zeros(n, np.float32)
+    y0 = np.zeros(m, np.float32)
+    for K in (1, 10, 100):
+        z, y = R.solve(z0, y0, MGneg, M, GL, pD, th, be, K)
+        out[f"ref_z_{K}"], out[f"ref_y_{K}"] = z, y
+    # warm-started run (z0, y0 nonzero) -- exercises the y_0 = y_{-1} initialisation
+    rng = np.random.default_rng(123)
+    zw = rng.normal(0, 0.1, n).astype(np.float32)
+    yw = np.abs(rng.normal(0, 0.1, m)).astype(np.float32)
+    z, y = R.solve(zw, yw, MGneg, M, GL, pD, th, be, 50)
+    out.update(warm_z0=zw, warm_y0=yw, ref_warm_z_50=z, ref_warm_y_50=y)
+    # one-step known-answer vectors (8a..8d) on a random state
+    ym1 = np.abs(rng.normal(0, 0.2, m)).astype(np.float32)
+    yv = np.abs(rng.normal(0, 0.2, m)).astype(np.float32)
+    zm1 = rng.normal(0, 0.2, n).astype(np.float32)
+    beta, theta = np.float32(be[57]), np.float32(th[52])
+    w = R.step1(yv, ym1, beta)
+    zh = R.step2(MGneg, w, M)
+    z = R.step3(theta, zm1, zh)
+    yp = R.step4(GL, w, pD, zh)
+    out.update(kat_y=yv, kat_ym1=ym1, kat_zm1=zm1, kat_beta=beta, kat_theta=theta, kat_w=w,
+               kat_zhat=zh, kat_z=z, kat_yp1=yp)
+    # fp64 MATLAB restatement (acceldualgrad.m) after 100 iterations
+    if qp.H is not None:
+        _, zm, ym = matlab_ref.acceldualgrad(qp.H, qp.q, qp.G, qp.g, 1, 100, L=qp.L)
+        out["matlab_z_100"], out["matlab_y_100"] = zm, ym
+        _, zp, yp_ = matlab_ref.acceldualgrad(qp.H, qp.q, qp.G, qp.g, 1, 100, kind="paper", L=qp.L)
+        out["matlab_paper_z_100"], out["matlab_paper_y_100"] = zp, yp_
+    # Algorithm 1 (tol = 1e-4, K = 10) from the oracle
+    z, y, it, conv = O.solve_f32(z0, y0, ML, M, G, g, 5000, L, 1e-4, 10)
+    out.update(tol_z=z, tol_y=y, tol_iters=np.int32(it), tol_conv=np.int32(conv))
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+    print(f"{name}: n={n} m={m} L={qp.L:.6g} tol-iters={it}")
+
+
+def main():
+    pyoracle.build(ref=True)
+    O = pyoracle.Oracle()
+    R = pyoracle.RefSeq()
+    for name, qp in problem_set().items():
+        make(name, qp, O, R)
+    # the reference's own step-3 known-answer files (data, copied verbatim)
+    if os.path.isdir(STEP3_SRC):
+        for k in range(1, 6):
+            dst = os.path.join(HERE, "step3", str(k))
+            os.makedirs(dst, exist_ok=True)
+            for f in ("input.txt", "output.txt"):
+                shutil.copyfile(os.path.join(STEP3_SRC, str(k), f), os.path.join(dst, f))
+        print("step3 fixtures copied")
+
+
+if __name__ == "__main__":
+    main()

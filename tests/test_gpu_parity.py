@@ -1,0 +1,274 @@
+"""GPU parity tests: the HIP path (libgpad.so, called through its C-ABI) against the oracle.
+
+Bar: fp32 results are BIT-EXACT with the reference CPU arithmetic (every kernel computes one
+sequential fmaf chain per row, as seq_functions.cpp does under FMA contraction); fp64 results
+match the fp64 oracle / MATLAB restatement within 1e-12 relative (elementwise op order of
+acceldualgrad.m vs seq_functions.cpp differs in the last bit).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN_SETS, f32_inputs, load_golden
+
+pytestmark = pytest.mark.gpu
+
+KERNELS = ["stream", "resident"]
+
+
+def kcode(name):
+    from gpad_mpc import _lib
+    return {"auto": _lib.KERNEL_AUTO, "stream": _lib.KERNEL_STREAM, "resident": _lib.KERNEL_RESIDENT,
+            "panel": _lib.KERNEL_PANEL}[name]
+
+
+def run_gpu(ML, M, G, g, L, N, tol=0.0, z0=None, y0=None, kernel="auto", shared=True,
+            schedule=0, check_every=10):
+    import gpad_mpc
+    n, m = ML.shape[-2], ML.shape[-1]
+    batch = M.shape[0] if M.ndim == 2 else 1
+    z = np.zeros((batch, n) if batch > 1 else n, ML.dtype) if z0 is None else np.array(z0, ML.dtype)
+    y = np.zeros((batch, m) if batch > 1 else m, ML.dtype) if y0 is None else np.array(y0, ML.dtype)
+    iters = np.zeros(batch, np.int32)
+    with gpad_mpc.GpadSolver(0) as s:
+        s.setup(np.ascontiguousarray(ML), np.ascontiguousarray(G), float(L), n=n, m=m, batch=batch,
+                shared=shared, kernel=kcode(kernel), schedule=schedule, check_every=check_every)
+        st = s.run(z, y, np.ascontiguousarray(M), np.ascontiguousarray(g), N, tol, iters=iters)
+    return z, y, st, iters
+
+
+def assert_bitexact(a, b, what=""):
+    a = np.asarray(a)
+    b = np.asarray(b)
+    assert a.shape == b.shape, what
+    if not np.array_equal(a, b):
+        d = np.abs(a.astype(np.float64) - b.astype(np.float64))
+        i = int(np.argmax(d))
+        raise AssertionError(f"{what}: {int((d > 0).sum())} of {a.size} differ, max |d| = {d.max():.3g}"
+                             f" at {i} ({a.flat[i]!r} vs {b.flat[i]!r})")
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("name", GOLDEN_SETS)
+@pytest.mark.parametrize("K", [1, 10, 100])
+def test_fixed_iterations_bitexact_vs_reference(gpu, kernel, name, K):
+    gd = load_golden(name)
+    ML, M, G, g, L = f32_inputs(gd)
+    z, y, st, _ = run_gpu(ML, M, G, g, L, K, kernel=kernel)
+    assert st["kernel"] == kernel and st["iterations"] == K
+    assert_bitexact(z, gd[f"ref_z_{K}"], f"{name} z K={K}")
+    assert_bitexact(y, gd[f"ref_y_{K}"], f"{name} y K={K}")
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("name", GOLDEN_SETS)
+def test_warm_start_bitexact(gpu, kernel, name):
+    gd = load_golden(name)
+    ML, M, G, g, L = f32_inputs(gd)
+    z, y, _, _ = run_gpu(ML, M, G, g, L, 50, z0=gd["warm_z0"], y0=gd["warm_y0"], kernel=kernel)
+    assert_bitexact(z, gd["ref_warm_z_50"], "warm z")
+    assert_bitexact(y, gd["ref_warm_y_50"], "warm y")
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("name", GOLDEN_SETS)
+def test_algorithm1_termination_bitexact(gpu, kernel, name):
+    gd = load_golden(name)
+    ML, M, G, g, L = f32_inputs(gd)
+    z, y, st, iters = run_gpu(ML, M, G, g, L, 5000, tol=1e-4, kernel=kernel)
+    assert st["converged"] == 1 and st["iterations"] == int(gd["tol_iters"])
+    assert_bitexact(z, gd["tol_z"], "tol z")
+    assert_bitexact(y, gd["tol_y"], "tol y")
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("nm", [(200, 200), (37, 53), (1, 5), (5, 1), (64, 64), (65, 129), (208, 180)])
+def test_shapes_bitexact_vs_oracle(gpu, oracle, kernel, nm):
+    """C2 (200 x 200) and ragged shapes (not multiples of 4 / 64, single row or column)."""
+    from gpad_mpc import problems
+    n, m = nm
+    qp = problems.synthetic_qp(n, m, seed=11)
+    ML, M, G, g = (qp.ML.astype(np.float32), qp.M.astype(np.float32), qp.G.astype(np.float32),
+                   qp.g.astype(np.float32))
+    L = np.float32(qp.L)
+    zo, yo, _, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), ML, M, G, g, 100, L)
+    z, y, st, _ = run_gpu(ML, M, G, g, L, 100, kernel=kernel)
+    assert_bitexact(z, zo, f"{nm} z")
+    assert_bitexact(y, yo, f"{nm} y")
+
+
+@pytest.mark.parametrize("nm", [(800, 800), (300, 1000), (1500, 257)])
+def test_large_shapes_stream_bitexact(gpu, oracle, nm):
+    """C5-sized instances (n = m = 800) and beyond the resident kernel's register budget."""
+    from gpad_mpc import problems
+    n, m = nm
+    qp = problems.synthetic_qp(n, m, seed=5)
+    ML, M, G, g = (qp.ML.astype(np.float32), qp.M.astype(np.float32), qp.G.astype(np.float32),
+                   qp.g.astype(np.float32))
+    L = np.float32(qp.L)
+    zo, yo, _, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), ML, M, G, g, 20, L)
+    z, y, st, _ = run_gpu(ML, M, G, g, L, 20, kernel="auto")
+    assert st["kernel"] == "stream"
+    assert_bitexact(z, zo, "z")
+    assert_bitexact(y, yo, "y")
+
+
+@pytest.mark.parametrize("kernel", ["auto", "stream", "resident"])
+def test_shared_batch_bitexact_per_instance(gpu, oracle, kernel):
+    """A battery-scenario-style batch: shared ML/G, per-instance M and g, Algorithm 1."""
+    from gpad_mpc import problems
+    B, n, m = 37, 40, 64
+    qp = problems.synthetic_qp(n, m, batch=B, seed=2)
+    ML, G = qp.ML.astype(np.float32), qp.G.astype(np.float32)
+    M, g = qp.M.astype(np.float32), qp.g.astype(np.float32)
+    L = np.float32(qp.L)
+    z, y, st, iters = run_gpu(ML, M, G, g, L, 3000, tol=1e-4, kernel=kernel)
+    for b in range(B):
+        zo, yo, it, conv = oracle.solve_f32(np.zeros(n), np.zeros(m), ML, M[b], G, g[b], 3000, L, 1e-4)
+        assert iters[b] == it
+        assert_bitexact(z[b], zo, f"instance {b} z")
+        assert_bitexact(y[b], yo, f"instance {b} y")
+    assert st["converged"] == B and st["total_iterations"] == int(iters.sum())
+
+
+@pytest.mark.parametrize("kernel", ["stream", "resident"])
+def test_distinct_batch_bitexact(gpu, oracle, kernel):
+    from gpad_mpc import problems
+    B, n, m = 9, 48, 72
+    qp = problems.synthetic_qp(n, m, batch=B, seed=4, shared=False)
+    f = lambda a: np.ascontiguousarray(a.astype(np.float32))  # noqa: E731
+    ML, G, M, g, L = f(qp.ML), f(qp.G), f(qp.M), f(qp.g), np.float32(qp.L)
+    z, y, st, iters = run_gpu(ML, M, G, g, L, 60, kernel=kernel, shared=False)
+    for b in range(B):
+        zo, yo, _, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), ML[b], M[b], G[b], g[b], 60, L)
+        assert_bitexact(z[b], zo, f"instance {b} z")
+        assert_bitexact(y[b], yo, f"instance {b} y")
+
+
+def test_paper_schedule_bitexact(gpu, oracle):
+    gd = load_golden("battery_c1")
+    ML, M, G, g, L = f32_inputs(gd)
+    n, m = ML.shape
+    zo, yo, _, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), ML, M, G, g, 100, L, schedule=1)
+    for k in KERNELS:
+        z, y, _, _ = run_gpu(ML, M, G, g, L, 100, kernel=k, schedule=1)
+        assert_bitexact(z, zo, k)
+        assert_bitexact(y, yo, k)
+
+
+@pytest.mark.parametrize("name", GOLDEN_SETS)
+def test_f64_vs_matlab_restatement(gpu, oracle, name):
+    gd = load_golden(name)
+    n, m = gd["ML"].shape
+    z, y, st, _ = run_gpu(gd["ML"], gd["M"], gd["G"], gd["g"], float(gd["L"]), 100)
+    assert st["kernel"] == "stream"
+    rel = lambda a, b: np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)  # noqa: E731
+    assert rel(z, gd["matlab_z_100"]) < 1e-12 and rel(y, gd["matlab_y_100"]) < 1e-12
+    zo, yo, _, _ = oracle.solve_f64(np.zeros(n), np.zeros(m), gd["ML"], gd["M"], gd["G"], gd["g"],
+                                    100, float(gd["L"]))
+    assert rel(z, zo) < 1e-12 and rel(y, yo) < 1e-12
+
+
+def test_zero_iterations_returns_inputs(gpu):
+    gd = load_golden("synth_small")
+    ML, M, G, g, L = f32_inputs(gd)
+    z0 = np.linspace(-1, 1, ML.shape[0]).astype(np.float32)
+    y0 = np.linspace(0, 1, ML.shape[1]).astype(np.float32)
+    for k in KERNELS:
+        z, y, st, _ = run_gpu(ML, M, G, g, L, 0, z0=z0, y0=y0, kernel=k)
+        assert st["iterations"] == 0
+        assert_bitexact(z, z0)
+        assert_bitexact(y, y0)
+
+
+def test_step_entry_points_vs_kats(gpu, oracle):
+    """gpad_step1..4 (the kernel_functions.h mirror) on device tensors vs the reference KATs."""
+    import torch
+    import gpad_mpc
+    gd = load_golden("battery_c1")
+    ML, M, G, g, L = f32_inputs(gd)
+    MGneg, GL, pD = oracle.scale(ML, G, g, L)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(gpu)  # noqa: E731
+    n, m = MGneg.shape
+    y, ym1, zm1 = t(gd["kat_y"]), t(gd["kat_ym1"]), t(gd["kat_zm1"])
+    w, zh, z, yp = (torch.empty(m, device=gpu), torch.empty(n, device=gpu), torch.empty(n, device=gpu),
+                    torch.empty(m, device=gpu))
+    with gpad_mpc.GpadSolver(0) as s:
+        s.step1(y, ym1, w, float(gd["kat_beta"]))
+        s.step2(t(MGneg), w, t(M), zh)
+        s.step3(float(gd["kat_theta"]), zm1, zh, z)
+        s.step4(t(GL), yp, w, t(pD), zh)
+        s.sync()
+    assert_bitexact(w.cpu().numpy(), gd["kat_w"], "8a")
+    assert_bitexact(zh.cpu().numpy(), gd["kat_zhat"], "8b")
+    assert_bitexact(z.cpu().numpy(), gd["kat_z"], "8c")
+    assert_bitexact(yp.cpu().numpy(), gd["kat_yp1"], "8d")
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 5])
+def test_step3_reference_fixtures_on_gpu(gpu, oracle, k):
+    import torch
+    import gpad_mpc
+    from test_oracle import read_step3
+    n_u, N, m, theta, zm1, zhat, out = read_step3(k)
+    z = torch.empty(zm1.size, device=gpu)
+    with gpad_mpc.GpadSolver(0) as s:
+        s.step3(float(theta), torch.from_numpy(zm1).to(gpu), torch.from_numpy(zhat).to(gpu), z)
+        s.sync()
+    zz = z.cpu().numpy()
+    assert_bitexact(zz, oracle.step3(theta, zm1, zhat))
+    assert np.max(np.abs(zz - out)) <= 1e-6 * max(1.0, float(np.max(np.abs(out))))
+
+
+def test_device_memory_async_and_one_shot_solve(gpu, oracle):
+    """Device tensors (MEM_DEVICE, async launch + last_stats) and the one-shot gpad_solve."""
+    import torch
+    import gpad_mpc
+    from gpad_mpc import problems
+    B, n, m = 20, 56, 88
+    qp = problems.synthetic_qp(n, m, batch=B, seed=9)
+    f = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(gpu)  # noqa: E731
+    ML, G, M, g = f(qp.ML), f(qp.G), f(qp.M), f(qp.g)
+    z = torch.zeros(B, n, device=gpu)
+    y = torch.zeros(B, m, device=gpu)
+    with gpad_mpc.GpadSolver(0) as s:
+        s.setup(ML, G, float(np.float32(qp.L)), n=n, m=m, batch=B)
+        assert s.run(z, y, M, g, 500, 1e-4, stats=False) is None
+        s.sync()
+        st = s.last_stats()
+    zo, yo, it, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), qp.ML.astype(np.float32),
+                                     qp.M[3].astype(np.float32), qp.G.astype(np.float32),
+                                     qp.g[3].astype(np.float32), 500, np.float32(qp.L), 1e-4)
+    assert_bitexact(z[3].cpu().numpy(), zo)
+    assert_bitexact(y[3].cpu().numpy(), yo)
+    assert st["iterations"] >= it and st["kernel_ms"] > 0
+    z2, y2, st2 = gpad_mpc.solve(np.zeros((B, n)), np.zeros((B, m)), qp.ML.astype(np.float32),
+                                 qp.M.astype(np.float32), qp.G.astype(np.float32),
+                                 qp.g.astype(np.float32), 500, float(np.float32(qp.L)), 1e-4)
+    assert_bitexact(z2, z.cpu().numpy())
+
+
+def test_error_paths(gpu):
+    import gpad_mpc
+    from gpad_mpc import _lib
+    s = gpad_mpc.GpadSolver(0)
+    z = np.zeros(4, np.float32)
+    with pytest.raises(gpad_mpc.GpadError) as e:
+        s.run(z, z, z, z, 10, 0.0)
+    assert e.value.code == _lib.ERR_NOT_SETUP
+    big = np.zeros((300, 300), np.float32)
+    s.setup(big, big, 1.0, n=300, m=300, kernel=_lib.KERNEL_RESIDENT)
+    with pytest.raises(gpad_mpc.GpadError) as e:
+        s.run(np.zeros(300, np.float32), np.zeros(300, np.float32), np.zeros(300, np.float32),
+              np.zeros(300, np.float32), 10, 0.0)
+    assert e.value.code == _lib.ERR_UNSUPPORTED
+    s.close()
+
+
+def test_acceldualgrad_mirror(gpu):
+    """The MATLAB-signature mirror returns u = z(1:n_u) of the fp64 path."""
+    import gpad_mpc
+    gd = load_golden("battery_10x4")
+    u, z, y = gpad_mpc.acceldualgrad(gd["H"], gd["q"], gd["G"], gd["g"], None, None, 10)
+    assert np.allclose(u, gd["matlab_z_100"][:10], rtol=1e-12, atol=1e-14)
