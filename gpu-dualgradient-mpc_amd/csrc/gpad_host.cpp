@@ -93,6 +93,7 @@ struct gpad_handle_s {
     bool scaled = false;
     int ldn = 0, ldm = 0;
     DevBuf MGt, GLt, frag, stage;
+    int frag_tiles = 0;
     DevBuf theta, beta;
     int sched_len = 0, sched_kind = -1, sched_dtype = -1;
     DevBuf work, counters;
@@ -255,12 +256,14 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
     }
     // fragment image for the MFMA panel kernel (shared f32 matrices only)
     h->frag.release();
+    h->frag_tiles = 0;
     if (d->shared && d->dtype == GPAD_DTYPE_F32) {
-        const size_t fb = gpad::panel_frag_bytes(n, m);
+        const size_t fb = gpad::panel_frag_bytes(n, m, d->batch);
         if (fb > 0) {
             if ((rc = h->frag.ensure(fb))) return rc;
-            HIP_TRY(gpad::launch_pack_panel((const float*)dA, (const float*)dB, n, m,
+            HIP_TRY(gpad::launch_pack_panel((const float*)dA, (const float*)dB, n, m, d->batch,
                                             (float)sa, sb, h->frag.p, h->stream));
+            h->frag_tiles = gpad::panel_tiles(n, m, d->batch);
         }
     }
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -282,9 +285,9 @@ static int ensure_schedule(gpad_handle_t h, int N, const void* theta_in, const v
     const int dt = h->dims.dtype;
     const size_t es = esize(dt);
     const bool custom = theta_in != nullptr || beta_in != nullptr;
-    if (!custom && h->sched_len >= N + 1 && h->sched_kind == h->dims.schedule && h->sched_dtype == dt)
+    if (!custom && h->sched_len >= N + 2 && h->sched_kind == h->dims.schedule && h->sched_dtype == dt)
         return GPAD_OK;
-    const int len = std::max(N + 1, 1);
+    const int len = N + 2;  // kernels prefetch theta[v+1], beta[v+2]
     std::vector<double> th(len, 0.0), be(len, 0.0);
     host_schedule(N, h->dims.schedule, th.data(), be.data());
     if (custom) {
@@ -294,7 +297,8 @@ static int ensure_schedule(gpad_handle_t h, int N, const void* theta_in, const v
             be[v] = dt == GPAD_DTYPE_F64 ? ((const double*)beta_in)[v] : ((const float*)beta_in)[v];
         }
     }
-    be[N] = 0.0;  // w for a non-existent iteration N: computed, never used
+    th[N] = th[N + 1] = 0.0;  // pads: read by the prefetch, never used
+    be[N] = be[N + 1] = 0.0;
     int rc;
     if ((rc = h->theta.ensure(es * len))) return rc;
     if ((rc = h->beta.ensure(es * len))) return rc;
@@ -383,6 +387,7 @@ static int run_typed(gpad_handle_t h, T* z, T* y, const T* M, const T* g, int N,
     a.strideA = d.shared ? 0 : (long long)m * h->ldn;
     a.strideB = d.shared ? 0 : (long long)n * h->ldm;
     a.frag = h->frag.p;
+    a.frag_tiles = h->frag_tiles;
     a.gP = dM;
     a.g = dg;
     a.ld_gP = n;

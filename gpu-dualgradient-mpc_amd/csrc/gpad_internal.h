@@ -17,6 +17,7 @@ struct SolveArgs {
     long long strideA;     // elements between consecutive instances' -ML images (0 = shared)
     long long strideB;     // elements between consecutive instances' G/L images (0 = shared)
     const void* frag;      // panel kernel: fragment-packed matrices (see gpad_panel.hip)
+    int frag_tiles;        // tile count the fragment image was packed for
     const T* gP;           // per-instance H^-1 q, [batch][ld_gP]
     const T* g;            // per-instance rhs,    [batch][ld_g]
     long long ld_gP, ld_g;
@@ -26,8 +27,8 @@ struct SolveArgs {
     int n, m, ldn, ldm;    // ldn = round_up(n,4), ldm = round_up(m,4)
     int batch, N, check_every;
     double tol, L;         // Algorithm 1: stop when L*viol <= tol (tol <= 0: fixed N)
-    const T* theta;        // [N+1] theta_v
-    const T* beta;         // [N+1] beta_v  (beta[N] = 0 pad)
+    const T* theta;        // [N+2] theta_v (two zero pads: kernels prefetch ahead)
+    const T* beta;         // [N+2] beta_v
     int* iters;            // [batch] iterations executed
     int* conv;             // [batch] 1 if the tolerance test passed
 };
@@ -37,8 +38,9 @@ template <typename T>
 hipError_t launch_stream(const SolveArgs<T>& a, hipStream_t s);
 hipError_t launch_resident(const SolveArgs<float>& a, hipStream_t s, bool* supported);
 hipError_t launch_panel(const SolveArgs<float>& a, hipStream_t s, bool* supported);
-size_t panel_frag_bytes(int n, int m);
-hipError_t launch_pack_panel(const float* ML, const float* G, int n, int m, float mg_sign,
+size_t panel_frag_bytes(int n, int m, int batch);
+int panel_tiles(int n, int m, int batch);
+hipError_t launch_pack_panel(const float* ML, const float* G, int n, int m, int batch, float mg_sign,
                              double g_scale, void* frag, hipStream_t s);
 
 // layout: out[k*ld + i] = (T)(scale * in[i*cols + k]) for i < rows, k < cols; zero pad i >= rows

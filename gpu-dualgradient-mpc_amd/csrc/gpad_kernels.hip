@@ -304,43 +304,38 @@ template hipError_t launch_stream<double>(const SolveArgs<double>&, hipStream_t)
 // =========================================================================================
 // gpad_resident_kernel: one matrix row per lane, held in VGPRs for the whole solve.
 // =========================================================================================
-// K = row-register capacity (multiple of 16, >= max(m, n)).  A lane owning primal row i
-// keeps -ML[i][0..m); a lane owning constraint row i keeps G_L[i][0..n).  Both roles use the
-// same register array r[] (they live in different waves).
+// Register-resident rows.  A lane owning primal row i keeps -ML[i][0..KA) (zero-padded past m);
+// a lane owning constraint row i keeps G_L[i][0..KB) (zero-padded past n).  Both roles use the
+// same register array r[] (they live in different waves).  KA/KB are compile-time, so the
+// chains carry no per-step predicates: padded steps are fma(0, 0, acc) = acc.
 //
-// The broadcast vector is read 8 floats (two ds_read_b128) one group ahead and a
-// sched_barrier closes every group: without it the scheduler hoists all K/4 LDS reads to
-// the top of the chain and the live vector copy spills r[] to scratch.
-constexpr int kResGroup = 8;
+// The broadcast vector is read one float4 (ds_read_b128, all lanes the same address) per
+// 4-step group, kResAhead groups ahead into a ring of registers (compile-time slots, no
+// copies).  An empty asm that reads/writes acc and clobbers memory closes each group: later
+// LDS reads cannot be hoisted above it (else all K/4 reads issue at once and r[] spills), and
+// being volatile it pins the chain in place (the compiler cannot sink it into the `live`
+// branch of the caller).
+constexpr int kResAhead = 3;
+constexpr int kResRing = kResAhead + 1;
 
-template <int K>
-__device__ __forceinline__ float chain_regs(const float (&r)[K], const float* v, int len) {
-    static_assert(K % kResGroup == 0, "K must be a multiple of the group");
-    float acc = 0.0f;
-    float4 c0 = *reinterpret_cast<const float4*>(v);
-    float4 c1 = *reinterpret_cast<const float4*>(v + 4);
+template <int KLEN, int K>
+__device__ __forceinline__ float chain_regs(const float (&r)[K], const float* v) {
+    static_assert(KLEN % 4 == 0 && KLEN <= K, "bad chain length");
+    constexpr int G = KLEN / 4;
+    float4 ring[kResRing];
 #pragma unroll
-    for (int k = 0; k < K; k += kResGroup) {
-        // wave-uniform skip (a constant trip count keeps r[] in VGPRs); r[] and v[] are
-        // zero-padded to K, so the tail of the last live group adds +0 products
-        if (k < len) {
-            float4 n0 = c0, n1 = c1;
-            if (k + kResGroup < K) {
-                n0 = *reinterpret_cast<const float4*>(v + k + kResGroup);
-                n1 = *reinterpret_cast<const float4*>(v + k + kResGroup + 4);
-            }
-            acc = __builtin_fmaf(r[k + 0], c0.x, acc);
-            acc = __builtin_fmaf(r[k + 1], c0.y, acc);
-            acc = __builtin_fmaf(r[k + 2], c0.z, acc);
-            acc = __builtin_fmaf(r[k + 3], c0.w, acc);
-            acc = __builtin_fmaf(r[k + 4], c1.x, acc);
-            acc = __builtin_fmaf(r[k + 5], c1.y, acc);
-            acc = __builtin_fmaf(r[k + 6], c1.z, acc);
-            acc = __builtin_fmaf(r[k + 7], c1.w, acc);
-            c0 = n0;
-            c1 = n1;
-            __builtin_amdgcn_sched_barrier(0);
-        }
+    for (int g = 0; g < kResAhead && g < G; ++g) ring[g] = *reinterpret_cast<const float4*>(v + 4 * g);
+    float acc = 0.0f;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        if (g + kResAhead < G)
+            ring[(g + kResAhead) % kResRing] = *reinterpret_cast<const float4*>(v + 4 * (g + kResAhead));
+        const float4 c = ring[g % kResRing];
+        acc = __builtin_fmaf(r[4 * g + 0], c.x, acc);
+        acc = __builtin_fmaf(r[4 * g + 1], c.y, acc);
+        acc = __builtin_fmaf(r[4 * g + 2], c.z, acc);
+        acc = __builtin_fmaf(r[4 * g + 3], c.w, acc);
+        asm volatile("" : "+v"(acc) : : "memory");
     }
     return acc;
 }
@@ -348,11 +343,12 @@ __device__ __forceinline__ float chain_regs(const float (&r)[K], const float* v,
 constexpr int kResidentMaxThreads = 512;
 constexpr int kResidentMaxRow = 208;
 
-template <int K>
+template <int KA, int KB>
 __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(SolveArgs<float> a) {
-    __shared__ __attribute__((aligned(16))) float w_l[K];   // w, broadcast to -ML rows
-    __shared__ __attribute__((aligned(16))) float zh_l[K];  // zhat, broadcast to G/L rows
-    __shared__ __attribute__((aligned(16))) float z_l[K];   // z, for the termination test
+    constexpr int K = KA > KB ? KA : KB;
+    __shared__ __attribute__((aligned(16))) float w_l[KA];   // w, broadcast to -ML rows
+    __shared__ __attribute__((aligned(16))) float zh_l[KB];  // zhat, broadcast to G/L rows
+    __shared__ __attribute__((aligned(16))) float z_l[KB];   // z, for the termination test
     __shared__ CheckSlot slots[kResidentMaxThreads / 64];
 
     const int tid = threadIdx.x;
@@ -368,7 +364,7 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
                                        : a.GLt + (size_t)b * a.strideB;
     const int ld = isA ? a.ldn : a.ldm;
 
-    // preload the row (k-major layout: consecutive lanes read consecutive words)
+    // preload the row once (k-major layout: consecutive lanes read consecutive words)
     float r[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) r[k] = (live && k < len) ? Mt[(size_t)k * ld + row] : 0.0f;
@@ -386,8 +382,8 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
         pdi = (float)(a.gscale * (double)a.g[(size_t)b * a.ld_g + row]);
         wi = __builtin_fmaf(a.beta[0], yi - yi, yi);
     }
-    for (int i = tid; i < K; i += blockDim.x) {
-        w_l[i] = 0.0f;
+    for (int i = tid; i < KA; i += blockDim.x) w_l[i] = 0.0f;
+    for (int i = tid; i < KB; i += blockDim.x) {
         zh_l[i] = 0.0f;
         z_l[i] = 0.0f;
     }
@@ -398,12 +394,14 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
     int it = 0;
     int done = 0;
     float zhi = 0.0f;
+    // theta/beta are prefetched one iteration ahead (tables hold N + 2 entries)
+    float th = a.theta[0], bn = a.beta[1];
     for (int v = 0; v < a.N; ++v) {
+        const float th_next = a.theta[v + 1], bn_next = a.beta[v + 2];
         const bool chk = a.tol > 0.0 && ((v + 1) % a.check_every) == 0;
         if (isA) {  // ---- 8b + 8c --------------------------------------------------------
-            const float acc = chain_regs<K>(r, w_l, m);
+            const float acc = chain_regs<KA, K>(r, w_l);
             if (live) {
-                const float th = a.theta[v];
                 const float zhv = acc - gpi;
                 zi = __builtin_fmaf(1.0f - th, zi, th * zhv);
                 zh_l[row] = zhv;
@@ -415,8 +413,8 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
         float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY;
         double gap = 0.0;
         if (!isA) {  // ---- 8d + next 8a ------------------------------------------------
-            const float c = chain_regs<K>(r, zh_l, n);
-            const float cz = chk ? chain_regs<K>(r, z_l, n) : 0.0f;
+            const float c = chain_regs<KB, K>(r, zh_l);
+            const float cz = chk ? chain_regs<KB, K>(r, z_l) : 0.0f;
             if (live) {
                 const float sv = (wi + pdi) + c;
                 const float yp = (__builtin_fabsf(sv) + sv) * 0.5f;
@@ -427,7 +425,7 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
                     gap = -((double)wi * (double)t);
                     violz = cz + pdi;
                 }
-                wi = __builtin_fmaf(a.beta[v + 1], yp - yi, yp);
+                wi = __builtin_fmaf(bn, yp - yi, yp);
                 yi = yp;
                 w_l[row] = wi;
             }
@@ -435,6 +433,8 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
         if (chk) check_publish<float>(slots, violz, violh, wmin, gap);
         __syncthreads();
         it = v + 1;
+        th = th_next;
+        bn = bn_next;
         if (chk) done = check_decide(slots, nwaves, a.L, a.tol);
         if (done) break;
     }
@@ -450,20 +450,41 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
     }
 }
 
+// chain-length buckets (multiples of 32 up to 192, then the 208 cap)
+static int res_bucket(int len) {
+    if (len > 192) return 208;
+    return (len + 31) / 32 * 32;
+}
+
+template <int KA>
+static void launch_res_b(int kb, dim3 g, dim3 bl, hipStream_t st, const SolveArgs<float>& a) {
+    switch (kb) {
+        case 32: hipLaunchKernelGGL((gpad_resident_kernel<KA, 32>), g, bl, 0, st, a); break;
+        case 64: hipLaunchKernelGGL((gpad_resident_kernel<KA, 64>), g, bl, 0, st, a); break;
+        case 96: hipLaunchKernelGGL((gpad_resident_kernel<KA, 96>), g, bl, 0, st, a); break;
+        case 128: hipLaunchKernelGGL((gpad_resident_kernel<KA, 128>), g, bl, 0, st, a); break;
+        case 160: hipLaunchKernelGGL((gpad_resident_kernel<KA, 160>), g, bl, 0, st, a); break;
+        case 192: hipLaunchKernelGGL((gpad_resident_kernel<KA, 192>), g, bl, 0, st, a); break;
+        default: hipLaunchKernelGGL((gpad_resident_kernel<KA, 208>), g, bl, 0, st, a); break;
+    }
+}
+
 hipError_t launch_resident(const SolveArgs<float>& a, hipStream_t st, bool* supported) {
     const int mx = a.n > a.m ? a.n : a.m;
     const int threads = 64 * (((a.n + 63) >> 6) + ((a.m + 63) >> 6));
     *supported = mx <= kResidentMaxRow && threads <= kResidentMaxThreads && a.n > 0 && a.m > 0;
     if (!*supported) return hipSuccess;
     const dim3 grid(a.batch), block(threads);
-    if (mx <= 64)
-        hipLaunchKernelGGL(gpad_resident_kernel<64>, grid, block, 0, st, a);
-    else if (mx <= 128)
-        hipLaunchKernelGGL(gpad_resident_kernel<128>, grid, block, 0, st, a);
-    else if (mx <= 192)
-        hipLaunchKernelGGL(gpad_resident_kernel<192>, grid, block, 0, st, a);
-    else
-        hipLaunchKernelGGL(gpad_resident_kernel<kResidentMaxRow>, grid, block, 0, st, a);
+    const int ka = res_bucket(a.m), kb = res_bucket(a.n);  // A rows run over m, B rows over n
+    switch (ka) {
+        case 32: launch_res_b<32>(kb, grid, block, st, a); break;
+        case 64: launch_res_b<64>(kb, grid, block, st, a); break;
+        case 96: launch_res_b<96>(kb, grid, block, st, a); break;
+        case 128: launch_res_b<128>(kb, grid, block, st, a); break;
+        case 160: launch_res_b<160>(kb, grid, block, st, a); break;
+        case 192: launch_res_b<192>(kb, grid, block, st, a); break;
+        default: launch_res_b<208>(kb, grid, block, st, a); break;
+    }
     return hipGetLastError();
 }
 

@@ -14,7 +14,7 @@ from conftest import GOLDEN_SETS, f32_inputs, load_golden
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = ["stream", "resident"]
+KERNELS = ["stream", "resident", "panel"]
 
 
 def kcode(name):
@@ -114,7 +114,7 @@ def test_large_shapes_stream_bitexact(gpu, oracle, nm):
     assert_bitexact(y, yo, "y")
 
 
-@pytest.mark.parametrize("kernel", ["auto", "stream", "resident"])
+@pytest.mark.parametrize("kernel", ["auto", "stream", "resident", "panel"])
 def test_shared_batch_bitexact_per_instance(gpu, oracle, kernel):
     """A battery-scenario-style batch: shared ML/G, per-instance M and g, Algorithm 1."""
     from gpad_mpc import problems
@@ -142,6 +142,26 @@ def test_distinct_batch_bitexact(gpu, oracle, kernel):
     z, y, st, iters = run_gpu(ML, M, G, g, L, 60, kernel=kernel, shared=False)
     for b in range(B):
         zo, yo, _, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), ML[b], M[b], G[b], g[b], 60, L)
+        assert_bitexact(z[b], zo, f"instance {b} z")
+        assert_bitexact(y[b], yo, f"instance {b} y")
+
+
+@pytest.mark.parametrize("nm", [(40, 64), (200, 200)])
+def test_panel_two_wave_panels_large_batch(gpu, oracle, nm):
+    """>= 512 panels selects 2-wave panels; spot-check instances across the whole grid."""
+    from gpad_mpc import problems
+    n, m = nm
+    B = 8192 + 5  # ragged last panel
+    base = problems.synthetic_qp(n, m, batch=1, seed=21)
+    rng = np.random.default_rng(0)
+    M = (base.M[None, :] * (1.0 + 0.3 * rng.normal(size=(B, 1)))).astype(np.float32)
+    g = (base.g[None, :] + 0.2 * rng.random((B, m))).astype(np.float32)
+    ML, G, L = base.ML.astype(np.float32), base.G.astype(np.float32), np.float32(base.L)
+    z, y, st, iters = run_gpu(ML, M, G, g, L, 2000, tol=1e-4, kernel="panel")
+    assert st["kernel"] == "panel"
+    for b in list(range(0, B, 997)) + [B - 1]:
+        zo, yo, it, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), ML, M[b], G, g[b], 2000, L, 1e-4)
+        assert iters[b] == it, b
         assert_bitexact(z[b], zo, f"instance {b} z")
         assert_bitexact(y[b], yo, f"instance {b} y")
 
