@@ -105,7 +105,7 @@ constexpr int kUnrollK = 8;
 
 template <typename T>
 struct StreamLds {
-    T *w, *zh, *zs, *ys, *gp, *pd;
+    T *w, *zh, *zs, *ys, *gp, *pd, *us;
     CheckSlot* slots;
 };
 
@@ -118,7 +118,8 @@ __device__ __forceinline__ StreamLds<T> stream_lds(unsigned char* smem, int ldn,
     s.ys = s.zs + ldn;                  // [ldm] y
     s.gp = s.ys + ldm;                  // [ldn] g_P
     s.pd = s.gp + ldn;                  // [ldm] p_D
-    s.slots = reinterpret_cast<CheckSlot*>(s.pd + ldm);
+    s.us = s.pd + ldm;                  // [ldm] u = G_L z (termination test, by recursion)
+    s.slots = reinterpret_cast<CheckSlot*>(s.us + ldm);
     return s;
 }
 
@@ -152,44 +153,6 @@ __device__ __forceinline__ void chain4(const T* __restrict__ Mt, int ld, int r0,
     }
 }
 
-// Two chains sharing the matrix stream (zhat and z for the termination test).
-template <typename T>
-__device__ __forceinline__ void chain4x2(const T* __restrict__ Mt, int ld, int r0, const T* v,
-                                         const T* u2, int K, T (&acc)[4], T (&acc2)[4]) {
-    using V = typename V4<T>::type;
-    const T* col = Mt + r0;
-    int k = 0;
-    for (; k + kUnrollK <= K; k += kUnrollK) {
-        V a[kUnrollK];
-#pragma unroll
-        for (int u = 0; u < kUnrollK; ++u) a[u] = *reinterpret_cast<const V*>(col + (size_t)(k + u) * ld);
-#pragma unroll
-        for (int u = 0; u < kUnrollK; ++u) {
-            const T vk = v[k + u], zk = u2[k + u];
-            acc[0] = fmad(a[u].x, vk, acc[0]);
-            acc[1] = fmad(a[u].y, vk, acc[1]);
-            acc[2] = fmad(a[u].z, vk, acc[2]);
-            acc[3] = fmad(a[u].w, vk, acc[3]);
-            acc2[0] = fmad(a[u].x, zk, acc2[0]);
-            acc2[1] = fmad(a[u].y, zk, acc2[1]);
-            acc2[2] = fmad(a[u].z, zk, acc2[2]);
-            acc2[3] = fmad(a[u].w, zk, acc2[3]);
-        }
-    }
-    for (; k < K; ++k) {
-        const V a = *reinterpret_cast<const V*>(col + (size_t)k * ld);
-        const T vk = v[k], zk = u2[k];
-        acc[0] = fmad(a.x, vk, acc[0]);
-        acc[1] = fmad(a.y, vk, acc[1]);
-        acc[2] = fmad(a.z, vk, acc[2]);
-        acc[3] = fmad(a.w, vk, acc[3]);
-        acc2[0] = fmad(a.x, zk, acc2[0]);
-        acc2[1] = fmad(a.y, zk, acc2[1]);
-        acc2[2] = fmad(a.z, zk, acc2[2]);
-        acc2[3] = fmad(a.w, zk, acc2[3]);
-    }
-}
-
 template <typename T>
 __global__ __launch_bounds__(kStreamBlock) void gpad_stream_kernel(SolveArgs<T> a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -217,6 +180,16 @@ __global__ __launch_bounds__(kStreamBlock) void gpad_stream_kernel(SolveArgs<T> 
         s.w[i] = fmad(beta0, yv - yv, yv);  // 8a with y_0 = y_{-1} (acceldualgrad.m:16,43)
     }
     __syncthreads();
+    const bool use_tol = a.tol > 0.0;
+    if (use_tol) {  // u = G_L z_{-1}; afterwards u follows the 8c recursion (u = G_L z exactly)
+        for (int r0 = 4 * tid; r0 < m; r0 += 4 * kStreamBlock) {
+            T c[4] = {T(0), T(0), T(0), T(0)};
+            chain4<T>(GLt, ldm, r0, s.zs, n, c);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (r0 + r < m) s.us[r0 + r] = c[r];
+        }
+    }
 
     const int nwaves = kStreamBlock / 64;
     int it = 0;
@@ -241,16 +214,12 @@ __global__ __launch_bounds__(kStreamBlock) void gpad_stream_kernel(SolveArgs<T> 
         }
         __syncthreads();
         // ---- phase 2: 8d + next 8a, rows of G/L ------------------------------------------
-        const bool chk = a.tol > 0.0 && ((v + 1) % a.check_every) == 0;
+        const bool chk = use_tol && ((v + 1) % a.check_every) == 0;
         T violz = neg_inf<T>(), violh = neg_inf<T>(), wmin = -neg_inf<T>();
         double gap = 0.0;
         for (int r0 = 4 * tid; r0 < m; r0 += 4 * kStreamBlock) {
             T c[4] = {T(0), T(0), T(0), T(0)};
-            T cz[4] = {T(0), T(0), T(0), T(0)};
-            if (chk)
-                chain4x2<T>(GLt, ldm, r0, s.zh, s.zs, n, c, cz);
-            else
-                chain4<T>(GLt, ldm, r0, s.zh, n, c);
+            chain4<T>(GLt, ldm, r0, s.zh, n, c);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int i = r0 + r;
@@ -258,12 +227,16 @@ __global__ __launch_bounds__(kStreamBlock) void gpad_stream_kernel(SolveArgs<T> 
                     const T wi = s.w[i], pdi = s.pd[i], yi = s.ys[i];
                     const T sv = (wi + pdi) + c[r];                 // seq_functions.cpp:84
                     const T yp = (absd(sv) + sv) * T(0.5);          // seq_functions.cpp:85
-                    if (chk) {
-                        const T t = c[r] + pdi;
-                        violh = fmax(violh, t);
-                        wmin = fmin(wmin, wi);
-                        gap -= (double)wi * (double)t;
-                        violz = fmax(violz, cz[r] + pdi);
+                    if (use_tol) {
+                        const T ui = fmad(omt, s.us[i], th * c[r]);  // u = G_L z (8c form)
+                        s.us[i] = ui;
+                        if (chk) {
+                            const T t = c[r] + pdi;
+                            violh = fmax(violh, t);
+                            wmin = fmin(wmin, wi);
+                            gap -= (double)wi * (double)t;
+                            violz = fmax(violz, ui + pdi);
+                        }
                     }
                     s.w[i] = fmad(bnext, yp - yi, yp);               // next 8a
                     s.ys[i] = yp;
@@ -287,7 +260,7 @@ __global__ __launch_bounds__(kStreamBlock) void gpad_stream_kernel(SolveArgs<T> 
 
 template <typename T>
 hipError_t launch_stream(const SolveArgs<T>& a, hipStream_t st) {
-    const size_t lds = sizeof(T) * (size_t)(3 * a.ldn + 3 * a.ldm) +
+    const size_t lds = sizeof(T) * (size_t)(3 * a.ldn + 4 * a.ldm) +
                        sizeof(CheckSlot) * (kStreamBlock / 64);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     if (lds > 64 * 1024) {
@@ -348,7 +321,7 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
     constexpr int K = KA > KB ? KA : KB;
     __shared__ __attribute__((aligned(16))) float w_l[KA];   // w, broadcast to -ML rows
     __shared__ __attribute__((aligned(16))) float zh_l[KB];  // zhat, broadcast to G/L rows
-    __shared__ __attribute__((aligned(16))) float z_l[KB];   // z, for the termination test
+    __shared__ __attribute__((aligned(16))) float z_l[KB];   // z_{-1}, to seed u = G_L z
     __shared__ CheckSlot slots[kResidentMaxThreads / 64];
 
     const int tid = threadIdx.x;
@@ -389,7 +362,11 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
     }
     __syncthreads();
     if (!isA && live) w_l[row] = wi;
+    if (isA && live) z_l[row] = zi;
     __syncthreads();
+    const bool use_tol = a.tol > 0.0;
+    float ui = 0.0f;  // u = G_L z: seeded once, then the 8c recursion (no extra chain per test)
+    if (use_tol && !isA) ui = chain_regs<KB, K>(r, z_l);
 
     int it = 0;
     int done = 0;
@@ -406,7 +383,6 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
                 zi = __builtin_fmaf(1.0f - th, zi, th * zhv);
                 zh_l[row] = zhv;
                 zhi = zhv;
-                if (chk) z_l[row] = zi;
             }
         }
         __syncthreads();
@@ -414,16 +390,16 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
         double gap = 0.0;
         if (!isA) {  // ---- 8d + next 8a ------------------------------------------------
             const float c = chain_regs<KB, K>(r, zh_l);
-            const float cz = chk ? chain_regs<KB, K>(r, z_l) : 0.0f;
             if (live) {
                 const float sv = (wi + pdi) + c;
                 const float yp = (__builtin_fabsf(sv) + sv) * 0.5f;
+                if (use_tol) ui = __builtin_fmaf(1.0f - th, ui, th * c);
                 if (chk) {
                     const float t = c + pdi;
                     violh = t;
                     wmin = wi;
                     gap = -((double)wi * (double)t);
-                    violz = cz + pdi;
+                    violz = ui + pdi;
                 }
                 wi = __builtin_fmaf(bn, yp - yi, yp);
                 yi = yp;

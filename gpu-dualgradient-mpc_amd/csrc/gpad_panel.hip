@@ -3,8 +3,12 @@
 // When every instance of a batch shares ML and G (one plant, many states: the battery
 // scenario batch), the two mat-vecs of a GPAD iteration over 16 instances are two skinny
 // GEMMs:  Zhat[n x 16] = (-ML) W[m x 16]  and  Y'[m x 16] = G_L Zhat[n x 16].  One workgroup
-// owns a panel of 16 instances for the whole solve (no inter-workgroup traffic at all);
-// its SPLIT waves split the 16-row tiles of each GEMM and exchange W / Zhat through LDS.
+// owns a panel of 16 instances for the whole solve (no inter-workgroup traffic at all).
+// Both GEMMs are padded to T tiles of 16 rows (T = ceil(max(n, m)/16)) and the workgroup has
+// T waves: wave t owns row tile t of BOTH GEMMs (one 4-register accumulator each), so every
+// per-row quantity (z, y, u = G_L z, g_P, p_D) of the panel lives in registers, and W / Zhat
+// are exchanged through LDS.  Many waves per SIMD hide the 40-cycle MFMA dependency and
+// overlap one wave's epilogue with another wave's MFMAs.
 //
 // MFMA: v_mfma_f32_16x16x4_f32 (f32 in, f32 accumulate).  Lane l holds A[l&15][k=l>>4],
 // B[k=l>>4][l&15] and C/D rows 4(l>>4)+r, column l&15 (r = 0..3).  Its result is bit-for-bit
@@ -17,7 +21,7 @@
 // So W and Zhat live in LDS in "fragment order" [tile][lane][4]: a ds_read_b128 per 16-k block
 // yields the four B registers, with no transposes and no bank conflicts.
 //
-// Packed operands in HBM/L2 (built once by pack_panel_kernel at setup):
+// Packed operands in HBM/L2 (built once by pack_panel_kernel at setup; T x T tiles each):
 //   PA1[b][t][lane][q] = -ML[16t + pi(lane&15)][16b + 4q + (lane>>4)]   (b < TM, t < TN)
 //   PA2[b][t][lane][q] = G_L[16t + pi(lane&15)][16b + 4q + (lane>>4)]   (b < TN, t < TM)
 // one float4 per lane per (block, tile): 1 KiB per wave-instruction, fully coalesced.
@@ -33,40 +37,16 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int pi16(int rho) { return 4 * (rho & 3) + (rho >> 2); }
 
-// Geometry.  A panel of 16 instances is owned by a workgroup of SPLIT waves; every GEMM's
-// rows are padded to T = NL*SPLIT tiles (the same T for n and m), so each wave owns exactly NL
-// tiles (t = u*SPLIT + w) and no MFMA sits behind a guard.  Padding rows/columns are zero in
-// the packed operands, so padded k-steps are fma(0, x, acc) = acc.
-struct PanelGeom {
-    int split, nl, tiles;
-};
-
-static constexpr int kNlSplit2[] = {1, 2, 4, 7};
-static constexpr int kNlSplit4[] = {1, 2, 4};
-
-static PanelGeom panel_geom(int n, int m, int batch) {
-    const int groups = (batch + 15) / 16;
-    const int need = ((n > m ? n : m) + 15) / 16;
-    PanelGeom g{groups >= 512 ? 2 : 4, 0, 0};  // aim for >= 4 waves per CU
-    if (g.split == 2) {
-        for (int nl : kNlSplit2)
-            if (nl * 2 >= need) { g.nl = nl; break; }
-    } else {
-        for (int nl : kNlSplit4)
-            if (nl * 4 >= need) { g.nl = nl; break; }
-        if (!g.nl) {  // too tall for 4-wave panels: try 2-wave panels
-            g.split = 2;
-            for (int nl : kNlSplit2)
-                if (nl * 2 >= need) { g.nl = nl; break; }
-        }
-    }
-    g.tiles = g.nl * g.split;
-    return g;
-}
-
 // ---------------------------------------------------------------------------------------
 // packing
 // ---------------------------------------------------------------------------------------
+constexpr int kPanelMaxTiles = 16;  // n, m <= 256 (1024-thread workgroups)
+
+static int panel_tiles_for(int n, int m) {
+    const int t = ((n > m ? n : m) + 15) / 16;
+    return t <= kPanelMaxTiles ? t : 0;
+}
+
 __global__ void pack_panel_kernel(const float* __restrict__ src, int rows, int cols, double scale,
                                   int T, float4* __restrict__ dst) {
     // dst[(b*T + t)*64 + lane] for b < T (16-col blocks), t < T (16-row tiles)
@@ -83,17 +63,17 @@ __global__ void pack_panel_kernel(const float* __restrict__ src, int rows, int c
     dst[idx] = make_float4(v[0], v[1], v[2], v[3]);
 }
 
-size_t panel_frag_bytes(int n, int m, int batch) {
-    const PanelGeom g = panel_geom(n, m, batch);
-    if (!g.nl) return 0;
-    return (size_t)2 * g.tiles * g.tiles * 64 * sizeof(float4);
+size_t panel_frag_bytes(int n, int m, int /*batch*/) {
+    const int T = panel_tiles_for(n, m);
+    return T ? (size_t)2 * T * T * 64 * sizeof(float4) : 0;
 }
 
-hipError_t launch_pack_panel(const float* ML, const float* G, int n, int m, int batch, float mg_sign,
-                             double g_scale, void* frag, hipStream_t s) {
-    const PanelGeom g = panel_geom(n, m, batch);
-    if (!g.nl) return hipSuccess;
-    const int T = g.tiles;
+int panel_tiles(int n, int m, int /*batch*/) { return panel_tiles_for(n, m); }
+
+hipError_t launch_pack_panel(const float* ML, const float* G, int n, int m, int /*batch*/,
+                             float mg_sign, double g_scale, void* frag, hipStream_t s) {
+    const int T = panel_tiles_for(n, m);
+    if (!T) return hipSuccess;
     float4* pa1 = reinterpret_cast<float4*>(frag);
     float4* pa2 = pa1 + (size_t)T * T * 64;
     const int tot = T * T * 64;
@@ -106,190 +86,152 @@ hipError_t launch_pack_panel(const float* ML, const float* G, int n, int m, int 
 }
 
 // ---------------------------------------------------------------------------------------
-// the panel kernel
+// the panel kernel: workgroup = panel of 16 instances, wave t = row tile t
 // ---------------------------------------------------------------------------------------
-struct PanelSlot {  // per wave, per instance partials of the Algorithm-1 test
+struct PanelSlot {  // per wave (row tile), per instance partials of the Algorithm-1 test
     float violz[16], violh[16], wmin[16];
     double gap[16];
 };
 
-// One 16-deep k-block: acc[u] += A[b][u*SPLIT + w] * B[b] (four MFMA k-steps per tile).
-template <int NL>
-__device__ __forceinline__ void panel_kblock(const float4 (&a)[NL], const float4 bf, f32x4 (&acc)[NL]) {
-#pragma unroll
-    for (int u = 0; u < NL; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].x, bf.x, acc[u], 0, 0, 0);
-#pragma unroll
-    for (int u = 0; u < NL; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].y, bf.y, acc[u], 0, 0, 0);
-#pragma unroll
-    for (int u = 0; u < NL; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].z, bf.z, acc[u], 0, 0, 0);
-#pragma unroll
-    for (int u = 0; u < NL; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u].w, bf.w, acc[u], 0, 0, 0);
+// acc = A[tile t] (T k-blocks, streamed from L2 one block ahead) x B (LDS, fragment order).
+// The MFMA k-order is ascending (block 0..T-1, step 0..3), i.e. the reference's sequential chain.
+// A is read with buffer loads: one 32-bit lane offset (t*1 KiB + lane*16 B) in a VGPR and the
+// k-block offset as a compile-time scalar, so the unrolled blocks cost no address registers.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float4 as_float4(u32x4 v) {
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                       __uint_as_float(v.w));
 }
 
-template <int SPLIT, int NL>
-__device__ __forceinline__ void panel_load(const float4* __restrict__ PA, int b, int w, int lane,
-                                           float4 (&a)[NL]) {
-    constexpr int T = NL * SPLIT;
+template <int T>
+__device__ __forceinline__ f32x4 panel_gemm(__amdgpu_buffer_rsrc_t PA, const float* Bl, int voff,
+                                            int lane) {
+    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    float4 a[2], b[2];
+    a[0] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, 0, 0));
+    b[0] = *reinterpret_cast<const float4*>(Bl + lane * 4);
 #pragma unroll
-    for (int u = 0; u < NL; ++u) a[u] = PA[((size_t)b * T + u * SPLIT + w) * 64 + lane];
-}
-
-// acc (+)= A * B over T k-blocks (T even); A streamed from L2 one k-block ahead, B fragments
-// from LDS in fragment order.  The empty asm bounds the prefetch to one k-block.
-template <int SPLIT, int NL>
-__device__ __forceinline__ void panel_gemm(const float4* __restrict__ PA, const float* Bl, int w, int lane,
-                                           f32x4 (&acc)[NL]) {
-    constexpr int T = NL * SPLIT;
-    float4 a0[NL], a1[NL];
-    panel_load<SPLIT, NL>(PA, 0, w, lane, a0);
-#pragma unroll 1
-    for (int b = 0; b < T; b += 2) {
-        panel_load<SPLIT, NL>(PA, b + 1, w, lane, a1);
-        float4 bf = *reinterpret_cast<const float4*>(Bl + (b * 64 + lane) * 4);
-        panel_kblock<NL>(a0, bf, acc);
-        asm volatile("" ::: "memory");
-        panel_load<SPLIT, NL>(PA, b + 2 < T ? b + 2 : b + 1, w, lane, a0);
-        bf = *reinterpret_cast<const float4*>(Bl + ((b + 1) * 64 + lane) * 4);
-        panel_kblock<NL>(a1, bf, acc);
-        asm volatile("" ::: "memory");
+    for (int kb = 0; kb < T; ++kb) {
+        const int cur = kb & 1, nxt = cur ^ 1;
+        if (kb + 1 < T) {
+            a[nxt] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb + 1) * T * 1024, 0));
+            b[nxt] = *reinterpret_cast<const float4*>(Bl + ((kb + 1) * 64 + lane) * 4);
+        }
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].x, b[cur].x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].y, b[cur].y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].z, b[cur].z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].w, b[cur].w, acc, 0, 0, 0);
+        asm volatile("" ::: "memory");  // keep the prefetch one k-block deep
     }
+    return acc;
 }
 
-template <int SPLIT, int NL>
-__global__ __launch_bounds__(64 * SPLIT) void gpad_panel_kernel(SolveArgs<float> a) {
-    constexpr int T = NL * SPLIT;  // 16-row tiles of both GEMMs (n and m padded to 16T)
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    float* Wl = lds;                  // [T][64][4]  w    (B of GEMM 1)
-    float* Zh = Wl + T * 256;         // [T][64][4]  zhat (B of GEMM 2)
-    float* Zs = Zh + T * 256;         // [T][64][4]  z
-    float* Gp = Zs + T * 256;         // [T][64][4]  g_P
-    float* Pd = Gp + T * 256;         // [T][64][4]  p_D
-    PanelSlot* slots = reinterpret_cast<PanelSlot*>(Pd + T * 256);
+template <int T>
+__global__ __launch_bounds__(64 * T) void gpad_panel_kernel(SolveArgs<float> a) {
+    __shared__ __attribute__((aligned(16))) float Wl[T * 256];  // [T][64][4] w    (B of GEMM 1)
+    __shared__ __attribute__((aligned(16))) float Zh[T * 256];  // [T][64][4] zhat (B of GEMM 2)
+    __shared__ PanelSlot slots[T];
 
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave index, provably uniform
+    const int lane = threadIdx.x & 63;
+    const int t = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // row tile of this wave
     const int j = lane >> 4, c = lane & 15;
     const int n = a.n, m = a.m;
     const int inst = blockIdx.x * 16 + c;
     const bool real = inst < a.batch;
-    const float4* PA1 = reinterpret_cast<const float4*>(a.frag);
-    const float4* PA2 = PA1 + (size_t)T * T * 64;
+    const int abytes = T * T * 1024;  // one packed operand
+    const __amdgpu_buffer_rsrc_t PA1 =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.frag), 0, abytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t PA2 = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)a.frag + abytes), 0, abytes, 0x00020000);
+    const int voff = t * 1024 + lane * 16;
+    const float4* Wl4 = reinterpret_cast<const float4*>(Wl);
+    float4* Wl4w = reinterpret_cast<float4*>(Wl);
+    float4* Zh4w = reinterpret_cast<float4*>(Zh);
+    const int slot = t * 64 + lane;  // this lane's float4 in Wl / Zh
 
-    // ---- prologue: per-instance vectors into fragment order ------------------------------
-    for (int e = tid; e < T * 256; e += 64 * SPLIT) {
-        const int t = e >> 8, l = (e >> 2) & 63, r = e & 3;
-        const int i = 16 * t + 4 * r + (l >> 4), ci = blockIdx.x * 16 + (l & 15);
-        const bool okn = i < n && ci < a.batch;
-        const bool okm = i < m && ci < a.batch;
-        Zs[e] = okn ? a.z[(size_t)ci * n + i] : 0.0f;
-        Gp[e] = okn ? a.gP[(size_t)ci * a.ld_gP + i] : 0.0f;
-        Zh[e] = 0.0f;
-        const float yv = okm ? a.y[(size_t)ci * m + i] : 0.0f;
-        Pd[e] = okm ? (float)(a.gscale * (double)a.g[(size_t)ci * a.ld_g + i]) : 0.0f;
-        Wl[e] = __builtin_fmaf(a.beta[0], yv - yv, yv);  // 8a with y_0 = y_{-1}
+    // ---- prologue: this wave's rows (register r <-> row 16t + 4r + j, instance c) ------------
+    float z[4], gp[4], y[4], pd[4], u[4], zh[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int i = 16 * t + 4 * r + j;
+        const bool okn = real && i < n, okm = real && i < m;
+        z[r] = okn ? a.z[(size_t)inst * n + i] : 0.0f;
+        gp[r] = okn ? a.gP[(size_t)inst * a.ld_gP + i] : 0.0f;
+        y[r] = okm ? a.y[(size_t)inst * m + i] : 0.0f;
+        pd[r] = okm ? (float)(a.gscale * (double)a.g[(size_t)inst * a.ld_g + i]) : 0.0f;
+        u[r] = 0.0f;
+        zh[r] = 0.0f;
     }
-    // y of this wave's constraint tiles stays in registers
-    float Y[NL][4];
+    const float b0 = a.beta[0];
+    Wl4w[slot] = make_float4(__builtin_fmaf(b0, y[0] - y[0], y[0]), __builtin_fmaf(b0, y[1] - y[1], y[1]),
+                             __builtin_fmaf(b0, y[2] - y[2], y[2]), __builtin_fmaf(b0, y[3] - y[3], y[3]));
+    const bool use_tol = a.tol > 0.0;
+    if (use_tol) {  // u = G_L z_{-1} (then carried by the 8c recursion)
+        Zh4w[slot] = make_float4(z[0], z[1], z[2], z[3]);
+        __syncthreads();
+        const f32x4 cz = panel_gemm<T>(PA2, Zh, voff, lane);
 #pragma unroll
-    for (int u = 0; u < NL; ++u) {
-        const int t = u * SPLIT + w;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int i = 16 * t + 4 * r + j;
-            Y[u][r] = (i < m && real) ? a.y[(size_t)inst * m + i] : 0.0f;
-        }
+        for (int r = 0; r < 4; ++r) u[r] = cz[r];
     }
     __syncthreads();
 
-    bool active = real;  // this lane's instance still iterating
+    bool active = real;
     int my_it = 0, my_code = 0;
     float th = a.theta[0], bn = a.beta[1];
-    const bool use_tol = a.tol > 0.0;
     for (int v = 0; v < a.N; ++v) {
         const float th_next = a.theta[v + 1], bn_next = a.beta[v + 2];
         const bool chk = use_tol && ((v + 1) % a.check_every) == 0;
-        // ---- GEMM 1: zhat = -ML w ------------------------------------------------------
-        f32x4 acc1[NL];
-#pragma unroll
-        for (int u = 0; u < NL; ++u) acc1[u] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        panel_gemm<SPLIT, NL>(PA1, Wl, w, lane, acc1);
-        // ---- epilogue 1: 8b tail + 8c ----------------------------------------------------
         const float omt = 1.0f - th;
+        // ---- GEMM 1 + epilogue: zhat = -ML w - g_P (8b), z = (1-th) z + th zhat (8c) -----
+        {
+            const f32x4 acc = panel_gemm<T>(PA1, Wl, voff, lane);
 #pragma unroll
-        for (int u = 0; u < NL; ++u) {
-            const int t = u * SPLIT + w;
-            float* zs = Zs + (t * 64 + lane) * 4;
-            const float4 gp = *reinterpret_cast<const float4*>(Gp + (t * 64 + lane) * 4);
-            const float4 z4 = *reinterpret_cast<const float4*>(zs);
-            float4 zh, zn;
-            zh.x = acc1[u][0] - gp.x;
-            zh.y = acc1[u][1] - gp.y;
-            zh.z = acc1[u][2] - gp.z;
-            zh.w = acc1[u][3] - gp.w;
-            zn.x = __builtin_fmaf(omt, z4.x, th * zh.x);
-            zn.y = __builtin_fmaf(omt, z4.y, th * zh.y);
-            zn.z = __builtin_fmaf(omt, z4.z, th * zh.z);
-            zn.w = __builtin_fmaf(omt, z4.w, th * zh.w);
-            *reinterpret_cast<float4*>(Zh + (t * 64 + lane) * 4) = zh;
-            if (active) *reinterpret_cast<float4*>(zs) = zn;
+            for (int r = 0; r < 4; ++r) {
+                zh[r] = acc[r] - gp[r];
+                const float zn = __builtin_fmaf(omt, z[r], th * zh[r]);
+                if (active) z[r] = zn;
+            }
+            Zh4w[slot] = make_float4(zh[0], zh[1], zh[2], zh[3]);
         }
         __syncthreads();
-        // ---- GEMM 2: G_L zhat -----------------------------------------------------------
-        f32x4 acc2[NL];
-#pragma unroll
-        for (int u = 0; u < NL; ++u) acc2[u] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        panel_gemm<SPLIT, NL>(PA2, Zh, w, lane, acc2);
-        // ---- epilogue 2: 8d + next 8a ----------------------------------------------------
-        float violh = -INFINITY, wmin = INFINITY;
+        // ---- GEMM 2 + epilogue: y+ = [w + G_L zhat + p_D]+ (8d), next w (8a) --------------
+        float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY;
         double gap = 0.0;
-#pragma unroll
-        for (int u = 0; u < NL; ++u) {
-            const int t = u * SPLIT + w;
-            float* wl = Wl + (t * 64 + lane) * 4;
-            const float4 w4 = *reinterpret_cast<const float4*>(wl);
-            const float4 p4 = *reinterpret_cast<const float4*>(Pd + (t * 64 + lane) * 4);
+        {
+            const f32x4 acc = panel_gemm<T>(PA2, Zh, voff, lane);
+            const float4 w4 = Wl4[slot];
             const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
-            const float pv[4] = {p4.x, p4.y, p4.z, p4.w};
             float wn[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const float cval = acc2[u][r];
-                const float sv = (wv[r] + pv[r]) + cval;
+                const float cv = acc[r];
+                const float sv = (wv[r] + pd[r]) + cv;
                 const float yp = (__builtin_fabsf(sv) + sv) * 0.5f;
-                if (chk && (16 * t + 4 * r + j) < m) {
-                    const float tt = cval + pv[r];
-                    violh = fmaxf(violh, tt);
-                    wmin = fminf(wmin, wv[r]);
-                    gap -= (double)wv[r] * (double)tt;
+                wn[r] = __builtin_fmaf(bn, yp - y[r], yp);
+                if (use_tol) {
+                    const float un = __builtin_fmaf(omt, u[r], th * cv);
+                    if (active) u[r] = un;
+                    if (chk && (16 * t + 4 * r + j) < m) {
+                        const float tt = cv + pd[r];
+                        violh = fmaxf(violh, tt);
+                        wmin = fminf(wmin, wv[r]);
+                        gap -= (double)wv[r] * (double)tt;
+                        violz = fmaxf(violz, u[r] + pd[r]);
+                    }
                 }
-                wn[r] = __builtin_fmaf(bn, yp - Y[u][r], yp);
-                if (active) Y[u][r] = yp;
+                if (active) y[r] = yp;
             }
-            if (active) *reinterpret_cast<float4*>(wl) = make_float4(wn[0], wn[1], wn[2], wn[3]);
+            if (active) Wl4w[slot] = make_float4(wn[0], wn[1], wn[2], wn[3]);
         }
-        __syncthreads();
         th = th_next;
         bn = bn_next;
+        if (active) my_it = v + 1;
         if (!chk) {
-            if (active) my_it = v + 1;
+            __syncthreads();
             continue;
         }
-        // ---- Algorithm 1 test: (A) needs G_L z --------------------------------------------
-        f32x4 accz[NL];
-#pragma unroll
-        for (int u = 0; u < NL; ++u) accz[u] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        panel_gemm<SPLIT, NL>(PA2, Zs, w, lane, accz);
-        float violz = -INFINITY;
-#pragma unroll
-        for (int u = 0; u < NL; ++u) {
-            const int t = u * SPLIT + w;
-            const float4 p4 = *reinterpret_cast<const float4*>(Pd + (t * 64 + lane) * 4);
-            const float pv[4] = {p4.x, p4.y, p4.z, p4.w};
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if ((16 * t + 4 * r + j) < m) violz = fmaxf(violz, accz[u][r] + pv[r]);
-        }
-        // per instance: reduce over the four lane groups j, then over waves through LDS
+        // ---- Algorithm 1 test, per instance: lane groups j, then row tiles through LDS ------
 #pragma unroll
         for (int o = 16; o < 64; o <<= 1) {
             violz = fmaxf(violz, __shfl_xor(violz, o, 64));
@@ -298,97 +240,78 @@ __global__ __launch_bounds__(64 * SPLIT) void gpad_panel_kernel(SolveArgs<float>
             gap += __shfl_xor(gap, o, 64);
         }
         if (j == 0) {
-            slots[w].violz[c] = violz;
-            slots[w].violh[c] = violh;
-            slots[w].wmin[c] = wmin;
-            slots[w].gap[c] = gap;
+            slots[t].violz[c] = violz;
+            slots[t].violh[c] = violh;
+            slots[t].wmin[c] = wmin;
+            slots[t].gap[c] = gap;
         }
         __syncthreads();
-        double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gp = 0.0;
+        double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gq = 0.0;
 #pragma unroll
-        for (int s = 0; s < SPLIT; ++s) {
+        for (int s = 0; s < T; ++s) {
             vz = fmax(vz, (double)slots[s].violz[c]);
             vh = fmax(vh, (double)slots[s].violh[c]);
             wm = fmin(wm, (double)slots[s].wmin[c]);
-            gp += slots[s].gap[c];
+            gq += slots[s].gap[c];
         }
         int code = 0;
         if (vz * a.L <= a.tol) code = 1;
-        else if ((vh * a.L <= a.tol) && (wm >= 0.0) && (gp * a.L <= a.tol)) code = 2;
-        if (active) {
-            my_it = v + 1;
-            if (code) {
-                my_code = code;
-                if (code == 2) {  // zhat certified: it becomes z* (own primal tiles)
+        else if ((vh * a.L <= a.tol) && (wm >= 0.0) && (gq * a.L <= a.tol)) code = 2;
+        if (active && code) {
+            my_code = code;
+            if (code == 2) {  // zhat certified: it becomes z*
 #pragma unroll
-                    for (int u = 0; u < NL; ++u) {
-                        const int t = u * SPLIT + w;
-                        const float4 zh = *reinterpret_cast<const float4*>(Zh + (t * 64 + lane) * 4);
-                        *reinterpret_cast<float4*>(Zs + (t * 64 + lane) * 4) = zh;
-                    }
-                }
-                active = false;
+                for (int r = 0; r < 4; ++r) z[r] = zh[r];
             }
+            active = false;
         }
-        // leave when no instance of the panel is still iterating (same answer in every wave)
-        if (!__any(active)) break;
-        __syncthreads();  // Zs / slots reads above complete before the next epilogue writes
+        // leave when no instance of the panel is still iterating (uniform: same LDS reads);
+        // the barrier also orders the slot reads above before the next check's writes
+        if (!__syncthreads_or(active ? 1 : 0)) break;
     }
-    // ---- write back -------------------------------------------------------------------
-    __syncthreads();
+    // ---- write back ---------------------------------------------------------------------
 #pragma unroll
-    for (int u = 0; u < NL; ++u) {
-        const int t = u * SPLIT + w;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int i = 16 * t + 4 * r + j;
-            if (i < m && real) a.y[(size_t)inst * m + i] = Y[u][r];
-        }
+    for (int r = 0; r < 4; ++r) {
+        const int i = 16 * t + 4 * r + j;
+        if (real && i < n) a.z[(size_t)inst * n + i] = z[r];
+        if (real && i < m) a.y[(size_t)inst * m + i] = y[r];
     }
-    for (int e = tid; e < T * 256; e += 64 * SPLIT) {
-        const int t = e >> 8, l = (e >> 2) & 63, r = e & 3;
-        const int i = 16 * t + 4 * r + (l >> 4), ci = blockIdx.x * 16 + (l & 15);
-        if (i < n && ci < a.batch) a.z[(size_t)ci * n + i] = Zs[e];
-    }
-    if (w == 0 && j == 0 && real) {
+    if (t == 0 && j == 0 && real) {
         a.iters[inst] = my_it;
         a.conv[inst] = my_code;
     }
 }
 
-template <int SPLIT, int NL>
+template <int T>
 static hipError_t launch_panel_t(const SolveArgs<float>& a, hipStream_t s) {
-    constexpr int T = NL * SPLIT;
-    const size_t lds = sizeof(float) * 256 * (size_t)(5 * T) + sizeof(PanelSlot) * SPLIT;
-    hipError_t e = hipFuncSetAttribute((const void*)gpad_panel_kernel<SPLIT, NL>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
     const int groups = (a.batch + 15) / 16;
-    hipLaunchKernelGGL((gpad_panel_kernel<SPLIT, NL>), dim3(groups), dim3(64 * SPLIT), lds, s, a);
+    hipLaunchKernelGGL(gpad_panel_kernel<T>, dim3(groups), dim3(64 * T), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_panel(const SolveArgs<float>& a, hipStream_t s, bool* supported) {
-    const PanelGeom g = panel_geom(a.n, a.m, a.batch);
-    // the fragment image must have been packed for this geometry (setup saw the same batch)
-    *supported = a.frag != nullptr && g.nl && a.strideA == 0 && a.strideB == 0 &&
-                 a.frag_tiles == g.tiles;
+    const int T = panel_tiles_for(a.n, a.m);
+    // the fragment image must have been packed for this geometry at setup
+    *supported = a.frag != nullptr && T && a.strideA == 0 && a.strideB == 0 && a.frag_tiles == T;
     if (!*supported) return hipSuccess;
-    if (g.split == 2) {
-        switch (g.nl) {
-            case 1: return launch_panel_t<2, 1>(a, s);
-            case 2: return launch_panel_t<2, 2>(a, s);
-            case 4: return launch_panel_t<2, 4>(a, s);
-            default: return launch_panel_t<2, 7>(a, s);
-        }
-    }
-    switch (g.nl) {
-        case 1: return launch_panel_t<4, 1>(a, s);
-        case 2: return launch_panel_t<4, 2>(a, s);
-        default: return launch_panel_t<4, 4>(a, s);
+    switch (T) {
+        case 1: return launch_panel_t<1>(a, s);
+        case 2: return launch_panel_t<2>(a, s);
+        case 3: return launch_panel_t<3>(a, s);
+        case 4: return launch_panel_t<4>(a, s);
+        case 5: return launch_panel_t<5>(a, s);
+        case 6: return launch_panel_t<6>(a, s);
+        case 7: return launch_panel_t<7>(a, s);
+        case 8: return launch_panel_t<8>(a, s);
+        case 9: return launch_panel_t<9>(a, s);
+        case 10: return launch_panel_t<10>(a, s);
+        case 11: return launch_panel_t<11>(a, s);
+        case 12: return launch_panel_t<12>(a, s);
+        case 13: return launch_panel_t<13>(a, s);
+        case 14: return launch_panel_t<14>(a, s);
+        case 15: return launch_panel_t<15>(a, s);
+        default: return launch_panel_t<16>(a, s);
     }
 }
-
-int panel_tiles(int n, int m, int batch) { return panel_geom(n, m, batch).tiles; }
 
 }  // namespace gpad

@@ -80,27 +80,26 @@ void orc_schedule(int N, int kind, double* theta, double* beta) {
  * branches computable from (ML, M, G, g, L)):
  *   (A) max_i (G z - g)_i <= tol                                   -> stop, return z     (1)
  *   (B) max_i (G zhat - g)_i <= tol, w >= 0, -w'(G zhat - g) <= tol -> stop, return zhat  (2)
- * with G x - g = L (GL x + pD) evaluated as an fmaf chain + pD, then scaled in fp64.  The
- * paper (sec. 4.2) returns whichever candidate passed; the commented MATLAB returns z_v in
- * both branches, which for (B) hands back a point that was never certified. */
-static int orc_check_f32(const float* GL, const float* pD, const float* z, const float* zhat,
-                         const float* w, int n, int m, float L, float tol) {
+ * with G x - g = L (GL x + pD).  GL zhat is the step-4 chain itself; GL z is carried by the
+ * same affine recursion as z (8c): u_v = (1-theta_v) u_{v-1} + theta_v (GL zhat_v), u_{-1} =
+ * GL z_{-1} -- equal to GL z_v in exact arithmetic, and it costs no extra mat-vec.  The paper
+ * (sec. 4.2) returns whichever candidate passed; the commented MATLAB returns z_v in both
+ * branches, which for (B) hands back a point that was never certified. */
+static float orc_chain(const float* row, const float* x, int n) {
+    float sum = 0.0f;
+    for (int j = 0; j < n; j++) sum = fmaf(row[j], x[j], sum);
+    return sum;
+}
+
+static int orc_check_f32(const float* u, const float* ch, const float* pD, const float* w, int m,
+                         float L, float tol) {
     float viol = -INFINITY;
-    for (int i = 0; i < m; i++) {
-        float sum = 0.0f;
-        const float* row = GL + (size_t)i * n;
-        for (int j = 0; j < n; j++) sum = fmaf(row[j], z[j], sum);
-        float t = sum + pD[i];
-        viol = fmaxf(viol, t);
-    }
+    for (int i = 0; i < m; i++) viol = fmaxf(viol, u[i] + pD[i]);
     if ((double)viol * (double)L <= (double)tol) return 1;
     float violh = -INFINITY, wmin = INFINITY;
     double gap = 0.0;
     for (int i = 0; i < m; i++) {
-        float sum = 0.0f;
-        const float* row = GL + (size_t)i * n;
-        for (int j = 0; j < n; j++) sum = fmaf(row[j], zhat[j], sum);
-        float t = sum + pD[i];
+        const float t = ch[i] + pD[i];
         violh = fmaxf(violh, t);
         wmin = fminf(wmin, w[i]);
         gap -= (double)w[i] * (double)t;
@@ -112,15 +111,21 @@ static int orc_check_f32(const float* GL, const float* pD, const float* z, const
 int orc_solve_f32(float* z, float* y, const float* MGneg, const float* gP, const float* GL,
                   const float* pD, int n, int m, int N, float L, float tol, int check_every,
                   const float* theta, const float* beta, int* converged) {
-    float* base = (float*)malloc(sizeof(float) * (size_t)(m > 0 ? m : 1) * 4);
+    const int mm = m > 0 ? m : 1;
+    float* base = (float*)malloc(sizeof(float) * (size_t)mm * 6);
     float* ycur = base;
-    float* yprev = ycur + (m > 0 ? m : 1);
-    float* w = yprev + (m > 0 ? m : 1);
-    float* ynew = w + (m > 0 ? m : 1);
+    float* yprev = ycur + mm;
+    float* w = yprev + mm;
+    float* ynew = w + mm;
+    float* u = ynew + mm;   /* GL z, by recursion */
+    float* ch = u + mm;     /* GL zhat (step-4 chains) */
     float* zhat = (float*)malloc(sizeof(float) * (size_t)(n > 0 ? n : 1));
     if (check_every <= 0) check_every = 10;
     memcpy(ycur, y, sizeof(float) * m);
     memcpy(yprev, y, sizeof(float) * m); /* acceldualgrad.m:16: y_0 = y_{-1} */
+    const int use_tol = tol > 0.0f;
+    if (use_tol)
+        for (int i = 0; i < m; i++) u[i] = orc_chain(GL + (size_t)i * n, z, n);
     int it = 0, conv = 0;
     for (int v = 0; v < N; v++) {
         orc_step1_f32(ycur, yprev, w, beta[v], m);          /* main.cu:163 */
@@ -129,12 +134,19 @@ int orc_solve_f32(float* z, float* y, const float* MGneg, const float* gP, const
         orc_step4_f32(GL, ynew, w, pD, zhat, n, m);         /* main.cu:171 */
         float* t = yprev; yprev = ycur; ycur = ynew; ynew = t; /* main.cu:167 + MATLAB :60-64 */
         it = v + 1;
-        if (tol > 0.0f && (it % check_every) == 0) {
-            const int c = orc_check_f32(GL, pD, z, zhat, w, n, m, L, tol);
-            if (c) {
-                if (c == 2) memcpy(z, zhat, sizeof(float) * n);
-                conv = c;
-                break;
+        if (use_tol) {
+            const float th = theta[v], omt = 1.0f - th;
+            for (int i = 0; i < m; i++) {
+                ch[i] = orc_chain(GL + (size_t)i * n, zhat, n);  /* = step 4's sum */
+                u[i] = fmaf(omt, u[i], th * ch[i]);
+            }
+            if ((it % check_every) == 0) {
+                const int c = orc_check_f32(u, ch, pD, w, m, L, tol);
+                if (c) {
+                    if (c == 2) memcpy(z, zhat, sizeof(float) * n);
+                    conv = c;
+                    break;
+                }
             }
         }
     }
@@ -146,20 +158,14 @@ int orc_solve_f32(float* z, float* y, const float* MGneg, const float* gP, const
 }
 
 /* ---- fp64, acceldualgrad.m operation order ------------------------------------- */
-static int orc_check_f64(const double* GL, const double* pD, const double* z, const double* zhat,
-                         const double* w, int n, int m, double L, double tol) {
+static int orc_check_f64(const double* u, const double* ch, const double* pD, const double* w,
+                         int m, double L, double tol) {
     double viol = -INFINITY;
-    for (int i = 0; i < m; i++) {
-        double sum = 0.0;
-        for (int j = 0; j < n; j++) sum = fma(GL[(size_t)i * n + j], z[j], sum);
-        viol = fmax(viol, sum + pD[i]);
-    }
+    for (int i = 0; i < m; i++) viol = fmax(viol, u[i] + pD[i]);
     if (viol * L <= tol) return 1;
     double violh = -INFINITY, wmin = INFINITY, gap = 0.0;
     for (int i = 0; i < m; i++) {
-        double sum = 0.0;
-        for (int j = 0; j < n; j++) sum = fma(GL[(size_t)i * n + j], zhat[j], sum);
-        double t = sum + pD[i];
+        const double t = ch[i] + pD[i];
         violh = fmax(violh, t);
         wmin = fmin(wmin, w[i]);
         gap -= w[i] * t;
@@ -180,6 +186,8 @@ int orc_solve_f64(double* z, double* y, const double* ML, const double* gP, cons
     double* zhat = (double*)malloc(sizeof(double) * (n + 1));
     double* th = (double*)malloc(sizeof(double) * (N + 1));
     double* be = (double*)malloc(sizeof(double) * (N + 1));
+    double* u = (double*)malloc(sizeof(double) * (m + 1));
+    double* ch = (double*)malloc(sizeof(double) * (m + 1));
     const double inv = 1.0 / L, ninv = -1.0 / L;
     for (size_t k = 0; k < nm; k++) GL[k] = inv * G[k];           /* acceldualgrad.m:22 */
     for (int i = 0; i < m; i++) pD[i] = ninv * g[i];              /* acceldualgrad.m:23 */
@@ -187,6 +195,13 @@ int orc_solve_f64(double* z, double* y, const double* ML, const double* gP, cons
     if (check_every <= 0) check_every = 10;
     memcpy(yv, y, sizeof(double) * m);
     memcpy(yvm1, y, sizeof(double) * m);
+    const int use_tol = tol > 0.0;
+    if (use_tol)
+        for (int i = 0; i < m; i++) {
+            double sum = 0.0;
+            for (int j = 0; j < n; j++) sum = fma(GL[(size_t)i * n + j], z[j], sum);
+            u[i] = sum;
+        }
     int it = 0, conv = 0;
     for (int v = 0; v < N; v++) {
         for (int i = 0; i < m; i++) w[i] = yv[i] + be[v] * (yv[i] - yvm1[i]);      /* :43 */
@@ -201,11 +216,13 @@ int orc_solve_f64(double* z, double* y, const double* ML, const double* gP, cons
             for (int j = 0; j < n; j++) sum = fma(GL[(size_t)i * n + j], zhat[j], sum);
             double s = (w[i] + sum) + pD[i];
             yp1[i] = s > 0.0 ? s : 0.0;
+            ch[i] = sum;
+            if (use_tol) u[i] = (1.0 - th[v]) * u[i] + th[v] * sum;
         }
         double* t = yvm1; yvm1 = yv; yv = yp1; yp1 = t;                               /* :60-64 */
         it = v + 1;
-        if (tol > 0.0 && (it % check_every) == 0) {
-            const int c = orc_check_f64(GL, pD, z, zhat, w, n, m, L, tol);
+        if (use_tol && (it % check_every) == 0) {
+            const int c = orc_check_f64(u, ch, pD, w, m, L, tol);
             if (c) {
                 if (c == 2) memcpy(z, zhat, sizeof(double) * n);
                 conv = c;
@@ -215,6 +232,7 @@ int orc_solve_f64(double* z, double* y, const double* ML, const double* gP, cons
     }
     memcpy(y, yv, sizeof(double) * m);
     free(GL); free(pD); free(yv); free(yvm1); free(w); free(yp1); free(zhat); free(th); free(be);
+    free(u); free(ch);
     if (converged) *converged = conv;
     return it;
 }
