@@ -101,6 +101,76 @@ def cpu_baseline(n, m, ML, G, L, M, g, iters_per_instance, budget_s=12.0):
             "single_thread_value": N / t1, "seconds": round(dt, 2)}
 
 
+def traffic_from_profile(kernel_prefix):
+    """HBM bytes per launch of the dominant kernel from the committed PMC profile of this same
+    bench command (tools/profile.sh -> profiles/r01_bench_summary.json; FETCH_SIZE x2 +
+    WRITE_SIZE, MI355X_MICROARCH.md §HBM).  None when absent."""
+    path = os.path.join(ROOT, "profiles", "r01_bench_summary.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    for k, v in d.get("pmc_per_launch", {}).items():
+        if k.startswith(kernel_prefix) and "hbm_bytes_per_launch" in v:
+            return v["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
+
+
+def hbm_leg(dev, batch=1024, n=800, m=800, N=20):
+    """C5: long horizon (N = 200 -> n = 800), m = 800, 1024 instances with DISTINCT matrices:
+    the matrices cannot stay on chip, so every iteration streams 5.1 MB per instance from HBM
+    (stream kernel).  Returns achieved algorithmic GB/s vs the 8 TB/s roofline."""
+    import torch
+
+    import gpad_mpc
+    g = torch.Generator(device=dev).manual_seed(0)
+    R = torch.randn(batch, n, n, device=dev, generator=g) / np.sqrt(n)
+    H = R.transpose(1, 2) @ R + torch.eye(n, device=dev)
+    G = torch.randn(batch, m, n, device=dev, generator=g) / np.sqrt(n)
+    Hi = torch.cholesky_inverse(torch.linalg.cholesky(H))
+    ML = (Hi @ G.transpose(1, 2)).contiguous()
+    L = float(torch.linalg.matrix_norm(G @ ML, "fro").max())
+    zf = torch.rand(batch, n, device=dev, generator=g) - 0.5
+    gv = (G @ zf.unsqueeze(2)).squeeze(2) + 0.1 + 0.9 * torch.rand(batch, m, device=dev, generator=g)
+    M = (Hi @ torch.randn(batch, n, 1, device=dev, generator=g)).squeeze(2).contiguous()
+    del R, H, Hi
+    z = torch.zeros(batch, n, device=dev)
+    y = torch.zeros(batch, m, device=dev)
+    with gpad_mpc.GpadSolver(dev.index or 0, stream=torch.cuda.current_stream(dev).cuda_stream) as s:
+        s.setup(ML, G.contiguous(), L, n=n, m=m, batch=batch, shared=False)
+        s.run(z, y, M, gv, N, 0.0)
+        best = 1e30
+        for _ in range(3):
+            st = s.run(z.zero_(), y.zero_(), M, gv, N, 0.0)
+            best = min(best, st["kernel_ms"])
+    per_it = 4 * (2 * n * m + 4 * m + 3 * n)
+    gbs = batch * N * per_it / (best / 1e3) / 1e9
+    return {"config": f"C5: {batch} distinct instances, N=200 (n={n}), m={m}, {N} iterations",
+            "kernel": st["kernel"], "iters_per_s": batch * N / (best / 1e3),
+            "achieved_GBs": gbs, "peak_GBs": HBM_PEAK_GBS, "frac": gbs / HBM_PEAK_GBS,
+            "bytes_per_instance_iter": per_it}
+
+
+def distinct_leg(dev, n, m, batch=8192, N=100):
+    """C2-shape instances with distinct matrices, register-resident (resident kernel)."""
+    import torch
+
+    import gpad_mpc
+    g = torch.Generator(device=dev).manual_seed(1)
+    ML = (torch.randn(batch, n, m, device=dev, generator=g) / np.sqrt(m) * 0.1).contiguous()
+    G = (torch.randn(batch, m, n, device=dev, generator=g) / np.sqrt(n)).contiguous()
+    M = torch.randn(batch, n, device=dev, generator=g)
+    gv = torch.rand(batch, m, device=dev, generator=g) + 0.1
+    z = torch.zeros(batch, n, device=dev)
+    y = torch.zeros(batch, m, device=dev)
+    with gpad_mpc.GpadSolver(dev.index or 0, stream=torch.cuda.current_stream(dev).cuda_stream) as s:
+        s.setup(ML, G, 10.0, n=n, m=m, batch=batch, shared=False)
+        s.run(z, y, M, gv, N, 0.0)
+        st = s.run(z.zero_(), y.zero_(), M, gv, N, 0.0)
+    return {"config": f"{batch} distinct {n}x{m} instances, {N} iterations", "kernel": st["kernel"],
+            "iters_per_s": batch * N / (st["kernel_ms"] / 1e3)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -114,6 +184,7 @@ def main():
     ap.add_argument("--max-iters", type=int, default=5000)
     ap.add_argument("--kernel", default="auto", choices=["auto", "stream", "resident", "panel"])
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the C2/C5 side legs")
     args = ap.parse_args()
 
     import torch
@@ -144,17 +215,18 @@ def main():
     solver = gpad_mpc.GpadSolver(local, stream=stream.cuda_stream)
     L32 = float(np.float32(L))
     solver.setup(dML, dG, L32, n=n, m=m, batch=B, shared=True, check_every=10, kernel=kern)
-    packed = torch.empty(B, n + m + 1, device=dev)
-    gathered = [torch.empty_like(packed) for _ in range(world)] if (world > 1 and rank == 0) else None
+    from gpad_mpc import parallel
+    packed = torch.empty(B, n + m, device=dev)
+    counts = [B] * world
 
     def step():
         z.zero_()
         y.zero_()
         solver.run(z, y, dM, dg, args.max_iters, args.tol, stats=False)
-        if world > 1:
+        if world > 1:  # one RCCL gather of (z*, y*) to rank 0
             packed[:, :n] = z
-            packed[:, n:n + m] = y
-            dist.gather(packed, gathered, dst=0)
+            packed[:, n:] = y
+            parallel.gather_rows(packed, world, rank, counts)
 
     for _ in range(args.warmup):
         step()
@@ -202,6 +274,7 @@ def main():
         mean_iters = iters_per_launch / B
         # C2 single instance (config 1): latency kernel, fixed 1000 iterations
         one = dict()
+        traffic, traffic_src = traffic_from_profile("gpad::gpad_" + st["kernel"])
         with gpad_mpc.GpadSolver(local, stream=stream.cuda_stream) as s1:
             s1.setup(dML, dG, L32, n=n, m=m, batch=1)
             z1 = torch.zeros(1, n, device=dev)
@@ -216,6 +289,10 @@ def main():
         cpu = None
         if not args.no_cpu and world == 1:
             cpu = cpu_baseline(n, m, ML, G, L, M, g, mean_iters)
+        extra = {}
+        if not args.no_extra and world == 1:
+            extra["hbm_bound_c5"] = hbm_leg(dev)
+            extra["distinct_c2_batch"] = distinct_leg(dev, n, m)
         out = {
             "metric": "GPAD iterations/s (instance-iterations, solve to eps=1e-4)",
             "value": value,
@@ -239,11 +316,14 @@ def main():
             "kernel": st["kernel"],
             "single_instance": one,
             "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP32_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved_tf / FP32_PEAK_TFLOPS, "traffic": None,
+                         "unit": "TFLOP/s", "frac": achieved_tf / FP32_PEAK_TFLOPS,
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "kernel_ms": avg_kernel_s * 1e3,
-                         "note": "fp32 FMA-bound (matrices stay on chip); F = 4nm+5m+4n per "
-                                 "instance-iteration"},
+                         "note": "fp32 matrix-core bound (shared matrices stay in L2, traffic = "
+                                 "per-instance vectors); achieved = useful flops (F = 4nm+5m+4n "
+                                 "per executed instance-iteration) / avg launch time"},
             "cpu_baseline": cpu,
+            "legs": extra,
         }
         print(json.dumps(out))
     solver.close()

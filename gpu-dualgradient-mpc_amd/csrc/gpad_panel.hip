@@ -118,6 +118,9 @@ __device__ __forceinline__ f32x4 panel_gemm(__amdgpu_buffer_rsrc_t PA, const flo
             a[nxt] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb + 1) * T * 1024, 0));
             b[nxt] = *reinterpret_cast<const float4*>(Bl + ((kb + 1) * 64 + lane) * 4);
         }
+        // the next block's loads issue BEFORE this block's MFMAs (else the scheduler sinks them
+        // below and waits on them at once: a full L2 round trip per k-block)
+        __builtin_amdgcn_sched_barrier(0);
         acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].x, b[cur].x, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].y, b[cur].y, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].z, b[cur].z, acc, 0, 0, 0);
