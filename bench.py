@@ -185,6 +185,8 @@ def main():
     ap.add_argument("--kernel", default="auto", choices=["auto", "stream", "resident", "panel"])
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C2/C5 side legs")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL) for real runs; gloo to rehearse ranks sharing one GPU")
     args = ap.parse_args()
 
     import torch
@@ -196,12 +198,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; --dist-backend gloo only to rehearse several ranks on one GPU
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))
+    torch.cuda.set_device(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    comm_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     stream = torch.cuda.current_stream(dev)
 
     n, m, B = args.nu * args.horizon, args.m, args.batch
@@ -212,7 +219,7 @@ def main():
     y = torch.zeros(B, m, device=dev)
     kern = {"auto": _lib.KERNEL_AUTO, "stream": _lib.KERNEL_STREAM, "resident": _lib.KERNEL_RESIDENT,
             "panel": _lib.KERNEL_PANEL}[args.kernel]
-    solver = gpad_mpc.GpadSolver(local, stream=stream.cuda_stream)
+    solver = gpad_mpc.GpadSolver(dev.index, stream=stream.cuda_stream)
     L32 = float(np.float32(L))
     solver.setup(dML, dG, L32, n=n, m=m, batch=B, shared=True, check_every=10, kernel=kern)
     from gpad_mpc import parallel
@@ -226,12 +233,20 @@ def main():
         if world > 1:  # one RCCL gather of (z*, y*) to rank 0
             packed[:, :n] = z
             packed[:, n:] = y
-            parallel.gather_rows(packed, world, rank, counts)
+            parallel.gather_rows(packed.to(comm_dev), world, rank, counts)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    st0 = solver.last_stats()
+    iters_host = np.zeros(B, np.int32)
+    st0 = solver.last_stats(iters=iters_host)
+    # batching losses of a lockstep panel (16 instances per MFMA column block): columns that
+    # converged early idle until their panel's slowest instance (panel_util), and panels that
+    # finished early idle until the slowest panel of the launch (tail_util)
+    pm = np.array([iters_host[i:i + 16].max() for i in range(0, B, 16)], np.float64)
+    util = {"panel_util": float(iters_host.sum() / (16.0 * pm.sum())) if pm.sum() else None,
+            "tail_util": float(pm.mean() / pm.max()) if pm.max() else None,
+            "max_iters": int(iters_host.max())}
 
     if world > 1:
         dist.barrier()
@@ -250,7 +265,7 @@ def main():
     dt = time.perf_counter() - t0
     # max time over ranks, sum of work over ranks
     stats = torch.tensor([dt, float(total_iters), kern_ms, float(st["converged"])], dtype=torch.float64,
-                         device=dev)
+                         device=comm_dev)
     if world > 1:
         tmax = stats[0:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -275,7 +290,7 @@ def main():
         # C2 single instance (config 1): latency kernel, fixed 1000 iterations
         one = dict()
         traffic, traffic_src = traffic_from_profile("gpad::gpad_" + st["kernel"])
-        with gpad_mpc.GpadSolver(local, stream=stream.cuda_stream) as s1:
+        with gpad_mpc.GpadSolver(dev.index, stream=stream.cuda_stream) as s1:
             s1.setup(dML, dG, L32, n=n, m=m, batch=1)
             z1 = torch.zeros(1, n, device=dev)
             y1 = torch.zeros(1, m, device=dev)
@@ -312,6 +327,7 @@ def main():
                        "parallelism": f"instance-sharded x{world}, RCCL gather"},
             "qp_solves_per_s": solves,
             "mean_iters_to_eps": mean_iters,
+            "batching": util,
             "converged": int(converged_all),
             "kernel": st["kernel"],
             "single_instance": one,
