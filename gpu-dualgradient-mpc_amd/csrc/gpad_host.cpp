@@ -86,7 +86,6 @@ void host_schedule(int N, int kind, double* theta, double* beta) {
 struct gpad_handle_s {
     int device = 0;
     hipStream_t stream = nullptr;
-    bool own_stream = false;
     bool ready = false;
     gpad_dims_t dims{};
     double L = 1.0;
@@ -132,12 +131,7 @@ int gpad_create(gpad_handle_t* out, int device, void* stream) {
     HIP_TRY(hipSetDevice(device));
     auto h = std::make_unique<gpad_handle_s>();
     h->device = device;
-    if (stream) {
-        h->stream = static_cast<hipStream_t>(stream);
-    } else {
-        HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
-        h->own_stream = true;
-    }
+    h->stream = static_cast<hipStream_t>(stream);  // NULL = the device's default (null) stream
     HIP_TRY(hipEventCreate(&h->ev0));
     HIP_TRY(hipEventCreate(&h->ev1));
     *out = h.release();
@@ -147,7 +141,7 @@ int gpad_create(gpad_handle_t* out, int device, void* stream) {
 int gpad_destroy(gpad_handle_t h) {
     if (!h) return GPAD_OK;
     (void)hipSetDevice(h->device);
-    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    (void)hipStreamSynchronize(h->stream);
     h->MGt.release();
     h->GLt.release();
     h->frag.release();
@@ -158,26 +152,15 @@ int gpad_destroy(gpad_handle_t h) {
     h->counters.release();
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
-    if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return GPAD_OK;
 }
 
 int gpad_set_stream(gpad_handle_t h, void* stream) {
     if (!h) return fail(GPAD_ERR_INVALID, "gpad_set_stream: null handle");
-    (void)hipSetDevice(h->device);
-    if (h->own_stream && h->stream) {
-        HIP_TRY(hipStreamSynchronize(h->stream));
-        HIP_TRY(hipStreamDestroy(h->stream));
-        h->own_stream = false;
-        h->stream = nullptr;
-    }
-    if (stream) {
-        h->stream = static_cast<hipStream_t>(stream);
-    } else {
-        HIP_TRY(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
-        h->own_stream = true;
-    }
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipStreamSynchronize(h->stream));  // work queued on the old stream completes first
+    h->stream = static_cast<hipStream_t>(stream);
     return GPAD_OK;
 }
 

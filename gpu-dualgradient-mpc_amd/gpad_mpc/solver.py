@@ -53,6 +53,7 @@ class GpadSolver:
         self.lib = _lib.load()
         self.h = C.c_void_p()
         if stream is None and self._torch_device_ready():
+            # order the solve after torch's pending work on this device (0 = HIP null stream)
             import torch
             stream = torch.cuda.current_stream(device).cuda_stream
         check(self.lib.gpad_create(C.byref(self.h), device, C.c_void_p(stream or 0)), "gpad_create")

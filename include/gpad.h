@@ -80,7 +80,8 @@ const char* gpad_version(void);
 const char* gpad_strerror(int status);
 const char* gpad_last_error(void); /* thread-local detail of the last failure */
 
-/* Handle bound to one device and one HIP stream (NULL stream -> the handle creates its own).
+/* Handle bound to one device and one HIP stream; every launch and copy of the handle is
+ * ordered on that stream.  NULL = the device's default (null) stream, as in every HIP API.
  * Replaces the implicit device/default-stream state of main.cu:116-147. */
 int gpad_create(gpad_handle_t* h, int device, void* hip_stream);
 int gpad_destroy(gpad_handle_t h);

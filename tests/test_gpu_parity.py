@@ -269,6 +269,38 @@ def test_device_memory_async_and_one_shot_solve(gpu, oracle):
     assert_bitexact(z2, z.cpu().numpy())
 
 
+@pytest.mark.parametrize("kernel", ["panel", "resident", "stream"])
+def test_async_runs_ordered_after_torch_work(gpu, oracle, kernel):
+    """Back-to-back asynchronous runs on torch's current stream with torch ops in between (no
+    host sync): every run must see the zeroed state (regression: a private stream raced)."""
+    import torch
+    import gpad_mpc
+    from gpad_mpc import problems
+    B, n, m = 300, 48, 80
+    qp = problems.synthetic_qp(n, m, batch=B, seed=31)
+    f = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(gpu)  # noqa: E731
+    ML, G, M, g = f(qp.ML), f(qp.G), f(qp.M), f(qp.g)
+    z = torch.empty(B, n, device=gpu)
+    y = torch.empty(B, m, device=gpu)
+    with gpad_mpc.GpadSolver(0) as s:
+        s.setup(ML, G, float(np.float32(qp.L)), n=n, m=m, batch=B, kernel=kcode(kernel))
+        for _ in range(4):
+            z.fill_(7.0)
+            y.fill_(3.0)
+            z.zero_()
+            y.zero_()
+            s.run(z, y, M, g, 3000, 1e-4, stats=False)
+        iters = np.zeros(B, np.int32)
+        s.last_stats(iters=iters)
+    for b in (0, 57, B - 1):
+        zo, yo, it, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), qp.ML.astype(np.float32),
+                                         qp.M[b].astype(np.float32), qp.G.astype(np.float32),
+                                         qp.g[b].astype(np.float32), 3000, np.float32(qp.L), 1e-4)
+        assert iters[b] == it
+        assert_bitexact(z[b].cpu().numpy(), zo)
+        assert_bitexact(y[b].cpu().numpy(), yo)
+
+
 def test_error_paths(gpu):
     import gpad_mpc
     from gpad_mpc import _lib
