@@ -240,13 +240,14 @@ def main():
     torch.cuda.synchronize(dev)
     iters_host = np.zeros(B, np.int32)
     st0 = solver.last_stats(iters=iters_host)
-    # batching losses of a lockstep panel (16 instances per MFMA column block): columns that
-    # converged early idle until their panel's slowest instance (panel_util), and panels that
-    # finished early idle until the slowest panel of the launch (tail_util)
+    # batching losses of lockstep panels (16 instances per MFMA column block; with the whole
+    # batch resident, instance i runs in panel i // 16): columns that converged early idle until
+    # their panel's slowest instance (panel_util); panels that finished early leave their CU
+    # share to the others until the slowest panel ends (tail_util)
     pm = np.array([iters_host[i:i + 16].max() for i in range(0, B, 16)], np.float64)
     util = {"panel_util": float(iters_host.sum() / (16.0 * pm.sum())) if pm.sum() else None,
             "tail_util": float(pm.mean() / pm.max()) if pm.max() else None,
-            "max_iters": int(iters_host.max())}
+            "min_iters": int(iters_host.min()), "max_iters": int(iters_host.max())}
 
     if world > 1:
         dist.barrier()

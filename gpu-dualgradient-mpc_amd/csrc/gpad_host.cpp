@@ -99,6 +99,7 @@ struct gpad_handle_s {
     std::vector<int> h_iters, h_conv;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int last_kernel = 0, last_batch = 0;
+    int num_cus = 256;
     bool timed = false;
 };
 
@@ -132,6 +133,11 @@ int gpad_create(gpad_handle_t* out, int device, void* stream) {
     auto h = std::make_unique<gpad_handle_s>();
     h->device = device;
     h->stream = static_cast<hipStream_t>(stream);  // NULL = the device's default (null) stream
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+            h->num_cus = prop.multiProcessorCount;
+    }
     HIP_TRY(hipEventCreate(&h->ev0));
     HIP_TRY(hipEventCreate(&h->ev1));
     *out = h.release();
@@ -346,7 +352,8 @@ static int run_typed(gpad_handle_t h, T* z, T* y, const T* M, const T* g, int N,
     const int n = d.n, m = d.m, batch = d.batch;
     int rc = ensure_schedule(h, N, theta_in, beta_in);
     if (rc) return rc;
-    if ((rc = h->counters.ensure(sizeof(int) * 2 * (size_t)batch))) return rc;
+    // [iters | conv | queue word (padded to 16 B)]
+    if ((rc = h->counters.ensure(sizeof(int) * (2 * (size_t)batch + 4)))) return rc;
     T *dz = z, *dy = y;
     const T *dM = M, *dg = g;
     const size_t zb = sizeof(T) * (size_t)batch * n, yb = sizeof(T) * (size_t)batch * m;
@@ -391,10 +398,18 @@ static int run_typed(gpad_handle_t h, T* z, T* y, const T* M, const T* g, int N,
     a.beta = (const T*)h->beta.p;
     a.iters = (int*)h->counters.p;
     a.conv = a.iters + batch;
+    a.queue = a.conv + batch;
+    a.num_cus = h->num_cus;
     int kernel = d.kernel;
-    HIP_TRY(hipEventRecord(h->ev0, h->stream));
     hipError_t e = hipSuccess;
     bool ok = false;
+    HIP_TRY(hipMemsetAsync(a.queue, 0, 4 * sizeof(int), h->stream));
+    HIP_TRY(hipEventRecord(h->ev0, h->stream));
+    if (N == 0) {  // nothing to iterate: outputs are the inputs, zero counts
+        HIP_TRY(hipMemsetAsync(a.iters, 0, sizeof(int) * 2 * (size_t)batch, h->stream));
+        kernel = d.kernel == GPAD_KERNEL_AUTO ? GPAD_KERNEL_STREAM : d.kernel;
+        goto launched;
+    }
     if constexpr (sizeof(T) == sizeof(float)) {
         if (kernel == GPAD_KERNEL_PANEL || (kernel == GPAD_KERNEL_AUTO && d.shared && batch >= 64)) {
             e = gpad::launch_panel(a, h->stream, &ok);
@@ -422,6 +437,7 @@ static int run_typed(gpad_handle_t h, T* z, T* y, const T* M, const T* g, int N,
                         std::string("stream kernel: ") + hipGetErrorString(e) +
                             " (n+m beyond the LDS budget?)");
     }
+launched:
     HIP_TRY(hipEventRecord(h->ev1, h->stream));
     h->timed = true;
     h->last_kernel = kernel;

@@ -30,7 +30,9 @@ struct SolveArgs {
     const T* theta;        // [N+2] theta_v (two zero pads: kernels prefetch ahead)
     const T* beta;         // [N+2] beta_v
     int* iters;            // [batch] iterations executed
-    int* conv;             // [batch] 1 if the tolerance test passed
+    int* conv;             // [batch] 0 = not converged, 1 = test (A) passed, 2 = test (B) passed
+    int* queue;            // panel kernel: device counter of handed-out instances (zeroed per run)
+    int num_cus;           // compute units of the device (persistent-grid sizing)
 };
 
 // launchers (return hipError_t of the launch)

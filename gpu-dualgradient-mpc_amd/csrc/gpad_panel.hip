@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 
 #include "gpad_internal.h"
 
@@ -130,61 +131,89 @@ __device__ __forceinline__ f32x4 panel_gemm(__amdgpu_buffer_rsrc_t PA, const flo
     return acc;
 }
 
-template <int T>
+// Continuous batching: a workgroup keeps 16 instance "columns" in flight.  A column that
+// converges (or reaches N) writes its z*, y* and counts, then pulls the next instance from a
+// device-wide queue, so no column and no CU idles while instances remain.  Every column has its
+// own iteration counter (theta/beta are per lane); columns are independent in the MFMA, so the
+// arithmetic of an instance does not depend on which column or workgroup runs it.
+template <int T, bool QUEUE>
 __global__ __launch_bounds__(64 * T) void gpad_panel_kernel(SolveArgs<float> a) {
     __shared__ __attribute__((aligned(16))) float Wl[T * 256];  // [T][64][4] w    (B of GEMM 1)
     __shared__ __attribute__((aligned(16))) float Zh[T * 256];  // [T][64][4] zhat (B of GEMM 2)
     __shared__ PanelSlot slots[T];
+    __shared__ int next_inst[16];  // refill hand-out per column (-1: none)
+    __shared__ int queue_dry;
 
     const int lane = threadIdx.x & 63;
     const int t = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // row tile of this wave
     const int j = lane >> 4, c = lane & 15;
-    const int n = a.n, m = a.m;
-    const int inst = blockIdx.x * 16 + c;
-    const bool real = inst < a.batch;
+    const int n = a.n, m = a.m, N = a.N;
     const int abytes = T * T * 1024;  // one packed operand
     const __amdgpu_buffer_rsrc_t PA1 =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.frag), 0, abytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t PA2 = __builtin_amdgcn_make_buffer_rsrc(
         (void*)((const char*)a.frag + abytes), 0, abytes, 0x00020000);
     const int voff = t * 1024 + lane * 16;
-    const float4* Wl4 = reinterpret_cast<const float4*>(Wl);
-    float4* Wl4w = reinterpret_cast<float4*>(Wl);
-    float4* Zh4w = reinterpret_cast<float4*>(Zh);
     const int slot = t * 64 + lane;  // this lane's float4 in Wl / Zh
-
-    // ---- prologue: this wave's rows (register r <-> row 16t + 4r + j, instance c) ------------
-    float z[4], gp[4], y[4], pd[4], u[4], zh[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int i = 16 * t + 4 * r + j;
-        const bool okn = real && i < n, okm = real && i < m;
-        z[r] = okn ? a.z[(size_t)inst * n + i] : 0.0f;
-        gp[r] = okn ? a.gP[(size_t)inst * a.ld_gP + i] : 0.0f;
-        y[r] = okm ? a.y[(size_t)inst * m + i] : 0.0f;
-        pd[r] = okm ? (float)(a.gscale * (double)a.g[(size_t)inst * a.ld_g + i]) : 0.0f;
-        u[r] = 0.0f;
-        zh[r] = 0.0f;
-    }
-    const float b0 = a.beta[0];
-    Wl4w[slot] = make_float4(__builtin_fmaf(b0, y[0] - y[0], y[0]), __builtin_fmaf(b0, y[1] - y[1], y[1]),
-                             __builtin_fmaf(b0, y[2] - y[2], y[2]), __builtin_fmaf(b0, y[3] - y[3], y[3]));
+    float4* Wl4 = reinterpret_cast<float4*>(Wl);
+    float4* Zh4 = reinterpret_cast<float4*>(Zh);
     const bool use_tol = a.tol > 0.0;
-    if (use_tol) {  // u = G_L z_{-1} (then carried by the 8c recursion)
-        Zh4w[slot] = make_float4(z[0], z[1], z[2], z[3]);
+    const int first = gridDim.x * 16;  // instances handed out statically; the queue serves the rest
+
+    // register r <-> row 16t + 4r + j of the lane's current instance (column c)
+    float z[4], gp[4], y[4], pd[4], u[4], zh[4];
+    int inst = blockIdx.x * 16 + c;
+    bool active = inst < a.batch;
+    int lc = 0;  // iterations done by this column's instance
+
+    auto load_instance = [&](bool on) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = 16 * t + 4 * r + j;
+            const bool okn = on && i < n, okm = on && i < m;
+            z[r] = okn ? a.z[(size_t)inst * n + i] : 0.0f;
+            gp[r] = okn ? a.gP[(size_t)inst * a.ld_gP + i] : 0.0f;
+            y[r] = okm ? a.y[(size_t)inst * m + i] : 0.0f;
+            pd[r] = okm ? (float)(a.gscale * (double)a.g[(size_t)inst * a.ld_g + i]) : 0.0f;
+            u[r] = 0.0f;
+        }
+        const float b0 = a.beta[0];
+        Wl4[slot] = make_float4(__builtin_fmaf(b0, y[0] - y[0], y[0]), __builtin_fmaf(b0, y[1] - y[1], y[1]),
+                                __builtin_fmaf(b0, y[2] - y[2], y[2]), __builtin_fmaf(b0, y[3] - y[3], y[3]));
+    };
+    // u = G_L z_{-1} for the columns in `fresh` (one GEMM for all of them; then the 8c recursion)
+    auto seed_u = [&](bool fresh) {
+        Zh4[slot] = make_float4(z[0], z[1], z[2], z[3]);
         __syncthreads();
         const f32x4 cz = panel_gemm<T>(PA2, Zh, voff, lane);
+        if (fresh) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) u[r] = cz[r];
-    }
+            for (int r = 0; r < 4; ++r) u[r] = cz[r];
+        }
+        __syncthreads();
+    };
+
+    load_instance(active);
+    if (c == 0 && t == 0 && j == 0) queue_dry = first >= a.batch;
+    if (use_tol) seed_u(active);
     __syncthreads();
 
-    bool active = real;
-    int my_it = 0, my_code = 0;
     float th = a.theta[0], bn = a.beta[1];
-    for (int v = 0; v < a.N; ++v) {
-        const float th_next = a.theta[v + 1], bn_next = a.beta[v + 2];
-        const bool chk = use_tol && ((v + 1) % a.check_every) == 0;
+    int v = 0;  // iterations of this launch (= lc of every active column when there is no queue)
+    while (true) {
+        // schedule, prefetched one iteration ahead (tables hold N + 2 entries): per column with a
+        // queue (columns restart at different times), uniform scalar loads without one
+        float th_next, bn_next;
+        if constexpr (QUEUE) {
+            const int lp = active ? lc : 0;
+            th_next = a.theta[lp + 1];
+            bn_next = a.beta[lp + 2];
+        } else {
+            th_next = a.theta[v + 1];
+            bn_next = a.beta[v + 2];
+        }
+        ++v;
+        const bool chk = use_tol && active && ((lc + 1) % a.check_every) == 0;
         const float omt = 1.0f - th;
         // ---- GEMM 1 + epilogue: zhat = -ML w - g_P (8b), z = (1-th) z + th zhat (8c) -----
         {
@@ -195,7 +224,7 @@ __global__ __launch_bounds__(64 * T) void gpad_panel_kernel(SolveArgs<float> a) 
                 const float zn = __builtin_fmaf(omt, z[r], th * zh[r]);
                 if (active) z[r] = zn;
             }
-            Zh4w[slot] = make_float4(zh[0], zh[1], zh[2], zh[3]);
+            Zh4[slot] = make_float4(zh[0], zh[1], zh[2], zh[3]);
         }
         __syncthreads();
         // ---- GEMM 2 + epilogue: y+ = [w + G_L zhat + p_D]+ (8d), next w (8a) --------------
@@ -225,70 +254,125 @@ __global__ __launch_bounds__(64 * T) void gpad_panel_kernel(SolveArgs<float> a) 
                 }
                 if (active) y[r] = yp;
             }
-            if (active) Wl4w[slot] = make_float4(wn[0], wn[1], wn[2], wn[3]);
+            if (active) Wl4[slot] = make_float4(wn[0], wn[1], wn[2], wn[3]);
         }
+        if (active) ++lc;
         th = th_next;
         bn = bn_next;
-        if (active) my_it = v + 1;
-        if (!chk) {
+        // Events (a test, or a column at N).  Without a queue every active column has done v
+        // iterations, so events are uniform and a plain barrier suffices; with a queue the one
+        // barrier per iteration doubles as the event probe (__syncthreads_or: LDS + barriers).
+        bool any_chk;
+        if constexpr (QUEUE) {
+            const bool at_n = active && lc >= N;
+            if (!__syncthreads_or((chk || at_n) ? 1 : 0)) continue;
+            any_chk = __syncthreads_or(chk ? 1 : 0);
+        } else {
             __syncthreads();
-            continue;
+            any_chk = use_tol && (v % a.check_every) == 0;
+            if (!any_chk && v < N) continue;
         }
-        // ---- Algorithm 1 test, per instance: lane groups j, then row tiles through LDS ------
-#pragma unroll
-        for (int o = 16; o < 64; o <<= 1) {
-            violz = fmaxf(violz, __shfl_xor(violz, o, 64));
-            violh = fmaxf(violh, __shfl_xor(violh, o, 64));
-            wmin = fminf(wmin, __shfl_xor(wmin, o, 64));
-            gap += __shfl_xor(gap, o, 64);
-        }
-        if (j == 0) {
-            slots[t].violz[c] = violz;
-            slots[t].violh[c] = violh;
-            slots[t].wmin[c] = wmin;
-            slots[t].gap[c] = gap;
-        }
-        __syncthreads();
-        double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gq = 0.0;
-#pragma unroll
-        for (int s = 0; s < T; ++s) {
-            vz = fmax(vz, (double)slots[s].violz[c]);
-            vh = fmax(vh, (double)slots[s].violh[c]);
-            wm = fmin(wm, (double)slots[s].wmin[c]);
-            gq += slots[s].gap[c];
-        }
+
+        // ---- Algorithm 1 test, per column: lane groups j, then row tiles through LDS ------
         int code = 0;
-        if (vz * a.L <= a.tol) code = 1;
-        else if ((vh * a.L <= a.tol) && (wm >= 0.0) && (gq * a.L <= a.tol)) code = 2;
-        if (active && code) {
-            my_code = code;
-            if (code == 2) {  // zhat certified: it becomes z*
+        if (any_chk) {
 #pragma unroll
-                for (int r = 0; r < 4; ++r) z[r] = zh[r];
+            for (int o = 16; o < 64; o <<= 1) {
+                violz = fmaxf(violz, __shfl_xor(violz, o, 64));
+                violh = fmaxf(violh, __shfl_xor(violh, o, 64));
+                wmin = fminf(wmin, __shfl_xor(wmin, o, 64));
+                gap += __shfl_xor(gap, o, 64);
+            }
+            if (j == 0) {
+                slots[t].violz[c] = violz;
+                slots[t].violh[c] = violh;
+                slots[t].wmin[c] = wmin;
+                slots[t].gap[c] = gap;
+            }
+            __syncthreads();
+            if (chk) {
+                double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gq = 0.0;
+#pragma unroll
+                for (int s2 = 0; s2 < T; ++s2) {
+                    vz = fmax(vz, (double)slots[s2].violz[c]);
+                    vh = fmax(vh, (double)slots[s2].violh[c]);
+                    wm = fmin(wm, (double)slots[s2].wmin[c]);
+                    gq += slots[s2].gap[c];
+                }
+                if (vz * a.L <= a.tol) code = 1;
+                else if ((vh * a.L <= a.tol) && (wm >= 0.0) && (gq * a.L <= a.tol)) code = 2;
+            }
+        }
+        // ---- finished columns: results out -------------------------------------------------
+        const bool fin = active && (code != 0 || lc >= N);
+        if (fin) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 * t + 4 * r + j;
+                if (i < n) a.z[(size_t)inst * n + i] = code == 2 ? zh[r] : z[r];  // (B) certifies zhat
+                if (i < m) a.y[(size_t)inst * m + i] = y[r];
+            }
+            if (t == 0 && j == 0) {
+                a.iters[inst] = lc;
+                a.conv[inst] = code;
             }
             active = false;
         }
-        // leave when no instance of the panel is still iterating (uniform: same LDS reads);
-        // the barrier also orders the slot reads above before the next check's writes
+        if constexpr (!QUEUE) {
+            if (v >= N || !__syncthreads_or(active ? 1 : 0)) break;
+            continue;
+        }
+        // ---- refill idle columns from the queue (one lane per column draws) -----------------
+        if (t == 0 && j == 0) {  // -2: did not draw, -1: drew from an empty queue
+            int nx = -2;
+            if (!active && !queue_dry) {
+                const int k = atomicAdd(a.queue, 1);
+                nx = first + k < a.batch ? first + k : -1;
+            }
+            next_inst[c] = nx;
+        }
+        __syncthreads();
+        if (t == 0 && lane == 0) {  // all draws of this round are done: record exhaustion
+            bool dry = queue_dry;
+            for (int q = 0; q < 16; ++q) dry = dry || next_inst[q] == -1;
+            queue_dry = dry;  // read only after the next barrier
+        }
+        const int nx = next_inst[c];
+        const bool fresh = !active && nx >= 0;
+        if (fresh) {
+            inst = nx;
+            active = true;
+            lc = 0;
+            load_instance(true);
+        }
+        if (__syncthreads_or(fresh ? 1 : 0)) {
+            if (use_tol) seed_u(fresh);
+            if (fresh) {
+                th = a.theta[0];
+                bn = a.beta[1];
+            }
+        }
         if (!__syncthreads_or(active ? 1 : 0)) break;
-    }
-    // ---- write back ---------------------------------------------------------------------
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int i = 16 * t + 4 * r + j;
-        if (real && i < n) a.z[(size_t)inst * n + i] = z[r];
-        if (real && i < m) a.y[(size_t)inst * m + i] = y[r];
-    }
-    if (t == 0 && j == 0 && real) {
-        a.iters[inst] = my_it;
-        a.conv[inst] = my_code;
     }
 }
 
 template <int T>
 static hipError_t launch_panel_t(const SolveArgs<float>& a, hipStream_t s) {
-    const int groups = (a.batch + 15) / 16;
-    hipLaunchKernelGGL(gpad_panel_kernel<T>, dim3(groups), dim3(64 * T), 0, s, a);
+    // Persistent grid = as many panels as can be resident (32 waves per CU): per-iteration
+    // throughput is highest with two 13-wave panels per CU, and with only ~2 instances per column
+    // a smaller grid loses more to the end-of-queue tail than it gains from refills (measured on
+    // C4).  Larger batches keep every resident column busy through the queue.
+    const int panels = (a.batch + 15) / 16;
+    const int resident = a.num_cus * (32 / T > 0 ? 32 / T : 1);
+    int grid = panels < resident ? panels : resident;
+    if (const char* cap = std::getenv("GPAD_PANEL_MAX_GRID")) {  // test knob: force refills
+        const int c = std::atoi(cap);
+        if (c > 0 && c < grid) grid = c;
+    }
+    if (grid < panels)
+        hipLaunchKernelGGL((gpad_panel_kernel<T, true>), dim3(grid), dim3(64 * T), 0, s, a);
+    else
+        hipLaunchKernelGGL((gpad_panel_kernel<T, false>), dim3(grid), dim3(64 * T), 0, s, a);
     return hipGetLastError();
 }
 

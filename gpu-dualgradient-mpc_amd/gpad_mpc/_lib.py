@@ -51,11 +51,13 @@ class GpadError(RuntimeError):
 _LIB = None
 
 
-def load(path: str = LIB_PATH) -> C.CDLL:
-    """Load libgpad.so once.  Raises (loudly) when the HIP library is absent."""
+def load(path: str | None = None) -> C.CDLL:
+    """Load libgpad.so once.  Raises (loudly) when the HIP library is absent.
+    ``GPAD_LIB`` may point at another build of the same library (A/B benchmarking)."""
     global _LIB
     if _LIB is not None:
         return _LIB
+    path = path or os.environ.get("GPAD_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise ImportError(f"libgpad.so not built at {path}: run `make -C gpu-dualgradient-mpc_amd` "
                           "(or __graft_entry__.build()); there is no CPU fallback")

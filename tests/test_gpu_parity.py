@@ -159,8 +159,31 @@ def test_panel_two_wave_panels_large_batch(gpu, oracle, nm):
     ML, G, L = base.ML.astype(np.float32), base.G.astype(np.float32), np.float32(base.L)
     z, y, st, iters = run_gpu(ML, M, G, g, L, 2000, tol=1e-4, kernel="panel")
     assert st["kernel"] == "panel"
-    for b in list(range(0, B, 997)) + [B - 1]:
+    for b in list(range(0, B, 257)) + [B - 1]:
         zo, yo, it, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), ML, M[b], G, g[b], 2000, L, 1e-4)
+        assert iters[b] == it, b
+        assert_bitexact(z[b], zo, f"instance {b} z")
+        assert_bitexact(y[b], yo, f"instance {b} y")
+
+
+@pytest.mark.parametrize("grid", [1, 3])
+@pytest.mark.parametrize("tol,N", [(1e-4, 3000), (0.0, 57)])
+def test_panel_queue_refill_bitexact(gpu, oracle, monkeypatch, grid, tol, N):
+    """Continuous batching: with the persistent grid capped, columns finish at different times
+    and pull new instances; every instance must still match its own oracle solve exactly."""
+    from gpad_mpc import problems
+    monkeypatch.setenv("GPAD_PANEL_MAX_GRID", str(grid))
+    B, n, m = 150, 40, 72
+    qp = problems.synthetic_qp(n, m, batch=B, seed=8)
+    ML, G = qp.ML.astype(np.float32), qp.G.astype(np.float32)
+    M, g = qp.M.astype(np.float32), qp.g.astype(np.float32)
+    L = np.float32(qp.L)
+    rng = np.random.default_rng(1)
+    z0 = (0.1 * rng.normal(size=(B, n))).astype(np.float32)  # warm starts: exercises the u seed
+    z, y, st, iters = run_gpu(ML, M, G, g, L, N, tol=tol, kernel="panel", z0=z0)
+    assert st["kernel"] == "panel"
+    for b in range(B):
+        zo, yo, it, _ = oracle.solve_f32(z0[b], np.zeros(m), ML, M[b], G, g[b], N, L, tol)
         assert iters[b] == it, b
         assert_bitexact(z[b], zo, f"instance {b} z")
         assert_bitexact(y[b], yo, f"instance {b} y")
