@@ -83,6 +83,8 @@ void host_schedule(int N, int kind, double* theta, double* beta) {
 
 }  // namespace
 
+int gpad::set_last_error(int code, const std::string& msg) { return fail(code, msg); }
+
 struct gpad_handle_s {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -96,9 +98,16 @@ struct gpad_handle_s {
     DevBuf theta, beta;
     int sched_len = 0, sched_kind = -1, sched_dtype = -1;
     DevBuf work, counters;
-    std::vector<int> h_iters, h_conv;
+    std::vector<int> h_counts;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    int last_kernel = 0, last_batch = 0;
+    int last_kernel = 0, last_batch = 0, last_steps = 1;
+    // plant binding (gpad_setup_plant): affine state maps and dynamics, device copies
+    int nx = 0, nu = 0;
+    bool plant_ready = false, plant_dyn = false;
+    DevBuf plant;                       // [PM n*nx | M0 n | Pg m*nx | g0 m | A nx*nx | B nx*nu]
+    bool has_M0 = false, has_g0 = false;
+    int plant_n = 0, plant_m = 0, plant_dtype = -1;
+    DevBuf state;                       // per-state workspaces (M(x), g(x), x ping-pong, ...)
     int num_cus = 256;
     bool timed = false;
 };
@@ -156,6 +165,8 @@ int gpad_destroy(gpad_handle_t h) {
     h->beta.release();
     h->work.release();
     h->counters.release();
+    h->plant.release();
+    h->state.release();
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     delete h;
@@ -311,23 +322,26 @@ static int ensure_schedule(gpad_handle_t h, int N, const void* theta_in, const v
     return GPAD_OK;
 }
 
+// Counters are laid out [steps][iters[batch] | conv[batch]] (+ the queue word after them).
 static int collect_stats(gpad_handle_t h, gpad_stats_t* st) {
     const int batch = h->last_batch;
-    h->h_iters.resize(batch);
-    h->h_conv.resize(batch);
-    int* dI = (int*)h->counters.p;
-    int* dC = dI + batch;
-    HIP_TRY(hipMemcpyAsync(h->h_iters.data(), dI, sizeof(int) * batch, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(hipMemcpyAsync(h->h_conv.data(), dC, sizeof(int) * batch, hipMemcpyDeviceToHost, h->stream));
+    const size_t entries = (size_t)batch * h->last_steps;
+    h->h_counts.resize(2 * entries);
+    HIP_TRY(hipMemcpyAsync(h->h_counts.data(), h->counters.p, sizeof(int) * 2 * entries,
+                           hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     st->iterations = 0;
     st->converged = 0;
     st->total_iterations = 0;
-    for (int b = 0; b < batch; ++b) {
-        st->iterations = std::max(st->iterations, h->h_iters[b]);
-        st->converged += h->h_conv[b] != 0;
-        st->total_iterations += h->h_iters[b];
-        if (st->iters) st->iters[b] = h->h_iters[b];
+    for (int t = 0; t < h->last_steps; ++t) {
+        const int* it = h->h_counts.data() + (size_t)2 * batch * t;
+        const int* cv = it + batch;
+        for (int b = 0; b < batch; ++b) {
+            st->iterations = std::max(st->iterations, it[b]);
+            st->converged += cv[b] != 0;
+            st->total_iterations += it[b];
+            if (st->iters) st->iters[(size_t)t * batch + b] = it[b];
+        }
     }
     st->kernel = h->last_kernel;
     float ms = 0.0f;
@@ -345,32 +359,13 @@ int gpad_last_stats(gpad_handle_t h, gpad_stats_t* st) {
 
 }  // extern "C"
 
+// Enqueue one fused solve on device buffers (no staging, no sync).  Counters: iters/conv
+// [batch] each, queue = 4 ints (zeroed here).  *kernel_out = the family that ran.
 template <typename T>
-static int run_typed(gpad_handle_t h, T* z, T* y, const T* M, const T* g, int N, double tol,
-                     const void* theta_in, const void* beta_in, bool scaled_vec, gpad_stats_t* st) {
+static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg, int N, double tol,
+                        bool scaled_vec, int* iters, int* conv, int* queue, int* kernel_out) {
     const gpad_dims_t& d = h->dims;
     const int n = d.n, m = d.m, batch = d.batch;
-    int rc = ensure_schedule(h, N, theta_in, beta_in);
-    if (rc) return rc;
-    // [iters | conv | queue word (padded to 16 B)]
-    if ((rc = h->counters.ensure(sizeof(int) * (2 * (size_t)batch + 4)))) return rc;
-    T *dz = z, *dy = y;
-    const T *dM = M, *dg = g;
-    const size_t zb = sizeof(T) * (size_t)batch * n, yb = sizeof(T) * (size_t)batch * m;
-    if (d.memory == GPAD_MEM_HOST) {
-        if ((rc = h->work.ensure(2 * zb + 2 * yb))) return rc;
-        char* base = (char*)h->work.p;
-        dz = (T*)base;
-        dy = (T*)(base + zb);
-        T* wM = (T*)(base + zb + yb);
-        T* wg = (T*)(base + 2 * zb + yb);
-        HIP_TRY(hipMemcpyAsync(dz, z, zb, hipMemcpyHostToDevice, h->stream));
-        HIP_TRY(hipMemcpyAsync(dy, y, yb, hipMemcpyHostToDevice, h->stream));
-        HIP_TRY(hipMemcpyAsync(wM, M, zb, hipMemcpyHostToDevice, h->stream));
-        HIP_TRY(hipMemcpyAsync(wg, g, yb, hipMemcpyHostToDevice, h->stream));
-        dM = wM;
-        dg = wg;
-    }
     gpad::SolveArgs<T> a{};
     a.MGt = (const T*)h->MGt.p;
     a.GLt = (const T*)h->GLt.p;
@@ -396,19 +391,19 @@ static int run_typed(gpad_handle_t h, T* z, T* y, const T* M, const T* g, int N,
     a.L = h->L;
     a.theta = (const T*)h->theta.p;
     a.beta = (const T*)h->beta.p;
-    a.iters = (int*)h->counters.p;
-    a.conv = a.iters + batch;
-    a.queue = a.conv + batch;
+    a.iters = iters;
+    a.conv = conv;
+    a.queue = queue;
     a.num_cus = h->num_cus;
     int kernel = d.kernel;
     hipError_t e = hipSuccess;
     bool ok = false;
     HIP_TRY(hipMemsetAsync(a.queue, 0, 4 * sizeof(int), h->stream));
-    HIP_TRY(hipEventRecord(h->ev0, h->stream));
     if (N == 0) {  // nothing to iterate: outputs are the inputs, zero counts
-        HIP_TRY(hipMemsetAsync(a.iters, 0, sizeof(int) * 2 * (size_t)batch, h->stream));
-        kernel = d.kernel == GPAD_KERNEL_AUTO ? GPAD_KERNEL_STREAM : d.kernel;
-        goto launched;
+        HIP_TRY(hipMemsetAsync(a.iters, 0, sizeof(int) * (size_t)batch, h->stream));
+        HIP_TRY(hipMemsetAsync(a.conv, 0, sizeof(int) * (size_t)batch, h->stream));
+        *kernel_out = d.kernel == GPAD_KERNEL_AUTO ? GPAD_KERNEL_STREAM : d.kernel;
+        return GPAD_OK;
     }
     if constexpr (sizeof(T) == sizeof(float)) {
         if (kernel == GPAD_KERNEL_PANEL || (kernel == GPAD_KERNEL_AUTO && d.shared && batch >= 64)) {
@@ -437,11 +432,47 @@ static int run_typed(gpad_handle_t h, T* z, T* y, const T* M, const T* g, int N,
                         std::string("stream kernel: ") + hipGetErrorString(e) +
                             " (n+m beyond the LDS budget?)");
     }
-launched:
+    *kernel_out = kernel;
+    return GPAD_OK;
+}
+
+template <typename T>
+static int run_typed(gpad_handle_t h, T* z, T* y, const T* M, const T* g, int N, double tol,
+                     const void* theta_in, const void* beta_in, bool scaled_vec, gpad_stats_t* st) {
+    const gpad_dims_t& d = h->dims;
+    const int n = d.n, m = d.m, batch = d.batch;
+    int rc = ensure_schedule(h, N, theta_in, beta_in);
+    if (rc) return rc;
+    // [iters | conv | queue word (padded to 16 B)]
+    if ((rc = h->counters.ensure(sizeof(int) * (2 * (size_t)batch + 4)))) return rc;
+    T *dz = z, *dy = y;
+    const T *dM = M, *dg = g;
+    const size_t zb = sizeof(T) * (size_t)batch * n, yb = sizeof(T) * (size_t)batch * m;
+    if (d.memory == GPAD_MEM_HOST) {
+        if ((rc = h->work.ensure(2 * zb + 2 * yb))) return rc;
+        char* base = (char*)h->work.p;
+        dz = (T*)base;
+        dy = (T*)(base + zb);
+        T* wM = (T*)(base + zb + yb);
+        T* wg = (T*)(base + 2 * zb + yb);
+        HIP_TRY(hipMemcpyAsync(dz, z, zb, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipMemcpyAsync(dy, y, yb, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipMemcpyAsync(wM, M, zb, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipMemcpyAsync(wg, g, yb, hipMemcpyHostToDevice, h->stream));
+        dM = wM;
+        dg = wg;
+    }
+    int* iters = (int*)h->counters.p;
+    int kernel = 0;
+    HIP_TRY(hipEventRecord(h->ev0, h->stream));
+    if ((rc = launch_solve<T>(h, dz, dy, dM, dg, N, tol, scaled_vec, iters, iters + batch,
+                              iters + 2 * batch, &kernel)))
+        return rc;
     HIP_TRY(hipEventRecord(h->ev1, h->stream));
     h->timed = true;
     h->last_kernel = kernel;
     h->last_batch = batch;
+    h->last_steps = 1;
     if (d.memory == GPAD_MEM_HOST) {
         HIP_TRY(hipMemcpyAsync(z, dz, zb, hipMemcpyDeviceToHost, h->stream));
         HIP_TRY(hipMemcpyAsync(y, dy, yb, hipMemcpyDeviceToHost, h->stream));
@@ -504,6 +535,177 @@ int gpad_solve(void* z0, void* y0, const void* ML, const void* M, const void* G,
     rc = gpad_run(cache.h, z0, y0, M, g, N, tol, st ? st : &local);
     if (rc) return rc;
     return gpad_sync(cache.h);
+}
+
+// ---- per-state QP data and closed-loop MPC (gpad.m:79-95) --------
+}  // extern "C"
+
+namespace {
+struct PlantOffsets {
+    size_t PM, M0, Pg, g0, A, B, total;
+};
+PlantOffsets plant_offsets(int n, int m, int nx, int nu) {
+    PlantOffsets o{};
+    o.PM = 0;
+    o.M0 = o.PM + (size_t)n * nx;
+    o.Pg = o.M0 + (size_t)n;
+    o.g0 = o.Pg + (size_t)m * nx;
+    o.A = o.g0 + (size_t)m;
+    o.B = o.A + (size_t)nx * nx;
+    o.total = o.B + (size_t)nx * nu;
+    return o;
+}
+}  // namespace
+
+extern "C" int gpad_setup_plant(gpad_handle_t h, int nx, int nu, const void* PM, const void* M0,
+                                const void* Pg, const void* g0, const void* A, const void* B) {
+    if (!h) return fail(GPAD_ERR_INVALID, "gpad_setup_plant: null handle");
+    if (!h->ready) return fail(GPAD_ERR_NOT_SETUP, "gpad_setup_plant: call gpad_setup first");
+    if (nx <= 0 || nu < 0 || !PM || !Pg) return fail(GPAD_ERR_INVALID, "gpad_setup_plant: bad arguments");
+    if ((A == nullptr) != (B == nullptr) || (A && nu == 0))
+        return fail(GPAD_ERR_INVALID, "gpad_setup_plant: give A and B together (nu >= 1)");
+    if (nu > h->dims.n) return fail(GPAD_ERR_INVALID, "gpad_setup_plant: nu > n");
+    HIP_TRY(hipSetDevice(h->device));
+    const int n = h->dims.n, m = h->dims.m;
+    const size_t es = esize(h->dims.dtype);
+    const PlantOffsets o = plant_offsets(n, m, nx, nu);
+    int rc;
+    if ((rc = h->plant.ensure(es * o.total))) return rc;
+    char* base = (char*)h->plant.p;
+    const hipMemcpyKind kind = h->dims.memory == GPAD_MEM_HOST ? hipMemcpyHostToDevice
+                                                                : hipMemcpyDeviceToDevice;
+    auto put = [&](size_t off, const void* src, size_t elems) -> int {
+        if (!src || elems == 0) return GPAD_OK;
+        HIP_TRY(hipMemcpyAsync(base + es * off, src, es * elems, kind, h->stream));
+        return GPAD_OK;
+    };
+    if ((rc = put(o.PM, PM, (size_t)n * nx)) || (rc = put(o.M0, M0, n)) ||
+        (rc = put(o.Pg, Pg, (size_t)m * nx)) || (rc = put(o.g0, g0, m)) ||
+        (rc = put(o.A, A, (size_t)nx * nx)) || (rc = put(o.B, B, (size_t)nx * nu)))
+        return rc;
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    h->nx = nx;
+    h->nu = nu;
+    h->has_M0 = M0 != nullptr;
+    h->has_g0 = g0 != nullptr;
+    h->plant_dyn = A != nullptr;
+    h->plant_ready = true;
+    h->plant_n = n;
+    h->plant_m = m;
+    h->plant_dtype = h->dims.dtype;
+    return GPAD_OK;
+}
+
+template <typename T>
+static int state_typed(gpad_handle_t h, T* x, T* z, T* y, int steps, int N, double tol, int warm,
+                       T* xs, T* us, gpad_stats_t* st) {
+    // steps == 0: one solve at x (gpad_run_state); steps >= 1: closed loop (gpad_closed_loop)
+    const gpad_dims_t& d = h->dims;
+    const int n = d.n, m = d.m, batch = d.batch, nx = h->nx, nu = h->nu;
+    const bool loop = steps > 0;
+    const int nsolve = loop ? steps : 1;
+    int rc = ensure_schedule(h, N, nullptr, nullptr);
+    if (rc) return rc;
+    if ((rc = h->counters.ensure(sizeof(int) * (2 * (size_t)batch * nsolve + 4)))) return rc;
+    const bool host = d.memory == GPAD_MEM_HOST;
+    const size_t zn = (size_t)batch * n, yn = (size_t)batch * m, xn = (size_t)batch * nx;
+    const size_t xsn = loop && xs ? (size_t)steps * xn : 0, usn = loop && us ? (size_t)steps * batch * nu : 0;
+    // workspace: M(x) | g(x) | x ping | x pong | (host) z | y | xs | us
+    size_t elems = zn + yn + 2 * xn;
+    if (host) elems += zn + yn + xsn + usn;
+    if ((rc = h->state.ensure(sizeof(T) * elems))) return rc;
+    T* Mx = (T*)h->state.p;
+    T* gx = Mx + zn;
+    T* xa = gx + yn;
+    T* xb = xa + xn;
+    T *dz = z, *dy = y, *dxs = xs, *dus = us;
+    if (host) {
+        dz = xb + xn;
+        dy = dz + zn;
+        dxs = xsn ? dy + yn : nullptr;
+        dus = usn ? dy + yn + xsn : nullptr;
+    }
+    const hipMemcpyKind in_kind = host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+    const hipMemcpyKind out_kind = host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    HIP_TRY(hipMemcpyAsync(xa, x, sizeof(T) * xn, in_kind, h->stream));
+    if (host && (!loop || warm)) {
+        HIP_TRY(hipMemcpyAsync(dz, z, sizeof(T) * zn, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipMemcpyAsync(dy, y, sizeof(T) * yn, hipMemcpyHostToDevice, h->stream));
+    }
+    const PlantOffsets o = plant_offsets(n, m, nx, nu);
+    const T* P = (const T*)h->plant.p;
+    int* counters = (int*)h->counters.p;
+    int* queue = counters + 2 * (size_t)batch * nsolve;
+    int kernel = 0;
+    HIP_TRY(hipEventRecord(h->ev0, h->stream));
+    T* xc = xa;
+    T* xnext = xb;
+    for (int t = 0; t < nsolve; ++t) {
+        HIP_TRY(gpad::launch_affine2<T>(P + o.PM, h->has_M0 ? P + o.M0 : nullptr, n, Mx, P + o.Pg,
+                                        h->has_g0 ? P + o.g0 : nullptr, m, gx, xc, nx, batch, h->stream));
+        if (loop && !warm) {  // acceldualgrad.m:16-17: every MPC step starts from z = y = 0
+            HIP_TRY(hipMemsetAsync(dz, 0, sizeof(T) * zn, h->stream));
+            HIP_TRY(hipMemsetAsync(dy, 0, sizeof(T) * yn, h->stream));
+        }
+        int* it = counters + 2 * (size_t)batch * t;
+        if ((rc = launch_solve<T>(h, dz, dy, Mx, gx, N, tol, false, it, it + batch, queue, &kernel)))
+            return rc;
+        if (loop) {  // gpad.m:91-94: u = z*(1:nu); x <- A x + B u
+            HIP_TRY(gpad::launch_plant_step<T>(P + o.A, P + o.B, xc, dz, n, xnext, nx, nu, batch,
+                                               dxs ? dxs + (size_t)t * xn : nullptr,
+                                               dus ? dus + (size_t)t * batch * nu : nullptr, h->stream));
+            std::swap(xc, xnext);
+        }
+    }
+    HIP_TRY(hipEventRecord(h->ev1, h->stream));
+    h->timed = true;
+    h->last_kernel = kernel;
+    h->last_batch = batch;
+    h->last_steps = nsolve;
+    if (loop) HIP_TRY(hipMemcpyAsync(x, xc, sizeof(T) * xn, out_kind, h->stream));
+    if (host) {
+        HIP_TRY(hipMemcpyAsync(z, dz, sizeof(T) * zn, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipMemcpyAsync(y, dy, sizeof(T) * yn, hipMemcpyDeviceToHost, h->stream));
+        if (xsn) HIP_TRY(hipMemcpyAsync(xs, dxs, sizeof(T) * xsn, hipMemcpyDeviceToHost, h->stream));
+        if (usn) HIP_TRY(hipMemcpyAsync(us, dus, sizeof(T) * usn, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+    }
+    if (st) return collect_stats(h, st);
+    return GPAD_OK;
+}
+
+static int state_impl(gpad_handle_t h, void* x, void* z, void* y, int steps, int N, double tol, int warm,
+                      void* xs, void* us, gpad_stats_t* st, const char* where) {
+    if (!h) return fail(GPAD_ERR_INVALID, std::string(where) + ": null handle");
+    if (!h->ready) return fail(GPAD_ERR_NOT_SETUP, std::string(where) + ": call gpad_setup first");
+    if (!h->plant_ready || h->plant_n != h->dims.n || h->plant_m != h->dims.m ||
+        h->plant_dtype != h->dims.dtype)
+        return fail(GPAD_ERR_NOT_SETUP, std::string(where) + ": call gpad_setup_plant after gpad_setup");
+    if (steps > 0 && !h->plant_dyn)
+        return fail(GPAD_ERR_NOT_SETUP, std::string(where) + ": plant bound without A, B");
+    if (!x || !z || !y) return fail(GPAD_ERR_INVALID, std::string(where) + ": null vector");
+    if (N < 0 || steps < 0) return fail(GPAD_ERR_INVALID, std::string(where) + ": N, steps must be >= 0");
+    if (!(tol <= 0.0) && !std::isfinite(tol)) return fail(GPAD_ERR_INVALID, std::string(where) + ": bad tol");
+    HIP_TRY(hipSetDevice(h->device));
+    if (h->dims.dtype == GPAD_DTYPE_F64)
+        return state_typed<double>(h, (double*)x, (double*)z, (double*)y, steps, N, tol, warm, (double*)xs,
+                                   (double*)us, st);
+    return state_typed<float>(h, (float*)x, (float*)z, (float*)y, steps, N, tol, warm, (float*)xs,
+                              (float*)us, st);
+}
+
+extern "C" {
+
+int gpad_run_state(gpad_handle_t h, const void* x, void* z0, void* y0, int N, double tol,
+                   gpad_stats_t* st) {
+    return state_impl(h, const_cast<void*>(x), z0, y0, 0, N, tol, 1, nullptr, nullptr, st,
+                      "gpad_run_state");
+}
+
+int gpad_closed_loop(gpad_handle_t h, void* x, void* z, void* y, int steps, int N, double tol, int warm,
+                     void* xs, void* us, gpad_stats_t* st) {
+    if (steps == 0) return GPAD_OK;
+    return state_impl(h, x, z, y, steps, N, tol, warm, xs, us, st, "gpad_closed_loop");
 }
 
 // ---- per-step entry points ---------------------------------------------------------------

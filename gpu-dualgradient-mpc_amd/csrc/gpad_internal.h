@@ -5,8 +5,12 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <string>
 
 namespace gpad {
+
+// gpad_last_error() detail for the calling thread; returns code (gpad_host.cpp)
+int set_last_error(int code, const std::string& msg);
 
 // Arguments of a fused solve launch (all kernel families).  Every instance b of the batch
 // reads its matrices at MGt + b*strideA / GLt + b*strideB (stride 0 = shared).
@@ -49,6 +53,15 @@ hipError_t launch_pack_panel(const float* ML, const float* G, int n, int m, int 
 template <typename T>
 hipError_t launch_pack_kmajor(const T* in, T* out, int rows, int cols, int ld, double scale,
                               int batch, long long in_stride, long long out_stride, hipStream_t s);
+
+// gpad_plant.hip: out1 = c1 + P1 x (rows1), out2 = c2 + P2 x (rows2) per instance; c may be null
+template <typename T>
+hipError_t launch_affine2(const T* P1, const T* c1, int rows1, T* out1, const T* P2, const T* c2,
+                          int rows2, T* out2, const T* x, int nx, int batch, hipStream_t s);
+// xn = A x + B z[:, 0:nu]; xs/us (nullable) receive x and z[:, 0:nu]
+template <typename T>
+hipError_t launch_plant_step(const T* A, const T* B, const T* x, const T* z, long long ldz, T* xn, int nx,
+                             int nu, int batch, T* xs, T* us, hipStream_t s);
 
 hipError_t launch_step1(const float* y, const float* ym1, float* w, float beta, int m, hipStream_t s);
 hipError_t launch_step2(const float* MGneg, const float* w, const float* gP, float* zhat, int n,

@@ -1,0 +1,115 @@
+// gpad_plant.hip -- per-state QP data and plant update on the device.
+//
+// The reference rebuilds the state-dependent QP data on the host for every MPC step
+// (gpad.m:80-85: f = x0'F, b_i(x0)) and then runs GPAD (acceldualgrad.m:20-23 precompute,
+// :38-64 loop).  For an LTI plant both vectors are affine in the state x:
+//     M(x) = M0 + PM x        (n;  PM = H^-1 F', so M = H^-1 f'   -- acceldualgrad.m:21)
+//     g(x) = g0 + Pg x        (m;  b_i(x), gpad.m:85)
+// and the receding-horizon update is x+ = A x + B u with u = z*[0:nu] (gpad.m:91-93).
+// These kernels evaluate both on the device so a batch of states (or a whole closed-loop
+// simulation) never leaves HBM.
+//
+// Arithmetic (restated by oracle/gpad_oracle.c orc_affine / orc_plant_step, bit-exact):
+//   affine:  acc = c0[i] (0 if absent); for k < nx: acc = fma(P[i][k], x[k], acc)
+//   plant :  acc = 0;  for k < nx: acc = fma(A[i][k], x[k], acc);
+//                      for j < nu: acc = fma(B[i][j], u[j], acc)
+// The work is O(batch (n + m) nx) per step -- a few hundred flops per instance against the
+// O(iterations n m) of the solve -- so one thread per output row with the short chain in
+// registers is the right shape; P rows are re-read from L2 by every instance.
+#include "gpad_internal.h"
+
+namespace gpad {
+
+// out1[b][i] = affine row i (i < rows1) ; out2[b][j] = affine row j (j < rows2)
+template <typename T>
+__global__ __launch_bounds__(256) void affine2_kernel(const T* __restrict__ P1, const T* __restrict__ c1,
+                                                      int rows1, T* __restrict__ out1,
+                                                      const T* __restrict__ P2, const T* __restrict__ c2,
+                                                      int rows2, T* __restrict__ out2,
+                                                      const T* __restrict__ x, int nx, int batch) {
+    const int per = rows1 + rows2;
+    const long long total = (long long)batch * per;
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        const int b = (int)(t / per);
+        int i = (int)(t - (long long)b * per);
+        const T* P = P1;
+        const T* c = c1;
+        T* out = out1 + (long long)b * rows1;
+        if (i >= rows1) {
+            i -= rows1;
+            P = P2;
+            c = c2;
+            out = out2 + (long long)b * rows2;
+        }
+        const T* xb = x + (long long)b * nx;
+        const T* Pi = P + (long long)i * nx;
+        T acc = c ? c[i] : T(0);
+        for (int k = 0; k < nx; ++k) acc = __builtin_fma(Pi[k], xb[k], acc);
+        out[i] = acc;
+    }
+}
+
+// xn[b] = A x[b] + B z[b][0:nu];  optional trajectories xs[b] = x[b], us[b] = z[b][0:nu]
+template <typename T>
+__global__ __launch_bounds__(256) void plant_step_kernel(const T* __restrict__ A, const T* __restrict__ B,
+                                                         const T* __restrict__ x, const T* __restrict__ z,
+                                                         long long ldz, T* __restrict__ xn, int nx, int nu,
+                                                         int batch, T* __restrict__ xs, T* __restrict__ us) {
+    const int per = nx > nu ? nx : nu;
+    const long long total = (long long)batch * per;
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        const int b = (int)(t / per);
+        const int i = (int)(t - (long long)b * per);
+        const T* xb = x + (long long)b * nx;
+        const T* ub = z + (long long)b * ldz;
+        if (i < nx) {
+            T acc = T(0);
+            const T* Ai = A + (long long)i * nx;
+            for (int k = 0; k < nx; ++k) acc = __builtin_fma(Ai[k], xb[k], acc);
+            const T* Bi = B + (long long)i * nu;
+            for (int j = 0; j < nu; ++j) acc = __builtin_fma(Bi[j], ub[j], acc);
+            xn[(long long)b * nx + i] = acc;
+            if (xs) xs[(long long)b * nx + i] = xb[i];
+        }
+        if (i < nu && us) us[(long long)b * nu + i] = ub[i];
+    }
+}
+
+static dim3 grid_for(long long total) {
+    long long blocks = (total + 255) / 256;
+    if (blocks > 65535) blocks = 65535;
+    if (blocks < 1) blocks = 1;
+    return dim3((unsigned)blocks);
+}
+
+template <typename T>
+hipError_t launch_affine2(const T* P1, const T* c1, int rows1, T* out1, const T* P2, const T* c2,
+                          int rows2, T* out2, const T* x, int nx, int batch, hipStream_t s) {
+    hipLaunchKernelGGL(affine2_kernel<T>, grid_for((long long)batch * (rows1 + rows2)), dim3(256), 0, s,
+                       P1, c1, rows1, out1, P2, c2, rows2, out2, x, nx, batch);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_plant_step(const T* A, const T* B, const T* x, const T* z, long long ldz, T* xn, int nx,
+                             int nu, int batch, T* xs, T* us, hipStream_t s) {
+    const int per = nx > nu ? nx : nu;
+    hipLaunchKernelGGL(plant_step_kernel<T>, grid_for((long long)batch * per), dim3(256), 0, s, A, B, x, z,
+                       ldz, xn, nx, nu, batch, xs, us);
+    return hipGetLastError();
+}
+
+template hipError_t launch_affine2<float>(const float*, const float*, int, float*, const float*,
+                                          const float*, int, float*, const float*, int, int, hipStream_t);
+template hipError_t launch_affine2<double>(const double*, const double*, int, double*, const double*,
+                                           const double*, int, double*, const double*, int, int,
+                                           hipStream_t);
+template hipError_t launch_plant_step<float>(const float*, const float*, const float*, const float*,
+                                             long long, float*, int, int, int, float*, float*, hipStream_t);
+template hipError_t launch_plant_step<double>(const double*, const double*, const double*, const double*,
+                                              long long, double*, int, int, int, double*, double*,
+                                              hipStream_t);
+
+}  // namespace gpad

@@ -27,7 +27,11 @@ EXPORTS = [
     "gpad_set_stream", "gpad_setup", "gpad_setup_scaled", "gpad_run", "gpad_run_scaled",
     "gpad_last_stats", "gpad_solve", "gpad_step1_extrapolate", "gpad_step2_primal",
     "gpad_step3_average", "gpad_step4_project", "gpad_schedule", "gpad_sync",
+    "gpad_setup_plant", "gpad_run_state", "gpad_closed_loop",
+    "gpad_datafile_read", "gpad_datafile_write", "gpad_datafile_free",
 ]
+
+FILE_ROWMAJOR, FILE_FLIPPED = 0, 1
 
 
 class Dims(C.Structure):
@@ -40,6 +44,14 @@ class Stats(C.Structure):
     _fields_ = [("iterations", C.c_int), ("converged", C.c_int),
                 ("total_iterations", C.c_longlong), ("kernel", C.c_int),
                 ("kernel_ms", C.c_double), ("iters", C.POINTER(C.c_int))]
+
+
+class DataFile(C.Structure):
+    """gpad_datafile_t (include/gpad.h): the reference's text data file (main.cu:29-67)."""
+    _fields_ = [("n_u", C.c_int), ("N", C.c_int), ("m", C.c_int), ("num_iterations", C.c_int),
+                ("L", C.c_float), ("M_G", C.POINTER(C.c_float)), ("g_P", C.POINTER(C.c_float)),
+                ("G_L", C.POINTER(C.c_float)), ("p_D", C.POINTER(C.c_float)),
+                ("theta", C.POINTER(C.c_float)), ("beta", C.POINTER(C.c_float))]
 
 
 class GpadError(RuntimeError):
@@ -84,10 +96,19 @@ def load(path: str | None = None) -> C.CDLL:
     L.gpad_step4_project.argtypes = [vp, vp, vp, vp, vp, vp, i, i]
     L.gpad_schedule.argtypes = [i, i, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     del f
+    L.gpad_setup_plant.argtypes = [vp, i, i, cvp, cvp, cvp, cvp, cvp, cvp]
+    L.gpad_run_state.argtypes = [vp, cvp, vp, vp, i, d, C.POINTER(Stats)]
+    L.gpad_closed_loop.argtypes = [vp, vp, vp, vp, i, i, d, i, vp, vp, C.POINTER(Stats)]
+    L.gpad_datafile_read.argtypes = [C.c_char_p, i, C.POINTER(DataFile)]
+    L.gpad_datafile_write.argtypes = [C.c_char_p, i, C.POINTER(DataFile)]
+    L.gpad_datafile_free.argtypes = [C.POINTER(DataFile)]
+    L.gpad_datafile_free.restype = None
     for name in ["gpad_create", "gpad_destroy", "gpad_set_stream", "gpad_sync", "gpad_setup",
                  "gpad_setup_scaled", "gpad_run", "gpad_run_scaled", "gpad_last_stats",
                  "gpad_solve", "gpad_step1_extrapolate", "gpad_step2_primal",
-                 "gpad_step3_average", "gpad_step4_project", "gpad_schedule"]:
+                 "gpad_step3_average", "gpad_step4_project", "gpad_schedule", "gpad_setup_plant",
+                 "gpad_run_state", "gpad_closed_loop", "gpad_datafile_read",
+                 "gpad_datafile_write"]:
         getattr(L, name).restype = i
     _LIB = L
     return L

@@ -134,6 +134,47 @@ def battery_scenarios(n_u: int, N: int, batch: int, seed: int = 0) -> QP:
               meta=dict(kind="battery_batch", n_u=n_u, N=N, X0=X0))
 
 
+@dataclass
+class Plant:
+    """Affine state dependence of the MPC QP and the plant model (gpad_setup_plant):
+    M(x) = M0 + PM x, g(x) = g0 + Pg x, x+ = A x + B u with u = z*[0:nu]."""
+
+    PM: np.ndarray  # n x nx
+    Pg: np.ndarray  # m x nx
+    A: np.ndarray   # nx x nx
+    B: np.ndarray   # nx x nu
+    M0: np.ndarray | None = None  # n
+    g0: np.ndarray | None = None  # m
+
+    @property
+    def nx(self) -> int:
+        return self.PM.shape[1]
+
+    @property
+    def nu(self) -> int:
+        return self.B.shape[1]
+
+
+def battery_plant(n_u: int = 4, N: int = 10, xmax: float = 0.5, xmin: float = -0.5,
+                  umax: float = 0.3, umin: float = -0.3):
+    """The battery-balancing MPC of gpad.m as (QP, Plant): the constant ML, G, L of the QP
+    and the affine maps of gpad.m:81-85 -- f = x0'F so M(x) = H^-1 F' x (M0 = 0);
+    b_i(x) = [xmax - M_ak x; -xmin + M_ak x; umax; -umin; 0; 0] -- plus x+ = A x + B u
+    (gpad.m:93).  Everything float64."""
+    mats = battery_matrices(n_u, N)
+    x0 = np.zeros(n_u)
+    f0, A_i, b0 = battery_constraints(mats, x0, n_u, N, xmax, xmin, umax, umin)
+    qp = gpad_precompute(mats["H"], f0, A_i, b0)
+    Hinv = np.linalg.inv(mats["H"])
+    PM = Hinv @ mats["F"].T
+    M_ak = mats["M_ak"]
+    z = np.zeros_like(M_ak)
+    Pg = np.vstack([-M_ak, M_ak, z, z, np.zeros((N, n_u)), np.zeros((N, n_u))])
+    plant = Plant(PM=PM, Pg=Pg, A=mats["A"], B=mats["B"], M0=None, g0=b0)
+    qp.meta = dict(kind="battery_plant", n_u=n_u, N=N)
+    return qp, plant
+
+
 def synthetic_qp(n: int, m: int, batch: int = 1, seed: int = 0, shared: bool = True) -> QP:
     """SURVEY.md §8d generic generator: M = R'R + I with R ~ N(0, 1/n); G ~ N(0, 1/n);
     b = G z_f + U(0.1, 1) with z_f ~ U(-0.5, 0.5) (strictly feasible); q ~ N(0, 1);

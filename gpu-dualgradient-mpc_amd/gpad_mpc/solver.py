@@ -138,6 +138,39 @@ class GpadSolver:
     def sync(self) -> None:
         check(self.lib.gpad_sync(self.h), "gpad_sync")
 
+    # ---- per-state QP data / closed loop (gpad.m:79-95; include/gpad.h gpad_setup_plant) ---
+    def setup_plant(self, PM, Pg, *, M0=None, g0=None, A=None, B=None) -> None:
+        """Bind M(x) = M0 + PM x, g(x) = g0 + Pg x and (optionally) x+ = A x + B u.
+        Same dtype / memory kind as the preceding ``setup``."""
+        nx = PM.shape[-1]
+        nu = 0 if B is None else B.shape[-1]
+        opt = lambda a: _ptr(a) if a is not None else None  # noqa: E731
+        check(self.lib.gpad_setup_plant(self.h, nx, nu, _ptr(PM), opt(M0), _ptr(Pg), opt(g0),
+                                        opt(A), opt(B)), "gpad_setup_plant")
+
+    def run_state(self, x, z, y, N: int, tol: float = 0.0, *, stats: bool = True):
+        """GPAD for every instance's state x [batch][nx] (M(x), g(x) formed on the device)."""
+        st = Stats()
+        want = stats or not _is_torch(z)
+        check(self.lib.gpad_run_state(self.h, _ptr(x), _ptr(z), _ptr(y), int(N), float(tol),
+                                      C.byref(st) if want else None), "gpad_run_state")
+        return self._stats_dict(st) if want else None
+
+    def closed_loop(self, x, z, y, steps: int, N: int, tol: float = 0.0, *, warm: bool = False,
+                    xs=None, us=None, iters=None, stats: bool = True):
+        """gpad.m:79-95 on the device: ``steps`` receding-horizon MPC steps for every instance.
+        x [batch][nx] is advanced in place; xs [steps][batch][nx] / us [steps][batch][nu]
+        receive the trajectories when given; ``iters`` (host int32 [steps*batch]) the counts."""
+        st = Stats()
+        if iters is not None:
+            st.iters = iters.ctypes.data_as(C.POINTER(C.c_int))
+        want = stats or iters is not None or not _is_torch(z)
+        opt = lambda a: _ptr(a) if a is not None else None  # noqa: E731
+        check(self.lib.gpad_closed_loop(self.h, _ptr(x), _ptr(z), _ptr(y), int(steps), int(N),
+                                        float(tol), int(bool(warm)), opt(xs), opt(us),
+                                        C.byref(st) if want else None), "gpad_closed_loop")
+        return self._stats_dict(st) if want else None
+
     # ---- per-step entry points (device tensors; kernel_functions.h one-for-one) ----------
     def step1(self, y, ym1, w, beta: float):
         check(self.lib.gpad_step1_extrapolate(self.h, _ptr(y), _ptr(ym1), _ptr(w), float(beta),

@@ -117,6 +117,63 @@ int gpad_run(gpad_handle_t h, void* z0, void* y0, const void* M, const void* g, 
 int gpad_run_scaled(gpad_handle_t h, void* z0, void* y0, const void* gP, const void* pD, int N,
                     double tol, const void* theta, const void* beta, gpad_stats_t* st);
 
+/* ---- per-state QP data and closed-loop MPC -------------------
+ * For an LTI plant the state-dependent QP data are affine in the state x (nx):
+ *   M(x) = M0 + PM x   (n;  PM = H^-1 F': the reference forms f = x0'F, gpad.m:81, and
+ *                            g_P = H^-1 f', acceldualgrad.m:21, on the host every MPC step)
+ *   g(x) = g0 + Pg x   (m;  b_i(x0), gpad.m:85)
+ * and the receding-horizon update is x+ = A x + B u with u = z*[0:nu] (gpad.m:91-93).
+ * gpad_setup_plant binds PM (n x nx), Pg (m x nx), optional M0 (n) / g0 (m) (NULL = 0) and,
+ * for closed-loop runs, A (nx x nx) and B (nx x nu).  Row-major, dims.dtype / dims.memory of
+ * the preceding gpad_setup, whose ML/G/L the solves use.  The fp32 evaluation order is
+ * acc = c0; acc = fma(P[i][k], x[k], acc) for k = 0..nx-1 (and A then B for the update). */
+int gpad_setup_plant(gpad_handle_t h, int nx, int nu, const void* PM, const void* M0, const void* Pg,
+                     const void* g0, const void* A, const void* B);
+
+/* gpad_run with M = M(x), g = g(x) evaluated on the device for every instance's state
+ * x [batch][nx] (no host round trip for the per-state precompute). */
+int gpad_run_state(gpad_handle_t h, const void* x, void* z0, void* y0, int N, double tol,
+                   gpad_stats_t* st);
+
+/* Closed-loop simulation of gpad.m:79-95 on the device, for every instance of the batch:
+ *   for t < steps:  M, g <- M(x), g(x);  z, y <- 0 (warm == 0, acceldualgrad.m:16-17) or kept
+ *                   from the previous step (warm != 0);  GPAD(N, tol);
+ *                   xs[t] = x;  us[t] = u = z*[0:nu];  x <- A x + B u
+ * x [batch][nx]: in x_0, out x_steps.  z [batch][n], y [batch][m]: the last step's solution.
+ * xs [steps][batch][nx], us [steps][batch][nu]: optional trajectories (NULL to skip).
+ * st->iters, when given, receives [steps][batch] iteration counts; the other stats aggregate
+ * over every (step, instance); kernel_ms times the whole loop. */
+int gpad_closed_loop(gpad_handle_t h, void* x, void* z, void* y, int steps, int N, double tol, int warm,
+                     void* xs, void* us, gpad_stats_t* st);
+
+/* ---- reference data-file boundary (main.cu:29-67 readData) ------------------------------
+ * Text file: "n_u N m num_iterations L", then M_G (n*m), g_P (n), G_L (n*m), p_D (m),
+ * theta (num_iterations), beta (num_iterations), n = n_u*N, whitespace-separated floats.
+ * M_G = -H^-1 G' (sign-folded), G_L = G/L, p_D = -g/L: the gpad_setup_scaled/run_scaled
+ * inputs.  The file's matrix layout is the reference build's choice: GPAD_FILE_ROWMAJOR is
+ * seq_functions.cpp's (M_G[i*m+j], G_L[i*n+j]); GPAD_FILE_FLIPPED is kernel_functions.cu's
+ * ENABLE_FLIPPING layout (M_G[j*n+i], G_L[j*m+i]).  The struct always holds the row-major
+ * mathematical orientation (M_G n x m, G_L m x n). */
+#define GPAD_FILE_ROWMAJOR 0
+#define GPAD_FILE_FLIPPED 1
+
+typedef struct gpad_datafile {
+    int n_u, N, m, num_iterations;
+    float L;
+    float* M_G;   /* n x m */
+    float* g_P;   /* n */
+    float* G_L;   /* m x n */
+    float* p_D;   /* m */
+    float* theta; /* num_iterations */
+    float* beta;  /* num_iterations */
+} gpad_datafile_t;
+
+/* Allocates the arrays (release with gpad_datafile_free).  GPAD_ERR_INVALID on a malformed or
+ * truncated file (the reference's readData only perror()s and continues). */
+int gpad_datafile_read(const char* path, int layout, gpad_datafile_t* out);
+int gpad_datafile_write(const char* path, int layout, const gpad_datafile_t* f);
+void gpad_datafile_free(gpad_datafile_t* f);
+
 /* Per-instance iteration counts / convergence flags of the last run (device work finished). */
 int gpad_last_stats(gpad_handle_t h, gpad_stats_t* st);
 

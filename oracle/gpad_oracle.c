@@ -259,3 +259,59 @@ long long orc_solve_batch_f32(float* z, float* y, const float* MGneg, const floa
     (void)threads;
     return total;
 }
+
+/* ---- per-state data and closed loop (gpad.m:79-95) ------------------------------------ */
+void orc_affine_f32(const float* P, const float* c0, const float* x, float* out, int rows, int nx) {
+    for (int i = 0; i < rows; i++) {
+        float acc = c0 ? c0[i] : 0.0f;
+        for (int k = 0; k < nx; k++) acc = fmaf(P[(size_t)i * nx + k], x[k], acc);
+        out[i] = acc;
+    }
+}
+
+void orc_plant_step_f32(const float* A, const float* B, const float* x, const float* u, float* xn,
+                        int nx, int nu) {
+    for (int i = 0; i < nx; i++) {
+        float acc = 0.0f;
+        for (int k = 0; k < nx; k++) acc = fmaf(A[(size_t)i * nx + k], x[k], acc);
+        for (int j = 0; j < nu; j++) acc = fmaf(B[(size_t)i * nu + j], u[j], acc);
+        xn[i] = acc;
+    }
+}
+
+long long orc_closed_loop_f32(float* x, float* z, float* y, const float* MGneg, const float* GL,
+                              float L, int n, int m, const float* PM, const float* M0,
+                              const float* Pg, const float* g0, const float* A, const float* B,
+                              int nx, int nu, int steps, int N, float tol, int check_every,
+                              const float* theta, const float* beta, int warm, float* xs,
+                              float* us, int* iters) {
+    float* gP = (float*)malloc(sizeof(float) * (n + 1));
+    float* g = (float*)malloc(sizeof(float) * (m + 1));
+    float* pD = (float*)malloc(sizeof(float) * (m + 1));
+    float* xn = (float*)malloc(sizeof(float) * (nx + 1));
+    const double ninv = -1.0 / (double)L;
+    long long total = 0;
+    for (int t = 0; t < steps; t++) {
+        orc_affine_f32(PM, M0, x, gP, n, nx);                 /* gpad.m:81 + acceldualgrad.m:21 */
+        orc_affine_f32(Pg, g0, x, g, m, nx);                  /* gpad.m:85 */
+        for (int i = 0; i < m; i++) pD[i] = (float)(ninv * (double)g[i]);  /* acceldualgrad.m:23 */
+        if (!warm) {                                          /* acceldualgrad.m:16-17 */
+            memset(z, 0, sizeof(float) * n);
+            memset(y, 0, sizeof(float) * m);
+        }
+        int conv = 0;
+        const int it = orc_solve_f32(z, y, MGneg, gP, GL, pD, n, m, N, L, tol, check_every, theta,
+                                     beta, &conv);
+        total += it;
+        if (iters) iters[t] = it;
+        if (xs) memcpy(xs + (size_t)t * nx, x, sizeof(float) * nx);
+        if (us) memcpy(us + (size_t)t * nu, z, sizeof(float) * nu);
+        orc_plant_step_f32(A, B, x, z, xn, nx, nu);           /* gpad.m:91-93 */
+        memcpy(x, xn, sizeof(float) * nx);
+    }
+    free(gP);
+    free(g);
+    free(pD);
+    free(xn);
+    return total;
+}

@@ -73,6 +73,25 @@ long long orc_solve_batch_f32(float* z, float* y, const float* MGneg, const floa
                               int shared, int N, float L, float tol, int check_every,
                               const float* theta, const float* beta, int* iters, int threads);
 
+/* ---- per-state data and closed loop (gpad_setup_plant / gpad_closed_loop) ----------
+ * gpad.m:79-95 restated: the state-dependent QP data are affine in x and the plant is LTI.
+ * These define the fp32 evaluation order the product path must match bit for bit.      */
+/* out[i] = c0[i] + sum_k P[i][k] x[k]: acc = c0[i] (0 if c0 == NULL); acc = fmaf(P, x, acc) */
+void orc_affine_f32(const float* P, const float* c0, const float* x, float* out, int rows, int nx);
+/* xn[i] = sum_k A[i][k] x[k] + sum_j B[i][j] u[j]: one fmaf chain from 0, A terms then B */
+void orc_plant_step_f32(const float* A, const float* B, const float* x, const float* u, float* xn,
+                        int nx, int nu);
+/* One instance, `steps` MPC steps of gpad.m:79-95: M = M(x), g = g(x); pD = fl32((-1/L)_64 g);
+ * (z, y) = 0 unless warm; orc_solve_f32; xs[t] = x; us[t] = z[0:nu]; x = A x + B u.
+ * MGneg/GL as orc_scale_f32 produces them.  xs [steps][nx], us [steps][nu], iters [steps]
+ * are optional.  Returns the total iteration count. */
+long long orc_closed_loop_f32(float* x, float* z, float* y, const float* MGneg, const float* GL,
+                              float L, int n, int m, const float* PM, const float* M0,
+                              const float* Pg, const float* g0, const float* A, const float* B,
+                              int nx, int nu, int steps, int N, float tol, int check_every,
+                              const float* theta, const float* beta, int warm, float* xs,
+                              float* us, int* iters);
+
 #ifdef __cplusplus
 }
 #endif

@@ -63,6 +63,12 @@ class Oracle:
         L.orc_solve_batch_f32.argtypes = [_f, _f, _f, _f, _f, _f, C.c_int, C.c_int, C.c_int, C.c_int,
                                           C.c_int, C.c_float, C.c_float, C.c_int, _f, _f, _i, C.c_int]
         L.orc_solve_batch_f32.restype = C.c_longlong
+        L.orc_affine_f32.argtypes = [_f, _f, _f, _f, C.c_int, C.c_int]
+        L.orc_plant_step_f32.argtypes = [_f, _f, _f, _f, _f, C.c_int, C.c_int]
+        L.orc_closed_loop_f32.argtypes = [_f, _f, _f, _f, _f, C.c_float, C.c_int, C.c_int, _f, _f, _f,
+                                          _f, _f, _f, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float,
+                                          C.c_int, _f, _f, C.c_int, _f, _f, _i]
+        L.orc_closed_loop_f32.restype = C.c_longlong
         self.lib = L
 
     # -- steps ------------------------------------------------------------------
@@ -168,6 +174,35 @@ class Oracle:
             np.float32(L), np.float32(tol), check_every, _fp(theta), _fp(beta),
             iters.ctypes.data_as(_i), threads)
         return Z, Y, iters, int(total)
+
+
+    # -- per-state data / closed loop (gpad.m:79-95) -----------------------------
+    def affine(self, P, c0, x):
+        P = np.ascontiguousarray(P, np.float32); rows, nx = P.shape
+        out = np.empty(rows, np.float32)
+        c = None if c0 is None else _fp(np.ascontiguousarray(c0, np.float32))
+        self.lib.orc_affine_f32(_fp(P), c, _fp(np.ascontiguousarray(x, np.float32)), _fp(out), rows, nx)
+        return out
+
+    def closed_loop_f32(self, x0, MGneg, GL, L, PM, Pg, A, B, steps, N, tol=0.0, M0=None, g0=None,
+                        check_every=10, warm=False, z0=None, y0=None, schedule=SCHEDULE_MATLAB):
+        """One instance: returns (x_T, z, y, xs [steps][nx], us [steps][nu], iters [steps])."""
+        MGneg = np.ascontiguousarray(MGneg, np.float32); n, m = MGneg.shape
+        c = lambda a: np.ascontiguousarray(a, np.float32)  # noqa: E731
+        PM, Pg, A, B = c(PM), c(Pg), c(A), c(B)
+        nx, nu = PM.shape[1], B.shape[1]
+        x = np.array(x0, np.float32, copy=True).reshape(nx)
+        z = np.zeros(n, np.float32) if z0 is None else np.array(z0, np.float32, copy=True)
+        y = np.zeros(m, np.float32) if y0 is None else np.array(y0, np.float32, copy=True)
+        xs = np.zeros((steps, nx), np.float32); us = np.zeros((steps, nu), np.float32)
+        iters = np.zeros(steps, np.int32)
+        theta, beta = self.schedule_f32(max(N, 1), schedule)
+        opt = lambda a: None if a is None else _fp(c(a))  # noqa: E731
+        self.lib.orc_closed_loop_f32(
+            _fp(x), _fp(z), _fp(y), _fp(MGneg), _fp(c(GL)), np.float32(L), n, m, _fp(PM), opt(M0),
+            _fp(Pg), opt(g0), _fp(A), _fp(B), nx, nu, steps, N, np.float32(tol), check_every,
+            _fp(theta), _fp(beta), int(bool(warm)), _fp(xs), _fp(us), iters.ctypes.data_as(_i))
+        return x, z, y, xs, us, iters
 
 
 class RefSeq:

@@ -83,12 +83,70 @@ def make(name, qp, O, R):
     print(f"{name}: n={n} m={m} L={qp.L:.6g} tol-iters={it}")
 
 
+def write_reference_datafile(path, d, flipped):
+    """A main.cu:29-67 data file written with plain numpy formatting (independent of the
+    libgpad writer, so the reader is tested against a file it did not produce)."""
+    n = d["M_G"].shape[0]
+    with open(path, "w") as fh:
+        fh.write(f"{d['n_u']} {d['N']} {d['m']} {len(d['theta'])} {d['L']:.8e}\n")
+        mg = d["M_G"].T if flipped else d["M_G"]          # flipped: M_G[j*n + i]
+        gl = d["G_L"].T if flipped else d["G_L"]          # flipped: G_L[j*m + i]
+        for arr in (mg.reshape(-1), d["g_P"], gl.reshape(-1), d["p_D"], d["theta"], d["beta"]):
+            fh.write(" ".join(f"{v:.8e}" for v in np.asarray(arr, np.float64)) + "\n")
+    assert n == d["n_u"] * d["N"]
+
+
+def make_datafile(O, R):
+    """gpad.m's default battery (n = 3 cells, p = 4: n = 12, m = 56) as a reference data file,
+    with the reference's own steps (RefSeq) run for N_v = 100 iterations on the file's values
+    (what main.cu computes, on the CPU steps it mirrors)."""
+    qp = problems.battery_mpc(3, 4, seed=5)
+    L = np.float32(qp.L)
+    f32 = lambda a: np.asarray(a, np.float64).astype(np.float32)  # noqa: E731
+    MGneg, GL, pD = O.scale(f32(qp.ML), f32(qp.G), f32(qp.g), L)
+    th, be = O.schedule_f32(120)
+    d = dict(n_u=3, N=4, m=qp.m, L=float(L), M_G=MGneg, g_P=f32(qp.M), G_L=GL, p_D=pD,
+             theta=th, beta=be)
+    write_reference_datafile(os.path.join(HERE, "datafile_battery_3x4.txt"), d, flipped=False)
+    write_reference_datafile(os.path.join(HERE, "datafile_battery_3x4_flipped.txt"), d, flipped=True)
+    # values as read back by fscanf("%f") == strtof of the printed text
+    rd = lambda a: np.array([np.float32(float(f"{v:.8e}")) for v in np.asarray(a, np.float64).reshape(-1)],  # noqa: E731
+                            np.float32).reshape(np.shape(a))
+    fd = {k: rd(d[k]) for k in ("M_G", "g_P", "G_L", "p_D", "theta", "beta")}
+    z0 = np.zeros(qp.n, np.float32)
+    y0 = np.zeros(qp.m, np.float32)
+    z, y = R.solve(z0, y0, fd["M_G"], fd["g_P"], fd["G_L"], fd["p_D"], fd["theta"], fd["beta"], 100)
+    np.savez_compressed(os.path.join(HERE, "datafile_battery_3x4.npz"), L=np.float32(rd(d["L"])),
+                        ref_z_100=z, ref_y_100=y, **fd)
+    print(f"datafile_battery_3x4: n={qp.n} m={qp.m}")
+
+
+def make_closed_loop():
+    """gpad.m:79-95 with n = 3 cells, p = 4, 40 samples, acceldualgrad's 100 iterations per
+    step, fp64 (numpy restatement of the MATLAB): x, u trajectories."""
+    n_u, N, steps = 3, 4, 40
+    mats = problems.battery_matrices(n_u, N)
+    x = np.random.default_rng(11).random(n_u) - 0.5           # gpad.m:14 (seeded)
+    xs, us = [], []
+    for _ in range(steps):
+        f, A_i, b_i = problems.battery_constraints(mats, x, n_u, N)
+        u, _, _ = matlab_ref.acceldualgrad(mats["H"], f, A_i, b_i, n_u, 100)
+        xs.append(x.copy())
+        us.append(u.copy())
+        x = mats["A"] @ x + mats["B"] @ u                      # gpad.m:93
+    np.savez_compressed(os.path.join(HERE, "closed_loop_battery_3x4.npz"), x0=xs[0],
+                        xs=np.array(xs), us=np.array(us), x_final=x)
+    print(f"closed_loop_battery_3x4: steps={steps}")
+
+
 def main():
     pyoracle.build(ref=True)
     O = pyoracle.Oracle()
     R = pyoracle.RefSeq()
     for name, qp in problem_set().items():
         make(name, qp, O, R)
+    make_datafile(O, R)
+    make_closed_loop()
     # the reference's own step-3 known-answer files (data, copied verbatim)
     if os.path.isdir(STEP3_SRC):
         for k in range(1, 6):
