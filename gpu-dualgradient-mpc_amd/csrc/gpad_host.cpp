@@ -97,7 +97,7 @@ struct gpad_handle_s {
     int frag_tiles = 0;
     DevBuf theta, beta;
     int sched_len = 0, sched_kind = -1, sched_dtype = -1;
-    DevBuf work, counters;
+    DevBuf work, counters, pwork;
     std::vector<int> h_counts;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int last_kernel = 0, last_batch = 0, last_steps = 1;
@@ -165,6 +165,7 @@ int gpad_destroy(gpad_handle_t h) {
     h->beta.release();
     h->work.release();
     h->counters.release();
+    h->pwork.release();
     h->plant.release();
     h->state.release();
     if (h->ev0) (void)hipEventDestroy(h->ev0);
@@ -322,7 +323,7 @@ static int ensure_schedule(gpad_handle_t h, int N, const void* theta_in, const v
     return GPAD_OK;
 }
 
-// Counters are laid out [steps][iters[batch] | conv[batch]] (+ the queue word after them).
+// Counters are laid out [steps][iters[batch] | conv[batch]].
 static int collect_stats(gpad_handle_t h, gpad_stats_t* st) {
     const int batch = h->last_batch;
     const size_t entries = (size_t)batch * h->last_steps;
@@ -360,10 +361,10 @@ int gpad_last_stats(gpad_handle_t h, gpad_stats_t* st) {
 }  // extern "C"
 
 // Enqueue one fused solve on device buffers (no staging, no sync).  Counters: iters/conv
-// [batch] each, queue = 4 ints (zeroed here).  *kernel_out = the family that ran.
+// [batch] each.  *kernel_out = the family that ran.
 template <typename T>
 static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg, int N, double tol,
-                        bool scaled_vec, int* iters, int* conv, int* queue, int* kernel_out) {
+                        bool scaled_vec, int* iters, int* conv, int* kernel_out) {
     const gpad_dims_t& d = h->dims;
     const int n = d.n, m = d.m, batch = d.batch;
     gpad::SolveArgs<T> a{};
@@ -393,12 +394,10 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
     a.beta = (const T*)h->beta.p;
     a.iters = iters;
     a.conv = conv;
-    a.queue = queue;
     a.num_cus = h->num_cus;
     int kernel = d.kernel;
     hipError_t e = hipSuccess;
     bool ok = false;
-    HIP_TRY(hipMemsetAsync(a.queue, 0, 4 * sizeof(int), h->stream));
     if (N == 0) {  // nothing to iterate: outputs are the inputs, zero counts
         HIP_TRY(hipMemsetAsync(a.iters, 0, sizeof(int) * (size_t)batch, h->stream));
         HIP_TRY(hipMemsetAsync(a.conv, 0, sizeof(int) * (size_t)batch, h->stream));
@@ -407,6 +406,11 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
     }
     if constexpr (sizeof(T) == sizeof(float)) {
         if (kernel == GPAD_KERNEL_PANEL || (kernel == GPAD_KERNEL_AUTO && d.shared && batch >= 64)) {
+            if (tol > 0.0 && h->frag.p) {  // phased compaction workspace (gpad_panel.hip)
+                int rc = h->pwork.ensure(gpad::panel_work_bytes(m, batch));
+                if (rc) return rc;
+                a.pwork = h->pwork.p;
+            }
             e = gpad::launch_panel(a, h->stream, &ok);
             if (e != hipSuccess) return fail(GPAD_ERR_HIP, std::string("panel: ") + hipGetErrorString(e));
             if (ok) kernel = GPAD_KERNEL_PANEL;
@@ -443,8 +447,8 @@ static int run_typed(gpad_handle_t h, T* z, T* y, const T* M, const T* g, int N,
     const int n = d.n, m = d.m, batch = d.batch;
     int rc = ensure_schedule(h, N, theta_in, beta_in);
     if (rc) return rc;
-    // [iters | conv | queue word (padded to 16 B)]
-    if ((rc = h->counters.ensure(sizeof(int) * (2 * (size_t)batch + 4)))) return rc;
+    // [iters | conv]
+    if ((rc = h->counters.ensure(sizeof(int) * 2 * (size_t)batch))) return rc;
     T *dz = z, *dy = y;
     const T *dM = M, *dg = g;
     const size_t zb = sizeof(T) * (size_t)batch * n, yb = sizeof(T) * (size_t)batch * m;
@@ -465,8 +469,7 @@ static int run_typed(gpad_handle_t h, T* z, T* y, const T* M, const T* g, int N,
     int* iters = (int*)h->counters.p;
     int kernel = 0;
     HIP_TRY(hipEventRecord(h->ev0, h->stream));
-    if ((rc = launch_solve<T>(h, dz, dy, dM, dg, N, tol, scaled_vec, iters, iters + batch,
-                              iters + 2 * batch, &kernel)))
+    if ((rc = launch_solve<T>(h, dz, dy, dM, dg, N, tol, scaled_vec, iters, iters + batch, &kernel)))
         return rc;
     HIP_TRY(hipEventRecord(h->ev1, h->stream));
     h->timed = true;
@@ -606,7 +609,7 @@ static int state_typed(gpad_handle_t h, T* x, T* z, T* y, int steps, int N, doub
     const int nsolve = loop ? steps : 1;
     int rc = ensure_schedule(h, N, nullptr, nullptr);
     if (rc) return rc;
-    if ((rc = h->counters.ensure(sizeof(int) * (2 * (size_t)batch * nsolve + 4)))) return rc;
+    if ((rc = h->counters.ensure(sizeof(int) * 2 * (size_t)batch * nsolve))) return rc;
     const bool host = d.memory == GPAD_MEM_HOST;
     const size_t zn = (size_t)batch * n, yn = (size_t)batch * m, xn = (size_t)batch * nx;
     const size_t xsn = loop && xs ? (size_t)steps * xn : 0, usn = loop && us ? (size_t)steps * batch * nu : 0;
@@ -635,7 +638,6 @@ static int state_typed(gpad_handle_t h, T* x, T* z, T* y, int steps, int N, doub
     const PlantOffsets o = plant_offsets(n, m, nx, nu);
     const T* P = (const T*)h->plant.p;
     int* counters = (int*)h->counters.p;
-    int* queue = counters + 2 * (size_t)batch * nsolve;
     int kernel = 0;
     HIP_TRY(hipEventRecord(h->ev0, h->stream));
     T* xc = xa;
@@ -648,7 +650,7 @@ static int state_typed(gpad_handle_t h, T* x, T* z, T* y, int steps, int N, doub
             HIP_TRY(hipMemsetAsync(dy, 0, sizeof(T) * yn, h->stream));
         }
         int* it = counters + 2 * (size_t)batch * t;
-        if ((rc = launch_solve<T>(h, dz, dy, Mx, gx, N, tol, false, it, it + batch, queue, &kernel)))
+        if ((rc = launch_solve<T>(h, dz, dy, Mx, gx, N, tol, false, it, it + batch, &kernel)))
             return rc;
         if (loop) {  // gpad.m:91-94: u = z*(1:nu); x <- A x + B u
             HIP_TRY(gpad::launch_plant_step<T>(P + o.A, P + o.B, xc, dz, n, xnext, nx, nu, batch,

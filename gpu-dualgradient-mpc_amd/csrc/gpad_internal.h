@@ -35,8 +35,16 @@ struct SolveArgs {
     const T* beta;         // [N+2] beta_v
     int* iters;            // [batch] iterations executed
     int* conv;             // [batch] 0 = not converged, 1 = test (A) passed, 2 = test (B) passed
-    int* queue;            // panel kernel: device counter of handed-out instances (zeroed per run)
     int num_cus;           // compute units of the device (persistent-grid sizing)
+    // panel kernel, phased compaction (set by launch_panel; see gpad_panel.hip)
+    void* pwork;           // workspace of panel_work_bytes(m, batch) bytes, or null (one phase)
+    int v_begin, v_end;    // iterations [v_begin, v_end) of this phase
+    const int* idx_in;     // instances of this phase (null: 0..batch-1)
+    const int* count_in;   // their number (device; null: batch)
+    int* idx_out;          // survivors appended here ...
+    int* count_out;        // ... and counted here (device)
+    float* wc;             // carried w  [batch][m]
+    float* uc;             // carried u = G_L z [batch][m]
 };
 
 // launchers (return hipError_t of the launch)
@@ -45,6 +53,7 @@ hipError_t launch_stream(const SolveArgs<T>& a, hipStream_t s);
 hipError_t launch_resident(const SolveArgs<float>& a, hipStream_t s, bool* supported);
 hipError_t launch_panel(const SolveArgs<float>& a, hipStream_t s, bool* supported);
 size_t panel_frag_bytes(int n, int m, int batch);
+size_t panel_work_bytes(int m, int batch);
 int panel_tiles(int n, int m, int batch);
 hipError_t launch_pack_panel(const float* ML, const float* G, int n, int m, int batch, float mg_sign,
                              double g_scale, void* frag, hipStream_t s);

@@ -42,6 +42,7 @@ __device__ __forceinline__ int pi16(int rho) { return 4 * (rho & 3) + (rho >> 2)
 // packing
 // ---------------------------------------------------------------------------------------
 constexpr int kPanelMaxTiles = 16;  // n, m <= 256 (1024-thread workgroups)
+constexpr int kPanelMaxPhases = 48;
 
 static int panel_tiles_for(int n, int m) {
     const int t = ((n > m ? n : m) + 15) / 16;
@@ -131,249 +132,607 @@ __device__ __forceinline__ f32x4 panel_gemm(__amdgpu_buffer_rsrc_t PA, const flo
     return acc;
 }
 
-// Continuous batching: a workgroup keeps 16 instance "columns" in flight.  A column that
-// converges (or reaches N) writes its z*, y* and counts, then pulls the next instance from a
-// device-wide queue, so no column and no CU idles while instances remain.  Every column has its
-// own iteration counter (theta/beta are per lane); columns are independent in the MFMA, so the
-// arithmetic of an instance does not depend on which column or workgroup runs it.
-template <int T, bool QUEUE>
+// Phased compaction (continuous batching at phase granularity).  A solve with a tolerance is
+// cut into phases of iterations [v_begin, v_end).  Within a phase every column runs the same
+// global iteration index v, so theta/beta and the test events (v % K == 0) are uniform scalars
+// and the per-iteration path has no per-column bookkeeping.  At a phase end the still-running
+// instances park their state (z, y in the output arrays, w and u in carry buffers) and append
+// their ids to a dense list; the next phase packs only those into panels.  Converged instances
+// therefore stop occupying MFMA columns after at most one phase, instead of idling until the
+// slowest instance of their static panel finishes.  Columns are independent in the MFMA, so an
+// instance's arithmetic does not depend on its column, panel or phase (bit-exact either way).
+// A workgroup walks panels grid-stride, so any batch size runs on a resident-sized grid.
+template <int T>
 __global__ __launch_bounds__(64 * T) void gpad_panel_kernel(SolveArgs<float> a) {
     __shared__ __attribute__((aligned(16))) float Wl[T * 256];  // [T][64][4] w    (B of GEMM 1)
     __shared__ __attribute__((aligned(16))) float Zh[T * 256];  // [T][64][4] zhat (B of GEMM 2)
+    // per-lane constants of the current instance, parked in LDS rather than VGPRs:
+    // g_P rows and p_D rows of tile t
+    __shared__ __attribute__((aligned(16))) float Gp[T * 256];
+    __shared__ __attribute__((aligned(16))) float Pd[T * 256];
     __shared__ PanelSlot slots[T];
-    __shared__ int next_inst[16];  // refill hand-out per column (-1: none)
-    __shared__ int queue_dry;
 
     const int lane = threadIdx.x & 63;
     const int t = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // row tile of this wave
     const int j = lane >> 4, c = lane & 15;
-    const int n = a.n, m = a.m, N = a.N;
+    const int n = a.n, m = a.m, N = a.N, K = a.check_every;
     const int abytes = T * T * 1024;  // one packed operand
     const __amdgpu_buffer_rsrc_t PA1 =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.frag), 0, abytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t PA2 = __builtin_amdgcn_make_buffer_rsrc(
         (void*)((const char*)a.frag + abytes), 0, abytes, 0x00020000);
     const int voff = t * 1024 + lane * 16;
-    const int slot = t * 64 + lane;  // this lane's float4 in Wl / Zh
+    const int slot = t * 64 + lane;  // this lane's float4 in Wl / Zh / Gp / Pd
     float4* Wl4 = reinterpret_cast<float4*>(Wl);
     float4* Zh4 = reinterpret_cast<float4*>(Zh);
+    float4* Gp4 = reinterpret_cast<float4*>(Gp);
+    float4* Pd4 = reinterpret_cast<float4*>(Pd);
     const bool use_tol = a.tol > 0.0;
-    const int first = gridDim.x * 16;  // instances handed out statically; the queue serves the rest
+    const bool fresh = a.v_begin == 0;      // first phase: start from the caller's z0, y0
+    const bool carry = a.v_end < N;         // not the last phase: park the survivors
+    const int count = a.count_in ? __builtin_amdgcn_readfirstlane(*a.count_in) : a.batch;
+    const int panels = (count + 15) / 16;
 
-    // register r <-> row 16t + 4r + j of the lane's current instance (column c)
-    float z[4], gp[4], y[4], pd[4], u[4], zh[4];
-    int inst = blockIdx.x * 16 + c;
-    bool active = inst < a.batch;
-    int lc = 0;  // iterations done by this column's instance
-
-    auto load_instance = [&](bool on) {
+    for (int p = blockIdx.x; p < panels; p += gridDim.x) {
+        // ---- load the panel: column c <-> instance idx[16p + c] -------------------------
+        const int k = 16 * p + c;
+        bool active = k < count;
+        const int inst = active ? (a.idx_in ? a.idx_in[k] : k) : 0;
+        // register r <-> row 16t + 4r + j of the column's instance
+        float z[4], y[4], u[4];
+        {
+            float gp[4], pd[4], w[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int i = 16 * t + 4 * r + j;
-            const bool okn = on && i < n, okm = on && i < m;
-            z[r] = okn ? a.z[(size_t)inst * n + i] : 0.0f;
-            gp[r] = okn ? a.gP[(size_t)inst * a.ld_gP + i] : 0.0f;
-            y[r] = okm ? a.y[(size_t)inst * m + i] : 0.0f;
-            pd[r] = okm ? (float)(a.gscale * (double)a.g[(size_t)inst * a.ld_g + i]) : 0.0f;
-            u[r] = 0.0f;
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 * t + 4 * r + j;
+                const bool okn = active && i < n, okm = active && i < m;
+                z[r] = okn ? a.z[(size_t)inst * n + i] : 0.0f;
+                gp[r] = okn ? a.gP[(size_t)inst * a.ld_gP + i] : 0.0f;
+                y[r] = okm ? a.y[(size_t)inst * m + i] : 0.0f;
+                pd[r] = okm ? (float)(a.gscale * (double)a.g[(size_t)inst * a.ld_g + i]) : 0.0f;
+                if (fresh) {  // w_0 = y_0 + beta_0 (y_0 - y_{-1}), y_{-1} = y_0; u set below
+                    w[r] = __builtin_fmaf(a.beta[0], y[r] - y[r], y[r]);
+                    u[r] = 0.0f;
+                } else {
+                    w[r] = okm ? a.wc[(size_t)inst * m + i] : 0.0f;
+                    u[r] = okm && use_tol ? a.uc[(size_t)inst * m + i] : 0.0f;
+                }
+            }
+            Gp4[slot] = make_float4(gp[0], gp[1], gp[2], gp[3]);
+            Pd4[slot] = make_float4(pd[0], pd[1], pd[2], pd[3]);
+            Wl4[slot] = make_float4(w[0], w[1], w[2], w[3]);
         }
-        const float b0 = a.beta[0];
-        Wl4[slot] = make_float4(__builtin_fmaf(b0, y[0] - y[0], y[0]), __builtin_fmaf(b0, y[1] - y[1], y[1]),
-                                __builtin_fmaf(b0, y[2] - y[2], y[2]), __builtin_fmaf(b0, y[3] - y[3], y[3]));
-    };
-    // u = G_L z_{-1} for the columns in `fresh` (one GEMM for all of them; then the 8c recursion)
-    auto seed_u = [&](bool fresh) {
-        Zh4[slot] = make_float4(z[0], z[1], z[2], z[3]);
-        __syncthreads();
-        const f32x4 cz = panel_gemm<T>(PA2, Zh, voff, lane);
-        if (fresh) {
+        if (fresh && use_tol) {  // u = G_L z_{-1} (one GEMM for the panel); then the 8c recursion
+            Zh4[slot] = make_float4(z[0], z[1], z[2], z[3]);
+            __syncthreads();
+            const f32x4 cz = panel_gemm<T>(PA2, Zh, voff, lane);
 #pragma unroll
             for (int r = 0; r < 4; ++r) u[r] = cz[r];
         }
         __syncthreads();
-    };
 
-    load_instance(active);
-    if (c == 0 && t == 0 && j == 0) queue_dry = first >= a.batch;
-    if (use_tol) seed_u(active);
-    __syncthreads();
-
-    float th = a.theta[0], bn = a.beta[1];
-    int v = 0;  // iterations of this launch (= lc of every active column when there is no queue)
-    while (true) {
-        // schedule, prefetched one iteration ahead (tables hold N + 2 entries): per column with a
-        // queue (columns restart at different times), uniform scalar loads without one
-        float th_next, bn_next;
-        if constexpr (QUEUE) {
-            const int lp = active ? lc : 0;
-            th_next = a.theta[lp + 1];
-            bn_next = a.beta[lp + 2];
-        } else {
-            th_next = a.theta[v + 1];
-            bn_next = a.beta[v + 2];
-        }
-        ++v;
-        const bool chk = use_tol && active && ((lc + 1) % a.check_every) == 0;
-        const float omt = 1.0f - th;
-        // ---- GEMM 1 + epilogue: zhat = -ML w - g_P (8b), z = (1-th) z + th zhat (8c) -----
-        {
-            const f32x4 acc = panel_gemm<T>(PA1, Wl, voff, lane);
+        int v = a.v_begin;
+        float th = a.theta[v], bn = a.beta[v + 1];
+        while (true) {
+            // schedule prefetched one iteration ahead (tables hold N + 2 entries)
+            const float th_next = a.theta[v + 1], bn_next = a.beta[v + 2];
+            ++v;
+            const bool chk = use_tol && (v % K) == 0;  // uniform: every column is at iteration v
+            const float omt = 1.0f - th;
+            // ---- GEMM 1 + epilogue: zhat = -ML w - g_P (8b), z = (1-th) z + th zhat (8c) ----
+            {
+                const f32x4 acc = panel_gemm<T>(PA1, Wl, voff, lane);
+                const float4 g4 = Gp4[slot];
+                const float gp[4] = {g4.x, g4.y, g4.z, g4.w};
+                float zh[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                zh[r] = acc[r] - gp[r];
-                const float zn = __builtin_fmaf(omt, z[r], th * zh[r]);
-                if (active) z[r] = zn;
+                for (int r = 0; r < 4; ++r) {
+                    zh[r] = acc[r] - gp[r];
+                    const float zn = __builtin_fmaf(omt, z[r], th * zh[r]);
+                    if (active) z[r] = zn;
+                }
+                Zh4[slot] = make_float4(zh[0], zh[1], zh[2], zh[3]);
             }
-            Zh4[slot] = make_float4(zh[0], zh[1], zh[2], zh[3]);
-        }
-        __syncthreads();
-        // ---- GEMM 2 + epilogue: y+ = [w + G_L zhat + p_D]+ (8d), next w (8a) --------------
-        float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY;
-        double gap = 0.0;
-        {
-            const f32x4 acc = panel_gemm<T>(PA2, Zh, voff, lane);
-            const float4 w4 = Wl4[slot];
-            const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
-            float wn[4];
+            __syncthreads();
+            // ---- GEMM 2 + epilogue: y+ = [w + G_L zhat + p_D]+ (8d), next w (8a) ----------
+            float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY;
+            double gap = 0.0;
+            {
+                const f32x4 acc = panel_gemm<T>(PA2, Zh, voff, lane);
+                const float4 w4 = Wl4[slot];
+                const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+                const float4 p4 = Pd4[slot];
+                const float pd[4] = {p4.x, p4.y, p4.z, p4.w};
+                float wn[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float cv = acc[r];
-                const float sv = (wv[r] + pd[r]) + cv;
-                const float yp = (__builtin_fabsf(sv) + sv) * 0.5f;
-                wn[r] = __builtin_fmaf(bn, yp - y[r], yp);
-                if (use_tol) {
-                    const float un = __builtin_fmaf(omt, u[r], th * cv);
-                    if (active) u[r] = un;
-                    if (chk && (16 * t + 4 * r + j) < m) {
-                        const float tt = cv + pd[r];
-                        violh = fmaxf(violh, tt);
-                        wmin = fminf(wmin, wv[r]);
-                        gap -= (double)wv[r] * (double)tt;
-                        violz = fmaxf(violz, u[r] + pd[r]);
+                for (int r = 0; r < 4; ++r) {
+                    const float cv = acc[r];
+                    const float sv = (wv[r] + pd[r]) + cv;
+                    const float yp = (__builtin_fabsf(sv) + sv) * 0.5f;
+                    wn[r] = __builtin_fmaf(bn, yp - y[r], yp);
+                    if (use_tol) {
+                        const float un = __builtin_fmaf(omt, u[r], th * cv);
+                        if (active) u[r] = un;
+                        if (chk && active && (16 * t + 4 * r + j) < m) {
+                            const float tt = cv + pd[r];
+                            violh = fmaxf(violh, tt);
+                            wmin = fminf(wmin, wv[r]);
+                            gap -= (double)wv[r] * (double)tt;
+                            violz = fmaxf(violz, u[r] + pd[r]);
+                        }
+                    }
+                    if (active) y[r] = yp;
+                }
+                if (active) Wl4[slot] = make_float4(wn[0], wn[1], wn[2], wn[3]);
+            }
+            th = th_next;
+            bn = bn_next;
+            __syncthreads();
+            if (!chk && v < a.v_end) continue;
+
+            // ---- Algorithm 1 test, per column: lane groups j, then row tiles through LDS ----
+            int code = 0;
+            if (chk) {
+#pragma unroll
+                for (int o = 16; o < 64; o <<= 1) {
+                    violz = fmaxf(violz, __shfl_xor(violz, o, 64));
+                    violh = fmaxf(violh, __shfl_xor(violh, o, 64));
+                    wmin = fminf(wmin, __shfl_xor(wmin, o, 64));
+                    gap += __shfl_xor(gap, o, 64);
+                }
+                if (j == 0) {
+                    slots[t].violz[c] = violz;
+                    slots[t].violh[c] = violh;
+                    slots[t].wmin[c] = wmin;
+                    slots[t].gap[c] = gap;
+                }
+                __syncthreads();
+                if (active) {
+                    double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gq = 0.0;
+#pragma unroll
+                    for (int s2 = 0; s2 < T; ++s2) {
+                        vz = fmax(vz, (double)slots[s2].violz[c]);
+                        vh = fmax(vh, (double)slots[s2].violh[c]);
+                        wm = fmin(wm, (double)slots[s2].wmin[c]);
+                        gq += slots[s2].gap[c];
+                    }
+                    if (vz * a.L <= a.tol) code = 1;
+                    else if ((vh * a.L <= a.tol) && (wm >= 0.0) && (gq * a.L <= a.tol)) code = 2;
+                }
+            }
+            // ---- finished columns: results out ---------------------------------------------
+            if (active && (code != 0 || v >= N)) {
+                const float4 h4 = Zh4[slot];  // this iteration's zhat (own slot, not yet overwritten)
+                const float zh[4] = {h4.x, h4.y, h4.z, h4.w};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 16 * t + 4 * r + j;
+                    if (i < n) a.z[(size_t)inst * n + i] = code == 2 ? zh[r] : z[r];  // (B): zhat
+                    if (i < m) a.y[(size_t)inst * m + i] = y[r];
+                }
+                if (t == 0 && j == 0) {
+                    a.iters[inst] = v;
+                    a.conv[inst] = code;
+                }
+                active = false;
+            }
+            if (v >= a.v_end || !__syncthreads_or(active ? 1 : 0)) break;
+        }
+        // ---- phase end: park the survivors for the next phase ------------------------------
+        if (carry && v >= a.v_end) {
+            if (active) {
+                const float4 w4 = Wl4[slot];  // w of iteration v (own slot)
+                const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 16 * t + 4 * r + j;
+                    if (i < n) a.z[(size_t)inst * n + i] = z[r];
+                    if (i < m) {
+                        a.y[(size_t)inst * m + i] = y[r];
+                        a.wc[(size_t)inst * m + i] = wv[r];
+                        if (use_tol) a.uc[(size_t)inst * m + i] = u[r];
                     }
                 }
-                if (active) y[r] = yp;
             }
-            if (active) Wl4[slot] = make_float4(wn[0], wn[1], wn[2], wn[3]);
+            if (t == 0) {  // lanes 0..15 (j == 0) speak for the 16 columns
+                const unsigned long long live = __ballot(active && j == 0);
+                int base = 0;
+                if (lane == 0) base = atomicAdd(a.count_out, (int)__popcll(live));
+                base = __shfl(base, 0, 64);
+                if (active && j == 0) a.idx_out[base + (int)__popcll(live & ((1ull << lane) - 1ull))] = inst;
+            }
         }
-        if (active) ++lc;
-        th = th_next;
-        bn = bn_next;
-        // Events (a test, or a column at N).  Without a queue every active column has done v
-        // iterations, so events are uniform and a plain barrier suffices; with a queue the one
-        // barrier per iteration doubles as the event probe (__syncthreads_or: LDS + barriers).
-        bool any_chk;
-        if constexpr (QUEUE) {
-            const bool at_n = active && lc >= N;
-            if (!__syncthreads_or((chk || at_n) ? 1 : 0)) continue;
-            any_chk = __syncthreads_or(chk ? 1 : 0);
-        } else {
-            __syncthreads();
-            any_chk = use_tol && (v % a.check_every) == 0;
-            if (!any_chk && v < N) continue;
-        }
+        __syncthreads();  // the next panel reuses the LDS tiles
+    }
+}
 
-        // ---- Algorithm 1 test, per column: lane groups j, then row tiles through LDS ------
-        int code = 0;
-        if (any_chk) {
+// ---------------------------------------------------------------------------------------
+// Panel pairs (8 < T <= 16): a 16-wave workgroup owns TWO panels, balanced over the SIMDs.
+// A 13-wave single-panel workgroup puts 4,3,3,3 waves (tile chains) on the CU's SIMDs, and a
+// second one is not co-resident at its register budget, so the busiest SIMD carries 4 chains
+// while the mean is 3.25.  Here the 2T (panel, tile) chains of two panels are dealt to 16 waves
+// (4 per SIMD, waves w, w+4, w+8, w+12 share one): D = 2T-16 "double" waves own tile w of BOTH
+// panels -- one A fragment feeds two MFMA chains, which also hides the 40-cycle MFMA
+// dependency -- and the 32-2T "single" waves own one (panel, tile) each.  Doubles go to waves
+// 0..D-1, i.e. round-robin over the SIMDs, so the SIMD loads differ by at most one chain
+// (T = 13: 7,7,6,6 for 26 chains).  When a phase has no more panels than workgroups, a
+// workgroup takes one panel (waves 0..T-1, one tile each): pairing would only idle CUs.
+// ---------------------------------------------------------------------------------------
+template <int T, bool DUAL>
+__device__ __forceinline__ void panel_gemm2(__amdgpu_buffer_rsrc_t PA, const float4* B0, const float4* B1,
+                                            int voff, int lane, f32x4& acc0, f32x4& acc1) {
+    acc0 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    acc1 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    float4 a[2], b0[2], b1[2];
+    a[0] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, 0, 0));
+    b0[0] = B0[lane];
+    if constexpr (DUAL) b1[0] = B1[lane];
 #pragma unroll
-            for (int o = 16; o < 64; o <<= 1) {
-                violz = fmaxf(violz, __shfl_xor(violz, o, 64));
-                violh = fmaxf(violh, __shfl_xor(violh, o, 64));
-                wmin = fminf(wmin, __shfl_xor(wmin, o, 64));
-                gap += __shfl_xor(gap, o, 64);
-            }
-            if (j == 0) {
-                slots[t].violz[c] = violz;
-                slots[t].violh[c] = violh;
-                slots[t].wmin[c] = wmin;
-                slots[t].gap[c] = gap;
-            }
-            __syncthreads();
-            if (chk) {
-                double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gq = 0.0;
-#pragma unroll
-                for (int s2 = 0; s2 < T; ++s2) {
-                    vz = fmax(vz, (double)slots[s2].violz[c]);
-                    vh = fmax(vh, (double)slots[s2].violh[c]);
-                    wm = fmin(wm, (double)slots[s2].wmin[c]);
-                    gq += slots[s2].gap[c];
-                }
-                if (vz * a.L <= a.tol) code = 1;
-                else if ((vh * a.L <= a.tol) && (wm >= 0.0) && (gq * a.L <= a.tol)) code = 2;
-            }
+    for (int kb = 0; kb < T; ++kb) {
+        const int cur = kb & 1, nxt = cur ^ 1;
+        if (kb + 1 < T) {
+            a[nxt] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb + 1) * T * 1024, 0));
+            b0[nxt] = B0[(kb + 1) * 64 + lane];
+            if constexpr (DUAL) b1[nxt] = B1[(kb + 1) * 64 + lane];
         }
-        // ---- finished columns: results out -------------------------------------------------
-        const bool fin = active && (code != 0 || lc >= N);
-        if (fin) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int i = 16 * t + 4 * r + j;
-                if (i < n) a.z[(size_t)inst * n + i] = code == 2 ? zh[r] : z[r];  // (B) certifies zhat
-                if (i < m) a.y[(size_t)inst * m + i] = y[r];
-            }
-            if (t == 0 && j == 0) {
-                a.iters[inst] = lc;
-                a.conv[inst] = code;
-            }
-            active = false;
-        }
-        if constexpr (!QUEUE) {
-            if (v >= N || !__syncthreads_or(active ? 1 : 0)) break;
-            continue;
-        }
-        // ---- refill idle columns from the queue (one lane per column draws) -----------------
-        if (t == 0 && j == 0) {  // -2: did not draw, -1: drew from an empty queue
-            int nx = -2;
-            if (!active && !queue_dry) {
-                const int k = atomicAdd(a.queue, 1);
-                nx = first + k < a.batch ? first + k : -1;
-            }
-            next_inst[c] = nx;
-        }
-        __syncthreads();
-        if (t == 0 && lane == 0) {  // all draws of this round are done: record exhaustion
-            bool dry = queue_dry;
-            for (int q = 0; q < 16; ++q) dry = dry || next_inst[q] == -1;
-            queue_dry = dry;  // read only after the next barrier
-        }
-        const int nx = next_inst[c];
-        const bool fresh = !active && nx >= 0;
-        if (fresh) {
-            inst = nx;
-            active = true;
-            lc = 0;
-            load_instance(true);
-        }
-        if (__syncthreads_or(fresh ? 1 : 0)) {
-            if (use_tol) seed_u(fresh);
-            if (fresh) {
-                th = a.theta[0];
-                bn = a.beta[1];
-            }
-        }
-        if (!__syncthreads_or(active ? 1 : 0)) break;
+        __builtin_amdgcn_sched_barrier(0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].x, b0[cur].x, acc0, 0, 0, 0);
+        if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].x, b1[cur].x, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].y, b0[cur].y, acc0, 0, 0, 0);
+        if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].y, b1[cur].y, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].z, b0[cur].z, acc0, 0, 0, 0);
+        if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].z, b1[cur].z, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].w, b0[cur].w, acc0, 0, 0, 0);
+        if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].w, b1[cur].w, acc1, 0, 0, 0);
+        // both chains advance together, one k-block per step (else the scheduler defers the
+        // second chain past the loop and keeps every B fragment live)
+        if constexpr (DUAL) asm volatile("" : "+v"(acc0), "+v"(acc1)::"memory");
+        else asm volatile("" : "+v"(acc0)::"memory");
     }
 }
 
 template <int T>
-static hipError_t launch_panel_t(const SolveArgs<float>& a, hipStream_t s) {
-    // Persistent grid = as many panels as can be resident (32 waves per CU): per-iteration
-    // throughput is highest with two 13-wave panels per CU, and with only ~2 instances per column
-    // a smaller grid loses more to the end-of-queue tail than it gains from refills (measured on
-    // C4).  Larger batches keep every resident column busy through the queue.
+struct Panel2Lds {
+    float4 Wl[2][T * 64];  // fragment order, per panel: w    (B of GEMM 1)
+    float4 Zh[2][T * 64];  //                            zhat (B of GEMM 2)
+    float4 Gp[2][T * 64];  //                            g_P rows
+    float4 Pd[2][T * 64];  //                            p_D rows
+    PanelSlot slots[2][T];
+};
+
+// The work of one wave role, NU = units per wave (2: double, 1: single, 0: idle).  Each role
+// is its own instantiation, so a single wave does not carry a double's registers; every role
+// executes the same sequence of barriers.
+template <int T, int NU>
+__device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<T>& L, int t, int p0,
+                                           bool pair, int items, int count) {
+    const int lane = threadIdx.x & 63;
+    const int j = lane >> 4, c = lane & 15;
+    const int n = a.n, m = a.m, N = a.N, K = a.check_every;
+    const int abytes = T * T * 1024;
+    const __amdgpu_buffer_rsrc_t PA1 =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.frag), 0, abytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t PA2 = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)((const char*)a.frag + abytes), 0, abytes, 0x00020000);
+    const bool use_tol = a.tol > 0.0;
+    const bool fresh = a.v_begin == 0;
+    const bool carry = a.v_end < N;
+    const int voff = t * 1024 + lane * 16;
+    const int slot = t * 64 + lane;
+    constexpr int Q = NU > 0 ? NU : 1;  // array extent
+
+    for (int it = blockIdx.x; it < items; it += gridDim.x) {
+        bool act[Q];
+        int inst[Q];
+        float z[Q][4], y[Q][4], u[Q][4];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            act[q] = false;
+            inst[q] = 0;
+            if constexpr (NU == 0) continue;
+            const int pq = p0 + q;
+            const int k = 16 * (pair ? 2 * it + pq : it) + c;
+            act[q] = k < count;
+            inst[q] = act[q] ? (a.idx_in ? a.idx_in[k] : k) : 0;
+            float gp[4], pd[4], wv[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 * t + 4 * r + j;
+                const bool okn = act[q] && i < n, okm = act[q] && i < m;
+                const size_t b = (size_t)inst[q];
+                z[q][r] = okn ? a.z[b * n + i] : 0.0f;
+                gp[r] = okn ? a.gP[b * a.ld_gP + i] : 0.0f;
+                y[q][r] = okm ? a.y[b * m + i] : 0.0f;
+                pd[r] = okm ? (float)(a.gscale * (double)a.g[b * a.ld_g + i]) : 0.0f;
+                if (fresh) {  // w_0 = y_0 + beta_0 (y_0 - y_{-1}), y_{-1} = y_0
+                    wv[r] = __builtin_fmaf(a.beta[0], y[q][r] - y[q][r], y[q][r]);
+                    u[q][r] = 0.0f;
+                } else {
+                    wv[r] = okm ? a.wc[b * m + i] : 0.0f;
+                    u[q][r] = okm && use_tol ? a.uc[b * m + i] : 0.0f;
+                }
+            }
+            L.Gp[pq][slot] = make_float4(gp[0], gp[1], gp[2], gp[3]);
+            L.Pd[pq][slot] = make_float4(pd[0], pd[1], pd[2], pd[3]);
+            L.Wl[pq][slot] = make_float4(wv[0], wv[1], wv[2], wv[3]);
+            if (fresh && use_tol) L.Zh[pq][slot] = make_float4(z[q][0], z[q][1], z[q][2], z[q][3]);
+        }
+        if (fresh && use_tol) {  // u = G_L z_{-1}
+            __syncthreads();
+            if constexpr (NU > 0) {
+                f32x4 c0, c1;
+                panel_gemm2<T, NU == 2>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, c0, c1);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) u[0][r] = c0[r];
+                if constexpr (NU == 2) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) u[Q - 1][r] = c1[r];
+                }
+            }
+        }
+        __syncthreads();
+
+        int v = a.v_begin;
+        float th = a.theta[v], bn = a.beta[v + 1];
+        while (true) {
+            const float th_next = a.theta[v + 1], bn_next = a.beta[v + 2];
+            ++v;
+            const bool chk = use_tol && (v % K) == 0;
+            const float omt = 1.0f - th;
+            // ---- GEMM 1 + epilogue: zhat = -ML w - g_P (8b), z = (1-th) z + th zhat (8c) ----
+            if constexpr (NU > 0) {
+                f32x4 acc[2];
+                panel_gemm2<T, NU == 2>(PA1, L.Wl[p0], L.Wl[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1]);
+#pragma unroll
+                for (int q = 0; q < Q; ++q) {
+                    const float4 g4 = L.Gp[p0 + q][slot];
+                    const float gp[4] = {g4.x, g4.y, g4.z, g4.w};
+                    float zh[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        zh[r] = acc[q][r] - gp[r];
+                        const float zn = __builtin_fmaf(omt, z[q][r], th * zh[r]);
+                        if (act[q]) z[q][r] = zn;
+                    }
+                    L.Zh[p0 + q][slot] = make_float4(zh[0], zh[1], zh[2], zh[3]);
+                }
+            }
+            __syncthreads();
+            // ---- GEMM 2 + epilogue: y+ = [w + G_L zhat + p_D]+ (8d), next w (8a) ----------
+            float violz[Q], violh[Q], wmin[Q];
+            double gap[Q];
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                violz[q] = violh[q] = -INFINITY;
+                wmin[q] = INFINITY;
+                gap[q] = 0.0;
+            }
+            if constexpr (NU > 0) {
+                f32x4 acc[2];
+                panel_gemm2<T, NU == 2>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1]);
+#pragma unroll
+                for (int q = 0; q < Q; ++q) {
+                    const float4 w4 = L.Wl[p0 + q][slot];
+                    const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+                    const float4 p4 = L.Pd[p0 + q][slot];
+                    const float pd[4] = {p4.x, p4.y, p4.z, p4.w};
+                    float wn[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float cv = acc[q][r];
+                        const float sv = (wv[r] + pd[r]) + cv;
+                        const float yp = (__builtin_fabsf(sv) + sv) * 0.5f;
+                        wn[r] = __builtin_fmaf(bn, yp - y[q][r], yp);
+                        if (use_tol) {
+                            const float un = __builtin_fmaf(omt, u[q][r], th * cv);
+                            if (act[q]) u[q][r] = un;
+                            if (chk && act[q] && (16 * t + 4 * r + j) < m) {
+                                const float tt = cv + pd[r];
+                                violh[q] = fmaxf(violh[q], tt);
+                                wmin[q] = fminf(wmin[q], wv[r]);
+                                gap[q] -= (double)wv[r] * (double)tt;
+                                violz[q] = fmaxf(violz[q], u[q][r] + pd[r]);
+                            }
+                        }
+                        if (act[q]) y[q][r] = yp;
+                    }
+                    if (act[q]) L.Wl[p0 + q][slot] = make_float4(wn[0], wn[1], wn[2], wn[3]);
+                }
+            }
+            th = th_next;
+            bn = bn_next;
+            __syncthreads();
+            if (!chk && v < a.v_end) continue;
+
+            // ---- Algorithm 1 test per column (tile partials through LDS) ----------------------
+            int code[Q];
+#pragma unroll
+            for (int q = 0; q < Q; ++q) code[q] = 0;
+            if (chk) {
+                if constexpr (NU > 0) {
+#pragma unroll
+                    for (int q = 0; q < Q; ++q) {
+#pragma unroll
+                        for (int o = 16; o < 64; o <<= 1) {
+                            violz[q] = fmaxf(violz[q], __shfl_xor(violz[q], o, 64));
+                            violh[q] = fmaxf(violh[q], __shfl_xor(violh[q], o, 64));
+                            wmin[q] = fminf(wmin[q], __shfl_xor(wmin[q], o, 64));
+                            gap[q] += __shfl_xor(gap[q], o, 64);
+                        }
+                        if (j == 0) {
+                            PanelSlot& S = L.slots[p0 + q][t];
+                            S.violz[c] = violz[q];
+                            S.violh[c] = violh[q];
+                            S.wmin[c] = wmin[q];
+                            S.gap[c] = gap[q];
+                        }
+                    }
+                }
+                __syncthreads();
+                if constexpr (NU > 0) {
+#pragma unroll
+                    for (int q = 0; q < Q; ++q) {
+                        if (!act[q]) continue;
+                        double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gq = 0.0;
+#pragma unroll 1
+                        for (int s2 = 0; s2 < T; ++s2) {  // not unrolled: keeps the test's
+                            const PanelSlot& S = L.slots[p0 + q][s2];  // registers off the loop
+                            vz = fmax(vz, (double)S.violz[c]);
+                            vh = fmax(vh, (double)S.violh[c]);
+                            wm = fmin(wm, (double)S.wmin[c]);
+                            gq += S.gap[c];
+                        }
+                        if (vz * a.L <= a.tol) code[q] = 1;
+                        else if ((vh * a.L <= a.tol) && (wm >= 0.0) && (gq * a.L <= a.tol)) code[q] = 2;
+                    }
+                }
+            }
+            // ---- finished columns: results out ---------------------------------------------
+            bool any = false;
+            if constexpr (NU > 0) {
+#pragma unroll
+                for (int q = 0; q < Q; ++q) {
+                    if (act[q] && (code[q] != 0 || v >= N)) {
+                        const float4 h4 = L.Zh[p0 + q][slot];
+                        const float zh[4] = {h4.x, h4.y, h4.z, h4.w};
+                        const size_t b = (size_t)inst[q];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int i = 16 * t + 4 * r + j;
+                            if (i < n) a.z[b * n + i] = code[q] == 2 ? zh[r] : z[q][r];  // (B): zhat
+                            if (i < m) a.y[b * m + i] = y[q][r];
+                        }
+                        if (t == 0 && j == 0) {
+                            a.iters[b] = v;
+                            a.conv[b] = code[q];
+                        }
+                        act[q] = false;
+                    }
+                    any = any || act[q];
+                }
+            }
+            if (v >= a.v_end || !__syncthreads_or(any ? 1 : 0)) break;
+        }
+        // ---- phase end: park the survivors -----------------------------------------------
+        if constexpr (NU > 0) {
+            if (carry && v >= a.v_end) {
+#pragma unroll
+                for (int q = 0; q < Q; ++q) {
+                    if (act[q]) {
+                        const float4 w4 = L.Wl[p0 + q][slot];
+                        const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+                        const size_t b = (size_t)inst[q];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int i = 16 * t + 4 * r + j;
+                            if (i < n) a.z[b * n + i] = z[q][r];
+                            if (i < m) {
+                                a.y[b * m + i] = y[q][r];
+                                a.wc[b * m + i] = wv[r];
+                                if (use_tol) a.uc[b * m + i] = u[q][r];
+                            }
+                        }
+                    }
+                    if (t == 0) {  // the tile-0 owner of panel p0+q appends its survivors
+                        const unsigned long long live = __ballot(act[q] && j == 0);
+                        int base = 0;
+                        if (lane == 0) base = atomicAdd(a.count_out, (int)__popcll(live));
+                        base = __shfl(base, 0, 64);
+                        if (act[q] && j == 0)
+                            a.idx_out[base + (int)__popcll(live & ((1ull << lane) - 1ull))] = inst[q];
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <int T>
+__global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
+    static_assert(T > 8 && T <= 16, "panel pairs need 8 < T <= 16");
+    constexpr int D = 2 * T - 16;  // double waves
+    __shared__ Panel2Lds<T> L;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int count = a.count_in ? __builtin_amdgcn_readfirstlane(*a.count_in) : a.batch;
+    const int panels = (count + 15) / 16;
+    const bool pair = panels > (int)gridDim.x;
+    const int items = pair ? (panels + 1) / 2 : panels;
+    if (pair) {
+        if (w < D) panel2_run<T, 2>(a, L, w, 0, true, items, count);
+        else panel2_run<T, 1>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
+    } else {
+        if (w < T) panel2_run<T, 1>(a, L, w, 0, false, items, count);
+        else panel2_run<T, 0>(a, L, 0, 0, false, items, count);
+    }
+}
+
+size_t panel_work_bytes(int m, int batch) {
+    // idx ping-pong [2][batch] | phase counts [kPanelMaxPhases] | carried w, u [batch][m] each
+    return sizeof(int) * (2 * (size_t)batch + kPanelMaxPhases) + 2 * sizeof(float) * (size_t)batch * m;
+}
+
+template <int T>
+static void launch_panel_kernel(const SolveArgs<float>& a, int grid, hipStream_t s) {
+    if constexpr (T > 8)
+        hipLaunchKernelGGL((gpad_panel2_kernel<T>), dim3(grid), dim3(1024), 0, s, a);
+    else
+        hipLaunchKernelGGL((gpad_panel_kernel<T>), dim3(grid), dim3(64 * T), 0, s, a);
+}
+
+template <int T>
+static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
+    // Grid = resident workgroups: a panel-pair workgroup (T > 8) fills a CU; T-wave panels
+    // (T <= 8) share one, 32/T of them.  Workgroups walk their panels grid-stride.
     const int panels = (a.batch + 15) / 16;
-    const int resident = a.num_cus * (32 / T > 0 ? 32 / T : 1);
+    const int resident = T > 8 ? a.num_cus : a.num_cus * (32 / T);
     int grid = panels < resident ? panels : resident;
-    if (const char* cap = std::getenv("GPAD_PANEL_MAX_GRID")) {  // test knob: force refills
+    if (const char* cap = std::getenv("GPAD_PANEL_MAX_GRID")) {  // test knob: grid-stride panels
         const int c = std::atoi(cap);
         if (c > 0 && c < grid) grid = c;
     }
-    if (grid < panels)
-        hipLaunchKernelGGL((gpad_panel_kernel<T, true>), dim3(grid), dim3(64 * T), 0, s, a);
-    else
-        hipLaunchKernelGGL((gpad_panel_kernel<T, false>), dim3(grid), dim3(64 * T), 0, s, a);
-    return hipGetLastError();
+    const bool phased = a.tol > 0.0 && a.pwork != nullptr;
+    if (!phased) {  // fixed N (or no workspace): one phase, nothing carried
+        a.v_begin = 0;
+        a.v_end = a.N;
+        a.idx_in = nullptr;
+        a.count_in = nullptr;
+        launch_panel_kernel<T>(a, grid, s);
+        return hipGetLastError();
+    }
+    int* idx0 = reinterpret_cast<int*>(a.pwork);
+    int* idx1 = idx0 + a.batch;
+    int* counts = idx1 + a.batch;
+    float* wc = reinterpret_cast<float*>(counts + kPanelMaxPhases);
+    a.wc = wc;
+    a.uc = wc + (size_t)a.batch * a.m;
+    hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * kPanelMaxPhases, s);
+    if (e != hipSuccess) return e;
+    // phase length: a multiple of the test period (phases end right after a test); default
+    // four tests, doubling after 16 phases so a long tail costs O(log N) launches
+    int len = 4 * a.check_every;
+    if (const char* pl = std::getenv("GPAD_PANEL_PHASE")) {
+        const int q = std::atoi(pl);
+        if (q > 0) len = q;
+    }
+    len = ((len + a.check_every - 1) / a.check_every) * a.check_every;
+    int v0 = 0;
+    for (int ph = 0; v0 < a.N; ++ph) {
+        int plen = len;
+        if (ph >= 16) plen = len << (ph - 15 < 20 ? ph - 15 : 20);
+        if (ph >= kPanelMaxPhases - 1) plen = a.N;  // last slot: run to N
+        const int v1 = (a.N - v0 <= plen) ? a.N : v0 + plen;
+        a.v_begin = v0;
+        a.v_end = v1;
+        a.idx_in = ph ? ((ph & 1) ? idx0 : idx1) : nullptr;
+        a.count_in = ph ? counts + ph - 1 : nullptr;
+        a.idx_out = (ph & 1) ? idx1 : idx0;
+        a.count_out = counts + ph;
+        launch_panel_kernel<T>(a, grid, s);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        v0 = v1;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_panel(const SolveArgs<float>& a, hipStream_t s, bool* supported) {

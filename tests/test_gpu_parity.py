@@ -83,11 +83,14 @@ def test_algorithm1_termination_bitexact(gpu, kernel, name):
 
 
 @pytest.mark.parametrize("kernel", KERNELS)
-@pytest.mark.parametrize("nm", [(200, 200), (37, 53), (1, 5), (5, 1), (64, 64), (65, 129), (208, 180)])
+@pytest.mark.parametrize("nm", [(200, 200), (37, 53), (1, 5), (5, 1), (64, 64), (65, 129), (208, 180),
+                                (256, 250), (144, 129)])
 def test_shapes_bitexact_vs_oracle(gpu, oracle, kernel, nm):
     """C2 (200 x 200) and ragged shapes (not multiples of 4 / 64, single row or column)."""
     from gpad_mpc import problems
     n, m = nm
+    if kernel == "resident" and max(n, m) > 208:
+        pytest.skip("resident kernel holds at most 208 rows per lane chain")
     qp = problems.synthetic_qp(n, m, seed=11)
     ML, M, G, g = (qp.ML.astype(np.float32), qp.M.astype(np.float32), qp.G.astype(np.float32),
                    qp.g.astype(np.float32))
@@ -166,14 +169,20 @@ def test_panel_two_wave_panels_large_batch(gpu, oracle, nm):
         assert_bitexact(y[b], yo, f"instance {b} y")
 
 
-@pytest.mark.parametrize("grid", [1, 3])
+@pytest.mark.parametrize("grid,phase", [(1, 0), (3, 0), (0, 10), (3, 20), (0, 0)])
 @pytest.mark.parametrize("tol,N", [(1e-4, 3000), (0.0, 57)])
-def test_panel_queue_refill_bitexact(gpu, oracle, monkeypatch, grid, tol, N):
-    """Continuous batching: with the persistent grid capped, columns finish at different times
-    and pull new instances; every instance must still match its own oracle solve exactly."""
+@pytest.mark.parametrize("nm,B", [((40, 72), 150), ((150, 130), 40), ((131, 256), 37)])
+def test_panel_phased_compaction_bitexact(gpu, oracle, monkeypatch, grid, phase, tol, N, nm, B):
+    """Phased compaction + grid-stride panels (+ panel pairs for T > 8 when panels outnumber
+    workgroups): survivors of each phase are re-packed into new panels (different columns,
+    workgroups, pairs and phases); every instance must still match its own oracle solve
+    exactly, including its iteration count."""
     from gpad_mpc import problems
-    monkeypatch.setenv("GPAD_PANEL_MAX_GRID", str(grid))
-    B, n, m = 150, 40, 72
+    if grid:
+        monkeypatch.setenv("GPAD_PANEL_MAX_GRID", str(grid))
+    if phase:
+        monkeypatch.setenv("GPAD_PANEL_PHASE", str(phase))
+    n, m = nm
     qp = problems.synthetic_qp(n, m, batch=B, seed=8)
     ML, G = qp.ML.astype(np.float32), qp.G.astype(np.float32)
     M, g = qp.M.astype(np.float32), qp.g.astype(np.float32)

@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gpu-dualgradient-mpc_amd"))
 
 
-def case(kernel, n, m, batch, N, shared=True, reps=3):
+def case(kernel, n, m, batch, N, shared=True, reps=3, tol=0.0):
     import torch
     import gpad_mpc
     from gpad_mpc import _lib, problems
@@ -41,18 +41,18 @@ def case(kernel, n, m, batch, N, shared=True, reps=3):
     y = torch.zeros(batch, m, device=dev)
     with gpad_mpc.GpadSolver(0) as s:
         s.setup(ML, G, L, n=n, m=m, batch=batch, shared=shared, kernel=kc)
-        s.run(z, y, M, g, N, 0.0)
+        s.run(z, y, M, g, N, tol)
         best = 1e30
         for _ in range(reps):
             z.zero_()
             y.zero_()
-            st = s.run(z, y, M, g, N, 0.0)
+            st = s.run(z, y, M, g, N, tol)
             best = min(best, st["kernel_ms"])
     us_it = best * 1e3 / N
     F = 4 * n * m + 5 * m + 4 * n
     B = 4 * (2 * n * m + 4 * m + 3 * n) if not shared else 4 * (2 * n * m / batch + 4 * m + 3 * n)
     rate = batch * N / (best / 1e3)
-    return dict(kernel=st["kernel"], n=n, m=m, batch=batch, shared=shared, N=N,
+    return dict(kernel=st["kernel"], n=n, m=m, batch=batch, shared=shared, N=N, tol=tol,
                 us_per_iter=round(us_it, 3), inst_it_per_s=rate, tflops=rate * F / 1e12,
                 alg_gbs=rate * B / 1e9)
 
@@ -61,6 +61,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--only", default="")
+    ap.add_argument("--tol", type=float, default=0.0,
+                    help="> 0: run the Algorithm-1 test path (tiny tol: never converges, N its)")
     args = ap.parse_args()
     cases = [
         ("resident", 40, 180, 1, 2000, True),
@@ -80,7 +82,7 @@ def main():
     for c in cases:
         if args.only and args.only not in c[0]:
             continue
-        print(json.dumps(case(*c)), flush=True)
+        print(json.dumps(case(*c, tol=args.tol)), flush=True)
 
 
 if __name__ == "__main__":
