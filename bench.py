@@ -101,6 +101,40 @@ def cpu_baseline(n, m, ML, G, L, M, g, iters_per_instance, budget_s=12.0):
             "single_thread_value": N / t1, "seconds": round(dt, 2)}
 
 
+def phase_schedule(N, K=10, len0=None):
+    """The panel kernel's phase boundaries (csrc/gpad_panel.hip launch_panel_t): phases of 4K
+    iterations, doubling after the 10th, the last one ending at N."""
+    len0 = len0 or 4 * K
+    out, v0, ph = [], 0, 0
+    while v0 < N:
+        plen = len0 if ph < 10 else len0 << min(ph - 9, 20)
+        v1 = N if N - v0 <= plen else v0 + plen
+        out.append((v0, v1))
+        v0, ph = v1, ph + 1
+    return out
+
+
+def phase_util(iters, N, K=10):
+    """Column utilisation of phased compaction, estimated from the per-instance iteration
+    counts: a phase [v0, v1) packs its survivors (iters > v0) into 16-column panels that run
+    until v1 or their last column's end; useful = sum of iterations.  Also the number of phase
+    launches per solve and how many of them had survivors."""
+    it = iters.astype(np.int64)  # survivors keep (roughly) index order in the kernel's lists
+    executed = 0
+    live_launches = 0
+    phases = phase_schedule(N, K)
+    for v0, v1 in phases:
+        surv = it[it > v0]
+        if surv.size == 0:
+            continue
+        live_launches += 1
+        for i in range(0, surv.size, 16):
+            executed += 16 * (min(v1, int(surv[i:i + 16].max())) - v0)
+    return {"column_util_est": float(it.sum() / executed) if executed else None,
+            "launches_per_solve": len(phases), "launches_with_survivors": live_launches,
+            "min_iters": int(it.min()), "max_iters": int(it.max())}
+
+
 def traffic_from_profile(kernel_prefix):
     """HBM bytes per launch of the dominant kernel from the committed PMC profile of this same
     bench command (tools/profile.sh -> profiles/r01_bench_summary.json; FETCH_SIZE x2 +
@@ -240,14 +274,7 @@ def main():
     torch.cuda.synchronize(dev)
     iters_host = np.zeros(B, np.int32)
     st0 = solver.last_stats(iters=iters_host)
-    # batching losses of lockstep panels (16 instances per MFMA column block; with the whole
-    # batch resident, instance i runs in panel i // 16): columns that converged early idle until
-    # their panel's slowest instance (panel_util); panels that finished early leave their CU
-    # share to the others until the slowest panel ends (tail_util)
-    pm = np.array([iters_host[i:i + 16].max() for i in range(0, B, 16)], np.float64)
-    util = {"panel_util": float(iters_host.sum() / (16.0 * pm.sum())) if pm.sum() else None,
-            "tail_util": float(pm.mean() / pm.max()) if pm.max() else None,
-            "min_iters": int(iters_host.min()), "max_iters": int(iters_host.max())}
+    util = phase_util(iters_host, args.max_iters, 10)
 
     if world > 1:
         dist.barrier()
@@ -291,6 +318,9 @@ def main():
         # C2 single instance (config 1): latency kernel, fixed 1000 iterations
         one = dict()
         traffic, traffic_src = traffic_from_profile("gpad::gpad_" + st["kernel"])
+        launches = util["launches_per_solve"] if st["kernel"] == "panel" else 1
+        if traffic is not None:
+            traffic *= launches  # PMC values are per phase launch; one solve = `launches` of them
         with gpad_mpc.GpadSolver(dev.index, stream=stream.cuda_stream) as s1:
             s1.setup(dML, dG, L32, n=n, m=m, batch=1)
             z1 = torch.zeros(1, n, device=dev)
@@ -335,10 +365,13 @@ def main():
             "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved_tf / FP32_PEAK_TFLOPS,
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel_ms": avg_kernel_s * 1e3,
+                         "kernel_ms": avg_kernel_s * 1e3, "launches_per_solve": launches,
                          "note": "fp32 matrix-core bound (shared matrices stay in L2, traffic = "
                                  "per-instance vectors); achieved = useful flops (F = 4nm+5m+4n "
-                                 "per executed instance-iteration) / avg launch time"},
+                                 "per executed instance-iteration) of one solve / its device time "
+                                 "(HIP events around the solve's chain of phase launches; rocprof "
+                                 "avg phase duration x launches_per_solve gives the same time); "
+                                 "traffic = PMC HBM bytes per phase launch x launches_per_solve"},
             "cpu_baseline": cpu,
             "legs": extra,
         }

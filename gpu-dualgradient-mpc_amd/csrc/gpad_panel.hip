@@ -391,6 +391,52 @@ __device__ __forceinline__ void panel_gemm2(__amdgpu_buffer_rsrc_t PA, const flo
     }
 }
 
+// A fragments of the first PD k-blocks, issued early (before the barrier that precedes the
+// GEMM: A is the constant matrix, so its L2 latency need not start at the barrier).
+template <int T, int PD>
+__device__ __forceinline__ void panel_a_prefetch(__amdgpu_buffer_rsrc_t PA, int voff, float4 (&ap)[PD]) {
+#pragma unroll
+    for (int p = 0; p < PD; ++p)
+        if (p < T) ap[p] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, p * T * 1024, 0));
+}
+
+// panel_gemm2 with an A ring PD blocks deep, seeded by panel_a_prefetch.
+template <int T, bool DUAL, int PD>
+__device__ __forceinline__ void panel_gemm3(__amdgpu_buffer_rsrc_t PA, const float4* B0, const float4* B1,
+                                            int voff, int lane, f32x4& acc0, f32x4& acc1,
+                                            const float4 (&ap)[PD]) {
+    acc0 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    acc1 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    constexpr int R = PD + 1;
+    float4 a[R], b0[2], b1[2];
+#pragma unroll
+    for (int p = 0; p < PD; ++p) a[p] = ap[p];
+    b0[0] = B0[lane];
+    if constexpr (DUAL) b1[0] = B1[lane];
+#pragma unroll
+    for (int kb = 0; kb < T; ++kb) {
+        const int cur = kb & 1, nxt = cur ^ 1;
+        const float4 ak = a[kb % R];
+        if (kb + PD < T)
+            a[(kb + PD) % R] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb + PD) * T * 1024, 0));
+        if (kb + 1 < T) {
+            b0[nxt] = B0[(kb + 1) * 64 + lane];
+            if constexpr (DUAL) b1[nxt] = B1[(kb + 1) * 64 + lane];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, b0[cur].x, acc0, 0, 0, 0);
+        if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, b1[cur].x, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, b0[cur].y, acc0, 0, 0, 0);
+        if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, b1[cur].y, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, b0[cur].z, acc0, 0, 0, 0);
+        if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, b1[cur].z, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, b0[cur].w, acc0, 0, 0, 0);
+        if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, b1[cur].w, acc1, 0, 0, 0);
+        if constexpr (DUAL) asm volatile("" : "+v"(acc0), "+v"(acc1)::"memory");
+        else asm volatile("" : "+v"(acc0)::"memory");
+    }
+}
+
 template <int T>
 struct Panel2Lds {
     float4 Wl[2][T * 64];  // fragment order, per panel: w    (B of GEMM 1)
@@ -403,6 +449,13 @@ struct Panel2Lds {
 // The work of one wave role, NU = units per wave (2: double, 1: single, 0: idle).  Each role
 // is its own instantiation, so a single wave does not carry a double's registers; every role
 // executes the same sequence of barriers.
+#ifndef PANEL_PD1
+#define PANEL_PD1 2  // A-ring depth of single waves
+#endif
+#ifndef PANEL_PD2
+#define PANEL_PD2 1  // ... and of double waves (2 spills at 128 VGPRs; measured no better)
+#endif
+
 template <int T, int NU>
 __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<T>& L, int t, int p0,
                                            bool pair, int items, int count) {
@@ -472,6 +525,9 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
         }
         __syncthreads();
 
+        constexpr int PD = NU == 2 ? PANEL_PD2 : PANEL_PD1;
+        float4 ap[PD];  // A blocks of the next GEMM, in flight across the barrier before it
+        if constexpr (NU > 0) panel_a_prefetch<T, PD>(PA1, voff, ap);
         int v = a.v_begin;
         float th = a.theta[v], bn = a.beta[v + 1];
         while (true) {
@@ -482,7 +538,8 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             // ---- GEMM 1 + epilogue: zhat = -ML w - g_P (8b), z = (1-th) z + th zhat (8c) ----
             if constexpr (NU > 0) {
                 f32x4 acc[2];
-                panel_gemm2<T, NU == 2>(PA1, L.Wl[p0], L.Wl[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1]);
+                panel_gemm3<T, NU == 2, PD>(PA1, L.Wl[p0], L.Wl[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1], ap);
+                panel_a_prefetch<T, PD>(PA2, voff, ap);
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
                     const float4 g4 = L.Gp[p0 + q][slot];
@@ -509,7 +566,8 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             }
             if constexpr (NU > 0) {
                 f32x4 acc[2];
-                panel_gemm2<T, NU == 2>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1]);
+                panel_gemm3<T, NU == 2, PD>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1], ap);
+                panel_a_prefetch<T, PD>(PA1, voff, ap);
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
                     const float4 w4 = L.Wl[p0 + q][slot];
@@ -709,7 +767,8 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * kPanelMaxPhases, s);
     if (e != hipSuccess) return e;
     // phase length: a multiple of the test period (phases end right after a test); default
-    // four tests, doubling after 16 phases so a long tail costs O(log N) launches
+    // four tests, doubling after 10 phases so a long tail costs O(log N) launches (a phase with
+    // no survivors left costs one empty launch, ~5 us)
     int len = 4 * a.check_every;
     if (const char* pl = std::getenv("GPAD_PANEL_PHASE")) {
         const int q = std::atoi(pl);
@@ -719,7 +778,7 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     int v0 = 0;
     for (int ph = 0; v0 < a.N; ++ph) {
         int plen = len;
-        if (ph >= 16) plen = len << (ph - 15 < 20 ? ph - 15 : 20);
+        if (ph >= 10) plen = len << (ph - 9 < 20 ? ph - 9 : 20);
         if (ph >= kPanelMaxPhases - 1) plen = a.N;  // last slot: run to N
         const int v1 = (a.N - v0 <= plen) ? a.N : v0 + plen;
         a.v_begin = v0;
