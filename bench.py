@@ -205,6 +205,52 @@ def distinct_leg(dev, n, m, batch=8192, N=100):
             "iters_per_s": batch * N / (st["kernel_ms"] / 1e3)}
 
 
+def closed_loop_leg(dev, batch=8192, steps=20, N=100, cpu=True):
+    """gpad.m:79-95 closed loop on the device for a batch of battery
+    packs (C1 plant: n_u = 4 cells, horizon 10 -> n = 40, m = 180), each MPC step = per-state
+    QP data + 100 GPAD iterations (acceldualgrad's fixed count) + plant update.  MPC steps/s
+    (all packs) and GPAD iterations/s; CPU: the oracle's closed loop (fp32 port, 1 thread) on
+    a bounded sample of packs."""
+    import torch
+
+    import gpad_mpc
+    from gpad_mpc import problems
+    qp, pl = problems.battery_plant(4, 10)
+    f32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)  # noqa: E731
+    L32 = float(np.float32(qp.L))
+    X0 = (np.random.default_rng(3).random((batch, 4)) - 0.5).astype(np.float32)
+    with gpad_mpc.GpadSolver(dev.index or 0, stream=torch.cuda.current_stream(dev).cuda_stream) as s:
+        s.setup(f32(qp.ML), f32(qp.G), L32, n=qp.n, m=qp.m, batch=batch)
+        s.setup_plant(f32(pl.PM), f32(pl.Pg), g0=f32(pl.g0), A=f32(pl.A), B=f32(pl.B))
+        X = torch.from_numpy(X0).to(dev)
+        Z = torch.zeros(batch, qp.n, device=dev)
+        Y = torch.zeros(batch, qp.m, device=dev)
+        s.closed_loop(X, Z, Y, steps, N, 0.0)
+        X.copy_(torch.from_numpy(X0))
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        st = s.closed_loop(X, Z, Y, steps, N, 0.0)
+        torch.cuda.synchronize(dev)
+        wall = time.perf_counter() - t0
+    out = {"config": f"{batch} battery packs (n_u=4, N=10: n={qp.n}, m={qp.m}), {steps} MPC steps "
+                     f"x {N} GPAD iterations, cold start (gpad.m)", "kernel": st["kernel"],
+           "mpc_steps_per_s": batch * steps / wall, "iters_per_s": batch * steps * N / wall,
+           "device_ms": st["kernel_ms"], "wall_ms": wall * 1e3}
+    if cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle
+        O = pyoracle.Oracle()
+        MGneg, GL, _ = O.scale(np.float32(qp.ML), np.float32(qp.G), np.float32(qp.g), np.float32(L32))
+        k, t0 = 0, time.perf_counter()
+        while k < 64 and time.perf_counter() - t0 < 3.0:
+            O.closed_loop_f32(X0[k], MGneg, GL, L32, pl.PM, pl.Pg, pl.A, pl.B, steps, N, g0=pl.g0)
+            k += 1
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"mpc_steps_per_s": k * steps / dt, "cores": 1, "kind": "port",
+                               "sample": f"{k} packs x {steps} steps (oracle closed loop, fp32)"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -339,6 +385,7 @@ def main():
         if not args.no_extra and world == 1:
             extra["hbm_bound_c5"] = hbm_leg(dev)
             extra["distinct_c2_batch"] = distinct_leg(dev, n, m)
+            extra["closed_loop_battery"] = closed_loop_leg(dev, cpu=not args.no_cpu)
         out = {
             "metric": "GPAD iterations/s (instance-iterations, solve to eps=1e-4)",
             "value": value,

@@ -27,6 +27,8 @@
 #include <cfloat>
 #include <cmath>
 
+#include <utility>
+
 #include "gpad_internal.h"
 
 namespace gpad {
@@ -282,34 +284,78 @@ template hipError_t launch_stream<double>(const SolveArgs<double>&, hipStream_t)
 // same register array r[] (they live in different waves).  KA/KB are compile-time, so the
 // chains carry no per-step predicates: padded steps are fma(0, 0, acc) = acc.
 //
-// The broadcast vector is read one float4 (ds_read_b128, all lanes the same address) per
-// 4-step group, kResAhead groups ahead into a ring of registers (compile-time slots, no
-// copies).  An empty asm that reads/writes acc and clobbers memory closes each group: later
-// LDS reads cannot be hoisted above it (else all K/4 reads issue at once and r[] spills), and
-// being volatile it pins the chain in place (the compiler cannot sink it into the `live`
-// branch of the caller).
-constexpr int kResAhead = 3;
-constexpr int kResRing = kResAhead + 1;
+// The broadcast vector reaches the lanes through DPP, not through LDS bandwidth: each 16-lane
+// row of the wave reads the same 64 consecutive elements (lane l: a float4 at 4*(l & 15)), and
+// step k of the chain is `v_fmac_f32_dpp acc, w4[k%4], r[k] row_newbcast:(k%64)/4` -- the
+// element is broadcast from lane (k%64)/4 of each row inside the FMA itself.  A wave thus reads
+// 64 elements per ds_read_b128 with 16 distinct addresses (a same-address float4 per 4 steps,
+// all 64 lanes, made the chains LDS-bandwidth bound: ~10 cycles per step with four waves).
+// v_fmac_f32 is a single-rounding fused multiply-add, so the chain is still exactly the
+// reference's sequential fmaf order.  One 64-element group is prefetched ahead; an empty asm
+// that reads/writes acc and clobbers memory closes each group (bounds the prefetch, pins the
+// chain in place).  The first use of each ring register in a group carries `s_nop 1`: a DPP
+// read 2 wait states after a VALU write of its source (only if the compiler ever copies a ring
+// value with a VALU move; the inline asm hides the DPP from the hazard recognizer).
+// 16 steps per asm statement (the compiler separates inline-asm statements with a wait state,
+// so few, long statements keep the chain issue-bound).  Steps KI..KI+15 are elements
+// 16J..16J+15 of the current 64-element group: lanes 4J..4J+3 of each row, components x..w.
+#define GPAD_FMAC(SRC, R, LANE) \
+    "v_fmac_f32_dpp %0, %" #SRC ", %" #R " row_newbcast:%" #LANE " row_mask:0xf bank_mask:0xf\n\t"
+#define GPAD_FMAC16                                                                            \
+    GPAD_FMAC(1, 5, 21) GPAD_FMAC(2, 6, 21) GPAD_FMAC(3, 7, 21) GPAD_FMAC(4, 8, 21)             \
+    GPAD_FMAC(1, 9, 22) GPAD_FMAC(2, 10, 22) GPAD_FMAC(3, 11, 22) GPAD_FMAC(4, 12, 22)          \
+    GPAD_FMAC(1, 13, 23) GPAD_FMAC(2, 14, 23) GPAD_FMAC(3, 15, 23) GPAD_FMAC(4, 16, 23)         \
+    GPAD_FMAC(1, 17, 24) GPAD_FMAC(2, 18, 24) GPAD_FMAC(3, 19, 24) GPAD_FMAC(4, 20, 24)
 
+template <int KLEN, int K, int KI, int J>
+__device__ __forceinline__ void chain_step16(float& acc, const float4& c, const float (&r)[K]) {
+    static_assert(KLEN % 16 == 0, "chain lengths are multiples of 16");
+    if constexpr (KI < KLEN) {
+#define GPAD_OPS                                                                                  \
+    : "+v"(acc)                                                                                   \
+    : "v"(c.x), "v"(c.y), "v"(c.z), "v"(c.w), "v"(r[KI + 0]), "v"(r[KI + 1]), "v"(r[KI + 2]),     \
+      "v"(r[KI + 3]), "v"(r[KI + 4]), "v"(r[KI + 5]), "v"(r[KI + 6]), "v"(r[KI + 7]),             \
+      "v"(r[KI + 8]), "v"(r[KI + 9]), "v"(r[KI + 10]), "v"(r[KI + 11]), "v"(r[KI + 12]),          \
+      "v"(r[KI + 13]), "v"(r[KI + 14]), "v"(r[KI + 15]), "i"(4 * J), "i"(4 * J + 1),              \
+      "i"(4 * J + 2), "i"(4 * J + 3)
+        if constexpr (J == 0)
+            asm("s_nop 1\n\t" GPAD_FMAC16 GPAD_OPS);
+        else
+            asm(GPAD_FMAC16 GPAD_OPS);
+#undef GPAD_OPS
+    }
+}
+#undef GPAD_FMAC16
+#undef GPAD_FMAC
+
+template <int KLEN, int K, int BASE, int... J>
+__device__ __forceinline__ void chain_group(float& acc, const float4& c, const float (&r)[K],
+                                            std::integer_sequence<int, J...>) {
+    (chain_step16<KLEN, K, BASE + 16 * J, J>(acc, c, r), ...);
+}
+
+template <int KLEN, int K, int H>
+__device__ __forceinline__ void chain_groups(float& acc, float4 (&ring)[2], const float (&r)[K],
+                                             const float* v, int q) {
+    constexpr int NH = (KLEN + 63) / 64;
+    if constexpr (H < NH) {
+        if constexpr (H + 1 < NH) ring[(H + 1) & 1] = *reinterpret_cast<const float4*>(v + 64 * (H + 1) + q);
+        chain_group<KLEN, K, 64 * H>(acc, ring[H & 1], r, std::make_integer_sequence<int, 4>{});
+        asm volatile("" : "+v"(acc) : : "memory");
+        chain_groups<KLEN, K, H + 1>(acc, ring, r, v, q);
+    }
+}
+
+// acc = sum_k r[k] * v[k], k = 0..KLEN-1, as one fmaf chain in ascending k.  v: LDS, padded to a
+// multiple of 64 elements (the last group's float4 reads may run past KLEN).
 template <int KLEN, int K>
 __device__ __forceinline__ float chain_regs(const float (&r)[K], const float* v) {
     static_assert(KLEN % 4 == 0 && KLEN <= K, "bad chain length");
-    constexpr int G = KLEN / 4;
-    float4 ring[kResRing];
-#pragma unroll
-    for (int g = 0; g < kResAhead && g < G; ++g) ring[g] = *reinterpret_cast<const float4*>(v + 4 * g);
+    const int q = 4 * (threadIdx.x & 15);
+    float4 ring[2];
+    ring[0] = *reinterpret_cast<const float4*>(v + q);
     float acc = 0.0f;
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        if (g + kResAhead < G)
-            ring[(g + kResAhead) % kResRing] = *reinterpret_cast<const float4*>(v + 4 * (g + kResAhead));
-        const float4 c = ring[g % kResRing];
-        acc = __builtin_fmaf(r[4 * g + 0], c.x, acc);
-        acc = __builtin_fmaf(r[4 * g + 1], c.y, acc);
-        acc = __builtin_fmaf(r[4 * g + 2], c.z, acc);
-        acc = __builtin_fmaf(r[4 * g + 3], c.w, acc);
-        asm volatile("" : "+v"(acc) : : "memory");
-    }
+    chain_groups<KLEN, K, 0>(acc, ring, r, v, q);
     return acc;
 }
 
@@ -319,9 +365,10 @@ constexpr int kResidentMaxRow = 208;
 template <int KA, int KB>
 __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(SolveArgs<float> a) {
     constexpr int K = KA > KB ? KA : KB;
-    __shared__ __attribute__((aligned(16))) float w_l[KA];   // w, broadcast to -ML rows
-    __shared__ __attribute__((aligned(16))) float zh_l[KB];  // zhat, broadcast to G/L rows
-    __shared__ __attribute__((aligned(16))) float z_l[KB];   // z_{-1}, to seed u = G_L z
+    constexpr int PA = (KA + 63) / 64 * 64, PB = (KB + 63) / 64 * 64;  // whole 64-element groups
+    __shared__ __attribute__((aligned(16))) float w_l[PA];   // w, broadcast to -ML rows
+    __shared__ __attribute__((aligned(16))) float zh_l[PB];  // zhat, broadcast to G/L rows
+    __shared__ __attribute__((aligned(16))) float z_l[PB];   // z_{-1}, to seed u = G_L z
     __shared__ CheckSlot slots[kResidentMaxThreads / 64];
 
     const int tid = threadIdx.x;
@@ -355,8 +402,8 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
         pdi = (float)(a.gscale * (double)a.g[(size_t)b * a.ld_g + row]);
         wi = __builtin_fmaf(a.beta[0], yi - yi, yi);
     }
-    for (int i = tid; i < KA; i += blockDim.x) w_l[i] = 0.0f;
-    for (int i = tid; i < KB; i += blockDim.x) {
+    for (int i = tid; i < PA; i += blockDim.x) w_l[i] = 0.0f;
+    for (int i = tid; i < PB; i += blockDim.x) {
         zh_l[i] = 0.0f;
         z_l[i] = 0.0f;
     }
