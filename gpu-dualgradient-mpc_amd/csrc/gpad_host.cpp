@@ -405,7 +405,10 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
         return GPAD_OK;
     }
     if constexpr (sizeof(T) == sizeof(float)) {
-        if (kernel == GPAD_KERNEL_PANEL || (kernel == GPAD_KERNEL_AUTO && d.shared && batch >= 64)) {
+        // shared matrices: panels once there are more instances than the latency kernel can
+        // run at ~one round (4 per CU: 4 x its 1/6-panel iteration time < one panel iteration)
+        const int panel_min = gpad::resident_supported(n, m) ? 4 * h->num_cus : 64;
+        if (kernel == GPAD_KERNEL_PANEL || (kernel == GPAD_KERNEL_AUTO && d.shared && batch > panel_min)) {
             if (tol > 0.0 && h->frag.p) {  // phased compaction workspace (gpad_panel.hip)
                 int rc = h->pwork.ensure(gpad::panel_work_bytes(m, batch));
                 if (rc) return rc;

@@ -45,12 +45,17 @@ struct SolveArgs {
     int* count_out;        // ... and counted here (device)
     float* wc;             // carried w  [batch][m]
     float* uc;             // carried u = G_L z [batch][m]
+    int fin_thresh;        // survivors <= this: the resident finisher takes them (0: none)
 };
 
 // launchers (return hipError_t of the launch)
 template <typename T>
 hipError_t launch_stream(const SolveArgs<T>& a, hipStream_t s);
 hipError_t launch_resident(const SolveArgs<float>& a, hipStream_t s, bool* supported);
+// resident kernel over the survivors of a phased panel solve (idx_in/count_in, carried state,
+// iterations v_begin..N); a no-op unless *count_in <= a.fin_thresh.  grid >= fin_thresh.
+hipError_t launch_resident_finisher(const SolveArgs<float>& a, int grid, hipStream_t s);
+bool resident_supported(int n, int m);
 hipError_t launch_panel(const SolveArgs<float>& a, hipStream_t s, bool* supported);
 size_t panel_frag_bytes(int n, int m, int batch);
 size_t panel_work_bytes(int m, int batch);

@@ -372,7 +372,14 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
     __shared__ CheckSlot slots[kResidentMaxThreads / 64];
 
     const int tid = threadIdx.x;
-    const int b = blockIdx.x;
+    // finisher mode (phased panel solves): this block takes survivor blockIdx.x of the list
+    const bool fin = a.count_in != nullptr;
+    if (fin) {
+        const int count = __builtin_amdgcn_readfirstlane(*a.count_in);
+        if (count > a.fin_thresh || (int)blockIdx.x >= count) return;
+    }
+    const int b = fin ? a.idx_in[blockIdx.x] : blockIdx.x;
+    const int v0 = fin ? a.v_begin : 0;  // resume at the carried iteration
     const int n = a.n, m = a.m;
     const int nA = (n + 63) >> 6;
     const int nwaves = blockDim.x >> 6;
@@ -400,7 +407,7 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
     } else if (live) {
         yi = yg[row];
         pdi = (float)(a.gscale * (double)a.g[(size_t)b * a.ld_g + row]);
-        wi = __builtin_fmaf(a.beta[0], yi - yi, yi);
+        wi = v0 == 0 ? __builtin_fmaf(a.beta[0], yi - yi, yi) : a.wc[(size_t)b * m + row];
     }
     for (int i = tid; i < PA; i += blockDim.x) w_l[i] = 0.0f;
     for (int i = tid; i < PB; i += blockDim.x) {
@@ -413,14 +420,17 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
     __syncthreads();
     const bool use_tol = a.tol > 0.0;
     float ui = 0.0f;  // u = G_L z: seeded once, then the 8c recursion (no extra chain per test)
-    if (use_tol && !isA) ui = chain_regs<KB, K>(r, z_l);
+    if (use_tol && !isA) {
+        const float us = chain_regs<KB, K>(r, z_l);  // (uniform control flow around the DPP chain)
+        ui = v0 == 0 ? us : (live ? a.uc[(size_t)b * m + row] : 0.0f);
+    }
 
     int it = 0;
     int done = 0;
     float zhi = 0.0f;
     // theta/beta are prefetched one iteration ahead (tables hold N + 2 entries)
-    float th = a.theta[0], bn = a.beta[1];
-    for (int v = 0; v < a.N; ++v) {
+    float th = a.theta[v0], bn = a.beta[v0 + 1];
+    for (int v = v0; v < a.N; ++v) {
         const float th_next = a.theta[v + 1], bn_next = a.beta[v + 2];
         const bool chk = a.tol > 0.0 && ((v + 1) % a.check_every) == 0;
         if (isA) {  // ---- 8b + 8c --------------------------------------------------------
@@ -492,12 +502,15 @@ static void launch_res_b(int kb, dim3 g, dim3 bl, hipStream_t st, const SolveArg
     }
 }
 
-hipError_t launch_resident(const SolveArgs<float>& a, hipStream_t st, bool* supported) {
-    const int mx = a.n > a.m ? a.n : a.m;
+bool resident_supported(int n, int m) {
+    const int mx = n > m ? n : m;
+    const int threads = 64 * (((n + 63) >> 6) + ((m + 63) >> 6));
+    return mx <= kResidentMaxRow && threads <= kResidentMaxThreads && n > 0 && m > 0;
+}
+
+static hipError_t launch_resident_grid(const SolveArgs<float>& a, int nblocks, hipStream_t st) {
     const int threads = 64 * (((a.n + 63) >> 6) + ((a.m + 63) >> 6));
-    *supported = mx <= kResidentMaxRow && threads <= kResidentMaxThreads && a.n > 0 && a.m > 0;
-    if (!*supported) return hipSuccess;
-    const dim3 grid(a.batch), block(threads);
+    const dim3 grid(nblocks), block(threads);
     const int ka = res_bucket(a.m), kb = res_bucket(a.n);  // A rows run over m, B rows over n
     switch (ka) {
         case 32: launch_res_b<32>(kb, grid, block, st, a); break;
@@ -509,6 +522,19 @@ hipError_t launch_resident(const SolveArgs<float>& a, hipStream_t st, bool* supp
         default: launch_res_b<208>(kb, grid, block, st, a); break;
     }
     return hipGetLastError();
+}
+
+hipError_t launch_resident(const SolveArgs<float>& a, hipStream_t st, bool* supported) {
+    *supported = resident_supported(a.n, a.m);
+    if (!*supported) return hipSuccess;
+    SolveArgs<float> b = a;
+    b.count_in = nullptr;  // whole batch, from iteration 0
+    b.idx_in = nullptr;
+    return launch_resident_grid(b, a.batch, st);
+}
+
+hipError_t launch_resident_finisher(const SolveArgs<float>& a, int grid, hipStream_t st) {
+    return launch_resident_grid(a, grid, st);
 }
 
 // =========================================================================================

@@ -171,6 +171,7 @@ __global__ __launch_bounds__(64 * T) void gpad_panel_kernel(SolveArgs<float> a) 
     const bool fresh = a.v_begin == 0;      // first phase: start from the caller's z0, y0
     const bool carry = a.v_end < N;         // not the last phase: park the survivors
     const int count = a.count_in ? __builtin_amdgcn_readfirstlane(*a.count_in) : a.batch;
+    if (a.count_in && count <= a.fin_thresh) return;  // the resident finisher has them
     const int panels = (count + 15) / 16;
 
     for (int p = blockIdx.x; p < panels; p += gridDim.x) {
@@ -713,6 +714,7 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
     __shared__ Panel2Lds<T> L;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int count = a.count_in ? __builtin_amdgcn_readfirstlane(*a.count_in) : a.batch;
+    if (a.count_in && count <= a.fin_thresh) return;  // the resident finisher has them
     const int panels = (count + 15) / 16;
     const bool pair = panels > (int)gridDim.x;
     const int items = pair ? (panels + 1) / 2 : panels;
@@ -750,6 +752,14 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
         if (c > 0 && c < grid) grid = c;
     }
     const bool phased = a.tol > 0.0 && a.pwork != nullptr;
+    // the tail of a phased solve (survivors <= 2 per CU) goes to the latency kernel: one
+    // instance per workgroup at ~1/6 of a panel's iteration time (when n, m fit it); measured
+    // on C4: 2/CU 5.42e8 it/s, 4/CU 5.35e8, 8/CU 5.35e8, no finisher 5.04e8
+    a.fin_thresh = phased && resident_supported(a.n, a.m) ? 2 * a.num_cus : 0;
+    if (const char* ft = std::getenv("GPAD_FINISH_THRESH")) {  // test / tuning knob
+        const int q = std::atoi(ft);
+        if (q >= 0 && a.fin_thresh) a.fin_thresh = q;
+    }
     if (!phased) {  // fixed N (or no workspace): one phase, nothing carried
         a.v_begin = 0;
         a.v_end = a.N;
@@ -787,6 +797,9 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
         a.count_in = ph ? counts + ph - 1 : nullptr;
         a.idx_out = (ph & 1) ? idx1 : idx0;
         a.count_out = counts + ph;
+        if (ph && a.fin_thresh) {  // few survivors left: one instance per workgroup, run to N
+            if ((e = launch_resident_finisher(a, a.fin_thresh, s)) != hipSuccess) return e;
+        }
         launch_panel_kernel<T>(a, grid, s);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         v0 = v1;

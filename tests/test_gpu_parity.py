@@ -169,19 +169,23 @@ def test_panel_two_wave_panels_large_batch(gpu, oracle, nm):
         assert_bitexact(y[b], yo, f"instance {b} y")
 
 
-@pytest.mark.parametrize("grid,phase", [(1, 0), (3, 0), (0, 10), (3, 20), (0, 0)])
+@pytest.mark.parametrize("grid,phase,fin", [(1, 0, None), (3, 0, 0), (0, 10, 0), (3, 20, 24),
+                                            (0, 0, None), (0, 10, 24)])
 @pytest.mark.parametrize("tol,N", [(1e-4, 3000), (0.0, 57)])
 @pytest.mark.parametrize("nm,B", [((40, 72), 150), ((150, 130), 40), ((131, 256), 37)])
-def test_panel_phased_compaction_bitexact(gpu, oracle, monkeypatch, grid, phase, tol, N, nm, B):
+def test_panel_phased_compaction_bitexact(gpu, oracle, monkeypatch, grid, phase, fin, tol, N, nm, B):
     """Phased compaction + grid-stride panels (+ panel pairs for T > 8 when panels outnumber
-    workgroups): survivors of each phase are re-packed into new panels (different columns,
-    workgroups, pairs and phases); every instance must still match its own oracle solve
-    exactly, including its iteration count."""
+    workgroups) + the resident finisher for the tail (fin = its threshold; 0 disables it):
+    survivors of each phase are re-packed into new panels (different columns, workgroups,
+    pairs and phases) or finished one per workgroup; every instance must still match its own
+    oracle solve exactly, including its iteration count."""
     from gpad_mpc import problems
     if grid:
         monkeypatch.setenv("GPAD_PANEL_MAX_GRID", str(grid))
     if phase:
         monkeypatch.setenv("GPAD_PANEL_PHASE", str(phase))
+    if fin is not None:
+        monkeypatch.setenv("GPAD_FINISH_THRESH", str(fin))
     n, m = nm
     qp = problems.synthetic_qp(n, m, batch=B, seed=8)
     ML, G = qp.ML.astype(np.float32), qp.G.astype(np.float32)
