@@ -205,6 +205,39 @@ def distinct_leg(dev, n, m, batch=8192, N=100):
             "iters_per_s": batch * N / (st["kernel_ms"] / 1e3)}
 
 
+def flat_leg(dev, batch=8192, N=100):
+    """the flat (equal-cell) battery path vs the full-matrix path on the
+    same C1 battery packs (n_u = 4, N = 10: n = 40, m = 180), fixed N iterations, fp32."""
+    import torch
+
+    import gpad_mpc
+    from gpad_mpc import problems
+    qp = problems.battery_scenarios(4, 10, batch, seed=9)
+    MGf, GLf, L = problems.flatten_battery(qp, 4, 10)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a, np.float64).astype(np.float32))).to(dev)  # noqa: E731
+    L32 = float(np.float32(L))
+    GP, G = t(qp.M), t(qp.g)
+    PD = (G * np.float32(-1.0 / np.float64(np.float32(L)))).contiguous()
+    out = {"config": f"{batch} battery packs (n_u=4, N=10: n={qp.n}, m={qp.m}), {N} iterations"}
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    for name in ("flat", "full"):
+        with gpad_mpc.GpadSolver(dev.index or 0, stream=stream) as s:
+            if name == "flat":
+                s.setup_flat(t(MGf), t(GLf), L32, n_u=4, batch=batch)
+            else:
+                s.setup(-t(qp.ML), t(qp.G) / np.float32(L32), L32, n=qp.n, m=qp.m, batch=batch,
+                        scaled=True)
+            Z = torch.zeros(batch, qp.n, device=dev)
+            Y = torch.zeros(batch, qp.m, device=dev)
+            s.run(Z, Y, GP, PD, N, 0.0, scaled=True)
+            best = 1e30
+            for _ in range(3):
+                st = s.run(Z.zero_(), Y.zero_(), GP, PD, N, 0.0, scaled=True)
+                best = min(best, st["kernel_ms"])
+        out[name] = {"kernel": st["kernel"], "iters_per_s": batch * N / (best / 1e3)}
+    return out
+
+
 def closed_loop_leg(dev, batch=8192, steps=20, N=100, cpu=True):
     """gpad.m:79-95 closed loop on the device for a batch of battery
     packs (C1 plant: n_u = 4 cells, horizon 10 -> n = 40, m = 180), each MPC step = per-state
@@ -386,6 +419,7 @@ def main():
             extra["hbm_bound_c5"] = hbm_leg(dev)
             extra["distinct_c2_batch"] = distinct_leg(dev, n, m)
             extra["closed_loop_battery"] = closed_loop_leg(dev, cpu=not args.no_cpu)
+            extra["flat_battery_c1"] = flat_leg(dev)
         out = {
             "metric": "GPAD iterations/s (instance-iterations, solve to eps=1e-4)",
             "value": value,

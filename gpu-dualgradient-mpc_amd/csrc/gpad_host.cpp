@@ -89,6 +89,8 @@ struct gpad_handle_s {
     int device = 0;
     hipStream_t stream = nullptr;
     bool ready = false;
+    bool flat = false;   // gpad_setup_flat: the flat battery path (gpad_flat.hip)
+    int n_u = 0;
     gpad_dims_t dims{};
     double L = 1.0;
     bool scaled = false;
@@ -218,6 +220,7 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
     if (!(L > 0.0) || !std::isfinite(L)) return fail(GPAD_ERR_INVALID, "gpad_setup: L must be > 0");
     HIP_TRY(hipSetDevice(h->device));
     h->ready = false;
+    h->flat = false;
     h->dims = *d;
     if (h->dims.check_every <= 0) h->dims.check_every = 10;
     h->L = L;
@@ -280,6 +283,49 @@ int gpad_setup(gpad_handle_t h, const gpad_dims_t* d, const void* ML, const void
 int gpad_setup_scaled(gpad_handle_t h, const gpad_dims_t* d, const void* MGneg, const void* GL,
                       double L) {
     return setup_impl(h, d, MGneg, GL, L, true);
+}
+
+int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* d, int n_u, const float* MGf, const float* GLf,
+                    double L) {
+    if (!h) return fail(GPAD_ERR_INVALID, "gpad_setup_flat: null handle");
+    int rc = validate_dims(d);
+    if (rc) return rc;
+    if (!MGf || !GLf) return fail(GPAD_ERR_INVALID, "gpad_setup_flat: null matrix");
+    if (!(L > 0.0) || !std::isfinite(L)) return fail(GPAD_ERR_INVALID, "gpad_setup_flat: L must be > 0");
+    if (d->dtype != GPAD_DTYPE_F32 || !d->shared)
+        return fail(GPAD_ERR_UNSUPPORTED, "gpad_setup_flat: f32 and shared matrices only");
+    if (n_u <= 0 || d->n % n_u != 0 || d->m < 4 * d->n)
+        return fail(GPAD_ERR_INVALID, "gpad_setup_flat: need n = n_u*N and m >= 4 n_u N");
+    HIP_TRY(hipSetDevice(h->device));
+    h->ready = false;
+    h->flat = false;
+    h->dims = *d;
+    if (h->dims.check_every <= 0) h->dims.check_every = 10;
+    h->L = L;
+    h->scaled = true;
+    const int Nh = d->n / n_u, m = d->m;
+    const size_t bytes = sizeof(float) * (size_t)Nh * m;
+    h->ldn = round4(d->n);
+    h->ldm = round4(m);
+    if ((rc = h->MGt.ensure(bytes)) || (rc = h->GLt.ensure(bytes))) return rc;
+    const void* dG = GLf;
+    if (d->memory == GPAD_MEM_HOST) {
+        if ((rc = h->stage.ensure(bytes))) return rc;
+        HIP_TRY(hipMemcpyAsync(h->MGt.p, MGf, bytes, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipMemcpyAsync(h->stage.p, GLf, bytes, hipMemcpyHostToDevice, h->stream));
+        dG = h->stage.p;
+    } else {
+        HIP_TRY(hipMemcpyAsync(h->MGt.p, MGf, bytes, hipMemcpyDeviceToDevice, h->stream));
+    }
+    HIP_TRY(gpad::launch_transpose_flat((const float*)dG, (float*)h->GLt.p, m, Nh, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    if (d->memory == GPAD_MEM_HOST) h->stage.release();
+    h->frag.release();
+    h->frag_tiles = 0;
+    h->n_u = n_u;
+    h->flat = true;
+    h->ready = true;
+    return GPAD_OK;
 }
 
 static int ensure_schedule(gpad_handle_t h, int N, const void* theta_in, const void* beta_in) {
@@ -405,6 +451,15 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
         return GPAD_OK;
     }
     if constexpr (sizeof(T) == sizeof(float)) {
+        if (h->flat) {  // structure-exploiting battery path (gpad_setup_flat)
+            a.n_u = h->n_u;
+            e = gpad::launch_flat(a, h->stream);
+            if (e != hipSuccess)
+                return fail(e == hipErrorInvalidValue ? GPAD_ERR_UNSUPPORTED : GPAD_ERR_HIP,
+                            std::string("flat kernel: ") + hipGetErrorString(e));
+            *kernel_out = GPAD_KERNEL_FLAT;
+            return GPAD_OK;
+        }
         // shared matrices: panels once there are more instances than the latency kernel can
         // run at ~one round (4 per CU: 4 x its 1/6-panel iteration time < one panel iteration)
         const int panel_min = gpad::resident_supported(n, m) ? 4 * h->num_cus : 64;
@@ -730,6 +785,24 @@ int gpad_step2_primal(gpad_handle_t h, const float* MGneg, const float* w, const
     if ((size_t)m * sizeof(float) > 64 * 1024) return fail(GPAD_ERR_UNSUPPORTED, "gpad_step2: m too large");
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(gpad::launch_step2(MGneg, w, gP, zhat, n, m, h->stream));
+    return GPAD_OK;
+}
+
+int gpad_step2_primal_flat(gpad_handle_t h, const float* MGf, const float* w, const float* gP,
+                           float* zhat, int N, int n_u, int m) {
+    if (!h || !MGf || !w || !gP || !zhat || N <= 0 || n_u <= 0 || m < 4 * n_u * N)
+        return fail(GPAD_ERR_INVALID, "gpad_step2_flat: bad arguments");
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(gpad::launch_step2_flat(MGf, w, gP, zhat, N, n_u, m, h->stream));
+    return GPAD_OK;
+}
+
+int gpad_step4_project_flat(gpad_handle_t h, const float* GLf, float* yp1, const float* w,
+                            const float* pD, const float* zhat, int N, int n_u, int m) {
+    if (!h || !GLf || !yp1 || !w || !pD || !zhat || N <= 0 || n_u <= 0 || m < 4 * n_u * N)
+        return fail(GPAD_ERR_INVALID, "gpad_step4_flat: bad arguments");
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(gpad::launch_step4_flat(GLf, yp1, w, pD, zhat, N, n_u, m, h->stream));
     return GPAD_OK;
 }
 

@@ -46,6 +46,8 @@ struct SolveArgs {
     float* wc;             // carried w  [batch][m]
     float* uc;             // carried u = G_L z [batch][m]
     int fin_thresh;        // survivors <= this: the resident finisher takes them (0: none)
+    int n_u;               // flat battery path: cells (n = n_u * horizon), see gpad_flat.hip
+    int flat_staged;       // flat path: matrices staged in LDS (set by launch_flat)
 };
 
 // launchers (return hipError_t of the launch)
@@ -76,6 +78,14 @@ hipError_t launch_affine2(const T* P1, const T* c1, int rows1, T* out1, const T*
 template <typename T>
 hipError_t launch_plant_step(const T* A, const T* B, const T* x, const T* z, long long ldz, T* xn, int nx,
                              int nu, int batch, T* xs, T* us, hipStream_t s);
+
+// gpad_flat.hip (flat battery path; MGt = flat -ML [Nh][m], GLt = flat G_L t-major [Nh][m])
+hipError_t launch_flat(const SolveArgs<float>& a, hipStream_t s);
+hipError_t launch_step2_flat(const float* MGf, const float* w, const float* gP, float* zhat, int Nh, int n_u,
+                             int m, hipStream_t s);
+hipError_t launch_step4_flat(const float* GLf, float* yp1, const float* w, const float* pD, const float* zhat,
+                             int Nh, int n_u, int m, hipStream_t s);
+hipError_t launch_transpose_flat(const float* in, float* out, int rows, int cols, hipStream_t s);
 
 hipError_t launch_step1(const float* y, const float* ym1, float* w, float beta, int m, hipStream_t s);
 hipError_t launch_step2(const float* MGneg, const float* w, const float* gP, float* zhat, int n,

@@ -84,7 +84,7 @@ void gpad_datafile_free(gpad_datafile_t* f) {
 
 int gpad_datafile_read(const char* path, int layout, gpad_datafile_t* out) {
     if (!path || !out) return io_fail("gpad_datafile_read: null argument");
-    if (layout != GPAD_FILE_ROWMAJOR && layout != GPAD_FILE_FLIPPED)
+    if (layout != GPAD_FILE_ROWMAJOR && layout != GPAD_FILE_FLIPPED && layout != GPAD_FILE_FLAT)
         return io_fail("gpad_datafile_read: bad layout");
     std::memset(out, 0, sizeof(*out));
     FILE* fp = std::fopen(path, "rb");
@@ -102,7 +102,8 @@ int gpad_datafile_read(const char* path, int layout, gpad_datafile_t* out) {
     if (f.n_u <= 0 || f.N <= 0 || f.m <= 0 || f.num_iterations < 0)
         return io_fail("gpad_datafile_read: header sizes must be positive");
     const int n = f.n_u * f.N, m = f.m;
-    const size_t nm = (size_t)n * m;
+    // flat files hold N x m / m x N matrices (main.cu:39-56 under ENABLE_FLATTEN_MATRICES)
+    const size_t nm = (size_t)(layout == GPAD_FILE_FLAT ? f.N : n) * m;
     auto alloc = [](size_t k) { return (float*)std::calloc(k ? k : 1, sizeof(float)); };
     f.M_G = alloc(nm);
     f.g_P = alloc(n);
@@ -135,7 +136,7 @@ int gpad_datafile_write(const char* path, int layout, const gpad_datafile_t* f) 
     if (!path || !f || !f->M_G || !f->g_P || !f->G_L || !f->p_D ||
         (f->num_iterations > 0 && (!f->theta || !f->beta)))
         return io_fail("gpad_datafile_write: null argument");
-    if (layout != GPAD_FILE_ROWMAJOR && layout != GPAD_FILE_FLIPPED)
+    if (layout != GPAD_FILE_ROWMAJOR && layout != GPAD_FILE_FLIPPED && layout != GPAD_FILE_FLAT)
         return io_fail("gpad_datafile_write: bad layout");
     if (f->n_u <= 0 || f->N <= 0 || f->m <= 0 || f->num_iterations < 0)
         return io_fail("gpad_datafile_write: bad sizes");
@@ -148,7 +149,7 @@ int gpad_datafile_write(const char* path, int layout, const gpad_datafile_t* f) 
         if (k == 0) std::fputc('\n', fp);
     };
     auto mat = [&](const float* a, int rows, int cols) {  // a is rows x cols row-major
-        if (layout == GPAD_FILE_ROWMAJOR) {
+        if (layout != GPAD_FILE_FLIPPED) {  // row-major and flat files: as stored
             for (int i = 0; i < rows; ++i) vec(a + (size_t)i * cols, cols);
         } else {
             std::vector<float> t((size_t)rows * cols);
@@ -156,9 +157,10 @@ int gpad_datafile_write(const char* path, int layout, const gpad_datafile_t* f) 
             for (int j = 0; j < cols; ++j) vec(t.data() + (size_t)j * rows, rows);
         }
     };
-    mat(f->M_G, n, m);
+    const int rows = layout == GPAD_FILE_FLAT ? f->N : n;  // flat: M_G N x m, G_L m x N
+    mat(f->M_G, rows, m);
     vec(f->g_P, n);
-    mat(f->G_L, m, n);
+    mat(f->G_L, m, rows);
     vec(f->p_D, m);
     vec(f->theta, f->num_iterations);
     vec(f->beta, f->num_iterations);

@@ -17,9 +17,9 @@ ERR_INVALID, ERR_HIP, ERR_NOMEM, ERR_UNSUPPORTED, ERR_NOT_SETUP, ERR_NO_DEVICE =
 SCHEDULE_MATLAB, SCHEDULE_PAPER = 0, 1
 MEM_HOST, MEM_DEVICE = 0, 1
 DTYPE_F32, DTYPE_F64 = 0, 1
-KERNEL_AUTO, KERNEL_STREAM, KERNEL_RESIDENT, KERNEL_PANEL = 0, 1, 2, 3
+KERNEL_AUTO, KERNEL_STREAM, KERNEL_RESIDENT, KERNEL_PANEL, KERNEL_FLAT = 0, 1, 2, 3, 4
 KERNEL_NAMES = {KERNEL_AUTO: "auto", KERNEL_STREAM: "stream", KERNEL_RESIDENT: "resident",
-                KERNEL_PANEL: "panel"}
+                KERNEL_PANEL: "panel", KERNEL_FLAT: "flat"}
 
 # every symbol include/gpad.h declares (checked by tests/test_abi.py)
 EXPORTS = [
@@ -29,9 +29,10 @@ EXPORTS = [
     "gpad_step3_average", "gpad_step4_project", "gpad_schedule", "gpad_sync",
     "gpad_setup_plant", "gpad_run_state", "gpad_closed_loop",
     "gpad_datafile_read", "gpad_datafile_write", "gpad_datafile_free",
+    "gpad_setup_flat", "gpad_step2_primal_flat", "gpad_step4_project_flat",
 ]
 
-FILE_ROWMAJOR, FILE_FLIPPED = 0, 1
+FILE_ROWMAJOR, FILE_FLIPPED, FILE_FLAT = 0, 1, 2
 
 
 class Dims(C.Structure):
@@ -103,12 +104,16 @@ def load(path: str | None = None) -> C.CDLL:
     L.gpad_datafile_write.argtypes = [C.c_char_p, i, C.POINTER(DataFile)]
     L.gpad_datafile_free.argtypes = [C.POINTER(DataFile)]
     L.gpad_datafile_free.restype = None
+    L.gpad_setup_flat.argtypes = [vp, C.POINTER(Dims), i, cvp, cvp, d]
+    L.gpad_step2_primal_flat.argtypes = [vp, vp, vp, vp, vp, i, i, i]
+    L.gpad_step4_project_flat.argtypes = [vp, vp, vp, vp, vp, vp, i, i, i]
     for name in ["gpad_create", "gpad_destroy", "gpad_set_stream", "gpad_sync", "gpad_setup",
                  "gpad_setup_scaled", "gpad_run", "gpad_run_scaled", "gpad_last_stats",
                  "gpad_solve", "gpad_step1_extrapolate", "gpad_step2_primal",
                  "gpad_step3_average", "gpad_step4_project", "gpad_schedule", "gpad_setup_plant",
                  "gpad_run_state", "gpad_closed_loop", "gpad_datafile_read",
-                 "gpad_datafile_write"]:
+                 "gpad_datafile_write", "gpad_setup_flat", "gpad_step2_primal_flat",
+                 "gpad_step4_project_flat"]:
         getattr(L, name).restype = i
     _LIB = L
     return L

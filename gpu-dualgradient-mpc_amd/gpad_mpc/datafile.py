@@ -15,9 +15,9 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
-from ._lib import FILE_FLIPPED, FILE_ROWMAJOR, DataFile, check
+from ._lib import FILE_FLAT, FILE_FLIPPED, FILE_ROWMAJOR, DataFile, check
 
-__all__ = ["GpadData", "read", "write", "from_qp", "FILE_ROWMAJOR", "FILE_FLIPPED"]
+__all__ = ["GpadData", "read", "write", "from_qp", "FILE_ROWMAJOR", "FILE_FLIPPED", "FILE_FLAT"]
 
 
 @dataclass
@@ -48,10 +48,11 @@ def read(path: str, layout: int = FILE_ROWMAJOR) -> GpadData:
     check(lib.gpad_datafile_read(str(path).encode(), layout, C.byref(f)), "gpad_datafile_read")
     try:
         n, m, k = f.n_u * f.N, f.m, f.num_iterations
+        rows = f.N if layout == FILE_FLAT else n  # flat files: M_G N x m, G_L m x N
         arr = lambda p, cnt: np.ctypeslib.as_array(p, shape=(max(cnt, 1),))[:cnt].copy()  # noqa: E731
         return GpadData(n_u=f.n_u, N=f.N, m=m, L=float(f.L),
-                        M_G=arr(f.M_G, n * m).reshape(n, m), g_P=arr(f.g_P, n),
-                        G_L=arr(f.G_L, n * m).reshape(m, n), p_D=arr(f.p_D, m),
+                        M_G=arr(f.M_G, rows * m).reshape(rows, m), g_P=arr(f.g_P, n),
+                        G_L=arr(f.G_L, rows * m).reshape(m, rows), p_D=arr(f.p_D, m),
                         theta=arr(f.theta, k), beta=arr(f.beta, k))
     finally:
         lib.gpad_datafile_free(C.byref(f))

@@ -175,6 +175,28 @@ def battery_plant(n_u: int = 4, N: int = 10, xmax: float = 0.5, xmin: float = -0
     return qp, plant
 
 
+def flatten_battery(qp: QP, n_u: int, N: int, L: float | None = None):
+    """The reference's "flat" battery data (ENABLE_FLATTEN_MATRICES; seq_functions.cpp:5-43) from
+    the full problem, valid for equal cell capacities: with H = kron(Hs, I_{n_u}), column k of
+    the first 4 n_u N constraints touches only cell k % n_u, and the 2N coupling rows touch all
+    cells equally.  Returns float64 (MGf (N x m) = flat -ML, GLf (m x N) = flat G/L, L);
+    M, g stay as in ``qp`` (g_P = M, p_D = -g/L)."""
+    L = float(qp.L if L is None else L)
+    n, m = qp.n, qp.m
+    mc = 4 * n_u * N
+    assert n == n_u * N and m >= mc
+    ML, G = np.asarray(qp.ML, np.float64), np.asarray(qp.G, np.float64)
+    MGf = np.empty((N, m))
+    GLf = np.empty((m, N))
+    for i in range(N):
+        for k in range(m):
+            MGf[i, k] = -ML[i * n_u + (k % n_u if k < mc else 0), k]
+    for r in range(m):
+        for t in range(N):
+            GLf[r, t] = G[r, t * n_u + (r % n_u if r < mc else 0)] / L
+    return MGf, GLf, L
+
+
 def synthetic_qp(n: int, m: int, batch: int = 1, seed: int = 0, shared: bool = True) -> QP:
     """SURVEY.md §8d generic generator: M = R'R + I with R ~ N(0, 1/n); G ~ N(0, 1/n);
     b = G z_f + U(0.1, 1) with z_f ~ U(-0.5, 0.5) (strictly feasible); q ~ N(0, 1);

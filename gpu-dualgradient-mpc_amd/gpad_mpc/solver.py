@@ -99,6 +99,17 @@ class GpadSolver:
         fn = self.lib.gpad_setup_scaled if scaled else self.lib.gpad_setup
         check(fn(self.h, C.byref(self.dims), _ptr(ML), _ptr(G), float(L)), "gpad_setup")
 
+    def setup_flat(self, MGf, GLf, L: float, *, n_u: int, batch: int = 1,
+                   schedule: int = _lib.SCHEDULE_MATLAB, check_every: int = 10) -> None:
+        """Bind the reference's flat battery data (seq_functions.cpp:5-43): MGf (N x m) flat
+        sign-folded M_G, GLf (m x N) flat G_L; then ``run(..., scaled=True)`` with g_P, p_D."""
+        Nh, m = MGf.shape
+        mem = _lib.MEM_DEVICE if _is_torch(MGf) else _lib.MEM_HOST
+        self.dims = Dims(n=n_u * Nh, m=m, batch=batch, shared=1, dtype=_lib.DTYPE_F32, memory=mem,
+                         schedule=schedule, check_every=check_every, kernel=_lib.KERNEL_AUTO)
+        check(self.lib.gpad_setup_flat(self.h, C.byref(self.dims), int(n_u), _ptr(MGf), _ptr(GLf),
+                                       float(L)), "gpad_setup_flat")
+
     def run(self, z, y, M, g, N: int, tol: float = 0.0, *, stats: bool = True, iters=None,
             scaled: bool = False, theta=None, beta=None):
         """Run GPAD in place on z [batch][n] / y [batch][m].  Returns a dict of stats, or None
@@ -180,6 +191,18 @@ class GpadSolver:
         n, m = MGneg.shape
         check(self.lib.gpad_step2_primal(self.h, _ptr(MGneg), _ptr(w), _ptr(gP), _ptr(zhat), n, m),
               "gpad_step2")
+
+    def step2_flat(self, MGf, w, gP, zhat, n_u: int):
+        """StepTwoGPADFlatSequential (seq_functions.cpp:5-20) on device tensors."""
+        Nh, m = MGf.shape
+        check(self.lib.gpad_step2_primal_flat(self.h, _ptr(MGf), _ptr(w), _ptr(gP), _ptr(zhat), Nh,
+                                              n_u, m), "gpad_step2_flat")
+
+    def step4_flat(self, GLf, yp1, w, pD, zhat, n_u: int):
+        """StepFourGPADFlatSequential / StepFourGPADFlatParRows on device tensors."""
+        m, Nh = GLf.shape
+        check(self.lib.gpad_step4_project_flat(self.h, _ptr(GLf), _ptr(yp1), _ptr(w), _ptr(pD),
+                                               _ptr(zhat), Nh, n_u, m), "gpad_step4_flat")
 
     def step3(self, theta: float, zm1, zhat, z):
         check(self.lib.gpad_step3_average(self.h, float(theta), _ptr(zm1), _ptr(zhat), _ptr(z),

@@ -52,6 +52,7 @@ extern "C" {
 #define GPAD_KERNEL_STREAM 1   /* matrices streamed (k-major) from HBM/L2; one workgroup/instance */
 #define GPAD_KERNEL_RESIDENT 2 /* matrix rows held in VGPRs; one workgroup/instance; n,m <= 208  */
 #define GPAD_KERNEL_PANEL 3    /* shared ML/G, f32 MFMA 16x16x4 panels; one wave per 16 instances */
+#define GPAD_KERNEL_FLAT 4     /* reported only: the flat battery path bound by gpad_setup_flat      */
 
 typedef struct gpad_dims {
     int n;           /* primal variables, n = n_u * N                                   */
@@ -97,6 +98,14 @@ int gpad_setup(gpad_handle_t h, const gpad_dims_t* dims, const void* ML, const v
  * (sign-folded as the file does) and GL = G/L already; L only scales tol. */
 int gpad_setup_scaled(gpad_handle_t h, const gpad_dims_t* dims, const void* MGneg, const void* GL,
                       double L);
+
+/* The reference's "flat" battery data (ENABLE_FLATTEN_MATRICES, main.cu:39-56; valid for equal
+ * cell capacities): MGf is the N x m flat sign-folded M_G, GLf the m x N flat G_L (row-major as
+ * seq_functions.cpp:5-43 index them), n = dims.n = n_u N, m = dims.m >= 4 n_u N.  Subsequent
+ * gpad_run / gpad_run_scaled use the structure-exploiting kernel with the arithmetic of
+ * StepTwoGPADFlatSequential / StepFourGPADFlatSequential (f32, shared matrices only). */
+int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* dims, int n_u, const float* MGf,
+                    const float* GLf, double L);
 
 /* Run GPAD on the bound problem for every instance of the batch.
  *   z0: in z_{-1}, out z*      [batch][n]   (acceldualgrad.m:17, :83)
@@ -156,13 +165,14 @@ int gpad_closed_loop(gpad_handle_t h, void* x, void* z, void* y, int steps, int 
  * mathematical orientation (M_G n x m, G_L m x n). */
 #define GPAD_FILE_ROWMAJOR 0
 #define GPAD_FILE_FLIPPED 1
+#define GPAD_FILE_FLAT 2 /* ENABLE_FLATTEN_MATRICES files: M_G is N x m, G_L is m x N (flat) */
 
 typedef struct gpad_datafile {
     int n_u, N, m, num_iterations;
     float L;
-    float* M_G;   /* n x m */
+    float* M_G;   /* n x m  (GPAD_FILE_FLAT: N x m) */
     float* g_P;   /* n */
-    float* G_L;   /* m x n */
+    float* G_L;   /* m x n  (GPAD_FILE_FLAT: m x N) */
     float* p_D;   /* m */
     float* theta; /* num_iterations */
     float* beta;  /* num_iterations */
@@ -198,6 +208,13 @@ int gpad_step3_average(gpad_handle_t h, float theta, const float* zm1, const flo
 /* 8d: yp1 = max(0, w + GL zhat + pD)        -- StepFourGPADFlippedParRows, kernel_functions.cu:142-200 */
 int gpad_step4_project(gpad_handle_t h, const float* GL, float* yp1, const float* w,
                        const float* pD, const float* zhat, int n, int m);
+/* flat battery steps (device pointers; MGf N x m, GLf m x N):
+ * StepTwoGPADFlatSequential seq_functions.cpp:5-20 / StepFourGPADFlatParRows kernel_functions.cu:74-109
+ * (with the CPU step's projection y < 0 -> 0, seq_functions.cpp:40-42). */
+int gpad_step2_primal_flat(gpad_handle_t h, const float* MGf, const float* w, const float* gP,
+                           float* zhat, int N, int n_u, int m);
+int gpad_step4_project_flat(gpad_handle_t h, const float* GLf, float* yp1, const float* w,
+                            const float* pD, const float* zhat, int N, int n_u, int m);
 /* 8e (host): theta[v], beta[v] for v < N   -- acceldualgrad.m:18,27,55-56 / main.cu:61-64    */
 int gpad_schedule(int N, int kind, double* theta, double* beta);
 

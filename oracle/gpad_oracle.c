@@ -315,3 +315,88 @@ long long orc_closed_loop_f32(float* x, float* z, float* y, const float* MGneg, 
     free(xn);
     return total;
 }
+
+/* ---- flat battery steps (seq_functions.cpp:5-43) -------------------------------------- */
+void orc_step2_flat_f32(const float* MGf, const float* w, const float* gP, float* zhat, int Nh,
+                        int n_u, int m) {
+    const int mc = 4 * n_u * Nh;
+    for (int i = 0; i < Nh; i++)
+        for (int j = 0; j < n_u; j++) {
+            float sum = 0.0f;
+            for (int k = j; k < mc; k += n_u) sum = fmaf(MGf[(size_t)i * m + k], w[k], sum);
+            for (int k = mc; k < m; k++) sum = fmaf(MGf[(size_t)i * m + k], w[k], sum);
+            zhat[i * n_u + j] = sum - gP[i * n_u + j];
+        }
+}
+
+static float orc_flat_row4(const float* GLf, const float* zhat, int r, int Nh, int n_u, int mc) {
+    float sum = 0.0f;
+    for (int t = 0; t < Nh; t++) {
+        const float g = GLf[(size_t)r * Nh + t];
+        if (r < mc) {
+            sum = fmaf(g, zhat[t * n_u + (r % n_u)], sum);
+        } else {
+            for (int k = 0; k < n_u; k++) sum = fmaf(g, zhat[t * n_u + k], sum);
+        }
+    }
+    return sum;
+}
+
+void orc_step4_flat_f32(const float* GLf, float* yp1, const float* w, const float* pD,
+                        const float* zhat, int Nh, int n_u, int m) {
+    const int mc = 4 * n_u * Nh;
+    for (int r = 0; r < m; r++) {
+        const float s = (orc_flat_row4(GLf, zhat, r, Nh, n_u, mc) + w[r]) + pD[r];
+        yp1[r] = s < 0.0f ? 0.0f : s;
+    }
+}
+
+int orc_solve_flat_f32(float* z, float* y, const float* MGf, const float* gP, const float* GLf,
+                       const float* pD, int Nh, int n_u, int m, int N, float L, float tol,
+                       int check_every, const float* theta, const float* beta, int* converged) {
+    const int n = n_u * Nh, mc = 4 * n_u * Nh;
+    const int mm = m > 0 ? m : 1;
+    float* base = (float*)malloc(sizeof(float) * (size_t)mm * 6);
+    float* ycur = base;
+    float* yprev = ycur + mm;
+    float* w = yprev + mm;
+    float* ynew = w + mm;
+    float* u = ynew + mm;
+    float* ch = u + mm;
+    float* zhat = (float*)malloc(sizeof(float) * (size_t)(n > 0 ? n : 1));
+    if (check_every <= 0) check_every = 10;
+    memcpy(ycur, y, sizeof(float) * m);
+    memcpy(yprev, y, sizeof(float) * m);
+    const int use_tol = tol > 0.0f;
+    if (use_tol)
+        for (int r = 0; r < m; r++) u[r] = orc_flat_row4(GLf, z, r, Nh, n_u, mc);
+    int it = 0, conv = 0;
+    for (int v = 0; v < N; v++) {
+        orc_step1_f32(ycur, yprev, w, beta[v], m);
+        orc_step2_flat_f32(MGf, w, gP, zhat, Nh, n_u, m);
+        orc_step3_f32(theta[v], n, z, zhat, z);
+        orc_step4_flat_f32(GLf, ynew, w, pD, zhat, Nh, n_u, m);
+        float* t = yprev; yprev = ycur; ycur = ynew; ynew = t;
+        it = v + 1;
+        if (use_tol) {
+            const float th = theta[v], omt = 1.0f - th;
+            for (int r = 0; r < m; r++) {
+                ch[r] = orc_flat_row4(GLf, zhat, r, Nh, n_u, mc);
+                u[r] = fmaf(omt, u[r], th * ch[r]);
+            }
+            if ((it % check_every) == 0) {
+                const int c = orc_check_f32(u, ch, pD, w, m, L, tol);
+                if (c) {
+                    if (c == 2) memcpy(z, zhat, sizeof(float) * n);
+                    conv = c;
+                    break;
+                }
+            }
+        }
+    }
+    memcpy(y, ycur, sizeof(float) * m);
+    free(base);
+    free(zhat);
+    if (converged) *converged = conv;
+    return it;
+}

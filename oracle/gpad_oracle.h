@@ -73,6 +73,22 @@ long long orc_solve_batch_f32(float* z, float* y, const float* MGneg, const floa
                               int shared, int N, float L, float tol, int check_every,
                               const float* theta, const float* beta, int* iters, int threads);
 
+/* ---- "flat" battery steps (equal cell capacities; seq_functions.cpp:5-43) --------------
+ * n_u cells, horizon Nh: n = n_u*Nh primal rows, m = 4 n_u Nh + 2 Nh constraints.  MGf is the
+ * flat Nh x m sign-folded M_G, GLf the flat m x Nh G_L (the reference's ENABLE_FLATTEN_MATRICES
+ * data).  Step 2: zhat[i n_u + j] = chain(k = j, j+n_u, .. < 4 n_u Nh; then k = 4 n_u Nh .. m-1)
+ * of MGf[i][k] w[k], minus gP.  Step 4: row r < 4 n_u Nh: chain over t of GLf[r][t] *
+ * zhat[t n_u + r % n_u]; row r >= 4 n_u Nh: chain over t, k of GLf[r][t] * zhat[t n_u + k];
+ * y = (sum + w) + pD, then y < 0 -> 0 (NOT the non-flat ((w + pD) + sum, (|s|+s)/2)). */
+void orc_step2_flat_f32(const float* MGf, const float* w, const float* gP, float* zhat, int Nh,
+                        int n_u, int m);
+void orc_step4_flat_f32(const float* GLf, float* yp1, const float* w, const float* pD,
+                        const float* zhat, int Nh, int n_u, int m);
+/* main_prof.cu flat loop order (steps 1, 2-flat, 3, 4-flat) + the same Algorithm 1 test. */
+int orc_solve_flat_f32(float* z, float* y, const float* MGf, const float* gP, const float* GLf,
+                       const float* pD, int Nh, int n_u, int m, int N, float L, float tol,
+                       int check_every, const float* theta, const float* beta, int* converged);
+
 /* ---- per-state data and closed loop (gpad_setup_plant / gpad_closed_loop) ----------
  * gpad.m:79-95 restated: the state-dependent QP data are affine in x and the plant is LTI.
  * These define the fp32 evaluation order the product path must match bit for bit.      */

@@ -69,6 +69,11 @@ class Oracle:
                                           _f, _f, _f, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float,
                                           C.c_int, _f, _f, C.c_int, _f, _f, _i]
         L.orc_closed_loop_f32.restype = C.c_longlong
+        L.orc_step2_flat_f32.argtypes = [_f, _f, _f, _f, C.c_int, C.c_int, C.c_int]
+        L.orc_step4_flat_f32.argtypes = [_f, _f, _f, _f, _f, C.c_int, C.c_int, C.c_int]
+        L.orc_solve_flat_f32.argtypes = [_f, _f, _f, _f, _f, _f, C.c_int, C.c_int, C.c_int, C.c_int,
+                                         C.c_float, C.c_float, C.c_int, _f, _f, _i]
+        L.orc_solve_flat_f32.restype = C.c_int
         self.lib = L
 
     # -- steps ------------------------------------------------------------------
@@ -176,6 +181,39 @@ class Oracle:
         return Z, Y, iters, int(total)
 
 
+    # -- flat battery steps (seq_functions.cpp:5-43) ------------------------------
+    def step2_flat(self, MGf, w, gP, n_u):
+        MGf = np.ascontiguousarray(MGf, np.float32); Nh, m = MGf.shape
+        zh = np.empty(Nh * n_u, np.float32)
+        self.lib.orc_step2_flat_f32(_fp(MGf), _fp(np.ascontiguousarray(w, np.float32)),
+                                    _fp(np.ascontiguousarray(gP, np.float32)), _fp(zh), Nh, n_u, m)
+        return zh
+
+    def step4_flat(self, GLf, w, pD, zhat, n_u):
+        GLf = np.ascontiguousarray(GLf, np.float32); m, Nh = GLf.shape
+        yp = np.empty(m, np.float32)
+        self.lib.orc_step4_flat_f32(_fp(GLf), _fp(yp), _fp(np.ascontiguousarray(w, np.float32)),
+                                    _fp(np.ascontiguousarray(pD, np.float32)),
+                                    _fp(np.ascontiguousarray(zhat, np.float32)), Nh, n_u, m)
+        return yp
+
+    def solve_flat_f32(self, z0, y0, MGf, gP, GLf, pD, n_u, N, L, tol=0.0, check_every=10,
+                       schedule=SCHEDULE_MATLAB, theta=None, beta=None):
+        MGf = np.ascontiguousarray(MGf, np.float32); Nh, m = MGf.shape
+        n = Nh * n_u
+        z = np.array(z0, np.float32, copy=True).reshape(n)
+        y = np.array(y0, np.float32, copy=True).reshape(m)
+        if theta is None:
+            theta, beta = self.schedule_f32(max(N, 1), schedule)
+        conv = C.c_int(0)
+        it = self.lib.orc_solve_flat_f32(_fp(z), _fp(y), _fp(MGf), _fp(np.ascontiguousarray(gP, np.float32)),
+                                         _fp(np.ascontiguousarray(GLf, np.float32)),
+                                         _fp(np.ascontiguousarray(pD, np.float32)), Nh, n_u, m, N,
+                                         np.float32(L), np.float32(tol), check_every,
+                                         _fp(np.ascontiguousarray(theta, np.float32)),
+                                         _fp(np.ascontiguousarray(beta, np.float32)), C.byref(conv))
+        return z, y, it, conv.value
+
     # -- per-state data / closed loop (gpad.m:79-95) -----------------------------
     def affine(self, P, c0, x):
         P = np.ascontiguousarray(P, np.float32); rows, nx = P.shape
@@ -218,6 +256,10 @@ class RefSeq:
         L.ref_solve_f32.argtypes = [_f, _f, _f, _f, _f, _f, C.c_int, C.c_int, C.c_int, _f, _f]
         L.ref_solve_batch_f32.argtypes = [_f, _f, _f, _f, _f, _f, C.c_int, C.c_int, C.c_int,
                                           C.c_int, C.c_int, _f, _f, C.c_int]
+        L.StepTwoGPADFlatSequential.argtypes = [_f, _f, _f, _f, C.c_int, C.c_int, C.c_int]
+        L.StepFourGPADFlatSequential.argtypes = [_f, _f, _f, _f, _f, C.c_int, C.c_int, C.c_int]
+        L.ref_solve_flat_f32.argtypes = [_f, _f, _f, _f, _f, _f, C.c_int, C.c_int, C.c_int, C.c_int,
+                                         _f, _f]
         self.lib = L
 
     @staticmethod
@@ -251,6 +293,32 @@ class RefSeq:
                                         _fp(np.ascontiguousarray(pD, np.float32)),
                                         _fp(np.ascontiguousarray(zhat, np.float32)), n, 1, m)
         return y
+
+    def step2_flat(self, MGf, w, gP, n_u):
+        MGf = np.ascontiguousarray(MGf, np.float32); Nh, m = MGf.shape
+        zh = np.empty(Nh * n_u, np.float32)
+        self.lib.StepTwoGPADFlatSequential(_fp(MGf), _fp(np.ascontiguousarray(w, np.float32)),
+                                           _fp(np.ascontiguousarray(gP, np.float32)), _fp(zh), Nh, n_u, m)
+        return zh
+
+    def step4_flat(self, GLf, w, pD, zhat, n_u):
+        GLf = np.ascontiguousarray(GLf, np.float32); m, Nh = GLf.shape
+        y = np.empty(m, np.float32)
+        self.lib.StepFourGPADFlatSequential(_fp(GLf), _fp(y), _fp(np.ascontiguousarray(w, np.float32)),
+                                            _fp(np.ascontiguousarray(pD, np.float32)),
+                                            _fp(np.ascontiguousarray(zhat, np.float32)), Nh, n_u, m)
+        return y
+
+    def solve_flat_c(self, z0, y0, MGf, gP, GLf, pD, n_u, theta, beta, N):
+        """The reference's flat steps in the main_prof.cu loop (oracle/ref_driver.c)."""
+        MGf = np.ascontiguousarray(MGf, np.float32); Nh, m = MGf.shape
+        z = np.array(z0, np.float32, copy=True); y = np.array(y0, np.float32, copy=True)
+        self.lib.ref_solve_flat_f32(_fp(z), _fp(y), _fp(MGf), _fp(np.ascontiguousarray(gP, np.float32)),
+                                    _fp(np.ascontiguousarray(GLf, np.float32)),
+                                    _fp(np.ascontiguousarray(pD, np.float32)), Nh, n_u, m, N,
+                                    _fp(np.ascontiguousarray(theta, np.float32)),
+                                    _fp(np.ascontiguousarray(beta, np.float32)))
+        return z, y
 
     def solve_c(self, z0, y0, MGneg, gP, GL, pD, theta, beta, N):
         """Same loop as ``solve`` but driven from C (oracle/ref_driver.c)."""

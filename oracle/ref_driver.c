@@ -58,3 +58,31 @@ void ref_solve_batch_f32(float* Z, float* Y, const float* MGneg, const float* GP
     }
     (void)threads;
 }
+
+/* The reference's FLAT battery steps (seq_functions.cpp:5-43, ENABLE_FLATTEN_MATRICES) in the
+ * main_prof.cu loop order: MGf is Nh x m, GLf is m x Nh. */
+void ref_solve_flat_f32(float* z, float* y, const float* MGf, const float* gP, const float* GLf,
+                        const float* pD, int Nh, int n_u, int m, int N, const float* theta,
+                        const float* beta) {
+    const int n = n_u * Nh;
+    float* buf = (float*)malloc(sizeof(float) * ((size_t)4 * m + n + 4));
+    float* ycur = buf;
+    float* yprev = ycur + m;
+    float* w = yprev + m;
+    float* ynew = w + m;
+    float* zhat = ynew + m;
+    memcpy(ycur, y, sizeof(float) * m);
+    memcpy(yprev, y, sizeof(float) * m);
+    for (int v = 0; v < N; v++) {
+        StepOneGPADSequential(ycur, yprev, w, beta[v], m);
+        StepTwoGPADFlatSequential(MGf, w, gP, zhat, Nh, n_u, m);
+        StepThreeGPADSequential(theta[v], n, z, zhat, z);
+        StepFourGPADFlatSequential(GLf, ynew, w, pD, zhat, Nh, n_u, m);
+        float* t = yprev;
+        yprev = ycur;
+        ycur = ynew;
+        ynew = t;
+    }
+    memcpy(y, ycur, sizeof(float) * m);
+    free(buf);
+}

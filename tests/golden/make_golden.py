@@ -121,6 +121,44 @@ def make_datafile(O, R):
     print(f"datafile_battery_3x4: n={qp.n} m={qp.m}")
 
 
+def make_flat(name, n_u, N, seed, O, R):
+    """The reference's FLAT battery steps (seq_functions.cpp:5-43) on the flattened battery
+    problem: end states after 1, 10, 100 iterations (reference's own steps, main_prof.cu loop),
+    one-step KATs, an Algorithm-1 run (oracle), and the ENABLE_FLATTEN_MATRICES data file."""
+    qp = problems.battery_mpc(n_u, N, seed=seed)
+    MGf, GLf, L = problems.flatten_battery(qp, n_u, N)
+    f32 = lambda a: np.asarray(a, np.float64).astype(np.float32)  # noqa: E731
+    L32 = np.float32(L)
+    MGf32, GLf32, gP = f32(MGf), f32(GLf), f32(qp.M)
+    pD = O.scale_vec(f32(qp.g), L32)
+    th, be = O.schedule_f32(100)
+    n, m = qp.n, qp.m
+    out = dict(MGf=MGf32, GLf=GLf32, gP=gP, pD=pD, L=L32, n_u=np.int32(n_u), N=np.int32(N),
+               theta100=th, beta100=be)
+    z0, y0 = np.zeros(n, np.float32), np.zeros(m, np.float32)
+    for K in (1, 10, 100):
+        z, y = R.solve_flat_c(z0, y0, MGf32, gP, GLf32, pD, n_u, th, be, K)
+        out[f"ref_z_{K}"], out[f"ref_y_{K}"] = z, y
+    rng = np.random.default_rng(7)
+    w = np.abs(rng.normal(0, 0.2, m)).astype(np.float32)
+    zh = rng.normal(0, 0.2, n).astype(np.float32)
+    out.update(kat_w=w, kat_zh_in=zh, kat_zhat=R.step2_flat(MGf32, w, gP, n_u),
+               kat_yp1=R.step4_flat(GLf32, w, pD, zh, n_u))
+    z, y, it, conv = O.solve_flat_f32(z0, y0, MGf32, gP, GLf32, pD, n_u, 5000, L32, 1e-4)
+    out.update(tol_z=z, tol_y=y, tol_iters=np.int32(it), tol_conv=np.int32(conv))
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+    print(f"{name}: n={n} m={m} tol-iters={it}")
+    return out
+
+
+def write_flat_datafile(path, d, n_u, N):
+    """ENABLE_FLATTEN_MATRICES data file (main.cu:39-56): M_G N x m, G_L m x N, numpy-formatted."""
+    with open(path, "w") as fh:
+        fh.write(f"{n_u} {N} {d['GLf'].shape[0]} 100 {float(d['L']):.8e}\n")
+        for arr in (d["MGf"].reshape(-1), d["gP"], d["GLf"].reshape(-1), d["pD"], d["theta100"], d["beta100"]):
+            fh.write(" ".join(f"{v:.8e}" for v in np.asarray(arr, np.float64)) + "\n")
+
+
 def make_closed_loop():
     """gpad.m:79-95 with n = 3 cells, p = 4, 40 samples, acceldualgrad's 100 iterations per
     step, fp64 (numpy restatement of the MATLAB): x, u trajectories."""
@@ -147,6 +185,9 @@ def main():
         make(name, qp, O, R)
     make_datafile(O, R)
     make_closed_loop()
+    make_flat("battery_flat_4x10", 4, 10, 0, O, R)
+    d = make_flat("battery_flat_3x4", 3, 4, 5, O, R)
+    write_flat_datafile(os.path.join(HERE, "datafile_battery_flat_3x4.txt"), d, 3, 4)
     # the reference's own step-3 known-answer files (data, copied verbatim)
     if os.path.isdir(STEP3_SRC):
         for k in range(1, 6):

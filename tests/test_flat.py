@@ -1,0 +1,193 @@
+"""Flat battery path: the reference's structure-exploiting steps
+StepTwoGPADFlatSequential / StepFourGPADFlatSequential (seq_functions.cpp:5-43) for equal cell
+capacities, and libgpad's gpad_setup_flat + flat kernel + per-step flat entry points.
+
+Parity pins: the golden end states come from the reference's OWN flat steps compiled from
+/root/reference (oracle/_ref, main_prof.cu loop order; tests/golden/make_golden.py).  The oracle's
+flat restatement must match them bit for bit (CPU), and the HIP path must match both (GPU).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, load_golden
+
+FLAT_SETS = ["battery_flat_4x10", "battery_flat_3x4"]
+
+
+# ---------------------------------------------------------------------------------- CPU
+@pytest.mark.parametrize("name", FLAT_SETS)
+def test_oracle_flat_matches_reference_steps(oracle, name):
+    gd = load_golden(name)
+    n_u = int(gd["n_u"])
+    n, m = gd["gP"].size, gd["pD"].size
+    for K in (1, 10, 100):
+        z, y, it, _ = oracle.solve_flat_f32(np.zeros(n), np.zeros(m), gd["MGf"], gd["gP"], gd["GLf"],
+                                            gd["pD"], n_u, K, gd["L"], theta=gd["theta100"],
+                                            beta=gd["beta100"])
+        assert it == K
+        np.testing.assert_array_equal(z, gd[f"ref_z_{K}"])
+        np.testing.assert_array_equal(y, gd[f"ref_y_{K}"])
+    np.testing.assert_array_equal(oracle.step2_flat(gd["MGf"], gd["kat_w"], gd["gP"], n_u), gd["kat_zhat"])
+    np.testing.assert_array_equal(oracle.step4_flat(gd["GLf"], gd["kat_w"], gd["pD"], gd["kat_zh_in"], n_u),
+                                  gd["kat_yp1"])
+
+
+def test_flatten_is_exact_for_equal_cells():
+    """The flat data reproduces the full battery matrices (gpad.m, equal capacities) to fp64
+    round-off: the structural zeros are zeros and the coupling columns are cell-independent."""
+    from gpad_mpc import problems
+    n_u, N = 4, 10
+    qp = problems.battery_mpc(n_u, N, seed=0)
+    MGf, GLf, L = problems.flatten_battery(qp, n_u, N)
+    n, m, mc = qp.n, qp.m, 4 * n_u * N
+    ML = np.zeros((n, m))
+    G = np.zeros((m, n))
+    for i in range(N):
+        for j in range(n_u):
+            for k in range(m):
+                if k >= mc or k % n_u == j:
+                    ML[i * n_u + j, k] = -MGf[i, k]
+    for r in range(m):
+        for t in range(N):
+            for c in range(n_u):
+                if r >= mc or r % n_u == c:
+                    G[r, t * n_u + c] = GLf[r, t] * L
+    assert np.abs(ML - qp.ML).max() <= 1e-15 * np.abs(qp.ML).max()
+    assert np.abs(G - qp.G).max() <= 1e-15 * np.abs(qp.G).max()
+
+
+def test_flat_solution_close_to_full(oracle):
+    """Flat and full fp32 paths solve the same QP; they differ only by rounding (the flat step 4
+    adds (s + w) + p_D where the full one adds (w + p_D) + s)."""
+    gd = load_golden("battery_flat_4x10")
+    full = load_golden("battery_c1")
+    rel = lambda a, b: np.abs(a - b).max() / np.abs(b).max()  # noqa: E731
+    assert rel(gd["ref_z_100"], full["ref_z_100"]) < 1e-5
+    assert rel(gd["ref_y_100"], full["ref_y_100"]) < 1e-5
+    assert int(gd["tol_iters"]) == int(full["tol_iters"])
+
+
+def test_flat_datafile_reads(tmp_path):
+    """ENABLE_FLATTEN_MATRICES files (main.cu:39-56): M_G N x m, G_L m x N; a write/read round trip
+    is exact and the numpy-written fixture reads at its print precision."""
+    from gpad_mpc import datafile
+    gd = load_golden("battery_flat_3x4")
+    d = datafile.read(os.path.join(GOLDEN, "datafile_battery_flat_3x4.txt"), datafile.FILE_FLAT)
+    assert d.M_G.shape == (4, 56) and d.G_L.shape == (56, 4) and d.n == 12
+    np.testing.assert_allclose(d.M_G, gd["MGf"], rtol=1e-7, atol=1e-12)
+    np.testing.assert_allclose(d.G_L, gd["GLf"], rtol=1e-7, atol=1e-12)
+    p = str(tmp_path / "flat.txt")
+    datafile.write(p, d, datafile.FILE_FLAT)
+    r = datafile.read(p, datafile.FILE_FLAT)
+    for k in ("M_G", "g_P", "G_L", "p_D", "theta", "beta"):
+        np.testing.assert_array_equal(getattr(r, k), getattr(d, k), err_msg=k)
+
+
+# ---------------------------------------------------------------------------------- GPU
+def _flat_solver(gd, batch=1):
+    import gpad_mpc
+    s = gpad_mpc.GpadSolver(0)
+    s.setup_flat(gd["MGf"], gd["GLf"], float(gd["L"]), n_u=int(gd["n_u"]), batch=batch)
+    return s
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", FLAT_SETS)
+def test_flat_kernel_matches_reference_steps(gpu, name):
+    """Fixed N = 1, 10, 100 with the reference's θ/β: bit-exact with its own flat steps."""
+    gd = load_golden(name)
+    s = _flat_solver(gd)
+    n, m = gd["gP"].size, gd["pD"].size
+    for K in (1, 10, 100):
+        z = np.zeros(n, np.float32)
+        y = np.zeros(m, np.float32)
+        st = s.run(z, y, gd["gP"], gd["pD"], K, 0.0, scaled=True, theta=gd["theta100"],
+                   beta=gd["beta100"])
+        assert st["kernel"] == "flat"
+        np.testing.assert_array_equal(z, gd[f"ref_z_{K}"])
+        np.testing.assert_array_equal(y, gd[f"ref_y_{K}"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", FLAT_SETS)
+def test_flat_kernel_algorithm1(gpu, name):
+    gd = load_golden(name)
+    s = _flat_solver(gd)
+    n, m = gd["gP"].size, gd["pD"].size
+    z = np.zeros(n, np.float32)
+    y = np.zeros(m, np.float32)
+    st = s.run(z, y, gd["gP"], gd["pD"], 5000, 1e-4, scaled=True)
+    assert st["iterations"] == int(gd["tol_iters"]) and st["converged"] == (1 if gd["tol_conv"] else 0)
+    np.testing.assert_array_equal(z, gd["tol_z"])
+    np.testing.assert_array_equal(y, gd["tol_y"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tol,N", [(0.0, 150), (1e-4, 4000)])
+def test_flat_batch_bitexact(gpu, oracle, tol, N):
+    """A battery-scenario batch (one plant, per-state g_P, p_D) on the flat kernel vs the
+    oracle's flat solve per instance."""
+    from gpad_mpc import problems
+    n_u, Nh, B = 4, 10, 48
+    qp = problems.battery_scenarios(n_u, Nh, B, seed=4)
+    MGf, GLf, L = problems.flatten_battery(qp, n_u, Nh)
+    f32 = lambda a: np.ascontiguousarray(np.asarray(a, np.float64).astype(np.float32))  # noqa: E731
+    L32 = np.float32(L)
+    MGf32, GLf32 = f32(MGf), f32(GLf)
+    GP = f32(qp.M)
+    PD = oracle.scale_vec(f32(qp.g), L32)
+    import gpad_mpc
+    s = gpad_mpc.GpadSolver(0)
+    s.setup_flat(MGf32, GLf32, float(L32), n_u=n_u, batch=B)
+    Z = np.zeros((B, qp.n), np.float32)
+    Y = np.zeros((B, qp.m), np.float32)
+    it = np.zeros(B, np.int32)
+    s.run(Z, Y, GP, np.ascontiguousarray(PD), N, tol, scaled=True, iters=it)
+    for b in range(B):
+        z, y, its, _ = oracle.solve_flat_f32(np.zeros(qp.n), np.zeros(qp.m), MGf32, GP[b], GLf32, PD[b],
+                                             n_u, N, L32, tol)
+        assert it[b] == its, b
+        np.testing.assert_array_equal(Z[b], z, err_msg=f"z[{b}]")
+        np.testing.assert_array_equal(Y[b], y, err_msg=f"y[{b}]")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", FLAT_SETS)
+def test_flat_step_entry_points(gpu, name):
+    """gpad_step2_primal_flat / gpad_step4_project_flat vs the reference's flat step KATs."""
+    import torch
+
+    import gpad_mpc
+    gd = load_golden(name)
+    n_u = int(gd["n_u"])
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(gpu)  # noqa: E731
+    s = gpad_mpc.GpadSolver(0)
+    zh = torch.empty(gd["gP"].size, device=gpu)
+    s.step2_flat(t(gd["MGf"]), t(gd["kat_w"]), t(gd["gP"]), zh, n_u)
+    yp = torch.empty(gd["pD"].size, device=gpu)
+    s.step4_flat(t(gd["GLf"]), yp, t(gd["kat_w"]), t(gd["pD"]), t(gd["kat_zh_in"]), n_u)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(zh.cpu().numpy(), gd["kat_zhat"])
+    np.testing.assert_array_equal(yp.cpu().numpy(), gd["kat_yp1"])
+
+
+@pytest.mark.gpu
+def test_flat_datafile_run(gpu, oracle):
+    """ENABLE_FLATTEN_MATRICES data file -> gpad_setup_flat -> 100 iterations with the file's θ/β:
+    bit-exact with the oracle's flat solve on the values read."""
+    from gpad_mpc import datafile
+    d = datafile.read(os.path.join(GOLDEN, "datafile_battery_flat_3x4.txt"), datafile.FILE_FLAT)
+    import gpad_mpc
+    s = gpad_mpc.GpadSolver(0)
+    s.setup_flat(d.M_G, d.G_L, float(d.L), n_u=d.n_u)
+    z = np.zeros(d.n, np.float32)
+    y = np.zeros(d.m, np.float32)
+    s.run(z, y, d.g_P, d.p_D, 100, 0.0, scaled=True, theta=d.theta, beta=d.beta)
+    zo, yo, _, _ = oracle.solve_flat_f32(np.zeros(d.n), np.zeros(d.m), d.M_G, d.g_P, d.G_L, d.p_D, d.n_u,
+                                         100, np.float32(d.L), theta=d.theta, beta=d.beta)
+    np.testing.assert_array_equal(z, zo)
+    np.testing.assert_array_equal(y, yo)
