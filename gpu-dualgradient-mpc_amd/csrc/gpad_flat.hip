@@ -264,4 +264,24 @@ hipError_t launch_transpose_flat(const float* in, float* out, int rows, int cols
     return hipGetLastError();
 }
 
+// flat G_L (m x Nh row-major) -> the full constraint rows as a k-major image out[k*ld + r]
+// (k < n = n_u Nh): row r < 4 n_u Nh touches column t n_u + r % n_u, coupling rows every column
+__global__ void expand_flat_gl_kernel(const float* __restrict__ GLf, float* __restrict__ out, int Nh,
+                                      int n_u, int m, int ld) {
+    const int n = Nh * n_u, mc = 4 * n_u * Nh;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n * ld) return;
+    const int k = e / ld, r = e % ld;
+    const int t = k / n_u, c = k % n_u;
+    float v = 0.0f;
+    if (r < m && (r >= mc || c == r % n_u)) v = GLf[(size_t)r * Nh + t];
+    out[e] = v;
+}
+
+hipError_t launch_expand_flat_gl(const float* GLf, float* out, int Nh, int n_u, int m, int ld, hipStream_t s) {
+    const int tot = Nh * n_u * ld;
+    hipLaunchKernelGGL(expand_flat_gl_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, GLf, out, Nh, n_u, m, ld);
+    return hipGetLastError();
+}
+
 }  // namespace gpad

@@ -96,6 +96,7 @@ struct gpad_handle_s {
     bool scaled = false;
     int ldn = 0, ldm = 0;
     DevBuf MGt, GLt, frag, stage;
+    DevBuf GLx;  // flat path: flat G_L expanded to the full k-major image (flat resident kernel)
     int frag_tiles = 0;
     DevBuf theta, beta;
     int sched_len = 0, sched_kind = -1, sched_dtype = -1;
@@ -161,6 +162,7 @@ int gpad_destroy(gpad_handle_t h) {
     (void)hipStreamSynchronize(h->stream);
     h->MGt.release();
     h->GLt.release();
+    h->GLx.release();
     h->frag.release();
     h->stage.release();
     h->theta.release();
@@ -318,6 +320,12 @@ int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* d, int n_u, const float*
         HIP_TRY(hipMemcpyAsync(h->MGt.p, MGf, bytes, hipMemcpyDeviceToDevice, h->stream));
     }
     HIP_TRY(gpad::launch_transpose_flat((const float*)dG, (float*)h->GLt.p, m, Nh, h->stream));
+    h->GLx.release();
+    if (gpad::flat_resident_supported(d->n, m, n_u)) {
+        if ((rc = h->GLx.ensure(sizeof(float) * (size_t)d->n * h->ldm))) return rc;
+        HIP_TRY(gpad::launch_expand_flat_gl((const float*)dG, (float*)h->GLx.p, Nh, n_u, m, h->ldm,
+                                            h->stream));
+    }
     HIP_TRY(hipStreamSynchronize(h->stream));
     if (d->memory == GPAD_MEM_HOST) h->stage.release();
     h->frag.release();
@@ -453,7 +461,13 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
     if constexpr (sizeof(T) == sizeof(float)) {
         if (h->flat) {  // structure-exploiting battery path (gpad_setup_flat)
             a.n_u = h->n_u;
-            e = gpad::launch_flat(a, h->stream);
+            if (h->GLx.p && kernel != GPAD_KERNEL_STREAM) {  // register-resident flat chains
+                a.GLt = (const T*)h->GLx.p;
+                a.strideA = a.strideB = 0;
+                e = gpad::launch_flat_resident(a, h->stream);
+            } else {
+                e = gpad::launch_flat(a, h->stream);
+            }
             if (e != hipSuccess)
                 return fail(e == hipErrorInvalidValue ? GPAD_ERR_UNSUPPORTED : GPAD_ERR_HIP,
                             std::string("flat kernel: ") + hipGetErrorString(e));

@@ -81,6 +81,12 @@ hipError_t launch_plant_step(const T* A, const T* B, const T* x, const T* z, lon
 
 // gpad_flat.hip (flat battery path; MGt = flat -ML [Nh][m], GLt = flat G_L t-major [Nh][m])
 hipError_t launch_flat(const SolveArgs<float>& a, hipStream_t s);
+// register-resident flat variant (gpad_kernels.hip): a.MGt = flat -ML (Nh x m), a.GLt = the
+// flat G_L expanded to the full k-major image [n][ldm]
+bool flat_resident_supported(int n, int m, int n_u);
+hipError_t launch_flat_resident(const SolveArgs<float>& a, hipStream_t s);
+// flat G_L (m x Nh) -> full k-major image out[k*ld + r] (k < n), zero off the structure
+hipError_t launch_expand_flat_gl(const float* GLf, float* out, int Nh, int n_u, int m, int ld, hipStream_t s);
 hipError_t launch_step2_flat(const float* MGf, const float* w, const float* gP, float* zhat, int Nh, int n_u,
                              int m, hipStream_t s);
 hipError_t launch_step4_flat(const float* GLf, float* yp1, const float* w, const float* pD, const float* zhat,

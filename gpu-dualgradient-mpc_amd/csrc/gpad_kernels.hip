@@ -362,11 +362,20 @@ __device__ __forceinline__ float chain_regs(const float (&r)[K], const float* v)
 constexpr int kResidentMaxThreads = 512;
 constexpr int kResidentMaxRow = 208;
 
-template <int KA, int KB>
+// FLAT = the structure-exploiting battery variant (gpad_flat.hip header; seq_functions.cpp:5-43):
+// a primal row (i, j) carries only its 6N structural coefficients (KA = bucket(6N)) and chains
+// over a per-cell permuted copy of w (wP[j][s] = w[j + n_u s], s < 4N; w[4 n_u N + s - 4N] after),
+// so the 8b half-iteration is 6N steps long instead of m.  A-lanes are laid out so every 16-lane
+// DPP row serves one cell j (lane = 16 times of that cell), hence one broadcast segment per row.
+// Constraint rows chain over the natural zhat with the flat G_L expanded to full rows (exact: the
+// added terms are exact zeros), with the flat step's epilogue (s + w) + p_D, y < 0 -> 0.
+constexpr int kFlatMaxCells = 16;
+
+template <int KA, int KB, bool FLAT>
 __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(SolveArgs<float> a) {
     constexpr int K = KA > KB ? KA : KB;
     constexpr int PA = (KA + 63) / 64 * 64, PB = (KB + 63) / 64 * 64;  // whole 64-element groups
-    __shared__ __attribute__((aligned(16))) float w_l[PA];   // w, broadcast to -ML rows
+    __shared__ __attribute__((aligned(16))) float w_l[FLAT ? kFlatMaxCells * PA : PA];  // w (flat: wP)
     __shared__ __attribute__((aligned(16))) float zh_l[PB];  // zhat, broadcast to G/L rows
     __shared__ __attribute__((aligned(16))) float z_l[PB];   // z_{-1}, to seed u = G_L z
     __shared__ CheckSlot slots[kResidentMaxThreads / 64];
@@ -381,20 +390,48 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
     const int b = fin ? a.idx_in[blockIdx.x] : blockIdx.x;
     const int v0 = fin ? a.v_begin : 0;  // resume at the carried iteration
     const int n = a.n, m = a.m;
-    const int nA = (n + 63) >> 6;
+    const int n_u = FLAT ? a.n_u : 1, Nh = FLAT ? n / n_u : 0, mc = 4 * n_u * Nh;
+    const int nq = (Nh + 15) >> 4;  // flat: 16-lane DPP rows per cell
+    const int nA = FLAT ? (n_u * nq * 16 + 63) >> 6 : (n + 63) >> 6;
     const int nwaves = blockDim.x >> 6;
     const bool isA = (tid >> 6) < nA;               // wave-uniform role
-    const int row = isA ? tid : tid - 64 * nA;
-    const bool live = isA ? row < n : row < m;
-    const int len = isA ? m : n;                     // chain length of this lane's row
-    const float* __restrict__ Mt = isA ? a.MGt + (size_t)b * a.strideA
-                                       : a.GLt + (size_t)b * a.strideB;
-    const int ld = isA ? a.ldn : a.ldm;
+    int row = isA ? tid : tid - 64 * nA;
+    int cell = 0;                                   // flat A-lanes: cell j of this lane
+    bool live = isA ? row < n : row < m;
+    if (FLAT && isA) {  // lane -> (cell j, time i): row r = i n_u + j
+        const int q = tid >> 4, i = 16 * (q % nq) + (tid & 15);
+        cell = q / nq;
+        live = cell < n_u && i < Nh;
+        row = live ? i * n_u + cell : 0;
+    }
 
-    // preload the row once (k-major layout: consecutive lanes read consecutive words)
+    // preload the row once
     float r[K];
+    if (FLAT && isA) {  // flat -ML row i (Nh x m, row-major): the 6N structural entries
+        const float* Mi = a.MGt + (size_t)(row / n_u) * m;
 #pragma unroll
-    for (int k = 0; k < K; ++k) r[k] = (live && k < len) ? Mt[(size_t)k * ld + row] : 0.0f;
+        for (int k = 0; k < K; ++k)
+            r[k] = (!live || k >= 6 * Nh) ? 0.0f : Mi[k < 4 * Nh ? cell + n_u * k : mc + (k - 4 * Nh)];
+    } else {  // k-major images: consecutive lanes read consecutive words
+        const int len = isA ? m : n;
+        const float* __restrict__ Mt = isA ? a.MGt + (size_t)b * a.strideA : a.GLt + (size_t)b * a.strideB;
+        const int ld = isA ? a.ldn : a.ldm;
+#pragma unroll
+        for (int k = 0; k < K; ++k) r[k] = (live && k < len) ? Mt[(size_t)k * ld + row] : 0.0f;
+    }
+    // where constraint row `row` lands in the A-side vector
+    auto put_w = [&](float wv) {
+        if constexpr (FLAT) {
+            if (row < mc) {
+                w_l[(row % n_u) * PA + row / n_u] = wv;
+            } else {
+                for (int j = 0; j < n_u; ++j) w_l[j * PA + 4 * Nh + (row - mc)] = wv;
+            }
+        } else {
+            w_l[row] = wv;
+        }
+    };
+    const float* wvec = FLAT ? w_l + cell * PA : w_l;  // this lane's broadcast segment
 
     float* zg = a.z + (size_t)b * n;
     float* yg = a.y + (size_t)b * m;
@@ -409,13 +446,13 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
         pdi = (float)(a.gscale * (double)a.g[(size_t)b * a.ld_g + row]);
         wi = v0 == 0 ? __builtin_fmaf(a.beta[0], yi - yi, yi) : a.wc[(size_t)b * m + row];
     }
-    for (int i = tid; i < PA; i += blockDim.x) w_l[i] = 0.0f;
+    for (int i = tid; i < (FLAT ? kFlatMaxCells * PA : PA); i += blockDim.x) w_l[i] = 0.0f;
     for (int i = tid; i < PB; i += blockDim.x) {
         zh_l[i] = 0.0f;
         z_l[i] = 0.0f;
     }
     __syncthreads();
-    if (!isA && live) w_l[row] = wi;
+    if (!isA && live) put_w(wi);
     if (isA && live) z_l[row] = zi;
     __syncthreads();
     const bool use_tol = a.tol > 0.0;
@@ -434,7 +471,7 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
         const float th_next = a.theta[v + 1], bn_next = a.beta[v + 2];
         const bool chk = a.tol > 0.0 && ((v + 1) % a.check_every) == 0;
         if (isA) {  // ---- 8b + 8c --------------------------------------------------------
-            const float acc = chain_regs<KA, K>(r, w_l);
+            const float acc = chain_regs<KA, K>(r, wvec);
             if (live) {
                 const float zhv = acc - gpi;
                 zi = __builtin_fmaf(1.0f - th, zi, th * zhv);
@@ -448,8 +485,14 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
         if (!isA) {  // ---- 8d + next 8a ------------------------------------------------
             const float c = chain_regs<KB, K>(r, zh_l);
             if (live) {
-                const float sv = (wi + pdi) + c;
-                const float yp = (__builtin_fabsf(sv) + sv) * 0.5f;
+                float sv, yp;
+                if constexpr (FLAT) {
+                    sv = (c + wi) + pdi;             // seq_functions.cpp:37
+                    yp = sv < 0.0f ? 0.0f : sv;      // seq_functions.cpp:40-42
+                } else {
+                    sv = (wi + pdi) + c;             // seq_functions.cpp:84
+                    yp = (__builtin_fabsf(sv) + sv) * 0.5f;
+                }
                 if (use_tol) ui = __builtin_fmaf(1.0f - th, ui, th * c);
                 if (chk) {
                     const float t = c + pdi;
@@ -460,7 +503,7 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
                 }
                 wi = __builtin_fmaf(bn, yp - yi, yp);
                 yi = yp;
-                w_l[row] = wi;
+                put_w(wi);
             }
         }
         if (chk) check_publish<float>(slots, violz, violh, wmin, gap);
@@ -489,16 +532,16 @@ static int res_bucket(int len) {
     return (len + 31) / 32 * 32;
 }
 
-template <int KA>
+template <int KA, bool FLAT = false>
 static void launch_res_b(int kb, dim3 g, dim3 bl, hipStream_t st, const SolveArgs<float>& a) {
     switch (kb) {
-        case 32: hipLaunchKernelGGL((gpad_resident_kernel<KA, 32>), g, bl, 0, st, a); break;
-        case 64: hipLaunchKernelGGL((gpad_resident_kernel<KA, 64>), g, bl, 0, st, a); break;
-        case 96: hipLaunchKernelGGL((gpad_resident_kernel<KA, 96>), g, bl, 0, st, a); break;
-        case 128: hipLaunchKernelGGL((gpad_resident_kernel<KA, 128>), g, bl, 0, st, a); break;
-        case 160: hipLaunchKernelGGL((gpad_resident_kernel<KA, 160>), g, bl, 0, st, a); break;
-        case 192: hipLaunchKernelGGL((gpad_resident_kernel<KA, 192>), g, bl, 0, st, a); break;
-        default: hipLaunchKernelGGL((gpad_resident_kernel<KA, 208>), g, bl, 0, st, a); break;
+        case 32: hipLaunchKernelGGL((gpad_resident_kernel<KA, 32, FLAT>), g, bl, 0, st, a); break;
+        case 64: hipLaunchKernelGGL((gpad_resident_kernel<KA, 64, FLAT>), g, bl, 0, st, a); break;
+        case 96: hipLaunchKernelGGL((gpad_resident_kernel<KA, 96, FLAT>), g, bl, 0, st, a); break;
+        case 128: hipLaunchKernelGGL((gpad_resident_kernel<KA, 128, FLAT>), g, bl, 0, st, a); break;
+        case 160: hipLaunchKernelGGL((gpad_resident_kernel<KA, 160, FLAT>), g, bl, 0, st, a); break;
+        case 192: hipLaunchKernelGGL((gpad_resident_kernel<KA, 192, FLAT>), g, bl, 0, st, a); break;
+        default: hipLaunchKernelGGL((gpad_resident_kernel<KA, 208, FLAT>), g, bl, 0, st, a); break;
     }
 }
 
@@ -535,6 +578,38 @@ hipError_t launch_resident(const SolveArgs<float>& a, hipStream_t st, bool* supp
 
 hipError_t launch_resident_finisher(const SolveArgs<float>& a, int grid, hipStream_t st) {
     return launch_resident_grid(a, grid, st);
+}
+
+// flat battery variant: primal chains of 6N, constraint chains of n (flat G_L expanded to the
+// k-major image a.GLt by the host at gpad_setup_flat); a.MGt = flat -ML (Nh x m row-major)
+bool flat_resident_supported(int n, int m, int n_u) {
+    if (n_u <= 0 || n_u > kFlatMaxCells || n % n_u) return false;
+    const int Nh = n / n_u;
+    const int laneA = n_u * ((Nh + 15) / 16) * 16;
+    const int threads = 64 * ((laneA + 63) / 64) + 64 * ((m + 63) / 64);
+    return 6 * Nh <= kResidentMaxRow && n <= kResidentMaxRow && threads <= kResidentMaxThreads &&
+           m >= 4 * n;
+}
+
+hipError_t launch_flat_resident(const SolveArgs<float>& a, hipStream_t st) {
+    const int Nh = a.n / a.n_u;
+    const int laneA = a.n_u * ((Nh + 15) / 16) * 16;
+    const int threads = 64 * ((laneA + 63) / 64) + 64 * ((a.m + 63) / 64);
+    SolveArgs<float> b = a;
+    b.count_in = nullptr;
+    b.idx_in = nullptr;
+    const dim3 grid(a.batch), block(threads);
+    const int ka = res_bucket(6 * Nh), kb = res_bucket(a.n);
+    switch (ka) {
+        case 32: launch_res_b<32, true>(kb, grid, block, st, b); break;
+        case 64: launch_res_b<64, true>(kb, grid, block, st, b); break;
+        case 96: launch_res_b<96, true>(kb, grid, block, st, b); break;
+        case 128: launch_res_b<128, true>(kb, grid, block, st, b); break;
+        case 160: launch_res_b<160, true>(kb, grid, block, st, b); break;
+        case 192: launch_res_b<192, true>(kb, grid, block, st, b); break;
+        default: launch_res_b<208, true>(kb, grid, block, st, b); break;
+    }
+    return hipGetLastError();
 }
 
 // =========================================================================================

@@ -100,13 +100,16 @@ class GpadSolver:
         check(fn(self.h, C.byref(self.dims), _ptr(ML), _ptr(G), float(L)), "gpad_setup")
 
     def setup_flat(self, MGf, GLf, L: float, *, n_u: int, batch: int = 1,
-                   schedule: int = _lib.SCHEDULE_MATLAB, check_every: int = 10) -> None:
+                   schedule: int = _lib.SCHEDULE_MATLAB, check_every: int = 10,
+                   kernel: int = _lib.KERNEL_AUTO) -> None:
         """Bind the reference's flat battery data (seq_functions.cpp:5-43): MGf (N x m) flat
-        sign-folded M_G, GLf (m x N) flat G_L; then ``run(..., scaled=True)`` with g_P, p_D."""
+        sign-folded M_G, GLf (m x N) flat G_L; then ``run(..., scaled=True)`` with g_P, p_D.
+        kernel=KERNEL_STREAM forces the LDS flat kernel (else the register-resident one when
+        6N, n <= 208)."""
         Nh, m = MGf.shape
         mem = _lib.MEM_DEVICE if _is_torch(MGf) else _lib.MEM_HOST
         self.dims = Dims(n=n_u * Nh, m=m, batch=batch, shared=1, dtype=_lib.DTYPE_F32, memory=mem,
-                         schedule=schedule, check_every=check_every, kernel=_lib.KERNEL_AUTO)
+                         schedule=schedule, check_every=check_every, kernel=kernel)
         check(self.lib.gpad_setup_flat(self.h, C.byref(self.dims), int(n_u), _ptr(MGf), _ptr(GLf),
                                        float(L)), "gpad_setup_flat")
 

@@ -88,19 +88,23 @@ def test_flat_datafile_reads(tmp_path):
 
 
 # ---------------------------------------------------------------------------------- GPU
-def _flat_solver(gd, batch=1):
+VARIANTS = [0, 1]  # KERNEL_AUTO: register-resident flat chains; KERNEL_STREAM: the LDS flat kernel
+
+
+def _flat_solver(gd, batch=1, kernel=0):
     import gpad_mpc
     s = gpad_mpc.GpadSolver(0)
-    s.setup_flat(gd["MGf"], gd["GLf"], float(gd["L"]), n_u=int(gd["n_u"]), batch=batch)
+    s.setup_flat(gd["MGf"], gd["GLf"], float(gd["L"]), n_u=int(gd["n_u"]), batch=batch, kernel=kernel)
     return s
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", FLAT_SETS)
-def test_flat_kernel_matches_reference_steps(gpu, name):
+@pytest.mark.parametrize("kernel", VARIANTS)
+def test_flat_kernel_matches_reference_steps(gpu, name, kernel):
     """Fixed N = 1, 10, 100 with the reference's θ/β: bit-exact with its own flat steps."""
     gd = load_golden(name)
-    s = _flat_solver(gd)
+    s = _flat_solver(gd, kernel=kernel)
     n, m = gd["gP"].size, gd["pD"].size
     for K in (1, 10, 100):
         z = np.zeros(n, np.float32)
@@ -114,9 +118,10 @@ def test_flat_kernel_matches_reference_steps(gpu, name):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", FLAT_SETS)
-def test_flat_kernel_algorithm1(gpu, name):
+@pytest.mark.parametrize("kernel", VARIANTS)
+def test_flat_kernel_algorithm1(gpu, name, kernel):
     gd = load_golden(name)
-    s = _flat_solver(gd)
+    s = _flat_solver(gd, kernel=kernel)
     n, m = gd["gP"].size, gd["pD"].size
     z = np.zeros(n, np.float32)
     y = np.zeros(m, np.float32)
@@ -128,11 +133,13 @@ def test_flat_kernel_algorithm1(gpu, name):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("tol,N", [(0.0, 150), (1e-4, 4000)])
-def test_flat_batch_bitexact(gpu, oracle, tol, N):
+@pytest.mark.parametrize("kernel", VARIANTS)
+@pytest.mark.parametrize("cells", [(4, 10), (3, 17), (5, 6)])
+def test_flat_batch_bitexact(gpu, oracle, tol, N, kernel, cells):
     """A battery-scenario batch (one plant, per-state g_P, p_D) on the flat kernel vs the
     oracle's flat solve per instance."""
     from gpad_mpc import problems
-    n_u, Nh, B = 4, 10, 48
+    (n_u, Nh), B = cells, 48
     qp = problems.battery_scenarios(n_u, Nh, B, seed=4)
     MGf, GLf, L = problems.flatten_battery(qp, n_u, Nh)
     f32 = lambda a: np.ascontiguousarray(np.asarray(a, np.float64).astype(np.float32))  # noqa: E731
@@ -142,7 +149,7 @@ def test_flat_batch_bitexact(gpu, oracle, tol, N):
     PD = oracle.scale_vec(f32(qp.g), L32)
     import gpad_mpc
     s = gpad_mpc.GpadSolver(0)
-    s.setup_flat(MGf32, GLf32, float(L32), n_u=n_u, batch=B)
+    s.setup_flat(MGf32, GLf32, float(L32), n_u=n_u, batch=B, kernel=kernel)
     Z = np.zeros((B, qp.n), np.float32)
     Y = np.zeros((B, qp.m), np.float32)
     it = np.zeros(B, np.int32)
