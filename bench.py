@@ -101,38 +101,51 @@ def cpu_baseline(n, m, ML, G, L, M, g, iters_per_instance, budget_s=12.0):
             "single_thread_value": N / t1, "seconds": round(dt, 2)}
 
 
-def phase_schedule(N, K=10, len0=None):
+def phase_schedule(N, K=10, len0=None, hint=0):
     """The panel kernel's phase boundaries (csrc/gpad_panel.hip launch_panel_t): phases of 4K
-    iterations, doubling after the 10th, the last one ending at N."""
+    iterations, doubling after the 10th, the last one ending at N; with a hint (the previous
+    solve's takeover point + one phase) the schedule closes there with one phase to N."""
     len0 = len0 or 4 * K
     out, v0, ph = [], 0, 0
     while v0 < N:
         plen = len0 if ph < 10 else len0 << min(ph - 9, 20)
+        if ph > 0 and hint > 0 and v0 >= hint:
+            plen = N
         v1 = N if N - v0 <= plen else v0 + plen
         out.append((v0, v1))
         v0, ph = v1, ph + 1
     return out
 
 
-def phase_util(iters, N, K=10):
+def phase_hint(iters, N, K=10, fin=512):
+    """gpad_panel.hip panel_phase_hint: first phase start with <= fin survivors, plus a phase."""
+    len0 = 4 * K
+    for v0, v1 in phase_schedule(N, K):
+        if v1 < N and int((iters > v1).sum()) <= fin:
+            return v1 + len0
+    return 0
+
+
+def phase_util(iters, N, K=10, fin=512):
     """Column utilisation of phased compaction, estimated from the per-instance iteration
     counts: a phase [v0, v1) packs its survivors (iters > v0) into 16-column panels that run
-    until v1 or their last column's end; useful = sum of iterations.  Also the number of phase
-    launches per solve and how many of them had survivors."""
+    until v1 or their last column's end, until the survivors fit the resident finisher (<= fin,
+    one instance per workgroup, no idle columns); useful = sum of iterations.  Also the phase
+    launches per solve (the schedule closes at the hint learned from the previous solve)."""
     it = iters.astype(np.int64)  # survivors keep (roughly) index order in the kernel's lists
     executed = 0
-    live_launches = 0
-    phases = phase_schedule(N, K)
+    phases = phase_schedule(N, K, hint=phase_hint(it, N, K, fin))
     for v0, v1 in phases:
         surv = it[it > v0]
         if surv.size == 0:
             continue
-        live_launches += 1
+        if v0 > 0 and surv.size <= fin:  # the finisher runs them to the end
+            executed += int((surv - v0).sum())
+            break
         for i in range(0, surv.size, 16):
             executed += 16 * (min(v1, int(surv[i:i + 16].max())) - v0)
     return {"column_util_est": float(it.sum() / executed) if executed else None,
-            "launches_per_solve": len(phases), "launches_with_survivors": live_launches,
-            "min_iters": int(it.min()), "max_iters": int(it.max())}
+            "launches_per_solve": len(phases), "min_iters": int(it.min()), "max_iters": int(it.max())}
 
 
 def traffic_from_profile(kernel_prefix):
@@ -399,7 +412,7 @@ def main():
         traffic, traffic_src = traffic_from_profile("gpad::gpad_" + st["kernel"])
         launches = util["launches_per_solve"] if st["kernel"] == "panel" else 1
         if traffic is not None:
-            traffic *= launches  # PMC values are per phase launch; one solve = `launches` of them
+            traffic *= launches  # PMC values are per panel-phase launch; one solve = `launches`
         with gpad_mpc.GpadSolver(dev.index, stream=stream.cuda_stream) as s1:
             s1.setup(dML, dG, L32, n=n, m=m, batch=1)
             z1 = torch.zeros(1, n, device=dev)

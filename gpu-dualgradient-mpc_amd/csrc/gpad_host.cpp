@@ -104,6 +104,9 @@ struct gpad_handle_s {
     std::vector<int> h_counts;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int last_kernel = 0, last_batch = 0, last_steps = 1;
+    // phased panel solves: the previous run's takeover point (see gpad::panel_phase_hint)
+    bool last_phased = false;
+    int last_N = 0, phase_hint = 0;
     // plant binding (gpad_setup_plant): affine state maps and dynamics, device copies
     int nx = 0, nu = 0;
     bool plant_ready = false, plant_dyn = false;
@@ -223,6 +226,7 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
     HIP_TRY(hipSetDevice(h->device));
     h->ready = false;
     h->flat = false;
+    h->phase_hint = 0;
     h->dims = *d;
     if (h->dims.check_every <= 0) h->dims.check_every = 10;
     h->L = L;
@@ -301,6 +305,7 @@ int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* d, int n_u, const float*
     HIP_TRY(hipSetDevice(h->device));
     h->ready = false;
     h->flat = false;
+    h->phase_hint = 0;
     h->dims = *d;
     if (h->dims.check_every <= 0) h->dims.check_every = 10;
     h->L = L;
@@ -398,6 +403,9 @@ static int collect_stats(gpad_handle_t h, gpad_stats_t* st) {
             if (st->iters) st->iters[(size_t)t * batch + b] = it[b];
         }
     }
+    if (h->last_phased && h->last_steps == 1)
+        h->phase_hint = gpad::panel_phase_hint(h->h_counts.data(), batch, h->dims.n, h->dims.m, h->last_N,
+                                               h->dims.check_every, h->num_cus);
     st->kernel = h->last_kernel;
     float ms = 0.0f;
     st->kernel_ms = 0.0;
@@ -482,6 +490,7 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
                 int rc = h->pwork.ensure(gpad::panel_work_bytes(m, batch));
                 if (rc) return rc;
                 a.pwork = h->pwork.p;
+                a.phase_hint = h->phase_hint;
             }
             e = gpad::launch_panel(a, h->stream, &ok);
             if (e != hipSuccess) return fail(GPAD_ERR_HIP, std::string("panel: ") + hipGetErrorString(e));
@@ -509,6 +518,8 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
                             " (n+m beyond the LDS budget?)");
     }
     *kernel_out = kernel;
+    h->last_phased = kernel == GPAD_KERNEL_PANEL && a.pwork != nullptr;
+    h->last_N = N;
     return GPAD_OK;
 }
 

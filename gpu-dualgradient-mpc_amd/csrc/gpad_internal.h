@@ -48,6 +48,7 @@ struct SolveArgs {
     int fin_thresh;        // survivors <= this: the resident finisher takes them (0: none)
     int n_u;               // flat battery path: cells (n = n_u * horizon), see gpad_flat.hip
     int flat_staged;       // flat path: matrices staged in LDS (set by launch_flat)
+    int phase_hint;        // panel phases: close the schedule at this iteration (0: none)
 };
 
 // launchers (return hipError_t of the launch)
@@ -61,6 +62,9 @@ bool resident_supported(int n, int m);
 hipError_t launch_panel(const SolveArgs<float>& a, hipStream_t s, bool* supported);
 size_t panel_frag_bytes(int n, int m, int batch);
 size_t panel_work_bytes(int m, int batch);
+int panel_phase_len(int check_every);
+int panel_fin_thresh(int n, int m, int num_cus);
+int panel_phase_hint(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus);
 int panel_tiles(int n, int m, int batch);
 hipError_t launch_pack_panel(const float* ML, const float* G, int n, int m, int batch, float mg_sign,
                              double g_scale, void* frag, hipStream_t s);

@@ -29,6 +29,7 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <vector>
 
 #include "gpad_internal.h"
 
@@ -727,6 +728,54 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
     }
 }
 
+// schedule parameters shared by the launcher and the host's phase hint
+int panel_phase_len(int check_every) {
+    // a multiple of the test period (phases end right after a test); default four tests
+    int len = 4 * check_every;
+    if (const char* pl = std::getenv("GPAD_PANEL_PHASE")) {  // test / tuning knob
+        const int q = std::atoi(pl);
+        if (q > 0) len = q;
+    }
+    return ((len + check_every - 1) / check_every) * check_every;
+}
+
+int panel_fin_thresh(int n, int m, int num_cus) {
+    // the tail of a phased solve (survivors <= 2 per CU) goes to the latency kernel: one
+    // instance per workgroup at ~1/6 of a panel's iteration time (when n, m fit it); measured
+    // on C4: 2/CU 5.42e8 it/s, 4/CU 5.35e8, 8/CU 5.35e8, no finisher 5.04e8
+    int f = resident_supported(n, m) ? 2 * num_cus : 0;
+    if (const char* ft = std::getenv("GPAD_FINISH_THRESH")) {  // test / tuning knob
+        const int q = std::atoi(ft);
+        if (q >= 0 && f) f = q;
+    }
+    return f;
+}
+
+// From a finished phased solve's per-instance iteration counts: the phase start at which the
+// finisher took over, plus one phase of margin (0: no takeover).  The next solve of the same
+// handle closes its schedule there (launch_panel_t, a.phase_hint).
+int panel_phase_hint(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus) {
+    const int fin = panel_fin_thresh(n, m, num_cus);
+    if (!fin || batch <= 0) return 0;
+    const int len = panel_phase_len(check_every);
+    std::vector<int> hist(N + 2, 0);
+    for (int b = 0; b < batch; ++b) hist[iters[b] < 0 ? 0 : (iters[b] > N ? N : iters[b])]++;
+    // survivors at v = #(iters > v)
+    int above = batch - hist[0];
+    int v0 = 0, prev = 0;
+    for (int ph = 0; v0 < N; ++ph) {
+        int plen = len;
+        if (ph >= 10) plen = len << (ph - 9 < 20 ? ph - 9 : 20);
+        const int v1 = (N - v0 <= plen) ? N : v0 + plen;
+        for (int v = prev + 1; v <= v1 && v <= N; ++v) above -= hist[v];
+        prev = v1;
+        // at the start of phase ph + 1 (v = v1) the survivors are `above`
+        if (v1 < N && above <= fin) return v1 + len;
+        v0 = v1;
+    }
+    return 0;
+}
+
 size_t panel_work_bytes(int m, int batch) {
     // idx ping-pong [2][batch] | phase counts [kPanelMaxPhases] | carried w, u [batch][m] each
     return sizeof(int) * (2 * (size_t)batch + kPanelMaxPhases) + 2 * sizeof(float) * (size_t)batch * m;
@@ -752,14 +801,7 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
         if (c > 0 && c < grid) grid = c;
     }
     const bool phased = a.tol > 0.0 && a.pwork != nullptr;
-    // the tail of a phased solve (survivors <= 2 per CU) goes to the latency kernel: one
-    // instance per workgroup at ~1/6 of a panel's iteration time (when n, m fit it); measured
-    // on C4: 2/CU 5.42e8 it/s, 4/CU 5.35e8, 8/CU 5.35e8, no finisher 5.04e8
-    a.fin_thresh = phased && resident_supported(a.n, a.m) ? 2 * a.num_cus : 0;
-    if (const char* ft = std::getenv("GPAD_FINISH_THRESH")) {  // test / tuning knob
-        const int q = std::atoi(ft);
-        if (q >= 0 && a.fin_thresh) a.fin_thresh = q;
-    }
+    a.fin_thresh = phased ? panel_fin_thresh(a.n, a.m, a.num_cus) : 0;
     if (!phased) {  // fixed N (or no workspace): one phase, nothing carried
         a.v_begin = 0;
         a.v_end = a.N;
@@ -779,17 +821,15 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     // phase length: a multiple of the test period (phases end right after a test); default
     // four tests, doubling after 10 phases so a long tail costs O(log N) launches (a phase with
     // no survivors left costs one empty launch, ~5 us)
-    int len = 4 * a.check_every;
-    if (const char* pl = std::getenv("GPAD_PANEL_PHASE")) {
-        const int q = std::atoi(pl);
-        if (q > 0) len = q;
-    }
-    len = ((len + a.check_every - 1) / a.check_every) * a.check_every;
+    const int len = panel_phase_len(a.check_every);
     int v0 = 0;
     for (int ph = 0; v0 < a.N; ++ph) {
         int plen = len;
         if (ph >= 10) plen = len << (ph - 9 < 20 ? ph - 9 : 20);
         if (ph >= kPanelMaxPhases - 1) plen = a.N;  // last slot: run to N
+        // the previous solve's finisher took over before this point: close with one phase to N
+        // (its finisher or panel launch does all that is left; saves the empty launches after)
+        if (ph > 0 && a.phase_hint > 0 && v0 >= a.phase_hint) plen = a.N;
         const int v1 = (a.N - v0 <= plen) ? a.N : v0 + plen;
         a.v_begin = v0;
         a.v_end = v1;

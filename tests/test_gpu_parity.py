@@ -202,6 +202,37 @@ def test_panel_phased_compaction_bitexact(gpu, oracle, monkeypatch, grid, phase,
         assert_bitexact(y[b], yo, f"instance {b} y")
 
 
+@pytest.mark.parametrize("fin", [None, 0])
+def test_panel_phase_hint_reuse_bitexact(gpu, oracle, monkeypatch, fin):
+    """A handle closes its phase schedule where the previous solve's finisher took over; a later
+    solve that needs more iterations must still be exact (the closing phase runs to N)."""
+    import gpad_mpc
+    from gpad_mpc import problems
+    if fin is not None:
+        monkeypatch.setenv("GPAD_FINISH_THRESH", str(fin))
+    monkeypatch.setenv("GPAD_PANEL_PHASE", "10")
+    n, m, B = 40, 72, 300
+    qp = problems.synthetic_qp(n, m, batch=B, seed=31)
+    ML, G = qp.ML.astype(np.float32), qp.G.astype(np.float32)
+    L = np.float32(qp.L)
+    rng = np.random.default_rng(5)
+    with gpad_mpc.GpadSolver(0) as s:
+        s.setup(ML, G, float(L), n=n, m=m, batch=B, kernel=kcode("panel"))
+        for scale, tol in ((1.0, 1e-3), (3.0, 1e-5), (1.0, 1e-4)):  # easy, harder, middle
+            M = (qp.M * scale).astype(np.float32)
+            g = (qp.g + 0.1 * rng.random((B, m))).astype(np.float32)
+            z = np.zeros((B, n), np.float32)
+            y = np.zeros((B, m), np.float32)
+            it = np.zeros(B, np.int32)
+            st = s.run(z, y, M, g, 4000, tol, iters=it)
+            assert st["kernel"] == "panel"
+            for b in range(0, B, 7):
+                zo, yo, ito, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), ML, M[b], G, g[b], 4000, L, tol)
+                assert it[b] == ito, (scale, b)
+                assert_bitexact(z[b], zo, f"{scale} z[{b}]")
+                assert_bitexact(y[b], yo, f"{scale} y[{b}]")
+
+
 def test_paper_schedule_bitexact(gpu, oracle):
     gd = load_golden("battery_c1")
     ML, M, G, g, L = f32_inputs(gd)
