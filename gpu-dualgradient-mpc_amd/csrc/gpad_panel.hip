@@ -402,11 +402,13 @@ __device__ __forceinline__ void panel_a_prefetch(__amdgpu_buffer_rsrc_t PA, int 
         if (p < T) ap[p] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, p * T * 1024, 0));
 }
 
-// panel_gemm2 with an A ring PD blocks deep, seeded by panel_a_prefetch.
+// panel_gemm2 with an A ring PD blocks deep, seeded by panel_a_prefetch.  The last k-block
+// issues only its first kq MFMA steps: k-steps past the matrix are zero in both operands, so
+// skipping them is exact (an accumulator started at +0 never holds -0).  kq is wave-uniform.
 template <int T, bool DUAL, int PD>
 __device__ __forceinline__ void panel_gemm3(__amdgpu_buffer_rsrc_t PA, const float4* B0, const float4* B1,
                                             int voff, int lane, f32x4& acc0, f32x4& acc1,
-                                            const float4 (&ap)[PD]) {
+                                            const float4 (&ap)[PD], int kq) {
     acc0 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     acc1 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     constexpr int R = PD + 1;
@@ -428,12 +430,63 @@ __device__ __forceinline__ void panel_gemm3(__amdgpu_buffer_rsrc_t PA, const flo
         __builtin_amdgcn_sched_barrier(0);
         acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, b0[cur].x, acc0, 0, 0, 0);
         if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, b1[cur].x, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, b0[cur].y, acc0, 0, 0, 0);
-        if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, b1[cur].y, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, b0[cur].z, acc0, 0, 0, 0);
-        if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, b1[cur].z, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, b0[cur].w, acc0, 0, 0, 0);
-        if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, b1[cur].w, acc1, 0, 0, 0);
+        if (kb + 1 < T || kq > 1) {
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, b0[cur].y, acc0, 0, 0, 0);
+            if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, b1[cur].y, acc1, 0, 0, 0);
+        }
+        if (kb + 1 < T || kq > 2) {
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, b0[cur].z, acc0, 0, 0, 0);
+            if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, b1[cur].z, acc1, 0, 0, 0);
+        }
+        if (kb + 1 < T || kq > 3) {
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, b0[cur].w, acc0, 0, 0, 0);
+            if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, b1[cur].w, acc1, 0, 0, 0);
+        }
+        if constexpr (DUAL) asm volatile("" : "+v"(acc0), "+v"(acc1)::"memory");
+        else asm volatile("" : "+v"(acc0)::"memory");
+    }
+}
+
+// Runtime-length variant for a GEMM whose K spans fewer k-blocks than the tile count
+// (n != m: e.g. the battery's n = 40 against m = 180 -> 3 of 12 blocks).  A plain loop with the
+// A/B rings rotated by register moves; soffset in an SGPR, so no per-block address VGPRs.
+template <int T, bool DUAL, int PD>
+__device__ __forceinline__ void panel_gemm_rt(__amdgpu_buffer_rsrc_t PA, const float4* B0, const float4* B1,
+                                              int voff, int lane, f32x4& acc0, f32x4& acc1,
+                                              const float4 (&ap)[PD], int nkb, int kq) {
+    acc0 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    acc1 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    float4 a[PD + 1];
+#pragma unroll
+    for (int p = 0; p < PD; ++p) a[p] = ap[p];
+    float4 b0 = B0[lane], b1 = DUAL ? B1[lane] : b0;
+    for (int kb = 0; kb < nkb; ++kb) {
+        const float4 ak = a[0];
+#pragma unroll
+        for (int p = 0; p < PD; ++p) a[p] = a[p + 1];
+        if (kb + PD < nkb)
+            a[PD - 1] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb + PD) * T * 1024, 0));
+        const float4 bk0 = b0, bk1 = b1;
+        if (kb + 1 < nkb) {
+            b0 = B0[(kb + 1) * 64 + lane];
+            if constexpr (DUAL) b1 = B1[(kb + 1) * 64 + lane];
+        }
+        const int steps = kb + 1 < nkb ? 4 : kq;
+        __builtin_amdgcn_sched_barrier(0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, bk0.x, acc0, 0, 0, 0);
+        if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, bk1.x, acc1, 0, 0, 0);
+        if (steps > 1) {
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, bk0.y, acc0, 0, 0, 0);
+            if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, bk1.y, acc1, 0, 0, 0);
+        }
+        if (steps > 2) {
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, bk0.z, acc0, 0, 0, 0);
+            if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, bk1.z, acc1, 0, 0, 0);
+        }
+        if (steps > 3) {
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, bk0.w, acc0, 0, 0, 0);
+            if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, bk1.w, acc1, 0, 0, 0);
+        }
         if constexpr (DUAL) asm volatile("" : "+v"(acc0), "+v"(acc1)::"memory");
         else asm volatile("" : "+v"(acc0)::"memory");
     }
@@ -475,6 +528,12 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
     const int voff = t * 1024 + lane * 16;
     const int slot = t * 64 + lane;
     constexpr int Q = NU > 0 ? NU : 1;  // array extent
+    // GEMM 1: K = m, output rows n; GEMM 2: K = n, output rows m.  The last k-block issues only
+    // the steps inside K when K is the padded dimension (kq), and a wave whose tile lies past
+    // the output rows skips its GEMM (zeros).
+    const int nkb1 = (m + 15) / 16, nkb2 = (n + 15) / 16;  // k-blocks of each GEMM (<= T)
+    const int kq1 = (m - 16 * (nkb1 - 1) + 3) / 4, kq2 = (n - 16 * (nkb2 - 1) + 3) / 4;
+    const bool on1 = 16 * t < n, on2 = 16 * t < m;
 
     for (int it = blockIdx.x; it < items; it += gridDim.x) {
         bool act[Q];
@@ -540,7 +599,14 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             // ---- GEMM 1 + epilogue: zhat = -ML w - g_P (8b), z = (1-th) z + th zhat (8c) ----
             if constexpr (NU > 0) {
                 f32x4 acc[2];
-                panel_gemm3<T, NU == 2, PD>(PA1, L.Wl[p0], L.Wl[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1], ap);
+                if (on1 && nkb1 == T)
+                    panel_gemm3<T, NU == 2, PD>(PA1, L.Wl[p0], L.Wl[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1],
+                                                ap, kq1);
+                else if (on1)
+                    panel_gemm_rt<T, NU == 2, PD>(PA1, L.Wl[p0], L.Wl[NU == 2 ? 1 : p0], voff, lane, acc[0],
+                                                  acc[1], ap, nkb1, kq1);
+                else
+                    acc[0] = acc[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
                 panel_a_prefetch<T, PD>(PA2, voff, ap);
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
@@ -568,7 +634,14 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             }
             if constexpr (NU > 0) {
                 f32x4 acc[2];
-                panel_gemm3<T, NU == 2, PD>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1], ap);
+                if (on2 && nkb2 == T)
+                    panel_gemm3<T, NU == 2, PD>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1],
+                                                ap, kq2);
+                else if (on2)
+                    panel_gemm_rt<T, NU == 2, PD>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, acc[0],
+                                                  acc[1], ap, nkb2, kq2);
+                else
+                    acc[0] = acc[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
                 panel_a_prefetch<T, PD>(PA1, voff, ap);
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
