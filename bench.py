@@ -101,7 +101,7 @@ def cpu_baseline(n, m, ML, G, L, M, g, iters_per_instance, budget_s=12.0):
             "single_thread_value": N / t1, "seconds": round(dt, 2)}
 
 
-def phase_schedule(N, K=10, len0=None, hint=0):
+def phase_schedule(N, K=10, len0=None, hint=0, first=0):
     """The panel kernel's phase boundaries (csrc/gpad_panel.hip launch_panel_t): phases of 4K
     iterations, doubling after the 10th, the last one ending at N; with a hint (the previous
     solve's takeover point + one phase) the schedule closes there with one phase to N."""
@@ -111,16 +111,25 @@ def phase_schedule(N, K=10, len0=None, hint=0):
         plen = len0 if ph < 10 else len0 << min(ph - 9, 20)
         if ph > 0 and hint > 0 and v0 >= hint:
             plen = N
+        if ph == 0 and first > plen:
+            plen = first
         v1 = N if N - v0 <= plen else v0 + plen
         out.append((v0, v1))
         v0, ph = v1, ph + 1
     return out
 
 
+def phase_first(iters, N, K=10):
+    """gpad_panel.hip panel_phase_first: the earliest convergence, in whole phases."""
+    len0 = 4 * K
+    f = (int(iters.min()) // len0) * len0
+    return f if f > len0 else 0
+
+
 def phase_hint(iters, N, K=10, fin=512):
     """gpad_panel.hip panel_phase_hint: first phase start with <= fin survivors, plus a phase."""
     len0 = 4 * K
-    for v0, v1 in phase_schedule(N, K):
+    for v0, v1 in phase_schedule(N, K, first=phase_first(iters, N, K)):
         if v1 < N and int((iters > v1).sum()) <= fin:
             return v1 + len0
     return 0
@@ -134,7 +143,7 @@ def phase_util(iters, N, K=10, fin=512):
     launches per solve (the schedule closes at the hint learned from the previous solve)."""
     it = iters.astype(np.int64)  # survivors keep (roughly) index order in the kernel's lists
     executed = 0
-    phases = phase_schedule(N, K, hint=phase_hint(it, N, K, fin))
+    phases = phase_schedule(N, K, hint=phase_hint(it, N, K, fin), first=phase_first(it, N, K))
     for v0, v1 in phases:
         surv = it[it > v0]
         if surv.size == 0:

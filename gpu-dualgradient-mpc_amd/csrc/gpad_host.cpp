@@ -106,7 +106,7 @@ struct gpad_handle_s {
     int last_kernel = 0, last_batch = 0, last_steps = 1;
     // phased panel solves: the previous run's takeover point (see gpad::panel_phase_hint)
     bool last_phased = false;
-    int last_N = 0, phase_hint = 0;
+    int last_N = 0, phase_hint = 0, phase_first = 0;
     // plant binding (gpad_setup_plant): affine state maps and dynamics, device copies
     int nx = 0, nu = 0;
     bool plant_ready = false, plant_dyn = false;
@@ -227,6 +227,7 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
     h->ready = false;
     h->flat = false;
     h->phase_hint = 0;
+    h->phase_first = 0;
     h->dims = *d;
     if (h->dims.check_every <= 0) h->dims.check_every = 10;
     h->L = L;
@@ -306,6 +307,7 @@ int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* d, int n_u, const float*
     h->ready = false;
     h->flat = false;
     h->phase_hint = 0;
+    h->phase_first = 0;
     h->dims = *d;
     if (h->dims.check_every <= 0) h->dims.check_every = 10;
     h->L = L;
@@ -403,9 +405,11 @@ static int collect_stats(gpad_handle_t h, gpad_stats_t* st) {
             if (st->iters) st->iters[(size_t)t * batch + b] = it[b];
         }
     }
-    if (h->last_phased && h->last_steps == 1)
+    if (h->last_phased && h->last_steps == 1) {
         h->phase_hint = gpad::panel_phase_hint(h->h_counts.data(), batch, h->dims.n, h->dims.m, h->last_N,
                                                h->dims.check_every, h->num_cus);
+        h->phase_first = gpad::panel_phase_first(h->h_counts.data(), batch, h->last_N, h->dims.check_every);
+    }
     st->kernel = h->last_kernel;
     float ms = 0.0f;
     st->kernel_ms = 0.0;
@@ -491,6 +495,7 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
                 if (rc) return rc;
                 a.pwork = h->pwork.p;
                 a.phase_hint = h->phase_hint;
+                a.phase_first = h->phase_first;
             }
             e = gpad::launch_panel(a, h->stream, &ok);
             if (e != hipSuccess) return fail(GPAD_ERR_HIP, std::string("panel: ") + hipGetErrorString(e));

@@ -49,6 +49,7 @@ struct SolveArgs {
     int n_u;               // flat battery path: cells (n = n_u * horizon), see gpad_flat.hip
     int flat_staged;       // flat path: matrices staged in LDS (set by launch_flat)
     int phase_hint;        // panel phases: close the schedule at this iteration (0: none)
+    int phase_first;       // panel phases: length of the first phase (0: the default)
 };
 
 // launchers (return hipError_t of the launch)
@@ -65,6 +66,7 @@ size_t panel_work_bytes(int m, int batch);
 int panel_phase_len(int check_every);
 int panel_fin_thresh(int n, int m, int num_cus);
 int panel_phase_hint(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus);
+int panel_phase_first(const int* iters, int batch, int N, int check_every);
 int panel_tiles(int n, int m, int batch);
 hipError_t launch_pack_panel(const float* ML, const float* G, int n, int m, int batch, float mg_sign,
                              double g_scale, void* frag, hipStream_t s);

@@ -827,6 +827,16 @@ int panel_fin_thresh(int n, int m, int num_cus) {
 // From a finished phased solve's per-instance iteration counts: the phase start at which the
 // finisher took over, plus one phase of margin (0: no takeover).  The next solve of the same
 // handle closes its schedule there (launch_panel_t, a.phase_hint).
+int panel_phase_first(const int* iters, int batch, int N, int check_every) {
+    // the earliest convergence of the previous solve, rounded down to whole phases: compacting
+    // before it re-packs panels that have no finished column (pure carry traffic)
+    const int len = panel_phase_len(check_every);
+    int mn = N;
+    for (int b = 0; b < batch; ++b) mn = iters[b] < mn ? iters[b] : mn;
+    const int first = (mn / len) * len;
+    return first > len ? first : 0;
+}
+
 int panel_phase_hint(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus) {
     const int fin = panel_fin_thresh(n, m, num_cus);
     if (!fin || batch <= 0) return 0;
@@ -836,9 +846,11 @@ int panel_phase_hint(const int* iters, int batch, int n, int m, int N, int check
     // survivors at v = #(iters > v)
     int above = batch - hist[0];
     int v0 = 0, prev = 0;
+    const int first = panel_phase_first(iters, batch, N, check_every);
     for (int ph = 0; v0 < N; ++ph) {
         int plen = len;
         if (ph >= 10) plen = len << (ph - 9 < 20 ? ph - 9 : 20);
+        if (ph == 0 && first > plen) plen = first;
         const int v1 = (N - v0 <= plen) ? N : v0 + plen;
         for (int v = prev + 1; v <= v1 && v <= N; ++v) above -= hist[v];
         prev = v1;
@@ -873,7 +885,7 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
         const int c = std::atoi(cap);
         if (c > 0 && c < grid) grid = c;
     }
-    const bool phased = a.tol > 0.0 && a.pwork != nullptr;
+    const bool phased = a.tol > 0.0 && a.pwork != nullptr && !std::getenv("GPAD_PANEL_NOPHASE");
     a.fin_thresh = phased ? panel_fin_thresh(a.n, a.m, a.num_cus) : 0;
     if (!phased) {  // fixed N (or no workspace): one phase, nothing carried
         a.v_begin = 0;
@@ -903,6 +915,8 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
         // the previous solve's finisher took over before this point: close with one phase to N
         // (its finisher or panel launch does all that is left; saves the empty launches after)
         if (ph > 0 && a.phase_hint > 0 && v0 >= a.phase_hint) plen = a.N;
+        // ... and it had no convergence before phase_first: one long first phase up to there
+        if (ph == 0 && a.phase_first > plen) plen = a.phase_first;
         const int v1 = (a.N - v0 <= plen) ? a.N : v0 + plen;
         a.v_begin = v0;
         a.v_end = v1;
