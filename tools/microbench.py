@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gpu-dualgradient-mpc_amd"))
 
 
-def case(kernel, n, m, batch, N, shared=True, reps=3, tol=0.0):
+def case(kernel, n, m, batch, N, shared=True, reps=3, tol=0.0, check_every=10):
     import torch
     import gpad_mpc
     from gpad_mpc import _lib, problems
@@ -40,7 +40,7 @@ def case(kernel, n, m, batch, N, shared=True, reps=3, tol=0.0):
     z = torch.zeros(batch, n, device=dev)
     y = torch.zeros(batch, m, device=dev)
     with gpad_mpc.GpadSolver(0) as s:
-        s.setup(ML, G, L, n=n, m=m, batch=batch, shared=shared, kernel=kc)
+        s.setup(ML, G, L, n=n, m=m, batch=batch, shared=shared, kernel=kc, check_every=check_every)
         s.run(z, y, M, g, N, tol)
         best = 1e30
         for _ in range(reps):
@@ -61,6 +61,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--only", default="")
+    ap.add_argument("--check-every", type=int, default=10)
     ap.add_argument("--tol", type=float, default=0.0,
                     help="> 0: run the Algorithm-1 test path (tiny tol: never converges, N its)")
     args = ap.parse_args()
@@ -82,7 +83,7 @@ def main():
     for c in cases:
         if args.only and args.only not in c[0]:
             continue
-        print(json.dumps(case(*c, tol=args.tol)), flush=True)
+        print(json.dumps(case(*c, tol=args.tol, check_every=args.check_every)), flush=True)
 
 
 if __name__ == "__main__":
