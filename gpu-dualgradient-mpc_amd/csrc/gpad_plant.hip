@@ -20,33 +20,35 @@
 
 namespace gpad {
 
-// out1[b][i] = affine row i (i < rows1) ; out2[b][j] = affine row j (j < rows2)
+// out1[b][i] = affine row i (i < rows1) ; out2[b][j] = affine row j (j < rows2).
+// grid.x covers the rows of one instance, grid.y the instances (grid-stride beyond 65535):
+// no integer division on the path, the state x[b] is a broadcast read per block.
 template <typename T>
 __global__ __launch_bounds__(256) void affine2_kernel(const T* __restrict__ P1, const T* __restrict__ c1,
                                                       int rows1, T* __restrict__ out1,
                                                       const T* __restrict__ P2, const T* __restrict__ c2,
                                                       int rows2, T* __restrict__ out2,
                                                       const T* __restrict__ x, int nx, int batch) {
-    const int per = rows1 + rows2;
-    const long long total = (long long)batch * per;
-    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total;
-         t += (long long)gridDim.x * blockDim.x) {
-        const int b = (int)(t / per);
-        int i = (int)(t - (long long)b * per);
-        const T* P = P1;
-        const T* c = c1;
-        T* out = out1 + (long long)b * rows1;
-        if (i >= rows1) {
-            i -= rows1;
-            P = P2;
-            c = c2;
-            out = out2 + (long long)b * rows2;
-        }
-        const T* xb = x + (long long)b * nx;
-        const T* Pi = P + (long long)i * nx;
-        T acc = c ? c[i] : T(0);
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rows1 + rows2) return;
+    const T* P = P1;
+    const T* c = c1;
+    T* out = out1;
+    int ld = rows1;
+    if (i >= rows1) {
+        i -= rows1;
+        P = P2;
+        c = c2;
+        out = out2;
+        ld = rows2;
+    }
+    const T* Pi = P + (size_t)i * nx;
+    const T c0 = c ? c[i] : T(0);
+    for (int b = blockIdx.y; b < batch; b += gridDim.y) {
+        const T* xb = x + (size_t)b * nx;
+        T acc = c0;
         for (int k = 0; k < nx; ++k) acc = __builtin_fma(Pi[k], xb[k], acc);
-        out[i] = acc;
+        out[(size_t)b * ld + i] = acc;
     }
 }
 
@@ -87,8 +89,9 @@ static dim3 grid_for(long long total) {
 template <typename T>
 hipError_t launch_affine2(const T* P1, const T* c1, int rows1, T* out1, const T* P2, const T* c2,
                           int rows2, T* out2, const T* x, int nx, int batch, hipStream_t s) {
-    hipLaunchKernelGGL(affine2_kernel<T>, grid_for((long long)batch * (rows1 + rows2)), dim3(256), 0, s,
-                       P1, c1, rows1, out1, P2, c2, rows2, out2, x, nx, batch);
+    const dim3 grid((rows1 + rows2 + 255) / 256, batch < 65535 ? batch : 65535);
+    hipLaunchKernelGGL(affine2_kernel<T>, grid, dim3(256), 0, s, P1, c1, rows1, out1, P2, c2, rows2, out2, x,
+                       nx, batch);
     return hipGetLastError();
 }
 
