@@ -101,60 +101,50 @@ def cpu_baseline(n, m, ML, G, L, M, g, iters_per_instance, budget_s=12.0):
             "single_thread_value": N / t1, "seconds": round(dt, 2)}
 
 
-def phase_schedule(N, K=10, len0=None, hint=0, first=0):
-    """The panel kernel's phase boundaries (csrc/gpad_panel.hip launch_panel_t): phases of 4K
-    iterations, doubling after the 10th, the last one ending at N; with a hint (the previous
-    solve's takeover point + one phase) the schedule closes there with one phase to N."""
-    len0 = len0 or 4 * K
+def phase_schedule(N, K=10, plan=None, fin=512):
+    """The phase boundaries a phased panel solve follows (csrc/gpad_panel.hip launch_panel_t):
+    the handle's plan (gpad_phase_plan: made from the previous solve's iteration counts), or
+    without one the default phases of 4K iterations, doubling after the 10th.  Returns
+    [(v0, v1, finisher threshold at v0)]."""
     out, v0, ph = [], 0, 0
+    ends = plan["ends"] if plan and plan.get("ends") else []
+    fins = plan["fins"] if ends else []
     while v0 < N:
-        plen = len0 if ph < 10 else len0 << min(ph - 9, 20)
-        if ph > 0 and hint > 0 and v0 >= hint:
-            plen = N
-        if ph == 0 and first > plen:
-            plen = first
+        plen = 4 * K if ph < 10 else (4 * K) << min(ph - 9, 20)
+        f = fin
+        if ph < len(ends):
+            plen, f = ends[ph] - v0, (fins[ph] if ph else fin)
         v1 = N if N - v0 <= plen else v0 + plen
-        out.append((v0, v1))
+        out.append((v0, v1, f))
         v0, ph = v1, ph + 1
     return out
 
 
-def phase_first(iters, N, K=10):
-    """gpad_panel.hip panel_phase_first: the earliest convergence, in whole phases."""
-    len0 = 4 * K
-    f = (int(iters.min()) // len0) * len0
-    return f if f > len0 else 0
-
-
-def phase_hint(iters, N, K=10, fin=512):
-    """gpad_panel.hip panel_phase_hint: first phase start with <= fin survivors, plus a phase."""
-    len0 = 4 * K
-    for v0, v1 in phase_schedule(N, K, first=phase_first(iters, N, K)):
-        if v1 < N and int((iters > v1).sum()) <= fin:
-            return v1 + len0
-    return 0
-
-
-def phase_util(iters, N, K=10, fin=512):
+def phase_util(iters, N, K=10, plan=None, fin=512):
     """Column utilisation of phased compaction, estimated from the per-instance iteration
     counts: a phase [v0, v1) packs its survivors (iters > v0) into 16-column panels that run
-    until v1 or their last column's end, until the survivors fit the resident finisher (<= fin,
-    one instance per workgroup, no idle columns); useful = sum of iterations.  Also the phase
-    launches per solve (the schedule closes at the hint learned from the previous solve)."""
+    until v1 or their last column's end, until the survivors fit the resident finisher (one
+    instance per workgroup, no idle columns); useful = sum of iterations.  Also the phase
+    launches per solve."""
     it = iters.astype(np.int64)  # survivors keep (roughly) index order in the kernel's lists
     executed = 0
-    phases = phase_schedule(N, K, hint=phase_hint(it, N, K, fin), first=phase_first(it, N, K))
-    for v0, v1 in phases:
+    phases = phase_schedule(N, K, plan, fin)
+    takeover = None
+    for v0, v1, f in phases:
         surv = it[it > v0]
         if surv.size == 0:
             continue
-        if v0 > 0 and surv.size <= fin:  # the finisher runs them to the end
+        if v0 > 0 and surv.size <= f:  # the finisher runs them to the end
             executed += int((surv - v0).sum())
+            takeover = v0
             break
         for i in range(0, surv.size, 16):
             executed += 16 * (min(v1, int(surv[i:i + 16].max())) - v0)
     return {"column_util_est": float(it.sum() / executed) if executed else None,
-            "launches_per_solve": len(phases), "min_iters": int(it.min()), "max_iters": int(it.max())}
+            "launches_per_solve": len(phases), "phase_ends": [p[1] for p in phases],
+            "finisher_takeover": takeover, "planned": bool(plan and plan.get("ends")),
+            "plan_model_us": plan.get("cost_us") if plan else None,
+            "min_iters": int(it.min()), "max_iters": int(it.max())}
 
 
 def traffic_from_profile(kernel_prefix):
@@ -376,7 +366,7 @@ def main():
     torch.cuda.synchronize(dev)
     iters_host = np.zeros(B, np.int32)
     st0 = solver.last_stats(iters=iters_host)
-    util = phase_util(iters_host, args.max_iters, 10)
+    util = phase_util(iters_host, args.max_iters, 10, solver.phase_plan())
 
     if world > 1:
         dist.barrier()

@@ -104,9 +104,10 @@ struct gpad_handle_s {
     std::vector<int> h_counts;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int last_kernel = 0, last_batch = 0, last_steps = 1;
-    // phased panel solves: the previous run's takeover point (see gpad::panel_phase_hint)
+    // phased panel solves: the plan made from the previous solve (gpad::panel_plan)
     bool last_phased = false;
-    int last_N = 0, phase_hint = 0, phase_first = 0;
+    int last_N = 0;
+    gpad::PanelPlan plan;
     // plant binding (gpad_setup_plant): affine state maps and dynamics, device copies
     int nx = 0, nu = 0;
     bool plant_ready = false, plant_dyn = false;
@@ -226,8 +227,7 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
     HIP_TRY(hipSetDevice(h->device));
     h->ready = false;
     h->flat = false;
-    h->phase_hint = 0;
-    h->phase_first = 0;
+    h->plan.nph = 0;
     h->dims = *d;
     if (h->dims.check_every <= 0) h->dims.check_every = 10;
     h->L = L;
@@ -306,8 +306,7 @@ int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* d, int n_u, const float*
     HIP_TRY(hipSetDevice(h->device));
     h->ready = false;
     h->flat = false;
-    h->phase_hint = 0;
-    h->phase_first = 0;
+    h->plan.nph = 0;
     h->dims = *d;
     if (h->dims.check_every <= 0) h->dims.check_every = 10;
     h->L = L;
@@ -406,9 +405,8 @@ static int collect_stats(gpad_handle_t h, gpad_stats_t* st) {
         }
     }
     if (h->last_phased && h->last_steps == 1) {
-        h->phase_hint = gpad::panel_phase_hint(h->h_counts.data(), batch, h->dims.n, h->dims.m, h->last_N,
-                                               h->dims.check_every, h->num_cus);
-        h->phase_first = gpad::panel_phase_first(h->h_counts.data(), batch, h->last_N, h->dims.check_every);
+        gpad::panel_plan(h->h_counts.data(), batch, h->dims.n, h->dims.m, h->last_N, h->dims.check_every,
+                         h->num_cus, &h->plan);
     }
     st->kernel = h->last_kernel;
     float ms = 0.0f;
@@ -422,6 +420,31 @@ int gpad_last_stats(gpad_handle_t h, gpad_stats_t* st) {
     if (h->last_batch <= 0) return fail(GPAD_ERR_NOT_SETUP, "gpad_last_stats: no run yet");
     HIP_TRY(hipSetDevice(h->device));
     return collect_stats(h, st);
+}
+
+int gpad_phase_plan(gpad_handle_t h, int* ends, int* fins, int cap, double* cost_us) {
+    if (!h) return fail(GPAD_ERR_INVALID, "gpad_phase_plan: null handle");
+    const int n = h->plan.nph;
+    for (int i = 0; i < n && i < cap; ++i) {
+        if (ends) ends[i] = h->plan.ends[i];
+        if (fins) fins[i] = h->plan.fins[i];
+    }
+    if (cost_us) *cost_us = h->plan.cost_us;
+    return n;
+}
+
+int gpad_plan_phases(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus,
+                     int* ends, int* fins, int cap, double* cost_us) {
+    if (!iters || batch <= 0 || n <= 0 || m <= 0 || N <= 0 || num_cus <= 0)
+        return fail(GPAD_ERR_INVALID, "gpad_plan_phases: bad argument");
+    gpad::PanelPlan p;
+    gpad::panel_plan(iters, batch, n, m, N, check_every, num_cus, &p);
+    for (int i = 0; i < p.nph && i < cap; ++i) {
+        if (ends) ends[i] = p.ends[i];
+        if (fins) fins[i] = p.fins[i];
+    }
+    if (cost_us) *cost_us = p.cost_us;
+    return p.nph;
 }
 
 }  // extern "C"
@@ -494,8 +517,7 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
                 int rc = h->pwork.ensure(gpad::panel_work_bytes(m, batch));
                 if (rc) return rc;
                 a.pwork = h->pwork.p;
-                a.phase_hint = h->phase_hint;
-                a.phase_first = h->phase_first;
+                a.plan = &h->plan;
             }
             e = gpad::launch_panel(a, h->stream, &ok);
             if (e != hipSuccess) return fail(GPAD_ERR_HIP, std::string("panel: ") + hipGetErrorString(e));

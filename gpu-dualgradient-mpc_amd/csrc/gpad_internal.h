@@ -48,8 +48,7 @@ struct SolveArgs {
     int fin_thresh;        // survivors <= this: the resident finisher takes them (0: none)
     int n_u;               // flat battery path: cells (n = n_u * horizon), see gpad_flat.hip
     int flat_staged;       // flat path: matrices staged in LDS (set by launch_flat)
-    int phase_hint;        // panel phases: close the schedule at this iteration (0: none)
-    int phase_first;       // panel phases: length of the first phase (0: the default)
+    const struct PanelPlan* plan;  // panel phases: host-side plan from the previous solve (or null)
 };
 
 // launchers (return hipError_t of the launch)
@@ -65,8 +64,16 @@ size_t panel_frag_bytes(int n, int m, int batch);
 size_t panel_work_bytes(int m, int batch);
 int panel_phase_len(int check_every);
 int panel_fin_thresh(int n, int m, int num_cus);
-int panel_phase_hint(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus);
-int panel_phase_first(const int* iters, int batch, int N, int check_every);
+// phase plan of a phased panel solve, from the previous solve's iteration counts (panel_plan)
+constexpr int kPanelMaxPhases = 48;
+struct PanelPlan {
+    int nph = 0;                  // phases planned (0: the default schedule)
+    int N = 0;                    // iteration limit the plan was made for
+    int ends[kPanelMaxPhases];    // phase ph covers [ends[ph-1], ends[ph]); the last ends at N
+    int fins[kPanelMaxPhases];    // finisher threshold at the start of phase ph (ph >= 1)
+    double cost_us = 0.0;         // modelled solve time
+};
+int panel_plan(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus, PanelPlan* out);
 int panel_tiles(int n, int m, int batch);
 hipError_t launch_pack_panel(const float* ML, const float* G, int n, int m, int batch, float mg_sign,
                              double g_scale, void* frag, hipStream_t s);

@@ -43,7 +43,6 @@ __device__ __forceinline__ int pi16(int rho) { return 4 * (rho & 3) + (rho >> 2)
 // packing
 // ---------------------------------------------------------------------------------------
 constexpr int kPanelMaxTiles = 16;  // n, m <= 256 (1024-thread workgroups)
-constexpr int kPanelMaxPhases = 48;
 
 static int panel_tiles_for(int n, int m) {
     const int t = ((n > m ? n : m) + 15) / 16;
@@ -824,41 +823,159 @@ int panel_fin_thresh(int n, int m, int num_cus) {
     return f;
 }
 
-// From a finished phased solve's per-instance iteration counts: the phase start at which the
-// finisher took over, plus one phase of margin (0: no takeover).  The next solve of the same
-// handle closes its schedule there (launch_panel_t, a.phase_hint).
-int panel_phase_first(const int* iters, int batch, int N, int check_every) {
-    // the earliest convergence of the previous solve, rounded down to whole phases: compacting
-    // before it re-packs panels that have no finished column (pure carry traffic)
-    const int len = panel_phase_len(check_every);
-    int mn = N;
-    for (int b = 0; b < batch; ++b) mn = iters[b] < mn ? iters[b] : mn;
-    const int first = (mn / len) * len;
-    return first > len ? first : 0;
-}
-
-int panel_phase_hint(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus) {
-    const int fin = panel_fin_thresh(n, m, num_cus);
-    if (!fin || batch <= 0) return 0;
-    const int len = panel_phase_len(check_every);
-    std::vector<int> hist(N + 2, 0);
-    for (int b = 0; b < batch; ++b) hist[iters[b] < 0 ? 0 : (iters[b] > N ? N : iters[b])]++;
-    // survivors at v = #(iters > v)
-    int above = batch - hist[0];
-    int v0 = 0, prev = 0;
-    const int first = panel_phase_first(iters, batch, N, check_every);
-    for (int ph = 0; v0 < N; ++ph) {
-        int plen = len;
-        if (ph >= 10) plen = len << (ph - 9 < 20 ? ph - 9 : 20);
-        if (ph == 0 && first > plen) plen = first;
-        const int v1 = (N - v0 <= plen) ? N : v0 + plen;
-        for (int v = prev + 1; v <= v1 && v <= N; ++v) above -= hist[v];
-        prev = v1;
-        // at the start of phase ph + 1 (v = v1) the survivors are `above`
-        if (v1 < N && above <= fin) return v1 + len;
-        v0 = v1;
+// ---------------------------------------------------------------------------------------------
+// Phase plan from the previous solve of the same handle.
+//
+// A phased solve's cost is set by where its phase boundaries fall against the survival curve
+// s(v) = #(instances still running past iteration v): a phase [v0, v1) costs (v1 - v0) panel
+// iterations whose time depends only on how many panels s(v0) fills (columns that converge
+// inside the phase idle until it ends), plus the launch, the carry traffic and the seed
+// product; handing the survivors to the resident finisher at v costs the longest remaining
+// solve at the latency kernel's iteration time, or the remaining instance-iterations at its
+// throughput, whichever is larger.  Given s(v) from the previous solve (receding-horizon and
+// scenario batches repeat it closely), a dynamic programme over the test-aligned boundaries
+// picks the cheapest schedule.  The plan only moves launch boundaries: every column runs the
+// same global iterations with the same tests whatever the schedule, so results are bit-identical
+// (tests/test_gpu_parity.py::test_panel_phase_plan_reuse_bitexact).
+//
+// Cost model (us; constants from profiles/r01_timeline.txt and profiles/r01_microbench.jsonl):
+//   panel iteration  = (busiest SIMD's MFMA chains) x t_chain,  t_chain = 0.055 (kb1 + kb2) + 0.2
+//                      single panels: ceil(T/4) chains, pairs: ceil(2T/4), T <= 8: co-resident
+//                      panels share the CU's four SIMDs
+//   phase overhead   = 2 launches (finisher + panel, 5 us each) + one seed iteration
+//                      + carried z, y, w, u (16 (n + m) bytes per survivor at 5 TB/s)
+//   finisher         = max(L t_lat, W 1.1 t_res / CUs) + 2 launches,  t_res = 0.0021 (n + m) + 0.38,
+//                      t_lat = 1.4 t_res (two workgroups per CU), L the longest remaining solve,
+//                      W the remaining instance-iterations.
+namespace {
+struct PlanModel {
+    int T, n, m, num_cus, grid;
+    double t_chain, t_res, t_launch = 5.0;
+    double iter_time(long long panels) const {
+        if (panels <= 0) return 0.0;
+        int chains;
+        if (T > 8) {
+            if (panels <= grid) {
+                chains = (T + 3) / 4;
+            } else {
+                const long long pairs = (panels + 1) / 2;
+                chains = (int)((pairs + grid - 1) / grid) * ((2 * T + 3) / 4);
+            }
+        } else {
+            const int per_cu_max = 32 / T;
+            const long long rounds = (panels + (long long)grid - 1) / grid;
+            const long long last = panels - (rounds - 1) * (long long)grid;
+            long long q = (last + num_cus - 1) / num_cus;
+            if (rounds > 1 || q > per_cu_max) q = per_cu_max;
+            chains = (int)(rounds - 1) * ((per_cu_max * T + 3) / 4) + (int)((q * T + 3) / 4);
+        }
+        return chains * t_chain;
     }
-    return 0;
+    double phase(int v0, int v1, long long s0) const {
+        const double it = iter_time((s0 + 15) / 16);
+        return 2 * t_launch + (v1 - v0 + 1) * it + (double)s0 * 16.0 * (n + m) / 5e6;
+    }
+    double finisher(int longest, long long work) const {
+        const double lat = longest * 1.4 * t_res;
+        const double thr = (double)work * 1.1 * t_res / num_cus;
+        return 2 * t_launch + (lat > thr ? lat : thr);
+    }
+};
+}  // namespace
+
+int panel_plan(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus, PanelPlan* out) {
+    out->nph = 0;
+    out->N = N;
+    const int T = panel_tiles_for(n, m);
+    if (!T || batch <= 0 || N <= 0 || std::getenv("GPAD_PANEL_NOPLAN")) return 0;
+    const int K = check_every > 0 ? check_every : 1;
+    int maxit = 0;
+    for (int b = 0; b < batch; ++b) maxit = iters[b] > maxit ? iters[b] : maxit;
+    if (maxit <= 0) return 0;
+    maxit = maxit < N ? maxit : N;
+    // boundaries: multiples of `step` (a multiple of the test period) up to the last iteration;
+    // coarse enough that the plan fits the phase-count slots with room for the run-out phases
+    const int slots = kPanelMaxPhases - 4;
+    int step = K;
+    while ((maxit + step - 1) / step > slots) step += K;
+    const int J = (maxit + step - 1) / step;  // boundary j is iteration j*step (J*step >= maxit)
+    std::vector<long long> surv(J + 1, 0), work(J + 1, 0);
+    std::vector<long long> hist(maxit + 2, 0);
+    for (int b = 0; b < batch; ++b) hist[iters[b] < 0 ? 0 : (iters[b] > maxit ? maxit : iters[b])]++;
+    // s(v) = #(iters > v), W(v) = sum_b max(0, iters_b - v)
+    std::vector<long long> s(maxit + 2, 0), W(maxit + 2, 0);
+    for (int v = maxit; v >= 0; --v) {
+        s[v] = s[v + 1] + hist[v + 1];
+        W[v] = W[v + 1] + s[v];
+    }
+    for (int j = 0; j <= J; ++j) {
+        const int v = j * step < maxit ? j * step : maxit;
+        surv[j] = s[v];
+        work[j] = W[v];
+    }
+    PlanModel md;
+    md.T = T;
+    md.n = n;
+    md.m = m;
+    md.num_cus = num_cus;
+    md.grid = T > 8 ? num_cus : num_cus * (32 / T);
+    md.t_chain = 0.055 * ((m + 15) / 16 + (n + 15) / 16) + 0.2;
+    md.t_res = 0.0021 * (n + m) + 0.38;
+    const bool fin_ok = resident_supported(n, m);
+    // best[j]: cheapest finish from boundary j (survivors surv[j] in panels); nxt[j] = next
+    // boundary (or -1: finisher takes over at j)
+    std::vector<double> best(J + 1, 0.0);
+    std::vector<int> nxt(J + 1, J);
+    for (int j = J - 1; j >= 0; --j) {
+        const int v = j * step;
+        double c = 1e300;
+        int arg = J;
+        if (surv[j] == 0) {
+            best[j] = 0.0;
+            nxt[j] = J;
+            continue;
+        }
+        if (fin_ok && j > 0) {
+            c = md.finisher(maxit - v, work[j]);
+            arg = -1;
+        }
+        for (int k = j + 1; k <= J; ++k) {
+            const int v1 = k * step < maxit ? k * step : maxit;
+            const double ck = md.phase(v, v1, surv[j]) + best[k];
+            if (ck < c) {
+                c = ck;
+                arg = k;
+            }
+        }
+        best[j] = c;
+        nxt[j] = arg;
+    }
+    // walk the plan: ends of the panel phases, then the takeover (finisher) or run-out phase
+    const int fin_default = panel_fin_thresh(n, m, num_cus);
+    int j = 0, ph = 0;
+    while (j < J && ph < slots) {
+        const int k = nxt[j];
+        if (k < 0) break;  // finisher at boundary j
+        out->fins[ph] = fin_default;
+        out->ends[ph++] = k * step;
+        j = k;
+        if (surv[j] == 0) break;
+    }
+    // the phase starting at the last boundary runs to N; the finisher takes it when the survivors
+    // fit its threshold, sized from the previous solve's survivors there (with margin)
+    long long sj = j < J ? surv[j] : 0;
+    long long thr = fin_default;
+    if (fin_ok && sj > 0 && 2 * sj + 64 > thr) thr = 2 * sj + 64;
+    if (thr > batch) thr = batch;
+    if (ph > 0 && out->ends[ph - 1] >= N) {
+        out->ends[ph - 1] = N;
+    } else {
+        out->fins[ph] = (int)thr;
+        out->ends[ph++] = N;
+    }
+    out->nph = ph;
+    out->cost_us = best[0];
+    return ph;
 }
 
 size_t panel_work_bytes(int m, int batch) {
@@ -907,16 +1024,19 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     // four tests, doubling after 10 phases so a long tail costs O(log N) launches (a phase with
     // no survivors left costs one empty launch, ~5 us)
     const int len = panel_phase_len(a.check_every);
+    const PanelPlan* plan = (a.plan && a.plan->nph > 0 && a.plan->N == a.N) ? a.plan : nullptr;
+    const int fin_default = a.fin_thresh;
     int v0 = 0;
     for (int ph = 0; v0 < a.N; ++ph) {
         int plen = len;
         if (ph >= 10) plen = len << (ph - 9 < 20 ? ph - 9 : 20);
+        a.fin_thresh = fin_default;
+        if (plan && ph < plan->nph) {  // the previous solve's plan (panel_plan)
+            plen = plan->ends[ph] - v0;
+            if (ph && fin_default) a.fin_thresh = plan->fins[ph];
+        }
+        if (plen < 1) plen = len;
         if (ph >= kPanelMaxPhases - 1) plen = a.N;  // last slot: run to N
-        // the previous solve's finisher took over before this point: close with one phase to N
-        // (its finisher or panel launch does all that is left; saves the empty launches after)
-        if (ph > 0 && a.phase_hint > 0 && v0 >= a.phase_hint) plen = a.N;
-        // ... and it had no convergence before phase_first: one long first phase up to there
-        if (ph == 0 && a.phase_first > plen) plen = a.phase_first;
         const int v1 = (a.N - v0 <= plen) ? a.N : v0 + plen;
         a.v_begin = v0;
         a.v_end = v1;

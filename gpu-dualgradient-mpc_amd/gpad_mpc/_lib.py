@@ -25,7 +25,8 @@ KERNEL_NAMES = {KERNEL_AUTO: "auto", KERNEL_STREAM: "stream", KERNEL_RESIDENT: "
 EXPORTS = [
     "gpad_version", "gpad_strerror", "gpad_last_error", "gpad_create", "gpad_destroy",
     "gpad_set_stream", "gpad_setup", "gpad_setup_scaled", "gpad_run", "gpad_run_scaled",
-    "gpad_last_stats", "gpad_solve", "gpad_step1_extrapolate", "gpad_step2_primal",
+    "gpad_last_stats", "gpad_phase_plan", "gpad_plan_phases", "gpad_solve", "gpad_step1_extrapolate",
+    "gpad_step2_primal",
     "gpad_step3_average", "gpad_step4_project", "gpad_schedule", "gpad_sync",
     "gpad_setup_plant", "gpad_run_state", "gpad_closed_loop",
     "gpad_datafile_read", "gpad_datafile_write", "gpad_datafile_free",
@@ -89,6 +90,8 @@ def load(path: str | None = None) -> C.CDLL:
     L.gpad_run.argtypes = [vp, vp, vp, cvp, cvp, i, d, C.POINTER(Stats)]
     L.gpad_run_scaled.argtypes = [vp, vp, vp, cvp, cvp, i, d, cvp, cvp, C.POINTER(Stats)]
     L.gpad_last_stats.argtypes = [vp, C.POINTER(Stats)]
+    L.gpad_phase_plan.argtypes = [vp, C.POINTER(i), C.POINTER(i), i, C.POINTER(d)]
+    L.gpad_plan_phases.argtypes = [vp, i, i, i, i, i, i, C.POINTER(i), C.POINTER(i), i, C.POINTER(d)]
     L.gpad_solve.argtypes = [vp, vp, cvp, cvp, cvp, cvp, i, d, d, C.POINTER(Dims), C.POINTER(Stats)]
     f = C.POINTER(C.c_float)
     L.gpad_step1_extrapolate.argtypes = [vp, vp, vp, vp, C.c_float, i]
@@ -109,7 +112,7 @@ def load(path: str | None = None) -> C.CDLL:
     L.gpad_step4_project_flat.argtypes = [vp, vp, vp, vp, vp, vp, i, i, i]
     for name in ["gpad_create", "gpad_destroy", "gpad_set_stream", "gpad_sync", "gpad_setup",
                  "gpad_setup_scaled", "gpad_run", "gpad_run_scaled", "gpad_last_stats",
-                 "gpad_solve", "gpad_step1_extrapolate", "gpad_step2_primal",
+                 "gpad_phase_plan", "gpad_plan_phases", "gpad_solve", "gpad_step1_extrapolate", "gpad_step2_primal",
                  "gpad_step3_average", "gpad_step4_project", "gpad_schedule", "gpad_setup_plant",
                  "gpad_run_state", "gpad_closed_loop", "gpad_datafile_read",
                  "gpad_datafile_write", "gpad_setup_flat", "gpad_step2_primal_flat",

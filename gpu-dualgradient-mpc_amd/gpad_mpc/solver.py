@@ -143,6 +143,32 @@ class GpadSolver:
         check(self.lib.gpad_last_stats(self.h, C.byref(st)), "gpad_last_stats")
         return self._stats_dict(st)
 
+    def phase_plan(self) -> dict:
+        """The phase plan the next phased panel solve follows (include/gpad.h gpad_phase_plan):
+        phase ends, finisher thresholds, modelled time; empty lists = the default schedule."""
+        cap = 64
+        ends = (C.c_int * cap)()
+        fins = (C.c_int * cap)()
+        cost = C.c_double(0.0)
+        n = self.lib.gpad_phase_plan(self.h, ends, fins, cap, C.byref(cost))
+        check(min(n, 0), "gpad_phase_plan")
+        return dict(ends=list(ends[:n]), fins=list(fins[:n]), cost_us=cost.value)
+
+    @staticmethod
+    def plan_phases(iters, n: int, m: int, N: int, check_every: int = 10, num_cus: int = 256) -> dict:
+        """gpad_plan_phases: the phase plan the panel solver would make from these per-instance
+        iteration counts (host-only; runs without a GPU)."""
+        L = _lib.load()
+        it = np.ascontiguousarray(iters, np.int32)
+        cap = 64
+        ends = (C.c_int * cap)()
+        fins = (C.c_int * cap)()
+        cost = C.c_double(0.0)
+        k = L.gpad_plan_phases(it.ctypes.data, it.size, n, m, N, check_every, num_cus, ends, fins, cap,
+                               C.byref(cost))
+        check(min(k, 0), "gpad_plan_phases")
+        return dict(ends=list(ends[:k]), fins=list(fins[:k]), cost_us=cost.value)
+
     @staticmethod
     def _stats_dict(st: Stats) -> dict:
         return dict(iterations=st.iterations, converged=st.converged,

@@ -187,6 +187,16 @@ void gpad_datafile_free(gpad_datafile_t* f);
 /* Per-instance iteration counts / convergence flags of the last run (device work finished). */
 int gpad_last_stats(gpad_handle_t h, gpad_stats_t* st);
 
+/* Diagnostics (no reference counterpart): the phase plan the next phased panel solve of this
+ * handle will follow, made from the previous solve's iteration counts by gpad_last_stats / a
+ * stats-collecting run.  Writes up to cap phase ends (iterations; the last is N) and finisher
+ * thresholds, and the modelled solve time in us; returns the number of phases (0: no plan,
+ * the default schedule applies). */
+int gpad_phase_plan(gpad_handle_t h, int* ends, int* fins, int cap, double* cost_us);
+/* The planner itself on given iteration counts (host only, no device work; for tests/tools). */
+int gpad_plan_phases(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus,
+                     int* ends, int* fins, int cap, double* cost_us);
+
 /* One-shot north-star surface: solve(z0, y0, ML, M, G, g, N, L, tol).  Equivalent to
  * create + setup + run + destroy (the handle is cached per thread and device). */
 int gpad_solve(void* z0, void* y0, const void* ML, const void* M, const void* G, const void* g,

@@ -95,3 +95,32 @@ def test_product_path_has_no_oracle_dependency():
         if f.endswith(".py"):
             src = open(os.path.join(PKG, "gpad_mpc", f)).read()
             assert "pyoracle" not in src and "liboracle" not in src, f
+
+
+def test_phase_planner_host_only():
+    """gpad_plan_phases (the panel solver's phase planner, csrc/gpad_panel.hip panel_plan) on
+    synthetic survival curves: ends strictly increasing and closing at N, takeover threshold
+    covering the previous solve's survivors, and the degenerate inputs."""
+    from gpad_mpc.solver import GpadSolver
+    rng = np.random.default_rng(0)
+    # a C4-like spread: convergence between 170 and 380 iterations
+    it = np.clip(rng.normal(265, 30, 8192), 170, 380).astype(np.int32)
+    p = GpadSolver.plan_phases(it, 200, 200, 5000)
+    e = p["ends"]
+    assert e and e[-1] == 5000 and all(a < b for a, b in zip(e, e[1:])), p
+    assert all(x % 10 == 0 for x in e[:-1])                       # phases end right after a test
+    assert e[0] <= int(it.min()) + 100                            # one long first phase, no earlier
+    v_take = e[-2] if len(e) > 1 else 0                           # the last phase starts here ...
+    assert p["fins"][-1] >= int((it > v_take).sum())              # ... and the finisher covers it
+    assert p["cost_us"] > 0
+    # nobody converges: one phase to N per plan slot at most, still closing at N
+    p2 = GpadSolver.plan_phases(np.full(1000, 300, np.int32), 200, 200, 300)
+    assert p2["ends"][-1] == 300 and len(p2["ends"]) <= 46
+    # everyone at iteration 10 (first test): plan is a single phase
+    p3 = GpadSolver.plan_phases(np.full(4096, 10, np.int32), 40, 180, 5000)
+    assert p3["ends"] == [5000] or p3["ends"][0] == 10
+    # shapes the panel kernels do not take: no plan
+    assert GpadSolver.plan_phases(it, 300, 300, 5000)["ends"] == []
+    from gpad_mpc import _lib
+    with pytest.raises(_lib.GpadError):
+        GpadSolver.plan_phases(it[:0], 200, 200, 5000)

@@ -203,9 +203,10 @@ def test_panel_phased_compaction_bitexact(gpu, oracle, monkeypatch, grid, phase,
 
 
 @pytest.mark.parametrize("fin", [None, 0])
-def test_panel_phase_hint_reuse_bitexact(gpu, oracle, monkeypatch, fin):
-    """A handle closes its phase schedule where the previous solve's finisher took over; a later
-    solve that needs more iterations must still be exact (the closing phase runs to N)."""
+def test_panel_phase_plan_reuse_bitexact(gpu, oracle, monkeypatch, fin):
+    """A handle plans its phases from the previous solve's iteration counts (csrc/gpad_panel.hip
+    panel_plan); a later solve that needs more (or fewer) iterations than the plan expects must
+    still be exact -- the plan moves launch boundaries and the finisher takeover only."""
     import gpad_mpc
     from gpad_mpc import problems
     if fin is not None:
@@ -224,8 +225,11 @@ def test_panel_phase_hint_reuse_bitexact(gpu, oracle, monkeypatch, fin):
             z = np.zeros((B, n), np.float32)
             y = np.zeros((B, m), np.float32)
             it = np.zeros(B, np.int32)
+            plan = s.phase_plan()
             st = s.run(z, y, M, g, 4000, tol, iters=it)
             assert st["kernel"] == "panel"
+            if scale != 1.0 or tol != 1e-3:  # planned from the previous solve
+                assert plan["ends"] and plan["ends"][-1] == 4000, plan
             for b in range(0, B, 7):
                 zo, yo, ito, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), ML, M[b], G, g[b], 4000, L, tol)
                 assert it[b] == ito, (scale, b)

@@ -1,0 +1,104 @@
+"""Per-launch timeline of one C4 solve (phase launches, finisher launches, gaps).
+
+  run   : python3 tools/timeline.py run [--reps R]     -- the bench's C4 shard, R solves
+  parse : python3 tools/timeline.py parse <rocprof dir> [--iters file.npy]
+
+On the GPU box:
+  rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tl -o run -- python3 tools/timeline.py run
+  python3 tools/timeline.py parse gpurun_out/tl
+prints, for the last solve, each launch's kernel, grid, duration and the idle gap before it,
+and (with the iteration counts the run step saves) the survivors each phase starts with.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+
+def run(args):
+    import torch
+
+    import bench
+    import gpad_mpc
+    dev = torch.device("cuda:0")
+    n, m, B = 200, 200, args.batch
+    ML, G, L, M, g = bench.make_shard(n, m, B, 0)
+    f32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)  # noqa: E731
+    dML, dG, dM, dg = f32(ML), f32(G), f32(M), f32(g)
+    z = torch.zeros(B, n, device=dev)
+    y = torch.zeros(B, m, device=dev)
+    s = gpad_mpc.GpadSolver(0)
+    s.setup(dML, dG, float(np.float32(L)), n=n, m=m, batch=B, shared=True, check_every=10)
+    it = np.zeros(B, np.int32)
+    for _ in range(args.reps):
+        z.zero_()
+        y.zero_()
+        s.run(z, y, dM, dg, 5000, 1e-4, stats=False)
+        st = s.last_stats(iters=it)
+    torch.cuda.synchronize()
+    np.save(args.out, it)
+    print(f"kernel {st['kernel']} kernel_ms {st['kernel_ms']:.4f} mean_iters {it.mean():.1f} "
+          f"min {it.min()} max {it.max()}")
+
+
+def parse(args):
+    files = glob.glob(os.path.join(args.dir, "**", "*kernel_trace.csv"), recursive=True)
+    if not files:
+        sys.exit(f"no kernel_trace.csv under {args.dir}")
+    rows = []
+    with open(files[0]) as f:
+        for r in csv.DictReader(f):
+            rows.append(r)
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    gpad = [r for r in rows if "gpad" in r["Kernel_Name"] and "pack" not in r["Kernel_Name"]]
+    # the last solve: launches after the last gap > 200 us
+    starts = [int(r["Start_Timestamp"]) for r in gpad]
+    ends = [int(r["End_Timestamp"]) for r in gpad]
+    cut = 0
+    for i in range(1, len(gpad)):
+        if starts[i] - ends[i - 1] > 200_000:
+            cut = i
+    last = gpad[cut:]
+    t0 = int(last[0]["Start_Timestamp"])
+    print(f"{'#':>3} {'kernel':<34} {'grid':>8} {'start_us':>9} {'dur_us':>9} {'gap_us':>7}")
+    prev = None
+    busy = 0
+    for i, r in enumerate(last):
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        gap = (s - prev) / 1e3 if prev is not None else 0.0
+        name = r["Kernel_Name"].split("(")[0][-34:]
+        grid = r.get("Grid_Size_X") or r.get("Grid_Size") or "?"
+        print(f"{i:>3} {name:<34} {grid:>8} {(s - t0) / 1e3:>9.1f} {(e - s) / 1e3:>9.1f} {gap:>7.1f}")
+        prev = e
+        busy += e - s
+    span = (ends[-1] - t0) / 1e3
+    print(f"solve span {span:.1f} us, busy {busy / 1e3:.1f} us, launches {len(last)}")
+    if args.iters and os.path.exists(args.iters):
+        it = np.load(args.iters)
+        for v in (0, 40, 80, 160, 170, 200, 240, 280, 320, 360, 380):
+            print(f"survivors past iteration {v:>4}: {(it > v).sum()}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    a = sub.add_parser("run")
+    a.add_argument("--reps", type=int, default=5)
+    a.add_argument("--batch", type=int, default=8192)
+    a.add_argument("--out", default="gpurun_out/tl_iters.npy")
+    b = sub.add_parser("parse")
+    b.add_argument("dir")
+    b.add_argument("--iters", default="gpurun_out/tl_iters.npy")
+    args = ap.parse_args()
+    run(args) if args.cmd == "run" else parse(args)
+
+
+if __name__ == "__main__":
+    main()
