@@ -46,6 +46,7 @@ struct SolveArgs {
     float* wc;             // carried w  [batch][m]
     float* uc;             // carried u = G_L z [batch][m]
     int fin_thresh;        // survivors <= this: the resident finisher takes them (0: none)
+    int* qctr;             // duo kernel: zeroed device counter of its work-list claims
     int n_u;               // flat battery path: cells (n = n_u * horizon), see gpad_flat.hip
     int flat_staged;       // flat path: matrices staged in LDS (set by launch_flat)
     const struct PanelPlan* plan;  // panel phases: host-side plan from the previous solve (or null)
@@ -58,6 +59,10 @@ hipError_t launch_resident(const SolveArgs<float>& a, hipStream_t s, bool* suppo
 // resident kernel over the survivors of a phased panel solve (idx_in/count_in, carried state,
 // iterations v_begin..N); a no-op unless *count_in <= a.fin_thresh.  grid >= fin_thresh.
 hipError_t launch_resident_finisher(const SolveArgs<float>& a, int grid, hipStream_t s);
+// two-instance ping-pong kernel over a work list (shared matrices; gpad_kernels.hip): the
+// list is idx_in/count_in (a no-op unless *count_in <= a.fin_thresh) or 0..batch-1; needs a
+// zeroed a.qctr.  Persistent grid of `grid` workgroups (one per CU).
+hipError_t launch_duo(const SolveArgs<float>& a, int grid, hipStream_t s);
 bool resident_supported(int n, int m);
 hipError_t launch_panel(const SolveArgs<float>& a, hipStream_t s, bool* supported);
 size_t panel_frag_bytes(int n, int m, int batch);

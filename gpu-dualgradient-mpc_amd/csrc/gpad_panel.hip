@@ -29,6 +29,7 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "gpad_internal.h"
@@ -979,8 +980,9 @@ int panel_plan(const int* iters, int batch, int n, int m, int N, int check_every
 }
 
 size_t panel_work_bytes(int m, int batch) {
-    // idx ping-pong [2][batch] | phase counts [kPanelMaxPhases] | carried w, u [batch][m] each
-    return sizeof(int) * (2 * (size_t)batch + kPanelMaxPhases) + 2 * sizeof(float) * (size_t)batch * m;
+    // idx ping-pong [2][batch] | phase counts [kPanelMaxPhases] | finisher queue counters
+    // [kPanelMaxPhases] | carried w, u [batch][m] each
+    return sizeof(int) * (2 * (size_t)batch + 2 * kPanelMaxPhases) + 2 * sizeof(float) * (size_t)batch * m;
 }
 
 template <int T>
@@ -1015,10 +1017,11 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     int* idx0 = reinterpret_cast<int*>(a.pwork);
     int* idx1 = idx0 + a.batch;
     int* counts = idx1 + a.batch;
-    float* wc = reinterpret_cast<float*>(counts + kPanelMaxPhases);
+    int* qctrs = counts + kPanelMaxPhases;
+    float* wc = reinterpret_cast<float*>(qctrs + kPanelMaxPhases);
     a.wc = wc;
     a.uc = wc + (size_t)a.batch * a.m;
-    hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * kPanelMaxPhases, s);
+    hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * 2 * kPanelMaxPhases, s);
     if (e != hipSuccess) return e;
     // phase length: a multiple of the test period (phases end right after a test); default
     // four tests, doubling after 10 phases so a long tail costs O(log N) launches (a phase with
@@ -1026,6 +1029,8 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     const int len = panel_phase_len(a.check_every);
     const PanelPlan* plan = (a.plan && a.plan->nph > 0 && a.plan->N == a.N) ? a.plan : nullptr;
     const int fin_default = a.fin_thresh;
+    const char* fk = std::getenv("GPAD_FINISHER");  // A/B knob: "resident" = one per workgroup
+    const bool duo = !(fk && std::string(fk) == "resident");
     int v0 = 0;
     for (int ph = 0; v0 < a.N; ++ph) {
         int plen = len;
@@ -1044,8 +1049,18 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
         a.count_in = ph ? counts + ph - 1 : nullptr;
         a.idx_out = (ph & 1) ? idx1 : idx0;
         a.count_out = counts + ph;
-        if (ph && a.fin_thresh) {  // few survivors left: one instance per workgroup, run to N
-            if ((e = launch_resident_finisher(a, a.fin_thresh, s)) != hipSuccess) return e;
+        if (ph && a.fin_thresh) {  // few survivors left: the latency kernels take them, run to N
+            if (duo) {  // two instances per CU in ping-pong, fed from the survivor list
+                a.qctr = qctrs + ph;
+                int g = a.fin_thresh < a.num_cus ? a.fin_thresh : a.num_cus;
+                if (const char* cap = std::getenv("GPAD_DUO_MAX_GRID")) {  // test knob: more claims
+                    const int q = std::atoi(cap);
+                    if (q > 0 && q < g) g = q;
+                }
+                if ((e = launch_duo(a, g, s)) != hipSuccess) return e;
+            } else if ((e = launch_resident_finisher(a, a.fin_thresh, s)) != hipSuccess) {
+                return e;  // one instance per workgroup
+            }
         }
         launch_panel_kernel<T>(a, grid, s);
         if ((e = hipGetLastError()) != hipSuccess) return e;

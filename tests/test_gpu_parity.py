@@ -202,6 +202,38 @@ def test_panel_phased_compaction_bitexact(gpu, oracle, monkeypatch, grid, phase,
         assert_bitexact(y[b], yo, f"instance {b} y")
 
 
+@pytest.mark.parametrize("finisher,grid", [("duo", 1), ("duo", 3), ("duo", 0), ("resident", 0)])
+@pytest.mark.parametrize("nm,B,z0s", [((200, 200), 120, 0.0), ((40, 180), 200, 0.1), ((131, 64), 97, 0.1)])
+def test_finisher_queue_bitexact(gpu, oracle, monkeypatch, finisher, grid, nm, B, z0s):
+    """The tail of a phased panel solve on the latency kernels: the duo kernel (two instances per
+    workgroup in ping-pong, slots refilled from the survivor list through a device counter;
+    grid capped to 1 or 3 workgroups to force many claims) or the one-per-workgroup resident
+    finisher.  The finisher takes over after the first 10-iteration phase, so nearly the whole
+    solve runs there; every instance must match its own oracle solve, iteration count included."""
+    from gpad_mpc import problems
+    monkeypatch.setenv("GPAD_FINISHER", finisher)
+    monkeypatch.setenv("GPAD_PANEL_PHASE", "10")
+    monkeypatch.setenv("GPAD_FINISH_THRESH", "100000")
+    if grid:
+        monkeypatch.setenv("GPAD_DUO_MAX_GRID", str(grid))
+    n, m = nm
+    qp = problems.synthetic_qp(n, m, batch=B, seed=12)
+    ML, G = qp.ML.astype(np.float32), qp.G.astype(np.float32)
+    M, g = qp.M.astype(np.float32), qp.g.astype(np.float32)
+    L = np.float32(qp.L)
+    rng = np.random.default_rng(2)
+    z0 = (z0s * rng.normal(size=(B, n))).astype(np.float32)
+    N = 1500
+    z, y, st, iters = run_gpu(ML, M, G, g, L, N, tol=1e-4, kernel="panel", z0=z0)
+    assert st["kernel"] == "panel"
+    assert iters.min() > 10  # the finisher ran every instance's tail
+    for b in range(B):
+        zo, yo, it, _ = oracle.solve_f32(z0[b], np.zeros(m), ML, M[b], G, g[b], N, L, 1e-4)
+        assert iters[b] == it, b
+        assert_bitexact(z[b], zo, f"instance {b} z")
+        assert_bitexact(y[b], yo, f"instance {b} y")
+
+
 @pytest.mark.parametrize("fin", [None, 0])
 def test_panel_phase_plan_reuse_bitexact(gpu, oracle, monkeypatch, fin):
     """A handle plans its phases from the previous solve's iteration counts (csrc/gpad_panel.hip
