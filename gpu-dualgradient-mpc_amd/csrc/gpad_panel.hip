@@ -536,6 +536,16 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
     const bool on1 = 16 * t < n, on2 = 16 * t < m;
 
     for (int it = blockIdx.x; it < items; it += gridDim.x) {
+        // columns still running, bit 16 pp + c for panel pp of this item: the same word in every
+        // wave (derived from uniform values and LDS), so the test needs no vote barrier
+        unsigned live = 0u;
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+            if (pp == 1 && !pair) break;
+            const int left = count - 16 * (pair ? 2 * it + pp : it);
+            const int cnt = left < 0 ? 0 : (left > 16 ? 16 : left);
+            live |= ((1u << cnt) - 1u) << (16 * pp);
+        }
         bool act[Q];
         int inst[Q];
         float z[Q][4], y[Q][4], u[Q][4];
@@ -670,21 +680,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                         if (act[q]) y[q][r] = yp;
                     }
                     if (act[q]) L.Wl[p0 + q][slot] = make_float4(wn[0], wn[1], wn[2], wn[3]);
-                }
-            }
-            th = th_next;
-            bn = bn_next;
-            __syncthreads();
-            if (!chk && v < a.v_end) continue;
-
-            // ---- Algorithm 1 test per column (tile partials through LDS) ----------------------
-            int code[Q];
-#pragma unroll
-            for (int q = 0; q < Q; ++q) code[q] = 0;
-            if (chk) {
-                if constexpr (NU > 0) {
-#pragma unroll
-                    for (int q = 0; q < Q; ++q) {
+                    if (chk) {  // this tile's per-column partials of the test -> LDS
 #pragma unroll
                         for (int o = 16; o < 64; o <<= 1) {
                             violz[q] = fmaxf(violz[q], __shfl_xor(violz[q], o, 64));
@@ -701,30 +697,43 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                         }
                     }
                 }
-                __syncthreads();
-                if constexpr (NU > 0) {
+            }
+            th = th_next;
+            bn = bn_next;
+            __syncthreads();
+            if (!chk && v < a.v_end) continue;
+
+            // ---- Algorithm 1 test per column: every wave reduces the tile partials of all the
+            // item's columns (lane 16 pp + cc <-> panel pp, column cc) and votes by ballot, so the
+            // outcome is uniform across the workgroup without a second barrier ---------------------
+            unsigned m1 = 0u, m2 = 0u;
+            if (chk) {
+                int cd = 0;
+                const int pp = (lane >> 4) & 1, cc = lane & 15;
+                if (lane < 32 && ((live >> lane) & 1u)) {
+                    double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gq = 0.0;
 #pragma unroll
-                    for (int q = 0; q < Q; ++q) {
-                        if (!act[q]) continue;
-                        double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gq = 0.0;
-#pragma unroll 1
-                        for (int s2 = 0; s2 < T; ++s2) {  // not unrolled: keeps the test's
-                            const PanelSlot& S = L.slots[p0 + q][s2];  // registers off the loop
-                            vz = fmax(vz, (double)S.violz[c]);
-                            vh = fmax(vh, (double)S.violh[c]);
-                            wm = fmin(wm, (double)S.wmin[c]);
-                            gq += S.gap[c];
-                        }
-                        if (vz * a.L <= a.tol) code[q] = 1;
-                        else if ((vh * a.L <= a.tol) && (wm >= 0.0) && (gq * a.L <= a.tol)) code[q] = 2;
+                    for (int s2 = 0; s2 < T; ++s2) {
+                        const PanelSlot& S = L.slots[pp][s2];
+                        vz = fmax(vz, (double)S.violz[cc]);
+                        vh = fmax(vh, (double)S.violh[cc]);
+                        wm = fmin(wm, (double)S.wmin[cc]);
+                        gq += S.gap[cc];
                     }
+                    if (vz * a.L <= a.tol) cd = 1;
+                    else if ((vh * a.L <= a.tol) && (wm >= 0.0) && (gq * a.L <= a.tol)) cd = 2;
                 }
+                m1 = (unsigned)__ballot(cd == 1);
+                m2 = (unsigned)__ballot(cd == 2);
             }
             // ---- finished columns: results out ---------------------------------------------
-            bool any = false;
             if constexpr (NU > 0) {
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
+                    const int bit = 16 * (p0 + q) + c;
+                    const int cdq = ((m1 >> bit) & 1u) ? 1 : (((m2 >> bit) & 1u) ? 2 : 0);
+                    int code[Q];
+                    code[q] = cdq;
                     if (act[q] && (code[q] != 0 || v >= N)) {
                         const float4 h4 = L.Zh[p0 + q][slot];
                         const float zh[4] = {h4.x, h4.y, h4.z, h4.w};
@@ -741,10 +750,11 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                         }
                         act[q] = false;
                     }
-                    any = any || act[q];
                 }
             }
-            if (v >= a.v_end || !__syncthreads_or(any ? 1 : 0)) break;
+            live &= ~(m1 | m2);
+            if (v >= N) live = 0u;
+            if (v >= a.v_end || live == 0u) break;
         }
         // ---- phase end: park the survivors -----------------------------------------------
         if constexpr (NU > 0) {
