@@ -518,6 +518,9 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
                 if (rc) return rc;
                 a.pwork = h->pwork.p;
                 a.plan = &h->plan;
+                // the previous phased solve's counts are still in `iters` for every instance this
+                // solve has not finished yet: the finisher orders its queue by them
+                if (h->last_phased && h->last_batch == batch && h->last_steps == 1) a.pred = iters;
             }
             e = gpad::launch_panel(a, h->stream, &ok);
             if (e != hipSuccess) return fail(GPAD_ERR_HIP, std::string("panel: ") + hipGetErrorString(e));

@@ -47,6 +47,8 @@ struct SolveArgs {
     float* uc;             // carried u = G_L z [batch][m]
     int fin_thresh;        // survivors <= this: the resident finisher takes them (0: none)
     int* qctr;             // duo kernel: zeroed device counter of its work-list claims
+    const int* pred;       // phased solves: per-instance iteration counts predicted from the
+                           // previous solve (or null); orders the finisher's queue longest first
     int n_u;               // flat battery path: cells (n = n_u * horizon), see gpad_flat.hip
     int flat_staged;       // flat path: matrices staged in LDS (set by launch_flat)
     const struct PanelPlan* plan;  // panel phases: host-side plan from the previous solve (or null)

@@ -548,6 +548,7 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
 struct DuoSlot {  // one instance slot; bookkeeping is uniform, the floats are this lane's rows
     int pos, vs, nextp;  // list position (>= count: empty), iterations done, pre-claimed next
     bool need8d;         // 8b done, 8d pending
+    float th, bn;        // theta_vs, beta_{vs+1}: loaded one step before their use
     float x0, x1, x2;    // -ML lanes: z, zhat, -;  G/L lanes: y, w, u = G_L z (g_P, p_D in LDS)
 };
 struct DuoCtx {
@@ -564,6 +565,8 @@ __device__ __forceinline__ void duo_refill(const SolveArgs<float>& a, const DuoC
     s.pos = p;
     s.vs = c.v0;
     s.need8d = false;
+    s.th = a.theta[c.v0];
+    s.bn = a.beta[c.v0 + 1];
     s.x0 = s.x1 = s.x2 = 0.0f;
     const bool has = p < c.count;
     if (has) {
@@ -615,7 +618,7 @@ __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx
     const bool chk = runB && c.use_tol && ((sb.vs + 1) % c.Kc) == 0;
     if (c.isA) {
         if (runA) {
-            const float th = a.theta[sa.vs];
+            const float th = sa.th;
             const float acc = chain_regs<KA, K>(r, wa_l);
             if (c.live) {
                 const float zhv = acc - gpa_l[c.row];
@@ -628,7 +631,7 @@ __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx
         float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY;
         double gap = 0.0;
         if (runB) {
-            const float th = a.theta[sb.vs], bn = a.beta[sb.vs + 1];
+            const float th = sb.th, bn = sb.bn;
             const float cv = chain_regs<KB, K>(r, zhb_l);
             if (c.live) {
                 const float pdi = pdb_l[c.row], wi = sb.x1;
@@ -654,6 +657,8 @@ __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx
     if (runB) {
         sb.need8d = false;
         const int v = ++sb.vs;
+        sb.th = a.theta[v];  // next iteration's schedule (tables hold N + 2 entries)
+        sb.bn = a.beta[v + 1];
         const int done = chk ? check_decide(slots_b + c.nA, c.nwaves - c.nA, a.L, a.tol) : 0;
         if (done || v >= c.N) {
             const size_t b = (size_t)(a.idx_in ? a.idx_in[sb.pos] : sb.pos);

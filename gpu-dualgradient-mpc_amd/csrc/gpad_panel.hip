@@ -995,6 +995,46 @@ size_t panel_work_bytes(int m, int batch) {
     return sizeof(int) * (2 * (size_t)batch + 2 * kPanelMaxPhases) + 2 * sizeof(float) * (size_t)batch * m;
 }
 
+// Longest-first order for the finisher's work list: the survivors idx[0..count) sorted by the
+// iteration count the previous solve needed (descending; ties by instance id), so the duo kernel's
+// queue starts the longest remaining solves first (list scheduling, LPT).  One workgroup, bitonic
+// sort in LDS; a no-op when the list is not the finisher's (count > thresh) or too long.
+constexpr int kSortMax = 8192;
+__global__ __launch_bounds__(1024) void survivor_sort_kernel(int* idx, const int* count_p, const int* pred,
+                                                             int thresh) {
+    __shared__ unsigned long long key[kSortMax];
+    const int count = *count_p;
+    if (count <= 1 || count > thresh || count > kSortMax) return;
+    int P = 1;
+    while (P < count) P <<= 1;
+    for (int i = threadIdx.x; i < P; i += blockDim.x) {
+        if (i < count) {
+            const unsigned id = (unsigned)idx[i];
+            key[i] = ((unsigned long long)(unsigned)pred[id] << 32) | (0xFFFFFFFFu - id);
+        } else {
+            key[i] = 0ull;  // padding sorts last
+        }
+    }
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < P; i += blockDim.x) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const unsigned long long x = key[i], y = key[l];
+                    if (((i & k) == 0) ? (x < y) : (x > y)) {
+                        key[i] = y;
+                        key[l] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = threadIdx.x; i < count; i += blockDim.x)
+        idx[i] = (int)(0xFFFFFFFFu - (unsigned)(key[i] & 0xFFFFFFFFull));
+}
+
 template <int T>
 static void launch_panel_kernel(const SolveArgs<float>& a, int grid, hipStream_t s) {
     if constexpr (T > 8)
@@ -1062,6 +1102,9 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
         if (ph && a.fin_thresh) {  // few survivors left: the latency kernels take them, run to N
             if (duo) {  // two instances per CU in ping-pong, fed from the survivor list
                 a.qctr = qctrs + ph;
+                if (a.pred && !std::getenv("GPAD_NO_LPT"))  // longest predicted solves first
+                    hipLaunchKernelGGL(survivor_sort_kernel, dim3(1), dim3(1024), 0, s, const_cast<int*>(a.idx_in),
+                                       a.count_in, a.pred, a.fin_thresh);
                 int g = a.fin_thresh < a.num_cus ? a.fin_thresh : a.num_cus;
                 if (const char* cap = std::getenv("GPAD_DUO_MAX_GRID")) {  // test knob: more claims
                     const int q = std::atoi(cap);
