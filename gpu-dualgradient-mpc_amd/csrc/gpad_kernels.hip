@@ -301,16 +301,33 @@ template hipError_t launch_stream<double>(const SolveArgs<double>&, hipStream_t)
 // 16J..16J+15 of the current 64-element group: lanes 4J..4J+3 of each row, components x..w.
 #define GPAD_FMAC(SRC, R, LANE) \
     "v_fmac_f32_dpp %0, %" #SRC ", %" #R " row_newbcast:%" #LANE " row_mask:0xf bank_mask:0xf\n\t"
-#define GPAD_FMAC16                                                                            \
+#define GPAD_FMAC8                                                                             \
     GPAD_FMAC(1, 5, 21) GPAD_FMAC(2, 6, 21) GPAD_FMAC(3, 7, 21) GPAD_FMAC(4, 8, 21)             \
-    GPAD_FMAC(1, 9, 22) GPAD_FMAC(2, 10, 22) GPAD_FMAC(3, 11, 22) GPAD_FMAC(4, 12, 22)          \
+    GPAD_FMAC(1, 9, 22) GPAD_FMAC(2, 10, 22) GPAD_FMAC(3, 11, 22) GPAD_FMAC(4, 12, 22)
+#define GPAD_FMAC16                                                                            \
+    GPAD_FMAC8                                                                                 \
     GPAD_FMAC(1, 13, 23) GPAD_FMAC(2, 14, 23) GPAD_FMAC(3, 15, 23) GPAD_FMAC(4, 16, 23)         \
     GPAD_FMAC(1, 17, 24) GPAD_FMAC(2, 18, 24) GPAD_FMAC(3, 19, 24) GPAD_FMAC(4, 20, 24)
 
+// a chain length that is 8 mod 16 (the 200 bucket) ends with an 8-step statement
+#define GPAD_FMAC8T                                                                            \
+    GPAD_FMAC(1, 5, 13) GPAD_FMAC(2, 6, 13) GPAD_FMAC(3, 7, 13) GPAD_FMAC(4, 8, 13)             \
+    GPAD_FMAC(1, 9, 14) GPAD_FMAC(2, 10, 14) GPAD_FMAC(3, 11, 14) GPAD_FMAC(4, 12, 14)
 template <int KLEN, int K, int KI, int J>
 __device__ __forceinline__ void chain_step16(float& acc, const float4& c, const float (&r)[K]) {
-    static_assert(KLEN % 16 == 0, "chain lengths are multiples of 16");
-    if constexpr (KI < KLEN) {
+    static_assert(KLEN % 8 == 0, "chain lengths are multiples of 8");
+    if constexpr (KI + 8 == KLEN) {
+#define GPAD_OPS8                                                                                 \
+    : "+v"(acc)                                                                                   \
+    : "v"(c.x), "v"(c.y), "v"(c.z), "v"(c.w), "v"(r[KI + 0]), "v"(r[KI + 1]), "v"(r[KI + 2]),     \
+      "v"(r[KI + 3]), "v"(r[KI + 4]), "v"(r[KI + 5]), "v"(r[KI + 6]), "v"(r[KI + 7]), "i"(4 * J),  \
+      "i"(4 * J + 1)
+        if constexpr (J == 0)
+            asm("s_nop 1\n\t" GPAD_FMAC8T GPAD_OPS8);
+        else
+            asm(GPAD_FMAC8T GPAD_OPS8);
+#undef GPAD_OPS8
+    } else if constexpr (KI < KLEN) {
 #define GPAD_OPS                                                                                  \
     : "+v"(acc)                                                                                   \
     : "v"(c.x), "v"(c.y), "v"(c.z), "v"(c.w), "v"(r[KI + 0]), "v"(r[KI + 1]), "v"(r[KI + 2]),     \
@@ -326,6 +343,8 @@ __device__ __forceinline__ void chain_step16(float& acc, const float4& c, const 
     }
 }
 #undef GPAD_FMAC16
+#undef GPAD_FMAC8
+#undef GPAD_FMAC8T
 #undef GPAD_FMAC
 
 template <int KLEN, int K, int BASE, int... J>
@@ -735,9 +754,10 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs
     }
 }
 
-// chain-length buckets (multiples of 32 up to 192, then the 208 cap)
+// chain-length buckets (multiples of 32 up to 192, then 200 and the 208 cap)
 static int res_bucket(int len) {
-    if (len > 192) return 208;
+    if (len > 200) return 208;
+    if (len > 192) return 200;
     return (len + 31) / 32 * 32;
 }
 
@@ -750,6 +770,7 @@ static void launch_res_b(int kb, dim3 g, dim3 bl, hipStream_t st, const SolveArg
         case 128: hipLaunchKernelGGL((gpad_resident_kernel<KA, 128, FLAT>), g, bl, 0, st, a); break;
         case 160: hipLaunchKernelGGL((gpad_resident_kernel<KA, 160, FLAT>), g, bl, 0, st, a); break;
         case 192: hipLaunchKernelGGL((gpad_resident_kernel<KA, 192, FLAT>), g, bl, 0, st, a); break;
+        case 200: hipLaunchKernelGGL((gpad_resident_kernel<KA, 200, FLAT>), g, bl, 0, st, a); break;
         default: hipLaunchKernelGGL((gpad_resident_kernel<KA, 208, FLAT>), g, bl, 0, st, a); break;
     }
 }
@@ -771,6 +792,7 @@ static hipError_t launch_resident_grid(const SolveArgs<float>& a, int nblocks, h
         case 128: launch_res_b<128>(kb, grid, block, st, a); break;
         case 160: launch_res_b<160>(kb, grid, block, st, a); break;
         case 192: launch_res_b<192>(kb, grid, block, st, a); break;
+        case 200: launch_res_b<200>(kb, grid, block, st, a); break;
         default: launch_res_b<208>(kb, grid, block, st, a); break;
     }
     return hipGetLastError();
@@ -798,6 +820,7 @@ static void launch_duo_b(int kb, dim3 g, dim3 bl, hipStream_t st, const SolveArg
         case 128: hipLaunchKernelGGL((gpad_duo_kernel<KA, 128>), g, bl, 0, st, a); break;
         case 160: hipLaunchKernelGGL((gpad_duo_kernel<KA, 160>), g, bl, 0, st, a); break;
         case 192: hipLaunchKernelGGL((gpad_duo_kernel<KA, 192>), g, bl, 0, st, a); break;
+        case 200: hipLaunchKernelGGL((gpad_duo_kernel<KA, 200>), g, bl, 0, st, a); break;
         default: hipLaunchKernelGGL((gpad_duo_kernel<KA, 208>), g, bl, 0, st, a); break;
     }
 }
@@ -815,6 +838,7 @@ hipError_t launch_duo(const SolveArgs<float>& a, int grid, hipStream_t st) {
         case 128: launch_duo_b<128>(kb, g, bl, st, a); break;
         case 160: launch_duo_b<160>(kb, g, bl, st, a); break;
         case 192: launch_duo_b<192>(kb, g, bl, st, a); break;
+        case 200: launch_duo_b<200>(kb, g, bl, st, a); break;
         default: launch_duo_b<208>(kb, g, bl, st, a); break;
     }
     return hipGetLastError();
@@ -847,6 +871,7 @@ hipError_t launch_flat_resident(const SolveArgs<float>& a, hipStream_t st) {
         case 128: launch_res_b<128, true>(kb, grid, block, st, b); break;
         case 160: launch_res_b<160, true>(kb, grid, block, st, b); break;
         case 192: launch_res_b<192, true>(kb, grid, block, st, b); break;
+        case 200: launch_res_b<200, true>(kb, grid, block, st, b); break;
         default: launch_res_b<208, true>(kb, grid, block, st, b); break;
     }
     return hipGetLastError();
