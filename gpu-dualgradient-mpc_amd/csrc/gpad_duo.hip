@@ -1,0 +1,256 @@
+// gpad_duo.hip -- the two-instance ping-pong latency kernel (shared matrices), separate from
+// gpad_kernels.hip so the two sets of template instantiations compile in parallel.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <utility>
+
+#include "gpad_chain.h"
+#include "gpad_internal.h"
+
+namespace gpad {
+
+// =========================================================================================
+// gpad_duo_kernel: shared matrices, TWO instances per workgroup in ping-pong, fed by a queue.
+// =========================================================================================
+// The resident kernel keeps one instance per CU, and its two half-iterations alternate: while
+// the -ML waves run the 8b chains the G/L waves wait at the barrier and vice versa, so each
+// SIMD issues one dependent fma chain at a time (~1/3 of its VALU issue rate).  With shared
+// matrices the same register-resident rows can serve two instances X, Y at once, one half-
+// iteration apart: in step s the -ML waves run 8b of slot s&1 while the G/L waves run 8d of the
+// other slot, so the A and B wave of every SIMD both issue (two independent chains interleave
+// on the SIMD).  Two instance-iterations per two steps instead of one, at the same per-step
+// latency.  Each slot is refilled from a work list (idx_in / count_in: the survivors of a
+// phased panel solve, or 0..batch-1) as its instance finishes: the first two instances of
+// workgroup g are list positions g and g + G, later ones are claimed from a device counter
+// (`qctr`, +2G) one refill ahead, so the matrix rows are loaded once per CU, not per instance.
+//
+// Slot bookkeeping (pos, vs, need8d) is computed identically by every wave from uniform values
+// and LDS words, so the control flow around the DPP chains and barriers stays uniform.  Per
+// instance the arithmetic is exactly the resident kernel's (same chains, same epilogues, same
+// test with the same wave reductions), hence bit-identical results and iteration counts.
+struct DuoSlot {  // one instance slot; bookkeeping is uniform, the floats are this lane's rows
+    int pos, vs, nextp;  // list position (>= count: empty), iterations done, pre-claimed next
+    bool need8d;         // 8b done, 8d pending
+    float th, bn;        // theta_vs, beta_{vs+1}: loaded one step before their use
+    float x0, x1, x2;    // -ML lanes: z, zhat, -;  G/L lanes: y, w, u = G_L z (g_P, p_D in LDS)
+};
+struct DuoCtx {
+    int tid, count, G, v0, n, m, N, Kc, nA, nwaves, row;
+    bool fresh, use_tol, isA, live;
+};
+
+// slot s takes list position p (empty if p >= count); uniform, contains barriers
+// gp_l / pd_l: this slot's per-row constants (g_P of the -ML rows, p_D of the G/L rows)
+template <int KB, int K>
+__device__ __forceinline__ void duo_refill(const SolveArgs<float>& a, const DuoCtx& c, DuoSlot& s, int p,
+                                           float* w_l, float* gp_l, float* pd_l, float* z_l,
+                                           const float (&r)[K]) {
+    s.pos = p;
+    s.vs = c.v0;
+    s.need8d = false;
+    s.th = a.theta[c.v0];
+    s.bn = a.beta[c.v0 + 1];
+    s.x0 = s.x1 = s.x2 = 0.0f;
+    const bool has = p < c.count;
+    if (has) {
+        const size_t b = (size_t)(a.idx_in ? a.idx_in[p] : p);
+        if (c.isA) {
+            if (c.live) {
+                s.x0 = a.z[b * c.n + c.row];
+                gp_l[c.row] = a.gP[b * a.ld_gP + c.row];
+                if (c.fresh && c.use_tol) z_l[c.row] = s.x0;
+            }
+        } else if (c.live) {
+            const float yv = a.y[b * c.m + c.row];
+            s.x0 = yv;
+            pd_l[c.row] = (float)(a.gscale * (double)a.g[b * a.ld_g + c.row]);
+            s.x1 = c.fresh ? __builtin_fmaf(a.beta[0], yv - yv, yv) : a.wc[b * c.m + c.row];
+            if (c.use_tol && !c.fresh) s.x2 = a.uc[b * c.m + c.row];
+            w_l[c.row] = s.x1;
+        }
+    }
+    __syncthreads();
+    if (has && c.fresh && c.use_tol) {  // u = G_L z_{-1}, then the 8c recursion
+        if (!c.isA) {
+            const float us = chain_regs<KB, K>(r, z_l);
+            s.x2 = c.live ? us : 0.0f;
+        }
+        __syncthreads();  // z_l free again
+    }
+}
+
+// consume the pre-claimed position of slot s, claim its next one (claim_l: this slot's cell)
+template <int KB, int K>
+__device__ __forceinline__ void duo_claim(const SolveArgs<float>& a, const DuoCtx& c, DuoSlot& s, int* claim_l,
+                                          float* w_l, float* gp_l, float* pd_l, float* z_l,
+                                          const float (&r)[K]) {
+    const int p = s.nextp;
+    if (c.tid == 0 && p < c.count) *claim_l = 2 * c.G + atomicAdd(a.qctr, 1);
+    duo_refill<KB, K>(a, c, s, p, w_l, gp_l, pd_l, z_l, r);  // (its barrier publishes *claim_l)
+    s.nextp = p < c.count ? *claim_l : c.count;
+}
+
+// one step: -ML waves run 8b+8c of slot sa, G/L waves 8d+8a (+ test) of slot sb
+template <int KA, int KB, int K>
+__device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx& c, DuoSlot& sa, DuoSlot& sb,
+                                         float* wa_l, float* zha_l, const float* gpa_l, float* wb_l,
+                                         const float* zhb_l, float* gpb_l, float* pdb_l, CheckSlot* slots_b,
+                                         int* claim_b, float* z_l, const float (&r)[K]) {
+    const bool runA = sa.pos < c.count && !sa.need8d;
+    const bool runB = sb.need8d;
+    const bool chk = runB && c.use_tol && ((sb.vs + 1) % c.Kc) == 0;
+    if (c.isA) {
+        if (runA) {
+            const float th = sa.th;
+            const float acc = chain_regs<KA, K>(r, wa_l);
+            if (c.live) {
+                const float zhv = acc - gpa_l[c.row];
+                sa.x0 = __builtin_fmaf(1.0f - th, sa.x0, th * zhv);
+                zha_l[c.row] = zhv;
+                sa.x1 = zhv;
+            }
+        }
+    } else {
+        float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY;
+        double gap = 0.0;
+        if (runB) {
+            const float th = sb.th, bn = sb.bn;
+            const float cv = chain_regs<KB, K>(r, zhb_l);
+            if (c.live) {
+                const float pdi = pdb_l[c.row], wi = sb.x1;
+                const float sv = (wi + pdi) + cv;                     // seq_functions.cpp:84
+                const float yp = (__builtin_fabsf(sv) + sv) * 0.5f;   // seq_functions.cpp:85
+                if (c.use_tol) sb.x2 = __builtin_fmaf(1.0f - th, sb.x2, th * cv);
+                if (chk) {
+                    const float t = cv + pdi;
+                    violh = t;
+                    wmin = wi;
+                    gap = -((double)wi * (double)t);
+                    violz = sb.x2 + pdi;
+                }
+                sb.x1 = __builtin_fmaf(bn, yp - sb.x0, yp);
+                sb.x0 = yp;
+                wb_l[c.row] = sb.x1;
+            }
+        }
+        if (chk) check_publish<float>(slots_b, violz, violh, wmin, gap);
+    }
+    __syncthreads();
+    if (runA) sa.need8d = true;
+    if (runB) {
+        sb.need8d = false;
+        const int v = ++sb.vs;
+        sb.th = a.theta[v];  // next iteration's schedule (tables hold N + 2 entries)
+        sb.bn = a.beta[v + 1];
+        const int done = chk ? check_decide(slots_b + c.nA, c.nwaves - c.nA, a.L, a.tol) : 0;
+        if (done || v >= c.N) {
+            const size_t b = (size_t)(a.idx_in ? a.idx_in[sb.pos] : sb.pos);
+            if (c.live) {
+                if (c.isA) a.z[b * c.n + c.row] = done == 2 ? sb.x1 : sb.x0;  // (B) certifies zhat
+                else a.y[b * c.m + c.row] = sb.x0;
+            }
+            if (c.tid == 0) {
+                a.iters[b] = v;
+                a.conv[b] = done;
+            }
+            duo_claim<KB, K>(a, c, sb, claim_b, wb_l, gpb_l, pdb_l, z_l, r);
+        }
+    }
+}
+
+template <int KA, int KB>
+__global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs<float> a) {
+    constexpr int K = KA > KB ? KA : KB;
+    constexpr int PA = (KA + 63) / 64 * 64, PB = (KB + 63) / 64 * 64;
+    __shared__ __attribute__((aligned(16))) float w_l[2][PA];   // w per slot (broadcast to -ML rows)
+    __shared__ __attribute__((aligned(16))) float zh_l[2][PB];  // zhat per slot (to G/L rows)
+    __shared__ __attribute__((aligned(16))) float z_l[PB];      // z_{-1} of a fresh instance (u seed)
+    __shared__ float gp_l[2][PB];                               // per slot: g_P of the -ML rows
+    __shared__ float pd_l[2][PA];                               //           p_D of the G/L rows
+    __shared__ CheckSlot slots[2][kResidentMaxThreads / 64];
+    __shared__ int claim_l[2];
+
+    DuoCtx c;
+    c.tid = threadIdx.x;
+    c.count = a.count_in ? __builtin_amdgcn_readfirstlane(*a.count_in) : a.batch;
+    if (a.count_in && c.count > a.fin_thresh) return;  // the panel phase has them
+    c.G = gridDim.x;
+    if ((int)blockIdx.x >= c.count) return;
+    c.v0 = a.v_begin;
+    c.fresh = c.v0 == 0;
+    c.use_tol = a.tol > 0.0;
+    c.n = a.n;
+    c.m = a.m;
+    c.N = a.N;
+    c.Kc = a.check_every;
+    c.nA = (c.n + 63) >> 6;
+    c.nwaves = blockDim.x >> 6;
+    c.isA = (c.tid >> 6) < c.nA;
+    c.row = c.isA ? c.tid : c.tid - 64 * c.nA;
+    c.live = c.isA ? c.row < c.n : c.row < c.m;
+
+    float r[K];
+    {
+        const int len = c.isA ? c.m : c.n;
+        const float* __restrict__ Mt = c.isA ? a.MGt : a.GLt;
+        const int ld = c.isA ? a.ldn : a.ldm;
+#pragma unroll
+        for (int k = 0; k < K; ++k) r[k] = (c.live && k < len) ? Mt[(size_t)k * ld + c.row] : 0.0f;
+    }
+    for (int i = c.tid; i < 2 * PA; i += blockDim.x) (&w_l[0][0])[i] = 0.0f;
+    for (int i = c.tid; i < 2 * PB; i += blockDim.x) (&zh_l[0][0])[i] = 0.0f;
+    for (int i = c.tid; i < PB; i += blockDim.x) z_l[i] = 0.0f;
+    if (c.tid == 0) {  // first claims of the queue (positions 2G, 2G+1, ...)
+        claim_l[0] = 2 * c.G + atomicAdd(a.qctr, 1);
+        claim_l[1] = 2 * c.G + atomicAdd(a.qctr, 1);
+    }
+    __syncthreads();
+    DuoSlot s0, s1;
+    s0.nextp = claim_l[0];
+    s1.nextp = claim_l[1];
+    duo_refill<KB, K>(a, c, s0, blockIdx.x, w_l[0], gp_l[0], pd_l[0], z_l, r);
+    duo_refill<KB, K>(a, c, s1, blockIdx.x + c.G, w_l[1], gp_l[1], pd_l[1], z_l, r);
+    while (s0.pos < c.count || s1.pos < c.count) {
+        duo_step<KA, KB, K>(a, c, s0, s1, w_l[0], zh_l[0], gp_l[0], w_l[1], zh_l[1], gp_l[1], pd_l[1], slots[1],
+                            &claim_l[1], z_l, r);
+        duo_step<KA, KB, K>(a, c, s1, s0, w_l[1], zh_l[1], gp_l[1], w_l[0], zh_l[0], gp_l[0], pd_l[0], slots[0],
+                            &claim_l[0], z_l, r);
+    }
+}
+
+template <int KA>
+static void launch_duo_b(int kb, dim3 g, dim3 bl, hipStream_t st, const SolveArgs<float>& a) {
+    switch (kb) {
+        case 32: hipLaunchKernelGGL((gpad_duo_kernel<KA, 32>), g, bl, 0, st, a); break;
+        case 64: hipLaunchKernelGGL((gpad_duo_kernel<KA, 64>), g, bl, 0, st, a); break;
+        case 96: hipLaunchKernelGGL((gpad_duo_kernel<KA, 96>), g, bl, 0, st, a); break;
+        case 128: hipLaunchKernelGGL((gpad_duo_kernel<KA, 128>), g, bl, 0, st, a); break;
+        case 160: hipLaunchKernelGGL((gpad_duo_kernel<KA, 160>), g, bl, 0, st, a); break;
+        case 192: hipLaunchKernelGGL((gpad_duo_kernel<KA, 192>), g, bl, 0, st, a); break;
+        case 200: hipLaunchKernelGGL((gpad_duo_kernel<KA, 200>), g, bl, 0, st, a); break;
+        default: hipLaunchKernelGGL((gpad_duo_kernel<KA, 208>), g, bl, 0, st, a); break;
+    }
+}
+
+hipError_t launch_duo(const SolveArgs<float>& a, int grid, hipStream_t st) {
+    if (!resident_supported(a.n, a.m) || a.strideA || a.strideB || !a.qctr || grid < 1)
+        return hipErrorInvalidValue;
+    const int threads = 64 * (((a.n + 63) >> 6) + ((a.m + 63) >> 6));
+    const dim3 g(grid), bl(threads);
+    const int ka = res_bucket(a.m), kb = res_bucket(a.n);
+    switch (ka) {
+        case 32: launch_duo_b<32>(kb, g, bl, st, a); break;
+        case 64: launch_duo_b<64>(kb, g, bl, st, a); break;
+        case 96: launch_duo_b<96>(kb, g, bl, st, a); break;
+        case 128: launch_duo_b<128>(kb, g, bl, st, a); break;
+        case 160: launch_duo_b<160>(kb, g, bl, st, a); break;
+        case 192: launch_duo_b<192>(kb, g, bl, st, a); break;
+        case 200: launch_duo_b<200>(kb, g, bl, st, a); break;
+        default: launch_duo_b<208>(kb, g, bl, st, a); break;
+    }
+    return hipGetLastError();
+}
+
+
+}  // namespace gpad

@@ -29,75 +29,10 @@
 
 #include <utility>
 
+#include "gpad_chain.h"
 #include "gpad_internal.h"
 
 namespace gpad {
-
-__device__ __forceinline__ float fmad(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
-__device__ __forceinline__ double fmad(double a, double b, double c) { return __builtin_fma(a, b, c); }
-__device__ __forceinline__ float absd(float a) { return __builtin_fabsf(a); }
-__device__ __forceinline__ double absd(double a) { return __builtin_fabs(a); }
-template <typename T> __device__ __forceinline__ T neg_inf();
-template <> __device__ __forceinline__ float neg_inf<float>() { return -INFINITY; }
-template <> __device__ __forceinline__ double neg_inf<double>() { return -INFINITY; }
-
-template <typename T> struct V4;
-template <> struct V4<float> { using type = float4; };
-template <> struct V4<double> { using type = double4; };
-
-// ---- wave64 reductions (DPP/permute lowered by the compiler) ---------------------------
-template <typename T>
-__device__ __forceinline__ T wave_max(T v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-    return v;
-}
-template <typename T>
-__device__ __forceinline__ T wave_min(T v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
-    return v;
-}
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-// Per-wave partials of the Algorithm-1 test -> LDS slot of the wave.
-struct CheckSlot {
-    double violz, violh, wmin, gap;
-};
-
-template <typename T>
-__device__ __forceinline__ void check_publish(CheckSlot* slots, T violz, T violh, T wmin,
-                                              double gap) {
-    const T a = wave_max(violz), b = wave_max(violh), c = wave_min(wmin);
-    const double d = wave_sum(gap);
-    if ((threadIdx.x & 63) == 0) {
-        CheckSlot& s = slots[threadIdx.x >> 6];
-        s.violz = (double)a;
-        s.violh = (double)b;
-        s.wmin = (double)c;
-        s.gap = d;
-    }
-}
-
-// Every thread evaluates the decision from the same LDS words -> uniform, no extra barrier.
-// 1: (A) L*max(G_L z + pD) <= tol              -> z certified
-// 2: (B) L*max(G_L zhat + pD) <= tol, w >= 0, -L w't <= tol -> zhat certified (returned as z*)
-__device__ __forceinline__ int check_decide(const CheckSlot* slots, int nwaves, double L,
-                                            double tol) {
-    double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gap = 0.0;
-    for (int i = 0; i < nwaves; ++i) {
-        vz = fmax(vz, slots[i].violz);
-        vh = fmax(vh, slots[i].violh);
-        wm = fmin(wm, slots[i].wmin);
-        gap += slots[i].gap;
-    }
-    if (vz * L <= tol) return 1;
-    return ((vh * L <= tol) && (wm >= 0.0) && (gap * L <= tol)) ? 2 : 0;
-}
 
 // =========================================================================================
 // gpad_stream_kernel
@@ -276,110 +211,6 @@ hipError_t launch_stream(const SolveArgs<T>& a, hipStream_t st) {
 template hipError_t launch_stream<float>(const SolveArgs<float>&, hipStream_t);
 template hipError_t launch_stream<double>(const SolveArgs<double>&, hipStream_t);
 
-// =========================================================================================
-// gpad_resident_kernel: one matrix row per lane, held in VGPRs for the whole solve.
-// =========================================================================================
-// Register-resident rows.  A lane owning primal row i keeps -ML[i][0..KA) (zero-padded past m);
-// a lane owning constraint row i keeps G_L[i][0..KB) (zero-padded past n).  Both roles use the
-// same register array r[] (they live in different waves).  KA/KB are compile-time, so the
-// chains carry no per-step predicates: padded steps are fma(0, 0, acc) = acc.
-//
-// The broadcast vector reaches the lanes through DPP, not through LDS bandwidth: each 16-lane
-// row of the wave reads the same 64 consecutive elements (lane l: a float4 at 4*(l & 15)), and
-// step k of the chain is `v_fmac_f32_dpp acc, w4[k%4], r[k] row_newbcast:(k%64)/4` -- the
-// element is broadcast from lane (k%64)/4 of each row inside the FMA itself.  A wave thus reads
-// 64 elements per ds_read_b128 with 16 distinct addresses (a same-address float4 per 4 steps,
-// all 64 lanes, made the chains LDS-bandwidth bound: ~10 cycles per step with four waves).
-// v_fmac_f32 is a single-rounding fused multiply-add, so the chain is still exactly the
-// reference's sequential fmaf order.  One 64-element group is prefetched ahead; an empty asm
-// that reads/writes acc and clobbers memory closes each group (bounds the prefetch, pins the
-// chain in place).  The first use of each ring register in a group carries `s_nop 1`: a DPP
-// read 2 wait states after a VALU write of its source (only if the compiler ever copies a ring
-// value with a VALU move; the inline asm hides the DPP from the hazard recognizer).
-// 16 steps per asm statement (the compiler separates inline-asm statements with a wait state,
-// so few, long statements keep the chain issue-bound).  Steps KI..KI+15 are elements
-// 16J..16J+15 of the current 64-element group: lanes 4J..4J+3 of each row, components x..w.
-#define GPAD_FMAC(SRC, R, LANE) \
-    "v_fmac_f32_dpp %0, %" #SRC ", %" #R " row_newbcast:%" #LANE " row_mask:0xf bank_mask:0xf\n\t"
-#define GPAD_FMAC8                                                                             \
-    GPAD_FMAC(1, 5, 21) GPAD_FMAC(2, 6, 21) GPAD_FMAC(3, 7, 21) GPAD_FMAC(4, 8, 21)             \
-    GPAD_FMAC(1, 9, 22) GPAD_FMAC(2, 10, 22) GPAD_FMAC(3, 11, 22) GPAD_FMAC(4, 12, 22)
-#define GPAD_FMAC16                                                                            \
-    GPAD_FMAC8                                                                                 \
-    GPAD_FMAC(1, 13, 23) GPAD_FMAC(2, 14, 23) GPAD_FMAC(3, 15, 23) GPAD_FMAC(4, 16, 23)         \
-    GPAD_FMAC(1, 17, 24) GPAD_FMAC(2, 18, 24) GPAD_FMAC(3, 19, 24) GPAD_FMAC(4, 20, 24)
-
-// a chain length that is 8 mod 16 (the 200 bucket) ends with an 8-step statement
-#define GPAD_FMAC8T                                                                            \
-    GPAD_FMAC(1, 5, 13) GPAD_FMAC(2, 6, 13) GPAD_FMAC(3, 7, 13) GPAD_FMAC(4, 8, 13)             \
-    GPAD_FMAC(1, 9, 14) GPAD_FMAC(2, 10, 14) GPAD_FMAC(3, 11, 14) GPAD_FMAC(4, 12, 14)
-template <int KLEN, int K, int KI, int J>
-__device__ __forceinline__ void chain_step16(float& acc, const float4& c, const float (&r)[K]) {
-    static_assert(KLEN % 8 == 0, "chain lengths are multiples of 8");
-    if constexpr (KI + 8 == KLEN) {
-#define GPAD_OPS8                                                                                 \
-    : "+v"(acc)                                                                                   \
-    : "v"(c.x), "v"(c.y), "v"(c.z), "v"(c.w), "v"(r[KI + 0]), "v"(r[KI + 1]), "v"(r[KI + 2]),     \
-      "v"(r[KI + 3]), "v"(r[KI + 4]), "v"(r[KI + 5]), "v"(r[KI + 6]), "v"(r[KI + 7]), "i"(4 * J),  \
-      "i"(4 * J + 1)
-        if constexpr (J == 0)
-            asm("s_nop 1\n\t" GPAD_FMAC8T GPAD_OPS8);
-        else
-            asm(GPAD_FMAC8T GPAD_OPS8);
-#undef GPAD_OPS8
-    } else if constexpr (KI < KLEN) {
-#define GPAD_OPS                                                                                  \
-    : "+v"(acc)                                                                                   \
-    : "v"(c.x), "v"(c.y), "v"(c.z), "v"(c.w), "v"(r[KI + 0]), "v"(r[KI + 1]), "v"(r[KI + 2]),     \
-      "v"(r[KI + 3]), "v"(r[KI + 4]), "v"(r[KI + 5]), "v"(r[KI + 6]), "v"(r[KI + 7]),             \
-      "v"(r[KI + 8]), "v"(r[KI + 9]), "v"(r[KI + 10]), "v"(r[KI + 11]), "v"(r[KI + 12]),          \
-      "v"(r[KI + 13]), "v"(r[KI + 14]), "v"(r[KI + 15]), "i"(4 * J), "i"(4 * J + 1),              \
-      "i"(4 * J + 2), "i"(4 * J + 3)
-        if constexpr (J == 0)
-            asm("s_nop 1\n\t" GPAD_FMAC16 GPAD_OPS);
-        else
-            asm(GPAD_FMAC16 GPAD_OPS);
-#undef GPAD_OPS
-    }
-}
-#undef GPAD_FMAC16
-#undef GPAD_FMAC8
-#undef GPAD_FMAC8T
-#undef GPAD_FMAC
-
-template <int KLEN, int K, int BASE, int... J>
-__device__ __forceinline__ void chain_group(float& acc, const float4& c, const float (&r)[K],
-                                            std::integer_sequence<int, J...>) {
-    (chain_step16<KLEN, K, BASE + 16 * J, J>(acc, c, r), ...);
-}
-
-template <int KLEN, int K, int H>
-__device__ __forceinline__ void chain_groups(float& acc, float4 (&ring)[2], const float (&r)[K],
-                                             const float* v, int q) {
-    constexpr int NH = (KLEN + 63) / 64;
-    if constexpr (H < NH) {
-        if constexpr (H + 1 < NH) ring[(H + 1) & 1] = *reinterpret_cast<const float4*>(v + 64 * (H + 1) + q);
-        chain_group<KLEN, K, 64 * H>(acc, ring[H & 1], r, std::make_integer_sequence<int, 4>{});
-        asm volatile("" : "+v"(acc) : : "memory");
-        chain_groups<KLEN, K, H + 1>(acc, ring, r, v, q);
-    }
-}
-
-// acc = sum_k r[k] * v[k], k = 0..KLEN-1, as one fmaf chain in ascending k.  v: LDS, padded to a
-// multiple of 64 elements (the last group's float4 reads may run past KLEN).
-template <int KLEN, int K>
-__device__ __forceinline__ float chain_regs(const float (&r)[K], const float* v) {
-    static_assert(KLEN % 4 == 0 && KLEN <= K, "bad chain length");
-    const int q = 4 * (threadIdx.x & 15);
-    float4 ring[2];
-    ring[0] = *reinterpret_cast<const float4*>(v + q);
-    float acc = 0.0f;
-    chain_groups<KLEN, K, 0>(acc, ring, r, v, q);
-    return acc;
-}
-
-constexpr int kResidentMaxThreads = 512;
-constexpr int kResidentMaxRow = 208;
 
 // FLAT = the structure-exploiting battery variant (gpad_flat.hip header; seq_functions.cpp:5-43):
 // a primal row (i, j) carries only its 6N structural coefficients (KA = bucket(6N)) and chains
@@ -545,221 +376,6 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
     }
 }
 
-// =========================================================================================
-// gpad_duo_kernel: shared matrices, TWO instances per workgroup in ping-pong, fed by a queue.
-// =========================================================================================
-// The resident kernel keeps one instance per CU, and its two half-iterations alternate: while
-// the -ML waves run the 8b chains the G/L waves wait at the barrier and vice versa, so each
-// SIMD issues one dependent fma chain at a time (~1/3 of its VALU issue rate).  With shared
-// matrices the same register-resident rows can serve two instances X, Y at once, one half-
-// iteration apart: in step s the -ML waves run 8b of slot s&1 while the G/L waves run 8d of the
-// other slot, so the A and B wave of every SIMD both issue (two independent chains interleave
-// on the SIMD).  Two instance-iterations per two steps instead of one, at the same per-step
-// latency.  Each slot is refilled from a work list (idx_in / count_in: the survivors of a
-// phased panel solve, or 0..batch-1) as its instance finishes: the first two instances of
-// workgroup g are list positions g and g + G, later ones are claimed from a device counter
-// (`qctr`, +2G) one refill ahead, so the matrix rows are loaded once per CU, not per instance.
-//
-// Slot bookkeeping (pos, vs, need8d) is computed identically by every wave from uniform values
-// and LDS words, so the control flow around the DPP chains and barriers stays uniform.  Per
-// instance the arithmetic is exactly the resident kernel's (same chains, same epilogues, same
-// test with the same wave reductions), hence bit-identical results and iteration counts.
-struct DuoSlot {  // one instance slot; bookkeeping is uniform, the floats are this lane's rows
-    int pos, vs, nextp;  // list position (>= count: empty), iterations done, pre-claimed next
-    bool need8d;         // 8b done, 8d pending
-    float th, bn;        // theta_vs, beta_{vs+1}: loaded one step before their use
-    float x0, x1, x2;    // -ML lanes: z, zhat, -;  G/L lanes: y, w, u = G_L z (g_P, p_D in LDS)
-};
-struct DuoCtx {
-    int tid, count, G, v0, n, m, N, Kc, nA, nwaves, row;
-    bool fresh, use_tol, isA, live;
-};
-
-// slot s takes list position p (empty if p >= count); uniform, contains barriers
-// gp_l / pd_l: this slot's per-row constants (g_P of the -ML rows, p_D of the G/L rows)
-template <int KB, int K>
-__device__ __forceinline__ void duo_refill(const SolveArgs<float>& a, const DuoCtx& c, DuoSlot& s, int p,
-                                           float* w_l, float* gp_l, float* pd_l, float* z_l,
-                                           const float (&r)[K]) {
-    s.pos = p;
-    s.vs = c.v0;
-    s.need8d = false;
-    s.th = a.theta[c.v0];
-    s.bn = a.beta[c.v0 + 1];
-    s.x0 = s.x1 = s.x2 = 0.0f;
-    const bool has = p < c.count;
-    if (has) {
-        const size_t b = (size_t)(a.idx_in ? a.idx_in[p] : p);
-        if (c.isA) {
-            if (c.live) {
-                s.x0 = a.z[b * c.n + c.row];
-                gp_l[c.row] = a.gP[b * a.ld_gP + c.row];
-                if (c.fresh && c.use_tol) z_l[c.row] = s.x0;
-            }
-        } else if (c.live) {
-            const float yv = a.y[b * c.m + c.row];
-            s.x0 = yv;
-            pd_l[c.row] = (float)(a.gscale * (double)a.g[b * a.ld_g + c.row]);
-            s.x1 = c.fresh ? __builtin_fmaf(a.beta[0], yv - yv, yv) : a.wc[b * c.m + c.row];
-            if (c.use_tol && !c.fresh) s.x2 = a.uc[b * c.m + c.row];
-            w_l[c.row] = s.x1;
-        }
-    }
-    __syncthreads();
-    if (has && c.fresh && c.use_tol) {  // u = G_L z_{-1}, then the 8c recursion
-        if (!c.isA) {
-            const float us = chain_regs<KB, K>(r, z_l);
-            s.x2 = c.live ? us : 0.0f;
-        }
-        __syncthreads();  // z_l free again
-    }
-}
-
-// consume the pre-claimed position of slot s, claim its next one (claim_l: this slot's cell)
-template <int KB, int K>
-__device__ __forceinline__ void duo_claim(const SolveArgs<float>& a, const DuoCtx& c, DuoSlot& s, int* claim_l,
-                                          float* w_l, float* gp_l, float* pd_l, float* z_l,
-                                          const float (&r)[K]) {
-    const int p = s.nextp;
-    if (c.tid == 0 && p < c.count) *claim_l = 2 * c.G + atomicAdd(a.qctr, 1);
-    duo_refill<KB, K>(a, c, s, p, w_l, gp_l, pd_l, z_l, r);  // (its barrier publishes *claim_l)
-    s.nextp = p < c.count ? *claim_l : c.count;
-}
-
-// one step: -ML waves run 8b+8c of slot sa, G/L waves 8d+8a (+ test) of slot sb
-template <int KA, int KB, int K>
-__device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx& c, DuoSlot& sa, DuoSlot& sb,
-                                         float* wa_l, float* zha_l, const float* gpa_l, float* wb_l,
-                                         const float* zhb_l, float* gpb_l, float* pdb_l, CheckSlot* slots_b,
-                                         int* claim_b, float* z_l, const float (&r)[K]) {
-    const bool runA = sa.pos < c.count && !sa.need8d;
-    const bool runB = sb.need8d;
-    const bool chk = runB && c.use_tol && ((sb.vs + 1) % c.Kc) == 0;
-    if (c.isA) {
-        if (runA) {
-            const float th = sa.th;
-            const float acc = chain_regs<KA, K>(r, wa_l);
-            if (c.live) {
-                const float zhv = acc - gpa_l[c.row];
-                sa.x0 = __builtin_fmaf(1.0f - th, sa.x0, th * zhv);
-                zha_l[c.row] = zhv;
-                sa.x1 = zhv;
-            }
-        }
-    } else {
-        float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY;
-        double gap = 0.0;
-        if (runB) {
-            const float th = sb.th, bn = sb.bn;
-            const float cv = chain_regs<KB, K>(r, zhb_l);
-            if (c.live) {
-                const float pdi = pdb_l[c.row], wi = sb.x1;
-                const float sv = (wi + pdi) + cv;                     // seq_functions.cpp:84
-                const float yp = (__builtin_fabsf(sv) + sv) * 0.5f;   // seq_functions.cpp:85
-                if (c.use_tol) sb.x2 = __builtin_fmaf(1.0f - th, sb.x2, th * cv);
-                if (chk) {
-                    const float t = cv + pdi;
-                    violh = t;
-                    wmin = wi;
-                    gap = -((double)wi * (double)t);
-                    violz = sb.x2 + pdi;
-                }
-                sb.x1 = __builtin_fmaf(bn, yp - sb.x0, yp);
-                sb.x0 = yp;
-                wb_l[c.row] = sb.x1;
-            }
-        }
-        if (chk) check_publish<float>(slots_b, violz, violh, wmin, gap);
-    }
-    __syncthreads();
-    if (runA) sa.need8d = true;
-    if (runB) {
-        sb.need8d = false;
-        const int v = ++sb.vs;
-        sb.th = a.theta[v];  // next iteration's schedule (tables hold N + 2 entries)
-        sb.bn = a.beta[v + 1];
-        const int done = chk ? check_decide(slots_b + c.nA, c.nwaves - c.nA, a.L, a.tol) : 0;
-        if (done || v >= c.N) {
-            const size_t b = (size_t)(a.idx_in ? a.idx_in[sb.pos] : sb.pos);
-            if (c.live) {
-                if (c.isA) a.z[b * c.n + c.row] = done == 2 ? sb.x1 : sb.x0;  // (B) certifies zhat
-                else a.y[b * c.m + c.row] = sb.x0;
-            }
-            if (c.tid == 0) {
-                a.iters[b] = v;
-                a.conv[b] = done;
-            }
-            duo_claim<KB, K>(a, c, sb, claim_b, wb_l, gpb_l, pdb_l, z_l, r);
-        }
-    }
-}
-
-template <int KA, int KB>
-__global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs<float> a) {
-    constexpr int K = KA > KB ? KA : KB;
-    constexpr int PA = (KA + 63) / 64 * 64, PB = (KB + 63) / 64 * 64;
-    __shared__ __attribute__((aligned(16))) float w_l[2][PA];   // w per slot (broadcast to -ML rows)
-    __shared__ __attribute__((aligned(16))) float zh_l[2][PB];  // zhat per slot (to G/L rows)
-    __shared__ __attribute__((aligned(16))) float z_l[PB];      // z_{-1} of a fresh instance (u seed)
-    __shared__ float gp_l[2][PB];                               // per slot: g_P of the -ML rows
-    __shared__ float pd_l[2][PA];                               //           p_D of the G/L rows
-    __shared__ CheckSlot slots[2][kResidentMaxThreads / 64];
-    __shared__ int claim_l[2];
-
-    DuoCtx c;
-    c.tid = threadIdx.x;
-    c.count = a.count_in ? __builtin_amdgcn_readfirstlane(*a.count_in) : a.batch;
-    if (a.count_in && c.count > a.fin_thresh) return;  // the panel phase has them
-    c.G = gridDim.x;
-    if ((int)blockIdx.x >= c.count) return;
-    c.v0 = a.v_begin;
-    c.fresh = c.v0 == 0;
-    c.use_tol = a.tol > 0.0;
-    c.n = a.n;
-    c.m = a.m;
-    c.N = a.N;
-    c.Kc = a.check_every;
-    c.nA = (c.n + 63) >> 6;
-    c.nwaves = blockDim.x >> 6;
-    c.isA = (c.tid >> 6) < c.nA;
-    c.row = c.isA ? c.tid : c.tid - 64 * c.nA;
-    c.live = c.isA ? c.row < c.n : c.row < c.m;
-
-    float r[K];
-    {
-        const int len = c.isA ? c.m : c.n;
-        const float* __restrict__ Mt = c.isA ? a.MGt : a.GLt;
-        const int ld = c.isA ? a.ldn : a.ldm;
-#pragma unroll
-        for (int k = 0; k < K; ++k) r[k] = (c.live && k < len) ? Mt[(size_t)k * ld + c.row] : 0.0f;
-    }
-    for (int i = c.tid; i < 2 * PA; i += blockDim.x) (&w_l[0][0])[i] = 0.0f;
-    for (int i = c.tid; i < 2 * PB; i += blockDim.x) (&zh_l[0][0])[i] = 0.0f;
-    for (int i = c.tid; i < PB; i += blockDim.x) z_l[i] = 0.0f;
-    if (c.tid == 0) {  // first claims of the queue (positions 2G, 2G+1, ...)
-        claim_l[0] = 2 * c.G + atomicAdd(a.qctr, 1);
-        claim_l[1] = 2 * c.G + atomicAdd(a.qctr, 1);
-    }
-    __syncthreads();
-    DuoSlot s0, s1;
-    s0.nextp = claim_l[0];
-    s1.nextp = claim_l[1];
-    duo_refill<KB, K>(a, c, s0, blockIdx.x, w_l[0], gp_l[0], pd_l[0], z_l, r);
-    duo_refill<KB, K>(a, c, s1, blockIdx.x + c.G, w_l[1], gp_l[1], pd_l[1], z_l, r);
-    while (s0.pos < c.count || s1.pos < c.count) {
-        duo_step<KA, KB, K>(a, c, s0, s1, w_l[0], zh_l[0], gp_l[0], w_l[1], zh_l[1], gp_l[1], pd_l[1], slots[1],
-                            &claim_l[1], z_l, r);
-        duo_step<KA, KB, K>(a, c, s1, s0, w_l[1], zh_l[1], gp_l[1], w_l[0], zh_l[0], gp_l[0], pd_l[0], slots[0],
-                            &claim_l[0], z_l, r);
-    }
-}
-
-// chain-length buckets (multiples of 32 up to 192, then 200 and the 208 cap)
-static int res_bucket(int len) {
-    if (len > 200) return 208;
-    if (len > 192) return 200;
-    return (len + 31) / 32 * 32;
-}
 
 template <int KA, bool FLAT = false>
 static void launch_res_b(int kb, dim3 g, dim3 bl, hipStream_t st, const SolveArgs<float>& a) {
@@ -809,39 +425,6 @@ hipError_t launch_resident(const SolveArgs<float>& a, hipStream_t st, bool* supp
 
 hipError_t launch_resident_finisher(const SolveArgs<float>& a, int grid, hipStream_t st) {
     return launch_resident_grid(a, grid, st);
-}
-
-template <int KA>
-static void launch_duo_b(int kb, dim3 g, dim3 bl, hipStream_t st, const SolveArgs<float>& a) {
-    switch (kb) {
-        case 32: hipLaunchKernelGGL((gpad_duo_kernel<KA, 32>), g, bl, 0, st, a); break;
-        case 64: hipLaunchKernelGGL((gpad_duo_kernel<KA, 64>), g, bl, 0, st, a); break;
-        case 96: hipLaunchKernelGGL((gpad_duo_kernel<KA, 96>), g, bl, 0, st, a); break;
-        case 128: hipLaunchKernelGGL((gpad_duo_kernel<KA, 128>), g, bl, 0, st, a); break;
-        case 160: hipLaunchKernelGGL((gpad_duo_kernel<KA, 160>), g, bl, 0, st, a); break;
-        case 192: hipLaunchKernelGGL((gpad_duo_kernel<KA, 192>), g, bl, 0, st, a); break;
-        case 200: hipLaunchKernelGGL((gpad_duo_kernel<KA, 200>), g, bl, 0, st, a); break;
-        default: hipLaunchKernelGGL((gpad_duo_kernel<KA, 208>), g, bl, 0, st, a); break;
-    }
-}
-
-hipError_t launch_duo(const SolveArgs<float>& a, int grid, hipStream_t st) {
-    if (!resident_supported(a.n, a.m) || a.strideA || a.strideB || !a.qctr || grid < 1)
-        return hipErrorInvalidValue;
-    const int threads = 64 * (((a.n + 63) >> 6) + ((a.m + 63) >> 6));
-    const dim3 g(grid), bl(threads);
-    const int ka = res_bucket(a.m), kb = res_bucket(a.n);
-    switch (ka) {
-        case 32: launch_duo_b<32>(kb, g, bl, st, a); break;
-        case 64: launch_duo_b<64>(kb, g, bl, st, a); break;
-        case 96: launch_duo_b<96>(kb, g, bl, st, a); break;
-        case 128: launch_duo_b<128>(kb, g, bl, st, a); break;
-        case 160: launch_duo_b<160>(kb, g, bl, st, a); break;
-        case 192: launch_duo_b<192>(kb, g, bl, st, a); break;
-        case 200: launch_duo_b<200>(kb, g, bl, st, a); break;
-        default: launch_duo_b<208>(kb, g, bl, st, a); break;
-    }
-    return hipGetLastError();
 }
 
 // flat battery variant: primal chains of 6N, constraint chains of n (flat G_L expanded to the
