@@ -84,7 +84,8 @@ def test_algorithm1_termination_bitexact(gpu, kernel, name):
 
 @pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("nm", [(200, 200), (37, 53), (1, 5), (5, 1), (64, 64), (65, 129), (208, 180),
-                                (256, 250), (144, 129)])
+                                (256, 250), (144, 129), (193, 201), (201, 193), (199, 200), (192, 200),
+                                (200, 8), (8, 196)])
 def test_shapes_bitexact_vs_oracle(gpu, oracle, kernel, nm):
     """C2 (200 x 200) and ragged shapes (not multiples of 4 / 64, single row or column)."""
     from gpad_mpc import problems
