@@ -147,19 +147,26 @@ def phase_util(iters, N, K=10, plan=None, fin=512):
             "min_iters": int(it.min()), "max_iters": int(it.max())}
 
 
-def traffic_from_profile(kernel_prefix):
-    """HBM bytes per launch of the dominant kernel from the committed PMC profile of this same
+def traffic_from_profile(kernel_name):
+    """HBM bytes per solve of the dominant kernel from the committed PMC profile of this same
     bench command (tools/profile.sh -> profiles/r01_bench_summary.json; FETCH_SIZE x2 +
-    WRITE_SIZE, MI355X_MICROARCH.md §HBM).  None when absent."""
+    WRITE_SIZE, MI355X_MICROARCH.md §HBM): the kernel's bytes summed over every launch of the
+    profiled run / the C4 solves that run made (its --warmup + --steps; the side legs launch other
+    kernel instantiations).  None when absent."""
     path = os.path.join(ROOT, "profiles", "r01_bench_summary.json")
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
         return None, None
-    for k, v in d.get("pmc_per_launch", {}).items():
-        if k.startswith(kernel_prefix) and "hbm_bytes_per_launch" in v:
-            return v["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
-    return None, None
+    args = d.get("bench_args", "").split()
+    try:
+        solves = int(args[args.index("--steps") + 1]) + int(args[args.index("--warmup") + 1])
+    except (ValueError, IndexError):
+        return None, None
+    v = d.get("pmc_per_launch", {}).get(kernel_name)
+    if not v or "hbm_bytes_total" not in v or solves <= 0:
+        return None, None
+    return v["hbm_bytes_total"] / solves, os.path.relpath(path, ROOT)
 
 
 def hbm_leg(dev, batch=1024, n=800, m=800, N=20):
@@ -409,10 +416,11 @@ def main():
         mean_iters = iters_per_launch / B
         # C2 single instance (config 1): latency kernel, fixed 1000 iterations
         one = dict()
-        traffic, traffic_src = traffic_from_profile("gpad::gpad_" + st["kernel"])
+        T = (max(n, m) + 15) // 16
+        kname = (f"gpad::gpad_panel2_kernel<{T}>" if T > 8 else f"gpad::gpad_panel_kernel<{T}>") \
+            if st["kernel"] == "panel" else f"gpad::gpad_{st['kernel']}_kernel"
+        traffic, traffic_src = traffic_from_profile(kname)
         launches = util["launches_per_solve"] if st["kernel"] == "panel" else 1
-        if traffic is not None:
-            traffic *= launches  # PMC values are per panel-phase launch; one solve = `launches`
         with gpad_mpc.GpadSolver(dev.index, stream=stream.cuda_stream) as s1:
             s1.setup(dML, dG, L32, n=n, m=m, batch=1)
             z1 = torch.zeros(1, n, device=dev)
@@ -465,7 +473,8 @@ def main():
                                  "per executed instance-iteration) of one solve / its device time "
                                  "(HIP events around the solve's chain of phase launches; rocprof "
                                  "avg phase duration x launches_per_solve gives the same time); "
-                                 "traffic = PMC HBM bytes per phase launch x launches_per_solve"},
+                                 "traffic = PMC HBM bytes of the panel kernel per solve (profiled "
+                                 "run's total / its solves)"},
             "cpu_baseline": cpu,
             "legs": extra,
         }

@@ -48,8 +48,13 @@ def main(d):
             e["effective_clock_ghz"] = e["GRBM_GUI_ACTIVE"] / 8.0 / ns
         if "SQ_INSTS_MFMA" in e and "SQ_INSTS_VALU" in e and e["SQ_INSTS_MFMA"] > 0:
             e["valu_non_mfma_per_mfma"] = (e["SQ_INSTS_VALU"] - e["SQ_INSTS_MFMA"]) / e["SQ_INSTS_MFMA"]
+        # totals over the profiled run (per-launch averages mix phases of very different length)
+        if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
+            e["launches"] = len(cs["FETCH_SIZE"])
+            e["hbm_bytes_total"] = 2.0 * sum(cs["FETCH_SIZE"]) * 1024.0 + sum(cs["WRITE_SIZE"]) * 1024.0
         pmc[k] = e
     out["pmc_per_launch"] = pmc
+    out["bench_args"] = os.environ.get("PROFILE_ARGS", "")
     print(json.dumps(out, indent=1, sort_keys=True))
 
 

@@ -22,5 +22,5 @@ run fetch --pmc FETCH_SIZE
 run write --pmc WRITE_SIZE
 run sq --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY
 run grbm --pmc GRBM_GUI_ACTIVE GRBM_COUNT
-python3 tools/pmc_summary.py $OUT > $OUT/summary.json
+PROFILE_ARGS="$ARGS" python3 tools/pmc_summary.py $OUT > $OUT/summary.json
 cat $OUT/summary.json
