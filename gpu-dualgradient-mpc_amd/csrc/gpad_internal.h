@@ -82,6 +82,12 @@ struct PanelPlan {
 };
 int panel_plan(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus, PanelPlan* out);
 int panel_tiles(int n, int m, int batch);
+// gpad_bigpanel.hip: shared f32 matrices with n or m in (256, 1024]
+bool bigpanel_supported(int n, int m);
+size_t bigpanel_frag_bytes(int n, int m);
+hipError_t launch_pack_bigpanel(const float* ML, const float* G, int n, int m, float mg_sign, double g_scale,
+                                void* frag, hipStream_t s);
+hipError_t launch_bigpanel(const SolveArgs<float>& a, int grid, hipStream_t s);
 hipError_t launch_pack_panel(const float* ML, const float* G, int n, int m, int batch, float mg_sign,
                              double g_scale, void* frag, hipStream_t s);
 

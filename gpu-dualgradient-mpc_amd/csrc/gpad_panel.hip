@@ -66,17 +66,24 @@ __global__ void pack_panel_kernel(const float* __restrict__ src, int rows, int c
     dst[idx] = make_float4(v[0], v[1], v[2], v[3]);
 }
 
+// n or m beyond 256 rows: the big-panel layout (gpad_bigpanel.hip), rectangular tile grids
 size_t panel_frag_bytes(int n, int m, int /*batch*/) {
     const int T = panel_tiles_for(n, m);
-    return T ? (size_t)2 * T * T * 64 * sizeof(float4) : 0;
+    if (!T) return bigpanel_frag_bytes(n, m);
+    return (size_t)2 * T * T * 64 * sizeof(float4);
 }
 
-int panel_tiles(int n, int m, int /*batch*/) { return panel_tiles_for(n, m); }
+int panel_tiles(int n, int m, int /*batch*/) {
+    const int T = panel_tiles_for(n, m);
+    if (T) return T;
+    return bigpanel_supported(n, m) ? ((n > m ? n : m) + 15) / 16 : 0;
+}
 
 hipError_t launch_pack_panel(const float* ML, const float* G, int n, int m, int /*batch*/,
                              float mg_sign, double g_scale, void* frag, hipStream_t s) {
     const int T = panel_tiles_for(n, m);
-    if (!T) return hipSuccess;
+    if (!T) return bigpanel_supported(n, m) ? launch_pack_bigpanel(ML, G, n, m, mg_sign, g_scale, frag, s)
+                                            : hipSuccess;
     float4* pa1 = reinterpret_cast<float4*>(frag);
     float4* pa2 = pa1 + (size_t)T * T * 64;
     const int tot = T * T * 64;
@@ -1035,9 +1042,12 @@ __global__ __launch_bounds__(1024) void survivor_sort_kernel(int* idx, const int
         idx[i] = (int)(0xFFFFFFFFu - (unsigned)(key[i] & 0xFFFFFFFFull));
 }
 
+// T = 0: the big-panel kernel (gpad_bigpanel.hip)
 template <int T>
 static void launch_panel_kernel(const SolveArgs<float>& a, int grid, hipStream_t s) {
-    if constexpr (T > 8)
+    if constexpr (T == 0)
+        (void)launch_bigpanel(a, grid, s);
+    else if constexpr (T > 8)
         hipLaunchKernelGGL((gpad_panel2_kernel<T>), dim3(grid), dim3(1024), 0, s, a);
     else
         hipLaunchKernelGGL((gpad_panel_kernel<T>), dim3(grid), dim3(64 * T), 0, s, a);
@@ -1048,7 +1058,7 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     // Grid = resident workgroups: a panel-pair workgroup (T > 8) fills a CU; T-wave panels
     // (T <= 8) share one, 32/T of them.  Workgroups walk their panels grid-stride.
     const int panels = (a.batch + 15) / 16;
-    const int resident = T > 8 ? a.num_cus : a.num_cus * (32 / T);
+    const int resident = (T == 0 || T > 8) ? a.num_cus : a.num_cus * (32 / T);
     int grid = panels < resident ? panels : resident;
     if (const char* cap = std::getenv("GPAD_PANEL_MAX_GRID")) {  // test knob: grid-stride panels
         const int c = std::atoi(cap);
@@ -1125,7 +1135,12 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
 hipError_t launch_panel(const SolveArgs<float>& a, hipStream_t s, bool* supported) {
     const int T = panel_tiles_for(a.n, a.m);
     // the fragment image must have been packed for this geometry at setup
-    *supported = a.frag != nullptr && T && a.strideA == 0 && a.strideB == 0 && a.frag_tiles == T;
+    if (!T) {  // big panels
+        *supported = a.frag != nullptr && bigpanel_supported(a.n, a.m) && a.strideA == 0 && a.strideB == 0 &&
+                     a.frag_tiles == panel_tiles(a.n, a.m, a.batch);
+        return *supported ? launch_panel_t<0>(a, s) : hipSuccess;
+    }
+    *supported = a.frag != nullptr && a.strideA == 0 && a.strideB == 0 && a.frag_tiles == T;
     if (!*supported) return hipSuccess;
     switch (T) {
         case 1: return launch_panel_t<1>(a, s);

@@ -203,6 +203,34 @@ def test_panel_phased_compaction_bitexact(gpu, oracle, monkeypatch, grid, phase,
         assert_bitexact(y[b], yo, f"instance {b} y")
 
 
+@pytest.mark.parametrize("tol,N", [(1e-4, 2000), (0.0, 37)])
+@pytest.mark.parametrize("nm,B", [((200, 900), 40), ((300, 300), 20), ((257, 130), 33), ((520, 600), 17), ((1000, 300), 9)])
+@pytest.mark.parametrize("grid,phase", [(0, 0), (2, 20)])
+def test_bigpanel_bitexact(gpu, oracle, monkeypatch, tol, N, nm, B, grid, phase):
+    """Shared matrices beyond 256 rows on the big-panel MFMA kernel (gpad_bigpanel.hip): GEMMs of
+    different tile counts, up to 4 row tiles per wave, grid-stride panels and phases; every
+    instance must match its own oracle solve exactly, iteration count included."""
+    from gpad_mpc import problems
+    if grid:
+        monkeypatch.setenv("GPAD_PANEL_MAX_GRID", str(grid))
+    if phase:
+        monkeypatch.setenv("GPAD_PANEL_PHASE", str(phase))
+    n, m = nm
+    qp = problems.synthetic_qp(n, m, batch=B, seed=17)
+    ML, G = qp.ML.astype(np.float32), qp.G.astype(np.float32)
+    M, g = qp.M.astype(np.float32), qp.g.astype(np.float32)
+    L = np.float32(qp.L)
+    rng = np.random.default_rng(3)
+    z0 = (0.1 * rng.normal(size=(B, n))).astype(np.float32)
+    z, y, st, iters = run_gpu(ML, M, G, g, L, N, tol=tol, kernel="panel", z0=z0)
+    assert st["kernel"] == "panel"
+    for b in range(B):
+        zo, yo, it, _ = oracle.solve_f32(z0[b], np.zeros(m), ML, M[b], G, g[b], N, L, tol)
+        assert iters[b] == it, b
+        assert_bitexact(z[b], zo, f"instance {b} z")
+        assert_bitexact(y[b], yo, f"instance {b} y")
+
+
 @pytest.mark.parametrize("finisher,grid", [("duo", 1), ("duo", 3), ("duo", 0), ("resident", 0)])
 @pytest.mark.parametrize("nm,B,z0s", [((200, 200), 120, 0.0), ((40, 180), 200, 0.1), ((131, 64), 97, 0.1)])
 def test_finisher_queue_bitexact(gpu, oracle, monkeypatch, finisher, grid, nm, B, z0s):
