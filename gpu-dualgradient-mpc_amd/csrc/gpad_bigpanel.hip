@@ -6,8 +6,9 @@
 // fragment order streamed from L2/MALL and B (w, zhat) in LDS in fragment order, every row chain
 // an ascending-k fmaf chain (bit-exact with the reference's sequential steps) -- but the two
 // GEMMs have different shapes: GEMM 1 has T1 = ceil(n/16) row tiles and T2 = ceil(m/16) k-blocks,
-// GEMM 2 the reverse, and up to 64 tiles of each.  Wave w (of 16) owns row tiles w, w+16, ... of
-// both GEMMs (NT1 / NT2 of them, compile-time) and runs their chains one after another; the
+// GEMM 2 the reverse, and up to 64 tiles of each.  Wave w (of 16) owns
+// row tiles w, w+16, ... of both GEMMs (NT1 / NT2 of them, compile-time) and runs their chains
+// (GEMM 2: two tiles interleaved, sharing the B fragments) one after another; the
 // per-row state of its tiles (z, g_P; y, w, u, p_D) lives in its registers.  The Algorithm-1 test
 // partials are reduced per wave over its tiles, then across the 16 waves in LDS.
 //
@@ -110,8 +111,52 @@ __device__ __forceinline__ bf32x4 big_gemm(__amdgpu_buffer_rsrc_t PA, const floa
     return acc;
 }
 
+// two row tiles t0, t1 of the same GEMM in one pass: the chains interleave (hiding the 40-cycle
+// MFMA dependency of each other) and share every B fragment (one LDS read for both)
+__device__ __forceinline__ void big_gemm2(__amdgpu_buffer_rsrc_t PA, const float4* B, int t0, int t1, int Tr,
+                                          int nkb, int kq, int lane, bf32x4& acc0, bf32x4& acc1) {
+    acc0 = bf32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    acc1 = bf32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    const int v0 = t0 * 1024 + lane * 16, v1 = t1 * 1024 + lane * 16, stride = Tr * 1024;
+    float4 a0 = bas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, v0, 0, 0));
+    float4 c0 = bas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, v1, 0, 0));
+    float4 a1 = a0, c1 = c0;
+    if (nkb > 1) {
+        a1 = bas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, v0, stride, 0));
+        c1 = bas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, v1, stride, 0));
+    }
+    float4 b0 = B[lane];
+    for (int kb = 0; kb < nkb; ++kb) {
+        const float4 ak = a0, ck = c0, bk = b0;
+        a0 = a1;
+        c0 = c1;
+        if (kb + 2 < nkb) {
+            a1 = bas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, v0, (kb + 2) * stride, 0));
+            c1 = bas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, v1, (kb + 2) * stride, 0));
+        }
+        if (kb + 1 < nkb) b0 = B[(kb + 1) * 64 + lane];
+        const int steps = kb + 1 < nkb ? 4 : kq;
+        __builtin_amdgcn_sched_barrier(0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, bk.x, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ck.x, bk.x, acc1, 0, 0, 0);
+        if (steps > 1) {
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, bk.y, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ck.y, bk.y, acc1, 0, 0, 0);
+        }
+        if (steps > 2) {
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, bk.z, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ck.z, bk.z, acc1, 0, 0, 0);
+        }
+        if (steps > 3) {
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, bk.w, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ck.w, bk.w, acc1, 0, 0, 0);
+        }
+        asm volatile("" : "+v"(acc0), "+v"(acc1)::"memory");
+    }
+}
+
 template <int NT1, int NT2>
-__global__ __launch_bounds__(1024) void gpad_bigpanel_kernel(SolveArgs<float> a) {
+__global__ __launch_bounds__(64 * kBigWaves) void gpad_bigpanel_kernel(SolveArgs<float> a) {
     extern __shared__ __attribute__((aligned(16))) float4 big_lds[];
     const int n = a.n, m = a.m, N = a.N, K = a.check_every;
     const int T1 = big_tiles(n), T2 = big_tiles(m);
@@ -225,11 +270,31 @@ __global__ __launch_bounds__(1024) void gpad_bigpanel_kernel(SolveArgs<float> a)
             // ---- GEMM 2 + epilogue: y+ (8d), next w (8a), test partials ----------------------------
             float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY;
             double gap = 0.0;
+            bf32x4 acc_next = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
             for (int q = 0; q < NT2; ++q) {
                 const int t = w + kBigWaves * q;
+                // tiles q, q + 1 of this wave in one interleaved pass (acc of q + 1 kept for the next q)
+                bf32x4 acc;
+#ifndef BIG_NOPAIR
+                constexpr bool kPair = NT2 > 1;
+#else
+                constexpr bool kPair = false;
+#endif
+                if constexpr (kPair) {
+                    if ((q & 1) == 0) {
+                        if (t + kBigWaves < T2) {
+                            big_gemm2(PA2, Zh, t, t + kBigWaves, T2, T1, kq2, lane, acc, acc_next);
+                        } else if (t < T2) {
+                            acc = big_gemm(PA2, Zh, t, T2, T1, kq2, lane);
+                        }
+                    } else {
+                        acc = acc_next;
+                    }
+                } else {
+                    if (t < T2) acc = big_gemm(PA2, Zh, t, T2, T1, kq2, lane);
+                }
                 if (t < T2) {
-                    const bf32x4 acc = big_gemm(PA2, Zh, t, T2, T1, kq2, lane);
                     const float4 w4 = Wl[t * 64 + lane];
                     const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
                     const float4 p4 = Pd[t * 64 + lane];
@@ -277,7 +342,7 @@ __global__ __launch_bounds__(1024) void gpad_bigpanel_kernel(SolveArgs<float> a)
             __syncthreads();
             if (!chk && v < a.v_end) continue;
 
-            // ---- Algorithm 1 test: every wave reduces the 16 slots for the 16 columns, ballot ----
+            // ---- Algorithm 1 test: every wave reduces the wave slots for the 16 columns, ballot ---
             unsigned m1 = 0u, m2 = 0u;
             if (chk) {
                 int cd = 0;
@@ -392,17 +457,15 @@ static int nt_of(int tiles) {  // row tiles per wave, rounded up to 1, 2 or 4
 // one phase launch of the big-panel kernel (the phase loop is launch_panel's)
 hipError_t launch_bigpanel(const SolveArgs<float>& a, int grid, hipStream_t s) {
     const int q1 = nt_of(big_tiles(a.n)), q2 = nt_of(big_tiles(a.m));
+#define BIG_CASE(A, B) \
+    case A * 8 + B: return launch_big_nt<A, B>(a, grid, s);
     switch (q1 * 8 + q2) {
-        case 9: return launch_big_nt<1, 1>(a, grid, s);
-        case 10: return launch_big_nt<1, 2>(a, grid, s);
-        case 12: return launch_big_nt<1, 4>(a, grid, s);
-        case 17: return launch_big_nt<2, 1>(a, grid, s);
-        case 18: return launch_big_nt<2, 2>(a, grid, s);
-        case 20: return launch_big_nt<2, 4>(a, grid, s);
-        case 33: return launch_big_nt<4, 1>(a, grid, s);
-        case 34: return launch_big_nt<4, 2>(a, grid, s);
+        BIG_CASE(1, 1) BIG_CASE(1, 2) BIG_CASE(1, 4)
+        BIG_CASE(2, 1) BIG_CASE(2, 2) BIG_CASE(2, 4)
+        BIG_CASE(4, 1) BIG_CASE(4, 2)
         default: return launch_big_nt<4, 4>(a, grid, s);
     }
+#undef BIG_CASE
 }
 
 }  // namespace gpad
