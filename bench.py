@@ -224,20 +224,21 @@ def distinct_leg(dev, n, m, batch=8192, N=100):
             "iters_per_s": batch * N / (st["kernel_ms"] / 1e3)}
 
 
-def flat_leg(dev, batch=8192, N=100):
+def flat_leg(dev, batch=8192, N=100, horizon=10):
     """the flat (equal-cell) battery path vs the full-matrix path on the
-    same C1 battery packs (n_u = 4, N = 10: n = 40, m = 180), fixed N iterations, fp32."""
+    same battery packs (n_u = 4; horizon 10: n = 40, m = 180 = C1; horizon 50: n = 200, m = 900,
+    the full path then on the big-panel kernel), fixed N iterations, fp32."""
     import torch
 
     import gpad_mpc
     from gpad_mpc import problems
-    qp = problems.battery_scenarios(4, 10, batch, seed=9)
-    MGf, GLf, L = problems.flatten_battery(qp, 4, 10)
+    qp = problems.battery_scenarios(4, horizon, batch, seed=9)
+    MGf, GLf, L = problems.flatten_battery(qp, 4, horizon)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a, np.float64).astype(np.float32))).to(dev)  # noqa: E731
     L32 = float(np.float32(L))
     GP, G = t(qp.M), t(qp.g)
     PD = (G * np.float32(-1.0 / np.float64(np.float32(L)))).contiguous()
-    out = {"config": f"{batch} battery packs (n_u=4, N=10: n={qp.n}, m={qp.m}), {N} iterations"}
+    out = {"config": f"{batch} battery packs (n_u=4, N={horizon}: n={qp.n}, m={qp.m}), {N} iterations"}
     stream = torch.cuda.current_stream(dev).cuda_stream
     for name in ("flat", "full"):
         with gpad_mpc.GpadSolver(dev.index or 0, stream=stream) as s:
@@ -441,6 +442,7 @@ def main():
             extra["distinct_c2_batch"] = distinct_leg(dev, n, m)
             extra["closed_loop_battery"] = closed_loop_leg(dev, cpu=not args.no_cpu)
             extra["flat_battery_c1"] = flat_leg(dev)
+            extra["battery_n50"] = flat_leg(dev, horizon=50, N=50)
         out = {
             "metric": "GPAD iterations/s (instance-iterations, solve to eps=1e-4)",
             "value": value,

@@ -1002,47 +1002,60 @@ size_t panel_work_bytes(int m, int batch) {
     return sizeof(int) * (2 * (size_t)batch + 2 * kPanelMaxPhases) + 2 * sizeof(float) * (size_t)batch * m;
 }
 
-// Longest-first order for the finisher's work list: the survivors idx[0..count) sorted by the
-// iteration count the previous solve needed (descending; ties by instance id), so the duo kernel's
-// queue starts the longest remaining solves first (list scheduling, LPT).  One workgroup, bitonic
-// sort in LDS; a no-op when the list is not the finisher's (count > thresh) or too long.
+// Longest-first order for the finisher's work list: the survivors idx[0..count) reordered by the
+// iteration count the previous solve needed (descending), so the duo kernel's queue starts the
+// longest remaining solves first (list scheduling, LPT).  One workgroup, counting sort on the
+// counts (4096 bins, larger counts share the last): histogram, descending exclusive scan, scatter.
+// The order inside a bin is arbitrary -- results never depend on it, only the schedule.
+// A no-op when the list is not the finisher's (count > thresh) or longer than kSortMax.
 constexpr int kSortMax = 8192;
+constexpr int kSortBins = 4096;
 __global__ __launch_bounds__(1024) void survivor_sort_kernel(int* idx, const int* count_p, const int* pred,
                                                              int thresh) {
-    __shared__ unsigned long long key[kSortMax];
+    __shared__ int hist[kSortBins];
+    __shared__ int ids[kSortMax];
+    __shared__ int part[1024];
     const int count = *count_p;
     if (count <= 1 || count > thresh || count > kSortMax) return;
-    int P = 1;
-    while (P < count) P <<= 1;
-    for (int i = threadIdx.x; i < P; i += blockDim.x) {
-        if (i < count) {
-            const unsigned id = (unsigned)idx[i];
-            key[i] = ((unsigned long long)(unsigned)pred[id] << 32) | (0xFFFFFFFFu - id);
-        } else {
-            key[i] = 0ull;  // padding sorts last
-        }
+    const int tid = threadIdx.x;
+    auto bin = [&](int id) {  // descending count -> ascending bin
+        const int p = pred[id];
+        const int k = p < 0 ? 0 : (p >= kSortBins ? kSortBins - 1 : p);
+        return kSortBins - 1 - k;
+    };
+    for (int i = tid; i < kSortBins; i += 1024) hist[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < count; i += 1024) {
+        const int id = idx[i];
+        ids[i] = id;
+        atomicAdd(&hist[bin(id)], 1);
     }
     __syncthreads();
-    for (int k = 2; k <= P; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < P; i += blockDim.x) {
-                const int l = i ^ j;
-                if (l > i) {
-                    const unsigned long long x = key[i], y = key[l];
-                    if (((i & k) == 0) ? (x < y) : (x > y)) {
-                        key[i] = y;
-                        key[l] = x;
-                    }
-                }
-            }
-            __syncthreads();
-        }
+    // exclusive scan of hist: thread tid owns bins 4 tid .. 4 tid + 3
+    int local[4], sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        local[q] = sum;
+        sum += hist[4 * tid + q];
     }
-    for (int i = threadIdx.x; i < count; i += blockDim.x)
-        idx[i] = (int)(0xFFFFFFFFu - (unsigned)(key[i] & 0xFFFFFFFFull));
+    part[tid] = sum;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {  // inclusive scan of the per-thread sums
+        const int v = tid >= off ? part[tid - off] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    const int base = part[tid] - sum;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) hist[4 * tid + q] = base + local[q];
+    __syncthreads();
+    for (int i = tid; i < count; i += 1024) {
+        const int id = ids[i];
+        idx[atomicAdd(&hist[bin(id)], 1)] = id;
+    }
 }
 
-// T = 0: the big-panel kernel (gpad_bigpanel.hip)
 template <int T>
 static void launch_panel_kernel(const SolveArgs<float>& a, int grid, hipStream_t s) {
     if constexpr (T == 0)
