@@ -1,0 +1,472 @@
+// gpad_flatpanel.hip -- the flat (equal-cell) battery path on the f32 MFMA pipe (gfx950).
+//
+// The flat data (ENABLE_FLATTEN_MATRICES, seq_functions.cpp:5-43; gpad_flat.hip header) define
+// the two mat-vecs by their structural nonzeros only.  Over a panel of 16 instances they are
+// n_u + n_u + 1 skinny GEMMs, each output row still ONE ascending-k fmaf chain in the
+// reference's order (bit-exact with StepTwo/StepFourGPADFlatSequential):
+//   8b, cell j (j < n_u):  zhat[i n_u + j] = A1_j[i][:] . B1_j - g_P, i < Nh, K1 = 4 Nh + E
+//        A1_j[i][s] = MGf[i][j + n_u s] (s < 4 Nh), MGf[i][mc + s - 4 Nh] (the E coupling terms)
+//        B1_j[s]    = w[j + n_u s],                 w[mc + s - 4 Nh]
+//   8d, cell c:  constraint rows r = c + n_u s (s < 4 Nh): A2_c[s][t] = GLf[r][t], K2 = Nh,
+//        B2_c[t] = zhat[t n_u + c]
+//   8d, coupling rows r = mc + e (e < E): A3[e][q] = GLf[r][q / n_u], K3 = n, B3 = zhat
+// (mc = 4 n_u Nh, E = m - mc).  ~3x fewer MFMAs than the full matrices at the battery shapes.
+// The epilogues scatter: zhat of row (i, j) goes to B2_j[i] and B3[i n_u + j]; w of a cell row
+// to B1_c[s], of a coupling row to every B1_j[4 Nh + e]; y+ = (s + w) + p_D, y+ < 0 -> 0 (the
+// flat steps' order).  A workgroup (16 waves) owns a panel of 16 instances for the whole solve;
+// the GEMM units (sub-GEMM, row tile) are dealt to the waves round-robin, each unit's row state
+// in the owning wave's registers.  Fragment images are packed at gpad_setup_flat.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "gpad_internal.h"
+
+namespace gpad {
+
+typedef float ff32x4 __attribute__((ext_vector_type(4)));
+constexpr int kFlatPanelWaves = 16;
+
+struct FlatGeom {  // sizes in tiles / k-blocks of 16 rows; image offsets in float4s
+    int n_u, Nh, n, m, mc, E;
+    int KBc, KBe, KB1, kq1;  // 8b per cell: K = 16 KBc (4 Nh cell terms, zero-padded) + the E coupling terms
+    int T1;                  // 8b row tiles per cell (= the k-blocks of the 8d cell GEMMs, K = Nh)
+    int kq2;                 // 8d per cell: T2 = KBc row tiles, KB2 = T1 k-blocks
+    int KB3, kq3;            // 8d coupling: KBe row tiles, K = n
+    int U1, U2;              // units (sub-GEMM, row tile) of the two phases
+    int off2, off3, total;   // images [n_u][KB1][T1], [n_u][T1][KBc], [KB3][KBe] of 64 float4
+};
+
+__host__ __device__ inline int fp_ceil16(int x) { return (x + 15) / 16; }
+__host__ __device__ inline int fp_kq(int K, int KB) { return (K - 16 * (KB - 1) + 3) / 4; }
+
+__host__ __device__ inline FlatGeom flat_geom(int n, int m, int n_u) {
+    FlatGeom g;
+    g.n_u = n_u;
+    g.Nh = n / n_u;
+    g.n = n;
+    g.m = m;
+    g.mc = 4 * n_u * g.Nh;
+    g.E = m - g.mc;
+    g.KBc = fp_ceil16(4 * g.Nh);
+    g.KBe = fp_ceil16(g.E);
+    g.KB1 = g.KBc + g.KBe;
+    g.kq1 = fp_kq(g.E, g.KBe);
+    g.T1 = fp_ceil16(g.Nh);
+    g.kq2 = fp_kq(g.Nh, g.T1);
+    g.KB3 = fp_ceil16(n);
+    g.kq3 = fp_kq(n, g.KB3);
+    g.U1 = n_u * g.T1;
+    g.U2 = g.KBe + n_u * g.KBc;
+    g.off2 = n_u * g.KB1 * g.T1 * 64;
+    g.off3 = g.off2 + n_u * g.T1 * g.KBc * 64;
+    g.total = g.off3 + g.KB3 * g.KBe * 64;
+    return g;
+}
+
+// LDS, 1 KiB per block of 16 rows x 16 instances (MFMA B-fragment order):
+//   W  [n_u][KBc]  w of each cell's constraint rows (row s of cell c = constraint c + n_u s)
+//   We [KBe]       w of the coupling rows (one copy, the tail of every cell's 8b chain)
+//   Zc [n_u][T1]   zhat per cell (row i of cell j = zhat[i n_u + j])
+//   Zn [KB3]       zhat in natural order (the coupling rows' operand)
+struct FlatPanelSlot {
+    float violz[16], violh[16], wmin[16];
+    double gap[16];
+};
+static size_t flatpanel_lds_bytes(const FlatGeom& g) {
+    return (size_t)(g.n_u * (g.KBc + g.T1) + g.KBe + g.KB3) * 1024 + kFlatPanelWaves * sizeof(FlatPanelSlot);
+}
+
+__device__ __forceinline__ int fp_pi16(int rho) { return 4 * (rho & 3) + (rho >> 2); }
+
+// A values from the flat data as the setup stores it: MGf row-major Nh x m (sign-folded -ML),
+// GLT t-major Nh x m (GLT[t][r] = GLf[r][t])
+__device__ __forceinline__ float flat_a1(const FlatGeom& g, const float* MGf, int j, int i, int s) {
+    if (i >= g.Nh) return 0.0f;
+    if (s < 16 * g.KBc) return s < 4 * g.Nh ? MGf[(size_t)i * g.m + j + g.n_u * s] : 0.0f;
+    const int e = s - 16 * g.KBc;
+    return e < g.E ? MGf[(size_t)i * g.m + g.mc + e] : 0.0f;
+}
+__device__ __forceinline__ float flat_a2(const FlatGeom& g, const float* GLT, int c, int s, int t) {
+    if (s >= 4 * g.Nh || t >= g.Nh) return 0.0f;
+    return GLT[(size_t)t * g.m + c + g.n_u * s];
+}
+__device__ __forceinline__ float flat_a3(const FlatGeom& g, const float* GLT, int e, int q) {
+    if (e >= g.E || q >= g.n) return 0.0f;
+    return GLT[(size_t)(q / g.n_u) * g.m + g.mc + e];
+}
+
+__global__ void pack_flatpanel_kernel(FlatGeom g, const float* __restrict__ MGf, const float* __restrict__ GLT,
+                                      float4* __restrict__ dst) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= g.total) return;
+    const int lane = idx & 63;
+    const int rrow = fp_pi16(lane & 15);  // row inside the tile (fragment-order permutation)
+    float v[4];
+    if (idx < g.off2) {  // [n_u][KB1][T1]
+        const int blk = idx >> 6;
+        const int t = blk % g.T1, b = (blk / g.T1) % g.KB1, j = blk / (g.T1 * g.KB1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = flat_a1(g, MGf, j, 16 * t + rrow, 16 * b + 4 * q + (lane >> 4));
+    } else if (idx < g.off3) {  // [n_u][T1 k-blocks][KBc tiles]
+        const int blk = (idx - g.off2) >> 6;
+        const int t = blk % g.KBc, b = (blk / g.KBc) % g.T1, c = blk / (g.KBc * g.T1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = flat_a2(g, GLT, c, 16 * t + rrow, 16 * b + 4 * q + (lane >> 4));
+    } else {  // [KB3 k-blocks][KBe tiles]
+        const int blk = (idx - g.off3) >> 6;
+        const int t = blk % g.KBe, b = blk / g.KBe;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = flat_a3(g, GLT, 16 * t + rrow, 16 * b + 4 * q + (lane >> 4));
+    }
+    dst[idx] = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+bool flatpanel_supported(int n, int m, int n_u) {
+    if (n_u <= 0 || n % n_u || m <= 4 * n) return false;
+    const FlatGeom g = flat_geom(n, m, n_u);
+    return flatpanel_lds_bytes(g) <= 160 * 1024 && g.U1 <= 4 * kFlatPanelWaves && g.U2 <= 4 * kFlatPanelWaves &&
+           (long long)g.total * 16 < (1LL << 31);
+}
+
+size_t flatpanel_frag_bytes(int n, int m, int n_u) {
+    return flatpanel_supported(n, m, n_u) ? (size_t)flat_geom(n, m, n_u).total * sizeof(float4) : 0;
+}
+
+hipError_t launch_pack_flatpanel(const float* MGf, const float* GLT, int n, int m, int n_u, void* frag,
+                                 hipStream_t s) {
+    const FlatGeom g = flat_geom(n, m, n_u);
+    hipLaunchKernelGGL(pack_flatpanel_kernel, dim3((unsigned)((g.total + 255) / 256)), dim3(256), 0, s, g, MGf, GLT,
+                       reinterpret_cast<float4*>(frag));
+    return hipGetLastError();
+}
+
+__device__ __forceinline__ float4 fas_float4(__attribute__((ext_vector_type(4))) unsigned v) {
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+
+// one unit's chain over nkb k-blocks (the last only its kq 4-steps): A by buffer loads at byte
+// offset voff + b * stride, two k-blocks in flight; B block b from Ba (b < kbs) or Bb (b >= kbs)
+__device__ __forceinline__ ff32x4 fp_gemm(__amdgpu_buffer_rsrc_t PA, int voff, int stride, int nkb, int kq,
+                                          const float4* Ba, int kbs, const float4* Bb, int lane) {
+    ff32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    float4 a0 = fas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, 0, 0));
+    float4 a1 = nkb > 1 ? fas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, stride, 0)) : a0;
+    float4 b0 = kbs > 0 ? Ba[lane] : Bb[lane];
+    for (int kb = 0; kb < nkb; ++kb) {
+        const float4 ak = a0, bk = b0;
+        a0 = a1;
+        if (kb + 2 < nkb) a1 = fas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb + 2) * stride, 0));
+        if (kb + 1 < nkb) b0 = kb + 1 < kbs ? Ba[(kb + 1) * 64 + lane] : Bb[(kb + 1 - kbs) * 64 + lane];
+        const int steps = kb + 1 < nkb ? 4 : kq;
+        __builtin_amdgcn_sched_barrier(0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, bk.x, acc, 0, 0, 0);
+        if (steps > 1) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, bk.y, acc, 0, 0, 0);
+        if (steps > 2) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, bk.z, acc, 0, 0, 0);
+        if (steps > 3) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, bk.w, acc, 0, 0, 0);
+        asm volatile("" : "+v"(acc)::"memory");
+    }
+    return acc;
+}
+
+// a phase-2 unit: the coupling tile t (u < KBe) or tile t of cell c's constraint rows
+struct FpUnit2 {
+    int cell, t;
+};
+__device__ __forceinline__ FpUnit2 fp_unit2(const FlatGeom& g, int u) {
+    FpUnit2 x;
+    if (u < g.KBe) {
+        x.cell = -1;
+        x.t = u;
+    } else {
+        x.cell = (u - g.KBe) / g.KBc;
+        x.t = (u - g.KBe) - x.cell * g.KBc;
+    }
+    return x;
+}
+// constraint row of output row rr of a phase-2 unit (-1: padding)
+__device__ __forceinline__ int fp_row2(const FlatGeom& g, FpUnit2 x, int rr) {
+    if (x.cell < 0) return rr < g.E ? g.mc + rr : -1;
+    return rr < 4 * g.Nh ? x.cell + g.n_u * rr : -1;
+}
+
+template <int NU1, int NU2>
+__global__ __launch_bounds__(64 * kFlatPanelWaves) void gpad_flatpanel_kernel(SolveArgs<float> a, FlatGeom g) {
+    extern __shared__ __attribute__((aligned(16))) float4 fp_lds[];
+    constexpr int W = kFlatPanelWaves;
+    float4* Wc = fp_lds;                    // [n_u][KBc * 64]
+    float4* We = Wc + g.n_u * g.KBc * 64;   // [KBe * 64]
+    float4* Zc = We + g.KBe * 64;           // [n_u][T1 * 64]
+    float4* Zn = Zc + g.n_u * g.T1 * 64;    // [KB3 * 64]
+    FlatPanelSlot* slots = reinterpret_cast<FlatPanelSlot*>(Zn + g.KB3 * 64);
+
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int jl = lane >> 4, c = lane & 15;
+    const int n = a.n, m = a.m, N = a.N, K = a.check_every;
+    const __amdgpu_buffer_rsrc_t PA =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.frag), 0, g.total * 16, 0x00020000);
+    const bool use_tol = a.tol > 0.0;
+    const int count = a.batch;
+    const int panels = (count + 15) / 16;
+    // Zn's rows past n are read by the last k-block of the coupling chains: zero once
+    for (int e = threadIdx.x; e < g.KB3 * 64; e += 64 * W) Zn[e] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+
+    for (int p = blockIdx.x; p < panels; p += gridDim.x) {
+        const int k = 16 * p + c;
+        bool active = k < count;
+        const size_t bi = (size_t)(active ? k : 0);
+        unsigned live;
+        {
+            const int left = count - 16 * p;
+            live = left >= 16 ? 0xFFFFu : ((1u << left) - 1u);
+        }
+        // ---- this wave's rows: z, g_P (phase 1), y, p_D (phase 2); w (and z_{-1}) into LDS --------
+        float z[NU1][4], gp[NU1][4];
+        float y[NU2][4], u[NU2][4], pd[NU2][4];
+#pragma unroll
+        for (int q = 0; q < NU1; ++q) {
+            const int un = w + W * q, j = un / g.T1, t = un - j * g.T1;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 * t + 4 * r + jl;
+                const bool ok = un < g.U1 && i < g.Nh && active;
+                z[q][r] = ok ? a.z[bi * n + i * g.n_u + j] : 0.0f;
+                gp[q][r] = ok ? a.gP[bi * a.ld_gP + i * g.n_u + j] : 0.0f;
+            }
+            if (un < g.U1 && use_tol) {  // z_{-1} as the B operand of u = G_L z_{-1}
+                Zc[(j * g.T1 + t) * 64 + lane] = make_float4(z[q][0], z[q][1], z[q][2], z[q][3]);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 16 * t + 4 * r + jl, kk = i * g.n_u + j;
+                    if (i < g.Nh)
+                        reinterpret_cast<float*>(&Zn[(kk >> 4) * 64 + (kk & 3) * 16 + c])[(kk >> 2) & 3] = z[q][r];
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NU2; ++q) {
+            const int un = w + W * q;
+            const FpUnit2 x = fp_unit2(g, un);
+            float wv[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = un < g.U2 ? fp_row2(g, x, 16 * x.t + 4 * r + jl) : -1;
+                const bool ok = row >= 0 && active;
+                y[q][r] = ok ? a.y[bi * m + row] : 0.0f;
+                pd[q][r] = ok ? (float)(a.gscale * (double)a.g[bi * a.ld_g + row]) : 0.0f;
+                u[q][r] = 0.0f;
+                wv[r] = __builtin_fmaf(a.beta[0], y[q][r] - y[q][r], y[q][r]);
+            }
+            if (un < g.U2) {
+                float4* wp = x.cell < 0 ? We + x.t * 64 + lane : Wc + (x.cell * g.KBc + x.t) * 64 + lane;
+                *wp = make_float4(wv[0], wv[1], wv[2], wv[3]);
+            }
+        }
+        __syncthreads();
+        if (use_tol) {  // u = G_L z_{-1}
+#pragma unroll
+            for (int q = 0; q < NU2; ++q) {
+                const int un = w + W * q;
+                if (un < g.U2) {
+                    const FpUnit2 x = fp_unit2(g, un);
+                    const bool cp = x.cell < 0;
+                    const int voff = (cp ? g.off3 + x.t * 64 : g.off2 + (x.cell * g.T1 * g.KBc + x.t) * 64) * 16 +
+                                     lane * 16;
+                    const ff32x4 cz = fp_gemm(PA, voff, (cp ? g.KBe : g.KBc) * 1024, cp ? g.KB3 : g.T1,
+                                              cp ? g.kq3 : g.kq2, cp ? Zn : Zc + x.cell * g.T1 * 64,
+                                              cp ? g.KB3 : g.T1, Zn, lane);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) u[q][r] = cz[r];
+                }
+            }
+            __syncthreads();  // the zhat arrays are rewritten by the first iteration
+        }
+
+        int v = 0;
+        float th = a.theta[0], bn = a.beta[1];
+        while (true) {
+            const float th_next = a.theta[v + 1], bn_next = a.beta[v + 2];
+            ++v;
+            const bool chk = use_tol && (v % K) == 0;
+            const float omt = 1.0f - th;
+            // ---- 8b + 8c: per-cell chains over (cell w, coupling w) ---------------------------------
+#pragma unroll
+            for (int q = 0; q < NU1; ++q) {
+                const int un = w + W * q;
+                if (un < g.U1) {
+                    const int j = un / g.T1, t = un - j * g.T1;
+                    const ff32x4 acc = fp_gemm(PA, (j * g.KB1 * g.T1 + t) * 1024 + lane * 16, g.T1 * 1024, g.KB1,
+                                               g.kq1, Wc + j * g.KBc * 64, g.KBc, We, lane);
+                    float zh[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        zh[r] = acc[r] - gp[q][r];  // seq_functions.cpp:18
+                        const float zn = __builtin_fmaf(omt, z[q][r], th * zh[r]);
+                        if (active) z[q][r] = zn;
+                    }
+                    Zc[(j * g.T1 + t) * 64 + lane] = make_float4(zh[0], zh[1], zh[2], zh[3]);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int i = 16 * t + 4 * r + jl, kk = i * g.n_u + j;
+                        if (i < g.Nh)
+                            reinterpret_cast<float*>(&Zn[(kk >> 4) * 64 + (kk & 3) * 16 + c])[(kk >> 2) & 3] = zh[r];
+                    }
+                }
+            }
+            __syncthreads();
+            // ---- 8d + next 8a: cell and coupling chains; w back to LDS ------------------------------
+            float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY;
+            double gap = 0.0;
+#pragma unroll
+            for (int q = 0; q < NU2; ++q) {
+                const int un = w + W * q;
+                if (un < g.U2) {
+                    const FpUnit2 x = fp_unit2(g, un);
+                    const bool cp = x.cell < 0;
+                    const int voff = (cp ? g.off3 + x.t * 64 : g.off2 + (x.cell * g.T1 * g.KBc + x.t) * 64) * 16 +
+                                     lane * 16;
+                    const ff32x4 acc = fp_gemm(PA, voff, (cp ? g.KBe : g.KBc) * 1024, cp ? g.KB3 : g.T1,
+                                               cp ? g.kq3 : g.kq2, cp ? Zn : Zc + x.cell * g.T1 * 64,
+                                               cp ? g.KB3 : g.T1, Zn, lane);
+                    float4* wp = cp ? We + x.t * 64 + lane : Wc + (x.cell * g.KBc + x.t) * 64 + lane;
+                    const float4 w4 = *wp;
+                    const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+                    const int lim = cp ? g.E : 4 * g.Nh;
+                    float wn[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float cv = acc[r], wi = wv[r], pdi = pd[q][r];
+                        const float sv = (cv + wi) + pdi;        // seq_functions.cpp:37
+                        const float yp = sv < 0.0f ? 0.0f : sv;  // seq_functions.cpp:40-42
+                        if (use_tol) {
+                            const float un2 = __builtin_fmaf(omt, u[q][r], th * cv);
+                            if (active) u[q][r] = un2;
+                            if (chk && active && 16 * x.t + 4 * r + jl < lim) {
+                                const float tt = cv + pdi;
+                                violh = fmaxf(violh, tt);
+                                wmin = fminf(wmin, wi);
+                                gap -= (double)wi * (double)tt;
+                                violz = fmaxf(violz, u[q][r] + pdi);
+                            }
+                        }
+                        wn[r] = __builtin_fmaf(bn, yp - y[q][r], yp);
+                        if (active) y[q][r] = yp;
+                    }
+                    if (active) *wp = make_float4(wn[0], wn[1], wn[2], wn[3]);
+                }
+            }
+            if (chk) {
+#pragma unroll
+                for (int o = 16; o < 64; o <<= 1) {
+                    violz = fmaxf(violz, __shfl_xor(violz, o, 64));
+                    violh = fmaxf(violh, __shfl_xor(violh, o, 64));
+                    wmin = fminf(wmin, __shfl_xor(wmin, o, 64));
+                    gap += __shfl_xor(gap, o, 64);
+                }
+                if (jl == 0) {
+                    slots[w].violz[c] = violz;
+                    slots[w].violh[c] = violh;
+                    slots[w].wmin[c] = wmin;
+                    slots[w].gap[c] = gap;
+                }
+            }
+            th = th_next;
+            bn = bn_next;
+            __syncthreads();
+            if (!chk && v < N) continue;
+
+            unsigned m1 = 0u, m2 = 0u;
+            if (chk) {
+                int cd = 0;
+                if (lane < 16 && ((live >> lane) & 1u)) {
+                    double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gq = 0.0;
+#pragma unroll
+                    for (int s2 = 0; s2 < W; ++s2) {
+                        vz = fmax(vz, (double)slots[s2].violz[lane]);
+                        vh = fmax(vh, (double)slots[s2].violh[lane]);
+                        wm = fmin(wm, (double)slots[s2].wmin[lane]);
+                        gq += slots[s2].gap[lane];
+                    }
+                    if (vz * a.L <= a.tol) cd = 1;
+                    else if ((vh * a.L <= a.tol) && (wm >= 0.0) && (gq * a.L <= a.tol)) cd = 2;
+                }
+                m1 = (unsigned)__ballot(cd == 1);
+                m2 = (unsigned)__ballot(cd == 2);
+            }
+            const int cdc = ((m1 >> c) & 1u) ? 1 : (((m2 >> c) & 1u) ? 2 : 0);
+            if (active && (cdc != 0 || v >= N)) {  // finished column: results out
+#pragma unroll
+                for (int q = 0; q < NU1; ++q) {
+                    const int un = w + W * q, j = un / g.T1, t = un - j * g.T1;
+                    if (un < g.U1) {
+                        const float4 zh4 = Zc[(j * g.T1 + t) * 64 + lane];  // test (B) returns zhat
+                        const float zhv[4] = {zh4.x, zh4.y, zh4.z, zh4.w};
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int i = 16 * t + 4 * r + jl;
+                            if (i < g.Nh) a.z[bi * n + i * g.n_u + j] = cdc == 2 ? zhv[r] : z[q][r];
+                        }
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < NU2; ++q) {
+                    const int un = w + W * q;
+                    const FpUnit2 x = fp_unit2(g, un);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int row = un < g.U2 ? fp_row2(g, x, 16 * x.t + 4 * r + jl) : -1;
+                        if (row >= 0) a.y[bi * m + row] = y[q][r];
+                    }
+                }
+                if (w == 0 && jl == 0) {
+                    a.iters[k] = v;
+                    a.conv[k] = cdc;
+                }
+                active = false;
+            }
+            live &= ~(m1 | m2);
+            if (v >= N) live = 0u;
+            if (live == 0u) break;
+        }
+        __syncthreads();  // the next panel reuses the LDS arrays
+    }
+}
+
+template <int NU1, int NU2>
+static hipError_t launch_fp_nt(const SolveArgs<float>& a, const FlatGeom& g, size_t lds, int grid, hipStream_t s) {
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute((const void*)gpad_flatpanel_kernel<NU1, NU2>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL((gpad_flatpanel_kernel<NU1, NU2>), dim3(grid), dim3(64 * kFlatPanelWaves), lds, s, a, g);
+    return hipGetLastError();
+}
+
+static int fp_nt(int units) {
+    const int q = (units + kFlatPanelWaves - 1) / kFlatPanelWaves;
+    return q <= 1 ? 1 : (q <= 2 ? 2 : 4);
+}
+
+// whole-batch solve (one launch, no phased compaction); a.frag = the flat fragment images
+hipError_t launch_flatpanel(const SolveArgs<float>& a, hipStream_t s) {
+    if (!flatpanel_supported(a.n, a.m, a.n_u) || !a.frag) return hipErrorInvalidValue;
+    const FlatGeom g = flat_geom(a.n, a.m, a.n_u);
+    const size_t lds = flatpanel_lds_bytes(g);
+    const int panels = (a.batch + 15) / 16;
+    int grid = a.num_cus * (lds * 2 <= 160 * 1024 ? 2 : 1);
+    if (grid > panels) grid = panels;
+    const int q1 = fp_nt(g.U1), q2 = fp_nt(g.U2);
+#define FP_CASE(A, B) \
+    case A * 8 + B: return launch_fp_nt<A, B>(a, g, lds, grid, s);
+    switch (q1 * 8 + q2) {
+        FP_CASE(1, 1) FP_CASE(1, 2) FP_CASE(1, 4)
+        FP_CASE(2, 1) FP_CASE(2, 2) FP_CASE(2, 4)
+        FP_CASE(4, 1) FP_CASE(4, 2)
+        default: return launch_fp_nt<4, 4>(a, g, lds, grid, s);
+    }
+#undef FP_CASE
+}
+
+}  // namespace gpad

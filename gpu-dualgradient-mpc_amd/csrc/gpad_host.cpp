@@ -332,10 +332,18 @@ int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* d, int n_u, const float*
         HIP_TRY(gpad::launch_expand_flat_gl((const float*)dG, (float*)h->GLx.p, Nh, n_u, m, h->ldm,
                                             h->stream));
     }
-    HIP_TRY(hipStreamSynchronize(h->stream));
-    if (d->memory == GPAD_MEM_HOST) h->stage.release();
     h->frag.release();
     h->frag_tiles = 0;
+    if (d->batch > 16) {  // MFMA panels over the flat data (gpad_flatpanel.hip)
+        const size_t fb = gpad::flatpanel_frag_bytes(d->n, m, n_u);
+        if (fb) {
+            if ((rc = h->frag.ensure(fb))) return rc;
+            HIP_TRY(gpad::launch_pack_flatpanel((const float*)h->MGt.p, (const float*)h->GLt.p, d->n, m, n_u,
+                                                h->frag.p, h->stream));
+        }
+    }
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    if (d->memory == GPAD_MEM_HOST) h->stage.release();
     h->n_u = n_u;
     h->flat = true;
     h->ready = true;
@@ -496,7 +504,11 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
     if constexpr (sizeof(T) == sizeof(float)) {
         if (h->flat) {  // structure-exploiting battery path (gpad_setup_flat)
             a.n_u = h->n_u;
-            if (h->GLx.p && kernel != GPAD_KERNEL_STREAM) {  // register-resident flat chains
+            const char* fpe = std::getenv("GPAD_FLAT_PANEL_MIN");  // tuning knob
+            const int fpm = fpe ? std::atoi(fpe) : 4 * h->num_cus;
+            if (h->frag.p && (kernel == GPAD_KERNEL_PANEL || (kernel == GPAD_KERNEL_AUTO && batch >= fpm))) {
+                e = gpad::launch_flatpanel(a, h->stream);
+            } else if (h->GLx.p && kernel != GPAD_KERNEL_STREAM) {  // register-resident flat chains
                 a.GLt = (const T*)h->GLx.p;
                 a.strideA = a.strideB = 0;
                 e = gpad::launch_flat_resident(a, h->stream);

@@ -111,6 +111,12 @@ hipError_t launch_flat(const SolveArgs<float>& a, hipStream_t s);
 // flat G_L expanded to the full k-major image [n][ldm]
 bool flat_resident_supported(int n, int m, int n_u);
 hipError_t launch_flat_resident(const SolveArgs<float>& a, hipStream_t s);
+// flat battery data on the MFMA pipe (gpad_flatpanel.hip): per-cell skinny GEMMs over panels
+bool flatpanel_supported(int n, int m, int n_u);
+size_t flatpanel_frag_bytes(int n, int m, int n_u);
+hipError_t launch_pack_flatpanel(const float* MGf, const float* GLT, int n, int m, int n_u, void* frag,
+                                 hipStream_t s);
+hipError_t launch_flatpanel(const SolveArgs<float>& a, hipStream_t s);
 // flat G_L (m x Nh) -> full k-major image out[k*ld + r] (k < n), zero off the structure
 hipError_t launch_expand_flat_gl(const float* GLf, float* out, int Nh, int n_u, int m, int ld, hipStream_t s);
 hipError_t launch_step2_flat(const float* MGf, const float* w, const float* gP, float* zhat, int Nh, int n_u,

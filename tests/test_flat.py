@@ -163,6 +163,38 @@ def test_flat_batch_bitexact(gpu, oracle, tol, N, kernel, cells):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("tol,N", [(0.0, 120), (1e-4, 4000)])
+@pytest.mark.parametrize("cells,B", [((4, 10), 40), ((3, 17), 33), ((5, 6), 16 * 3 + 1), ((4, 50), 24),
+                                     ((2, 30), 20)])
+def test_flat_panel_bitexact(gpu, oracle, tol, N, cells, B):
+    """The flat MFMA panel kernel (gpad_flatpanel.hip, forced with KERNEL_PANEL): per-cell
+    skinny GEMMs over 16-instance panels, ragged last panel, vs the oracle's flat solve."""
+    from gpad_mpc import problems
+    import gpad_mpc
+    n_u, Nh = cells
+    qp = problems.battery_scenarios(n_u, Nh, B, seed=11)
+    MGf, GLf, L = problems.flatten_battery(qp, n_u, Nh)
+    f32 = lambda a: np.ascontiguousarray(np.asarray(a, np.float64).astype(np.float32))  # noqa: E731
+    L32 = np.float32(L)
+    MGf32, GLf32 = f32(MGf), f32(GLf)
+    GP = f32(qp.M)
+    PD = np.ascontiguousarray(oracle.scale_vec(f32(qp.g), L32))
+    s = gpad_mpc.GpadSolver(0)
+    s.setup_flat(MGf32, GLf32, float(L32), n_u=n_u, batch=B, kernel=gpad_mpc.KERNEL_PANEL)
+    Z = np.zeros((B, qp.n), np.float32)
+    Y = np.zeros((B, qp.m), np.float32)
+    it = np.zeros(B, np.int32)
+    st = s.run(Z, Y, GP, PD, N, tol, scaled=True, iters=it)
+    assert st["kernel"] == "flat"
+    for b in range(B):
+        z, y, its, _ = oracle.solve_flat_f32(np.zeros(qp.n), np.zeros(qp.m), MGf32, GP[b], GLf32, PD[b],
+                                             n_u, N, L32, tol)
+        assert it[b] == its, b
+        np.testing.assert_array_equal(Z[b], z, err_msg=f"z[{b}]")
+        np.testing.assert_array_equal(Y[b], y, err_msg=f"y[{b}]")
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name", FLAT_SETS)
 def test_flat_step_entry_points(gpu, name):
     """gpad_step2_primal_flat / gpad_step4_project_flat vs the reference's flat step KATs."""

@@ -25,10 +25,12 @@ def main():
             GP = t(qp.M).reshape(batch, -1)
             PD = (t(qp.g).reshape(batch, -1) * np.float32(-1.0 / np.float64(np.float32(L)))).contiguous()
             row = {"n_u": n_u, "N": Nh, "n": qp.n, "m": qp.m, "batch": batch}
-            for name in ("flat", "full"):
+            for name in ("flat", "flat_chains", "full"):
                 s = gpad_mpc.GpadSolver(0)
-                if name == "flat":
+                if name == "flat":  # auto: the MFMA flat panels at large batches
                     s.setup_flat(t(MGf), t(GLf), L32, n_u=n_u, batch=batch)
+                elif name == "flat_chains":  # the per-instance flat kernels (register / LDS chains)
+                    s.setup_flat(t(MGf), t(GLf), L32, n_u=n_u, batch=batch, kernel=_lib.KERNEL_RESIDENT)
                 else:
                     s.setup(-t(qp.ML), t(qp.G) / np.float32(L32), L32, n=qp.n, m=qp.m, batch=batch,
                             scaled=True)
