@@ -18,7 +18,9 @@
 // in the owning wave's registers.  Fragment images are packed at gpad_setup_flat.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "gpad_internal.h"
 
@@ -26,6 +28,7 @@ namespace gpad {
 
 typedef float ff32x4 __attribute__((ext_vector_type(4)));
 constexpr int kFlatPanelWaves = 16;
+constexpr int kFlatPanelWavesMax = 16;
 
 struct FlatGeom {  // sizes in tiles / k-blocks of 16 rows; image offsets in float4s
     int n_u, Nh, n, m, mc, E;
@@ -35,6 +38,11 @@ struct FlatGeom {  // sizes in tiles / k-blocks of 16 rows; image offsets in flo
     int KB3, kq3;            // 8d coupling: KBe row tiles, K = n
     int U1, U2;              // units (sub-GEMM, row tile) of the two phases
     int off2, off3, total;   // images [n_u][KB1][T1], [n_u][T1][KBc], [KB3][KBe] of 64 float4
+    int PB;                  // LDS blocks per panel
+    int P;                   // panels per workgroup (set by the launcher)
+    // unit descriptors (set by the launcher): pp << 16 | (cell + 1) << 8 | t
+    int d1[4 * kFlatPanelWavesMax];
+    int d2[4 * kFlatPanelWavesMax];
 };
 
 __host__ __device__ inline int fp_ceil16(int x) { return (x + 15) / 16; }
@@ -61,6 +69,8 @@ __host__ __device__ inline FlatGeom flat_geom(int n, int m, int n_u) {
     g.off2 = n_u * g.KB1 * g.T1 * 64;
     g.off3 = g.off2 + n_u * g.T1 * g.KBc * 64;
     g.total = g.off3 + g.KB3 * g.KBe * 64;
+    g.PB = n_u * (g.KBc + g.T1) + g.KBe + g.KB3;
+    g.P = 1;
     return g;
 }
 
@@ -69,12 +79,13 @@ __host__ __device__ inline FlatGeom flat_geom(int n, int m, int n_u) {
 //   We [KBe]       w of the coupling rows (one copy, the tail of every cell's 8b chain)
 //   Zc [n_u][T1]   zhat per cell (row i of cell j = zhat[i n_u + j])
 //   Zn [KB3]       zhat in natural order (the coupling rows' operand)
+// test partials: one slot per phase-2 unit (its 16 columns, reduced over the unit's rows)
 struct FlatPanelSlot {
     float violz[16], violh[16], wmin[16];
     double gap[16];
 };
-static size_t flatpanel_lds_bytes(const FlatGeom& g) {
-    return (size_t)(g.n_u * (g.KBc + g.T1) + g.KBe + g.KB3) * 1024 + kFlatPanelWaves * sizeof(FlatPanelSlot);
+static size_t flatpanel_lds_bytes(const FlatGeom& g, int P) {
+    return (size_t)P * g.PB * 1024 + (size_t)P * g.U2 * sizeof(FlatPanelSlot);
 }
 
 __device__ __forceinline__ int fp_pi16(int rho) { return 4 * (rho & 3) + (rho >> 2); }
@@ -125,8 +136,8 @@ __global__ void pack_flatpanel_kernel(FlatGeom g, const float* __restrict__ MGf,
 bool flatpanel_supported(int n, int m, int n_u) {
     if (n_u <= 0 || n % n_u || m <= 4 * n) return false;
     const FlatGeom g = flat_geom(n, m, n_u);
-    return flatpanel_lds_bytes(g) <= 160 * 1024 && g.U1 <= 4 * kFlatPanelWaves && g.U2 <= 4 * kFlatPanelWaves &&
-           (long long)g.total * 16 < (1LL << 31);
+    return flatpanel_lds_bytes(g, 1) <= 160 * 1024 && g.U1 <= 4 * kFlatPanelWaves && g.U2 <= 4 * kFlatPanelWaves &&
+           (long long)g.total * 16 < (1LL << 31) && n_u < 255 && g.KBc < 256 && g.T1 < 256;
 }
 
 size_t flatpanel_frag_bytes(int n, int m, int n_u) {
@@ -190,15 +201,101 @@ __device__ __forceinline__ int fp_row2(const FlatGeom& g, FpUnit2 x, int rr) {
     return rr < 4 * g.Nh ? x.cell + g.n_u * rr : -1;
 }
 
-template <int NU1, int NU2>
+// A fragment prefetch of a unit's first two k-blocks (issued before the barrier that precedes
+// its chain: the L2 latency overlaps the barrier and the epilogue)
+struct FpPre {
+    float4 a0, a1;
+};
+// A operand source: the fragment image in global memory (L2-resident, buffer loads) or a copy
+// of it in LDS (ALDS: when it fits beside the panels' vectors)
+template <bool ALDS>
+__device__ __forceinline__ float4 fp_lda(__amdgpu_buffer_rsrc_t PA, const float4* As, int voff, int off) {
+    if constexpr (ALDS) return As[(voff + off) >> 4];
+    else return fas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, off, 0));
+}
+template <bool ALDS>
+__device__ __forceinline__ FpPre fp_pre(__amdgpu_buffer_rsrc_t PA, const float4* As, int voff, int stride, int nkb) {
+    FpPre f;
+    f.a0 = fp_lda<ALDS>(PA, As, voff, 0);
+    f.a1 = nkb > 1 ? fp_lda<ALDS>(PA, As, voff, stride) : f.a0;
+    return f;
+}
+// one unit's chain over nkb k-blocks (the last only its kq 4-steps); A blocks RING ahead (the
+// first two prefetched by fp_pre), B block b from Ba (b < kbs) or Bb (b >= kbs)
+template <bool ALDS, int RING>
+__device__ __forceinline__ ff32x4 fp_chain(__amdgpu_buffer_rsrc_t PA, const float4* As, FpPre f, int voff, int stride,
+                                           int nkb, int kq, const float4* Ba, int kbs, const float4* Bb, int lane) {
+    ff32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    float4 ar[RING];
+    ar[0] = f.a0;
+    ar[1] = f.a1;
+#pragma unroll
+    for (int i = 2; i < RING; ++i) ar[i] = i < nkb ? fp_lda<ALDS>(PA, As, voff, i * stride) : f.a0;
+    float4 b0 = kbs > 0 ? Ba[lane] : Bb[lane];
+    for (int kb = 0; kb < nkb; ++kb) {
+        const float4 ak = ar[0], bk = b0;
+#pragma unroll
+        for (int i = 0; i + 1 < RING; ++i) ar[i] = ar[i + 1];
+        if (kb + RING < nkb) ar[RING - 1] = fp_lda<ALDS>(PA, As, voff, (kb + RING) * stride);
+        if (kb + 1 < nkb) b0 = kb + 1 < kbs ? Ba[(kb + 1) * 64 + lane] : Bb[(kb + 1 - kbs) * 64 + lane];
+        const int steps = kb + 1 < nkb ? 4 : kq;
+        __builtin_amdgcn_sched_barrier(0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, bk.x, acc, 0, 0, 0);
+        if (steps > 1) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, bk.y, acc, 0, 0, 0);
+        if (steps > 2) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, bk.z, acc, 0, 0, 0);
+        if (steps > 3) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, bk.w, acc, 0, 0, 0);
+        asm volatile("" : "+v"(acc)::"memory");
+    }
+    return acc;
+}
+
+// unit geometry (uniform), from the launcher's descriptor tables.  The unit index goes through an
+// empty asm so that nothing derived from it is hoisted out of the iteration loop (the derived
+// offsets are a few scalar ops; holding them across the loop would spill).
+__device__ __forceinline__ int fp_opq(int x) {
+    asm volatile("" : "+s"(x));
+    return x;
+}
+struct FpU1 {
+    int pp, j, t;
+};
+__device__ __forceinline__ FpU1 fp_u1(const FlatGeom& g, int un) {
+    const int d = g.d1[fp_opq(un)];
+    FpU1 x;
+    x.pp = d >> 16;
+    x.j = ((d >> 8) & 0xFF) - 1;
+    x.t = d & 0xFF;
+    return x;
+}
+struct FpU2 {
+    int pp, cell, t;
+};
+__device__ __forceinline__ FpU2 fp_u2(const FlatGeom& g, int un) {
+    const int d = g.d2[fp_opq(un)];
+    FpU2 x;
+    x.pp = d >> 16;
+    x.cell = ((d >> 8) & 0xFF) - 1;
+    x.t = d & 0xFF;
+    return x;
+}
+__device__ __forceinline__ int fp_voff1(const FlatGeom& g, FpU1 x, int lane) {
+    return (x.j * g.KB1 * g.T1 + x.t) * 1024 + lane * 16;
+}
+__device__ __forceinline__ int fp_voff2(const FlatGeom& g, FpU2 x, int lane) {
+    return (x.cell < 0 ? g.off3 + x.t * 64 : g.off2 + (x.cell * g.T1 * g.KBc + x.t) * 64) * 16 + lane * 16;
+}
+
+template <int NU1, int NU2, bool ALDS>
 __global__ __launch_bounds__(64 * kFlatPanelWaves) void gpad_flatpanel_kernel(SolveArgs<float> a, FlatGeom g) {
+    constexpr int RING = 2;  // a 3-block A ring measured no faster at N = 50 (r01_flatpanel_v2.jsonl)
     extern __shared__ __attribute__((aligned(16))) float4 fp_lds[];
     constexpr int W = kFlatPanelWaves;
-    float4* Wc = fp_lds;                    // [n_u][KBc * 64]
-    float4* We = Wc + g.n_u * g.KBc * 64;   // [KBe * 64]
-    float4* Zc = We + g.KBe * 64;           // [n_u][T1 * 64]
-    float4* Zn = Zc + g.n_u * g.T1 * 64;    // [KB3 * 64]
-    FlatPanelSlot* slots = reinterpret_cast<FlatPanelSlot*>(Zn + g.KB3 * 64);
+    const int P = g.P;
+    // per panel pp at fp_lds + pp * PB * 64:  Wc [n_u][KBc] | We [KBe] | Zc [n_u][T1] | Zn [KB3]
+    const int oWe = g.n_u * g.KBc * 64, oZc = oWe + g.KBe * 64, oZn = oZc + g.n_u * g.T1 * 64;
+    const int PBf = g.PB * 64;
+    FlatPanelSlot* slots = reinterpret_cast<FlatPanelSlot*>(fp_lds + P * PBf);  // [P * U2]
+    float4* As = fp_lds + P * PBf + (P * g.U2 * (int)sizeof(FlatPanelSlot)) / 16;  // ALDS: the A image
 
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -208,59 +305,74 @@ __global__ __launch_bounds__(64 * kFlatPanelWaves) void gpad_flatpanel_kernel(So
         __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.frag), 0, g.total * 16, 0x00020000);
     const bool use_tol = a.tol > 0.0;
     const int count = a.batch;
-    const int panels = (count + 15) / 16;
+    const int groups = (count + 16 * P - 1) / (16 * P);
+    const int nu1 = P * g.U1, nu2 = P * g.U2;
+    if constexpr (ALDS) {
+        const float4* src = reinterpret_cast<const float4*>(a.frag);
+        for (int e = threadIdx.x; e < g.total; e += 64 * W) As[e] = src[e];
+    }
     // Zn's rows past n are read by the last k-block of the coupling chains: zero once
-    for (int e = threadIdx.x; e < g.KB3 * 64; e += 64 * W) Zn[e] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    for (int pp = 0; pp < P; ++pp)
+        for (int e = threadIdx.x; e < g.KB3 * 64; e += 64 * W)
+            fp_lds[pp * PBf + oZn + e] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 
-    for (int p = blockIdx.x; p < panels; p += gridDim.x) {
-        const int k = 16 * p + c;
-        bool active = k < count;
-        const size_t bi = (size_t)(active ? k : 0);
-        unsigned live;
-        {
-            const int left = count - 16 * p;
-            live = left >= 16 ? 0xFFFFu : ((1u << left) - 1u);
+    for (int grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+        const int k0 = 16 * P * grp;  // first column of the group; column (pp, c) = k0 + 16 pp + c
+        unsigned long long live = 0ull;
+        for (int pp = 0; pp < P; ++pp) {
+            const int left = count - k0 - 16 * pp;
+            const unsigned msk = left >= 16 ? 0xFFFFu : (left > 0 ? ((1u << left) - 1u) : 0u);
+            live |= (unsigned long long)msk << (16 * pp);
         }
         // ---- this wave's rows: z, g_P (phase 1), y, p_D (phase 2); w (and z_{-1}) into LDS --------
         float z[NU1][4], gp[NU1][4];
         float y[NU2][4], u[NU2][4], pd[NU2][4];
 #pragma unroll
         for (int q = 0; q < NU1; ++q) {
-            const int un = w + W * q, j = un / g.T1, t = un - j * g.T1;
+            const int un = w + W * q;
+            const FpU1 x = fp_u1(g, un < nu1 ? un : 0);
+            const int col = k0 + 16 * x.pp + c;
+            const bool act = un < nu1 && col < count;
+            const size_t bi = (size_t)(act ? col : 0);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int i = 16 * t + 4 * r + jl;
-                const bool ok = un < g.U1 && i < g.Nh && active;
-                z[q][r] = ok ? a.z[bi * n + i * g.n_u + j] : 0.0f;
-                gp[q][r] = ok ? a.gP[bi * a.ld_gP + i * g.n_u + j] : 0.0f;
+                const int i = 16 * x.t + 4 * r + jl;
+                const bool ok = act && i < g.Nh;
+                z[q][r] = ok ? a.z[bi * n + i * g.n_u + x.j] : 0.0f;
+                gp[q][r] = ok ? a.gP[bi * a.ld_gP + i * g.n_u + x.j] : 0.0f;
             }
-            if (un < g.U1 && use_tol) {  // z_{-1} as the B operand of u = G_L z_{-1}
-                Zc[(j * g.T1 + t) * 64 + lane] = make_float4(z[q][0], z[q][1], z[q][2], z[q][3]);
+            if (un < nu1 && use_tol) {  // z_{-1} as the B operand of u = G_L z_{-1}
+                float4* L = fp_lds + x.pp * PBf;
+                L[oZc + (x.j * g.T1 + x.t) * 64 + lane] = make_float4(z[q][0], z[q][1], z[q][2], z[q][3]);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int i = 16 * t + 4 * r + jl, kk = i * g.n_u + j;
+                    const int i = 16 * x.t + 4 * r + jl, kk = i * g.n_u + x.j;
                     if (i < g.Nh)
-                        reinterpret_cast<float*>(&Zn[(kk >> 4) * 64 + (kk & 3) * 16 + c])[(kk >> 2) & 3] = z[q][r];
+                        reinterpret_cast<float*>(&L[oZn + (kk >> 4) * 64 + (kk & 3) * 16 + c])[(kk >> 2) & 3] = z[q][r];
                 }
             }
         }
 #pragma unroll
         for (int q = 0; q < NU2; ++q) {
             const int un = w + W * q;
-            const FpUnit2 x = fp_unit2(g, un);
+            const FpU2 x = fp_u2(g, un < nu2 ? un : 0);
+            const int col = k0 + 16 * x.pp + c;
+            const bool act = un < nu2 && col < count;
+            const size_t bi = (size_t)(act ? col : 0);
             float wv[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int row = un < g.U2 ? fp_row2(g, x, 16 * x.t + 4 * r + jl) : -1;
-                const bool ok = row >= 0 && active;
+                const int row = fp_row2(g, FpUnit2{x.cell, x.t}, 16 * x.t + 4 * r + jl);
+                const bool ok = row >= 0 && act;
                 y[q][r] = ok ? a.y[bi * m + row] : 0.0f;
                 pd[q][r] = ok ? (float)(a.gscale * (double)a.g[bi * a.ld_g + row]) : 0.0f;
                 u[q][r] = 0.0f;
                 wv[r] = __builtin_fmaf(a.beta[0], y[q][r] - y[q][r], y[q][r]);
             }
-            if (un < g.U2) {
-                float4* wp = x.cell < 0 ? We + x.t * 64 + lane : Wc + (x.cell * g.KBc + x.t) * 64 + lane;
-                *wp = make_float4(wv[0], wv[1], wv[2], wv[3]);
+            if (un < nu2) {
+                float4* L = fp_lds + x.pp * PBf;
+                L[(x.cell < 0 ? oWe + x.t * 64 : (x.cell * g.KBc + x.t) * 64) + lane] =
+                    make_float4(wv[0], wv[1], wv[2], wv[3]);
             }
         }
         __syncthreads();
@@ -268,14 +380,15 @@ __global__ __launch_bounds__(64 * kFlatPanelWaves) void gpad_flatpanel_kernel(So
 #pragma unroll
             for (int q = 0; q < NU2; ++q) {
                 const int un = w + W * q;
-                if (un < g.U2) {
-                    const FpUnit2 x = fp_unit2(g, un);
+                if (un < nu2) {
+                    const FpU2 x = fp_u2(g, un);
                     const bool cp = x.cell < 0;
-                    const int voff = (cp ? g.off3 + x.t * 64 : g.off2 + (x.cell * g.T1 * g.KBc + x.t) * 64) * 16 +
-                                     lane * 16;
-                    const ff32x4 cz = fp_gemm(PA, voff, (cp ? g.KBe : g.KBc) * 1024, cp ? g.KB3 : g.T1,
-                                              cp ? g.kq3 : g.kq2, cp ? Zn : Zc + x.cell * g.T1 * 64,
-                                              cp ? g.KB3 : g.T1, Zn, lane);
+                    const float4* L = fp_lds + x.pp * PBf;
+                    const int voff = fp_voff2(g, x, lane), stride = (cp ? g.KBe : g.KBc) * 1024;
+                    const int nkb = cp ? g.KB3 : g.T1;
+                    const ff32x4 cz = fp_chain<ALDS, RING>(PA, As, fp_pre<ALDS>(PA, As, voff, stride, nkb), voff, stride, nkb,
+                                               cp ? g.kq3 : g.kq2, cp ? L + oZn : L + oZc + x.cell * g.T1 * 64,
+                                               nkb, L + oZn, lane);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) u[q][r] = cz[r];
                 }
@@ -283,9 +396,27 @@ __global__ __launch_bounds__(64 * kFlatPanelWaves) void gpad_flatpanel_kernel(So
             __syncthreads();  // the zhat arrays are rewritten by the first iteration
         }
 
+        // first units' A fragments, one barrier ahead
+        FpPre pre1{}, pre2{};
+        if (w < nu1) {
+            const FpU1 x = fp_u1(g, w);
+            pre1 = fp_pre<ALDS>(PA, As, fp_voff1(g, x, lane), g.T1 * 1024, g.KB1);
+        }
         int v = 0;
         float th = a.theta[0], bn = a.beta[1];
+#ifdef FP_TIMING
+        unsigned long long tm[5] = {0, 0, 0, 0, 0}, tlast = __builtin_amdgcn_s_memtime();
+#define FP_T(i)                                                \
+    {                                                          \
+        const unsigned long long tt_ = __builtin_amdgcn_s_memtime(); \
+        tm[(i) - 1] += tt_ - tlast;                             \
+        tlast = tt_;                                           \
+    }
+#else
+#define FP_T(i)
+#endif
         while (true) {
+            FP_T(5);
             const float th_next = a.theta[v + 1], bn_next = a.beta[v + 2];
             ++v;
             const bool chk = use_tol && (v % K) == 0;
@@ -294,46 +425,60 @@ __global__ __launch_bounds__(64 * kFlatPanelWaves) void gpad_flatpanel_kernel(So
 #pragma unroll
             for (int q = 0; q < NU1; ++q) {
                 const int un = w + W * q;
-                if (un < g.U1) {
-                    const int j = un / g.T1, t = un - j * g.T1;
-                    const ff32x4 acc = fp_gemm(PA, (j * g.KB1 * g.T1 + t) * 1024 + lane * 16, g.T1 * 1024, g.KB1,
-                                               g.kq1, Wc + j * g.KBc * 64, g.KBc, We, lane);
+                if (un < nu1) {
+                    const FpU1 x = fp_u1(g, un);
+                    const bool act = (live >> (16 * x.pp + c)) & 1ull;
+                    float4* L = fp_lds + x.pp * PBf;
+                    const int voff = fp_voff1(g, x, lane);
+                    const FpPre f = q == 0 ? pre1 : fp_pre<ALDS>(PA, As, voff, g.T1 * 1024, g.KB1);
+                    const ff32x4 acc = fp_chain<ALDS, RING>(PA, As, f, voff, g.T1 * 1024, g.KB1, g.kq1, L + x.j * g.KBc * 64, g.KBc,
+                                                L + oWe, lane);
                     float zh[4];
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         zh[r] = acc[r] - gp[q][r];  // seq_functions.cpp:18
                         const float zn = __builtin_fmaf(omt, z[q][r], th * zh[r]);
-                        if (active) z[q][r] = zn;
+                        if (act) z[q][r] = zn;
                     }
-                    Zc[(j * g.T1 + t) * 64 + lane] = make_float4(zh[0], zh[1], zh[2], zh[3]);
+                    L[oZc + (x.j * g.T1 + x.t) * 64 + lane] = make_float4(zh[0], zh[1], zh[2], zh[3]);
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const int i = 16 * t + 4 * r + jl, kk = i * g.n_u + j;
+                        const int i = 16 * x.t + 4 * r + jl, kk = i * g.n_u + x.j;
                         if (i < g.Nh)
-                            reinterpret_cast<float*>(&Zn[(kk >> 4) * 64 + (kk & 3) * 16 + c])[(kk >> 2) & 3] = zh[r];
+                            reinterpret_cast<float*>(&L[oZn + (kk >> 4) * 64 + (kk & 3) * 16 + c])[(kk >> 2) & 3] =
+                                zh[r];
                     }
                 }
             }
+            if (w < nu2) {
+                const FpU2 x = fp_u2(g, w);
+                pre2 = fp_pre<ALDS>(PA, As, fp_voff2(g, x, lane), (x.cell < 0 ? g.KBe : g.KBc) * 1024,
+                              x.cell < 0 ? g.KB3 : g.T1);
+            }
+            FP_T(1);
             __syncthreads();
-            // ---- 8d + next 8a: cell and coupling chains; w back to LDS ------------------------------
-            float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY;
-            double gap = 0.0;
+            FP_T(2);
+            // ---- 8d + next 8a: cell and coupling chains; w back to LDS; test partials per unit -------
 #pragma unroll
             for (int q = 0; q < NU2; ++q) {
                 const int un = w + W * q;
-                if (un < g.U2) {
-                    const FpUnit2 x = fp_unit2(g, un);
+                if (un < nu2) {
+                    const FpU2 x = fp_u2(g, un);
+                    const bool act = (live >> (16 * x.pp + c)) & 1ull;
                     const bool cp = x.cell < 0;
-                    const int voff = (cp ? g.off3 + x.t * 64 : g.off2 + (x.cell * g.T1 * g.KBc + x.t) * 64) * 16 +
-                                     lane * 16;
-                    const ff32x4 acc = fp_gemm(PA, voff, (cp ? g.KBe : g.KBc) * 1024, cp ? g.KB3 : g.T1,
-                                               cp ? g.kq3 : g.kq2, cp ? Zn : Zc + x.cell * g.T1 * 64,
-                                               cp ? g.KB3 : g.T1, Zn, lane);
-                    float4* wp = cp ? We + x.t * 64 + lane : Wc + (x.cell * g.KBc + x.t) * 64 + lane;
+                    float4* L = fp_lds + x.pp * PBf;
+                    const int voff = fp_voff2(g, x, lane), stride = (cp ? g.KBe : g.KBc) * 1024;
+                    const int nkb = cp ? g.KB3 : g.T1;
+                    const FpPre f = q == 0 ? pre2 : fp_pre<ALDS>(PA, As, voff, stride, nkb);
+                    const ff32x4 acc = fp_chain<ALDS, RING>(PA, As, f, voff, stride, nkb, cp ? g.kq3 : g.kq2,
+                                                cp ? L + oZn : L + oZc + x.cell * g.T1 * 64, nkb, L + oZn, lane);
+                    float4* wp = L + (cp ? oWe + x.t * 64 : (x.cell * g.KBc + x.t) * 64) + lane;
                     const float4 w4 = *wp;
                     const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
                     const int lim = cp ? g.E : 4 * g.Nh;
                     float wn[4];
+                    float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY;
+                    double gap = 0.0;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const float cv = acc[r], wi = wv[r], pdi = pd[q][r];
@@ -341,8 +486,8 @@ __global__ __launch_bounds__(64 * kFlatPanelWaves) void gpad_flatpanel_kernel(So
                         const float yp = sv < 0.0f ? 0.0f : sv;  // seq_functions.cpp:40-42
                         if (use_tol) {
                             const float un2 = __builtin_fmaf(omt, u[q][r], th * cv);
-                            if (active) u[q][r] = un2;
-                            if (chk && active && 16 * x.t + 4 * r + jl < lim) {
+                            if (act) u[q][r] = un2;
+                            if (chk && act && 16 * x.t + 4 * r + jl < lim) {
                                 const float tt = cv + pdi;
                                 violh = fmaxf(violh, tt);
                                 wmin = fminf(wmin, wi);
@@ -351,97 +496,121 @@ __global__ __launch_bounds__(64 * kFlatPanelWaves) void gpad_flatpanel_kernel(So
                             }
                         }
                         wn[r] = __builtin_fmaf(bn, yp - y[q][r], yp);
-                        if (active) y[q][r] = yp;
+                        if (act) y[q][r] = yp;
                     }
-                    if (active) *wp = make_float4(wn[0], wn[1], wn[2], wn[3]);
+                    if (act) *wp = make_float4(wn[0], wn[1], wn[2], wn[3]);
+                    if (chk) {  // this unit's partials per column -> its slot
+#pragma unroll
+                        for (int o = 16; o < 64; o <<= 1) {
+                            violz = fmaxf(violz, __shfl_xor(violz, o, 64));
+                            violh = fmaxf(violh, __shfl_xor(violh, o, 64));
+                            wmin = fminf(wmin, __shfl_xor(wmin, o, 64));
+                            gap += __shfl_xor(gap, o, 64);
+                        }
+                        if (jl == 0) {
+                            slots[un].violz[c] = violz;
+                            slots[un].violh[c] = violh;
+                            slots[un].wmin[c] = wmin;
+                            slots[un].gap[c] = gap;
+                        }
+                    }
                 }
             }
-            if (chk) {
-#pragma unroll
-                for (int o = 16; o < 64; o <<= 1) {
-                    violz = fmaxf(violz, __shfl_xor(violz, o, 64));
-                    violh = fmaxf(violh, __shfl_xor(violh, o, 64));
-                    wmin = fminf(wmin, __shfl_xor(wmin, o, 64));
-                    gap += __shfl_xor(gap, o, 64);
-                }
-                if (jl == 0) {
-                    slots[w].violz[c] = violz;
-                    slots[w].violh[c] = violh;
-                    slots[w].wmin[c] = wmin;
-                    slots[w].gap[c] = gap;
-                }
+            if (w < nu1) {
+                const FpU1 x = fp_u1(g, w);
+                pre1 = fp_pre<ALDS>(PA, As, fp_voff1(g, x, lane), g.T1 * 1024, g.KB1);
             }
             th = th_next;
             bn = bn_next;
+            FP_T(3);
             __syncthreads();
+            FP_T(4);
             if (!chk && v < N) continue;
 
-            unsigned m1 = 0u, m2 = 0u;
-            if (chk) {
+            unsigned long long m1 = 0ull, m2 = 0ull;
+            if (chk) {  // lane = (panel lane >> 4, column lane & 15): reduce that panel's unit slots
                 int cd = 0;
-                if (lane < 16 && ((live >> lane) & 1u)) {
+                const int pp = lane >> 4;
+                if (pp < P && ((live >> lane) & 1ull)) {
                     double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gq = 0.0;
-#pragma unroll
-                    for (int s2 = 0; s2 < W; ++s2) {
-                        vz = fmax(vz, (double)slots[s2].violz[lane]);
-                        vh = fmax(vh, (double)slots[s2].violh[lane]);
-                        wm = fmin(wm, (double)slots[s2].wmin[lane]);
-                        gq += slots[s2].gap[lane];
+                    for (int s2 = pp * g.U2; s2 < (pp + 1) * g.U2; ++s2) {
+                        vz = fmax(vz, (double)slots[s2].violz[c]);
+                        vh = fmax(vh, (double)slots[s2].violh[c]);
+                        wm = fmin(wm, (double)slots[s2].wmin[c]);
+                        gq += slots[s2].gap[c];
                     }
                     if (vz * a.L <= a.tol) cd = 1;
                     else if ((vh * a.L <= a.tol) && (wm >= 0.0) && (gq * a.L <= a.tol)) cd = 2;
                 }
-                m1 = (unsigned)__ballot(cd == 1);
-                m2 = (unsigned)__ballot(cd == 2);
+                m1 = __ballot(cd == 1);
+                m2 = __ballot(cd == 2);
             }
-            const int cdc = ((m1 >> c) & 1u) ? 1 : (((m2 >> c) & 1u) ? 2 : 0);
-            if (active && (cdc != 0 || v >= N)) {  // finished column: results out
+            const unsigned long long fin = v >= N ? live : (live & (m1 | m2));
+            if (fin) {  // finished columns: results out
 #pragma unroll
                 for (int q = 0; q < NU1; ++q) {
-                    const int un = w + W * q, j = un / g.T1, t = un - j * g.T1;
-                    if (un < g.U1) {
-                        const float4 zh4 = Zc[(j * g.T1 + t) * 64 + lane];  // test (B) returns zhat
-                        const float zhv[4] = {zh4.x, zh4.y, zh4.z, zh4.w};
+                    const int un = w + W * q;
+                    if (un < nu1) {
+                        const FpU1 x = fp_u1(g, un);
+                        const int bit = 16 * x.pp + c;
+                        if ((fin >> bit) & 1ull) {
+                            const size_t bi = (size_t)(k0 + bit);
+                            const float4 zh4 = fp_lds[x.pp * PBf + oZc + (x.j * g.T1 + x.t) * 64 + lane];
+                            const float zhv[4] = {zh4.x, zh4.y, zh4.z, zh4.w};
+                            const bool tb = (m2 >> bit) & 1ull && !((m1 >> bit) & 1ull);  // test (B): zhat
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const int i = 16 * t + 4 * r + jl;
-                            if (i < g.Nh) a.z[bi * n + i * g.n_u + j] = cdc == 2 ? zhv[r] : z[q][r];
+                            for (int r = 0; r < 4; ++r) {
+                                const int i = 16 * x.t + 4 * r + jl;
+                                if (i < g.Nh) a.z[bi * n + i * g.n_u + x.j] = tb ? zhv[r] : z[q][r];
+                            }
                         }
                     }
                 }
 #pragma unroll
                 for (int q = 0; q < NU2; ++q) {
                     const int un = w + W * q;
-                    const FpUnit2 x = fp_unit2(g, un);
+                    if (un < nu2) {
+                        const FpU2 x = fp_u2(g, un);
+                        const int bit = 16 * x.pp + c;
+                        if ((fin >> bit) & 1ull) {
+                            const size_t bi = (size_t)(k0 + bit);
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int row = un < g.U2 ? fp_row2(g, x, 16 * x.t + 4 * r + jl) : -1;
-                        if (row >= 0) a.y[bi * m + row] = y[q][r];
+                            for (int r = 0; r < 4; ++r) {
+                                const int row = fp_row2(g, FpUnit2{x.cell, x.t}, 16 * x.t + 4 * r + jl);
+                                if (row >= 0) a.y[bi * m + row] = y[q][r];
+                            }
+                        }
                     }
                 }
-                if (w == 0 && jl == 0) {
-                    a.iters[k] = v;
-                    a.conv[k] = cdc;
+                if (w == 0 && ((fin >> lane) & 1ull)) {
+                    a.iters[k0 + lane] = v;
+                    a.conv[k0 + lane] = (m1 >> lane) & 1ull ? 1 : ((m2 >> lane) & 1ull ? 2 : 0);
                 }
-                active = false;
             }
-            live &= ~(m1 | m2);
-            if (v >= N) live = 0u;
-            if (live == 0u) break;
+            live &= ~fin;
+            if (live == 0ull) break;
         }
-        __syncthreads();  // the next panel reuses the LDS arrays
+        __syncthreads();  // the next group reuses the LDS arrays
+#ifdef FP_TIMING
+        if (blockIdx.x == 0 && lane == 0 && grp == 0) printf("fpt w%d v%d p1 %llu b1 %llu p2 %llu b2 %llu chk %llu\n", w, v, tm[0], tm[1], tm[2], tm[3], tm[4]);
+#endif
     }
 }
 
-template <int NU1, int NU2>
-static hipError_t launch_fp_nt(const SolveArgs<float>& a, const FlatGeom& g, size_t lds, int grid, hipStream_t s) {
+template <int NU1, int NU2, bool ALDS>
+static hipError_t launch_fp_k(const SolveArgs<float>& a, const FlatGeom& g, size_t lds, int grid, hipStream_t s) {
     if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)gpad_flatpanel_kernel<NU1, NU2>,
+        hipError_t e = hipFuncSetAttribute((const void*)gpad_flatpanel_kernel<NU1, NU2, ALDS>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((gpad_flatpanel_kernel<NU1, NU2>), dim3(grid), dim3(64 * kFlatPanelWaves), lds, s, a, g);
+    hipLaunchKernelGGL((gpad_flatpanel_kernel<NU1, NU2, ALDS>), dim3(grid), dim3(64 * kFlatPanelWaves), lds, s, a, g);
     return hipGetLastError();
+}
+template <int NU1, int NU2>
+static hipError_t launch_fp_nt(const SolveArgs<float>& a, const FlatGeom& g, size_t lds, bool alds, int grid,
+                               hipStream_t s) {
+    return alds ? launch_fp_k<NU1, NU2, true>(a, g, lds, grid, s) : launch_fp_k<NU1, NU2, false>(a, g, lds, grid, s);
 }
 
 static int fp_nt(int units) {
@@ -449,22 +618,49 @@ static int fp_nt(int units) {
     return q <= 1 ? 1 : (q <= 2 ? 2 : 4);
 }
 
-// whole-batch solve (one launch, no phased compaction); a.frag = the flat fragment images
+// whole-batch solve (one launch, no phased compaction); a.frag = the flat fragment images.
+// P panels per workgroup: as many as keep every CU busy (groups >= CUs), the phase-1 units within
+// one per wave and the phase-2 units within 4 per wave, and the LDS within 160 KiB.
 hipError_t launch_flatpanel(const SolveArgs<float>& a, hipStream_t s) {
     if (!flatpanel_supported(a.n, a.m, a.n_u) || !a.frag) return hipErrorInvalidValue;
-    const FlatGeom g = flat_geom(a.n, a.m, a.n_u);
-    const size_t lds = flatpanel_lds_bytes(g);
+    FlatGeom g = flat_geom(a.n, a.m, a.n_u);
     const int panels = (a.batch + 15) / 16;
+    int P = 1;
+    for (int q = 4; q > 1; --q) {
+        if (q * g.U1 <= kFlatPanelWaves && q * g.U2 <= 4 * kFlatPanelWaves &&
+            flatpanel_lds_bytes(g, q) <= 160 * 1024 && (panels + q - 1) / q >= a.num_cus) {
+            P = q;
+            break;
+        }
+    }
+    if (const char* e = std::getenv("GPAD_FLAT_PANELS")) P = std::max(1, std::min(4, std::atoi(e)));  // A/B knob
+    while (P > 1 && (P * g.U1 > 4 * kFlatPanelWaves || P * g.U2 > 4 * kFlatPanelWaves ||
+                     flatpanel_lds_bytes(g, P) > 160 * 1024))
+        --P;
+    g.P = P;
+    for (int un = 0; un < 4 * kFlatPanelWavesMax; ++un) {
+        const int pp = un / g.U1, uu = un % g.U1;
+        g.d1[un] = un < P * g.U1 ? (pp << 16) | ((uu / g.T1 + 1) << 8) | (uu % g.T1) : 0;
+        const int qq = un / g.U2, vv = un % g.U2;
+        const int cell = vv < g.KBe ? -1 : (vv - g.KBe) / g.KBc;
+        const int t = vv < g.KBe ? vv : (vv - g.KBe) % g.KBc;
+        g.d2[un] = un < P * g.U2 ? (qq << 16) | ((cell + 1) << 8) | t : 0;
+    }
+    size_t lds = flatpanel_lds_bytes(g, P);
+    const size_t abytes = (size_t)g.total * 16;
+    const bool alds = lds + abytes <= 160 * 1024 && !std::getenv("GPAD_FLAT_NO_ALDS");  // A image in LDS
+    if (alds) lds += abytes;
+    const int groups = (panels + P - 1) / P;
     int grid = a.num_cus * (lds * 2 <= 160 * 1024 ? 2 : 1);
-    if (grid > panels) grid = panels;
-    const int q1 = fp_nt(g.U1), q2 = fp_nt(g.U2);
+    if (grid > groups) grid = groups;
+    const int q1 = fp_nt(P * g.U1), q2 = fp_nt(P * g.U2);
 #define FP_CASE(A, B) \
-    case A * 8 + B: return launch_fp_nt<A, B>(a, g, lds, grid, s);
+    case A * 8 + B: return launch_fp_nt<A, B>(a, g, lds, alds, grid, s);
     switch (q1 * 8 + q2) {
         FP_CASE(1, 1) FP_CASE(1, 2) FP_CASE(1, 4)
         FP_CASE(2, 1) FP_CASE(2, 2) FP_CASE(2, 4)
         FP_CASE(4, 1) FP_CASE(4, 2)
-        default: return launch_fp_nt<4, 4>(a, g, lds, grid, s);
+        default: return launch_fp_nt<4, 4>(a, g, lds, alds, grid, s);
     }
 #undef FP_CASE
 }
