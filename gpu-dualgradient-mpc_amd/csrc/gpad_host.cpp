@@ -685,6 +685,70 @@ PlantOffsets plant_offsets(int n, int m, int nx, int nu) {
 }
 }  // namespace
 
+extern "C" int gpad_precompute(gpad_handle_t h, int n, int m, int batch, int shared, int memory, const double* H,
+                               const double* A, const double* f, double* ML, double* gP, double* L) {
+    if (!h) return fail(GPAD_ERR_INVALID, "gpad_precompute: null handle");
+    if (n <= 0 || m < 0 || batch <= 0 || !H || !A || !ML || !L || (f == nullptr) != (gP == nullptr) ||
+        (memory != GPAD_MEM_HOST && memory != GPAD_MEM_DEVICE))
+        return fail(GPAD_ERR_INVALID, "gpad_precompute: bad arguments");
+    HIP_TRY(hipSetDevice(h->device));
+    const bool host = memory == GPAD_MEM_HOST;
+    const int nmat = shared ? 1 : batch;  // eliminations
+    const size_t nH = (size_t)nmat * n * n, nA = (size_t)nmat * m * n, nML = (size_t)nmat * n * m;
+    const size_t nF = f ? (size_t)batch * n : 0;
+    // shared: one elimination of [H | A' | I] gives ML and inv(H); gP = inv(H) f' per row after
+    const int fchunk = shared ? (f ? n : 0) : (f ? 1 : 0);
+    if (!gpad::precompute_supported(n, m, fchunk))
+        return fail(GPAD_ERR_UNSUPPORTED, "gpad_precompute: 2n + m too large for the LDS pivot row");
+    // device views of the operands (host memory: staged copies)
+    DevBuf stage, work;
+    const double *dH = H, *dA = A, *df = f;
+    double *dML = ML, *dgP = gP, *dL = L;
+    const size_t tot = nH + nA + nF + nML + nF + nmat;
+    int rc;
+    if (host) {
+        if ((rc = stage.ensure(sizeof(double) * tot))) return rc;
+        double* b = (double*)stage.p;
+        double* sH = b;
+        double* sA = sH + nH;
+        double* sf = sA + nA;
+        dML = sf + nF;
+        dgP = f ? dML + nML : nullptr;
+        dL = dML + nML + nF;
+        HIP_TRY(hipMemcpyAsync(sH, H, sizeof(double) * nH, hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(hipMemcpyAsync(sA, A, sizeof(double) * nA, hipMemcpyHostToDevice, h->stream));
+        if (f) HIP_TRY(hipMemcpyAsync(sf, f, sizeof(double) * nF, hipMemcpyHostToDevice, h->stream));
+        dH = sH;
+        dA = sA;
+        df = f ? sf : nullptr;
+    }
+    if (shared) {
+        const size_t wb = gpad::precompute_work_bytes(n, m, fchunk, 1);
+        if ((rc = work.ensure(wb + (f ? sizeof(double) * (size_t)n * n : 0)))) return rc;
+        double* Hinv = f ? (double*)((char*)work.p + wb) : nullptr;
+        HIP_TRY(gpad::launch_precompute(n, m, fchunk, dH, 0, dA, 0, nullptr, 0, (double*)work.p, dML, Hinv, dL, 0, 1,
+                                        h->stream));
+        if (f) HIP_TRY(gpad::launch_apply_inv(n, batch, Hinv, df, dgP, h->stream));
+    } else {
+        const size_t per = gpad::precompute_work_bytes(n, m, fchunk, 1);
+        int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)batch, ((size_t)1 << 30) / per));
+        chunk = std::min(chunk, 4 * h->num_cus);
+        if ((rc = work.ensure(per * chunk))) return rc;
+        for (int b0 = 0; b0 < batch; b0 += chunk) {
+            const int cnt = std::min(chunk, batch - b0);
+            HIP_TRY(gpad::launch_precompute(n, m, fchunk, dH, (long long)n * n, dA, (long long)m * n, df, n,
+                                            (double*)work.p, dML, dgP, dL, b0, cnt, h->stream));
+        }
+    }
+    if (host) {
+        HIP_TRY(hipMemcpyAsync(ML, dML, sizeof(double) * nML, hipMemcpyDeviceToHost, h->stream));
+        if (f) HIP_TRY(hipMemcpyAsync(gP, dgP, sizeof(double) * nF, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipMemcpyAsync(L, dL, sizeof(double) * nmat, hipMemcpyDeviceToHost, h->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return GPAD_OK;
+}
+
 extern "C" int gpad_setup_plant(gpad_handle_t h, int nx, int nu, const void* PM, const void* M0,
                                 const void* Pg, const void* g0, const void* A, const void* B) {
     if (!h) return fail(GPAD_ERR_INVALID, "gpad_setup_plant: null handle");

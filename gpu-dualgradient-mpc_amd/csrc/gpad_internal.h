@@ -111,6 +111,13 @@ hipError_t launch_flat(const SolveArgs<float>& a, hipStream_t s);
 // flat G_L expanded to the full k-major image [n][ldm]
 bool flat_resident_supported(int n, int m, int n_u);
 hipError_t launch_flat_resident(const SolveArgs<float>& a, hipStream_t s);
+// one-time QP precompute (gpad_precompute.hip): Gauss-Jordan on [H | A' | f'] per instance
+size_t precompute_work_bytes(int n, int m, int nf, int count);
+bool precompute_supported(int n, int m, int nf);
+hipError_t launch_precompute(int n, int m, int nf, const double* H, long long sH, const double* A, long long sA,
+                             const double* f, long long sF, double* work, double* ML, double* gP, double* L, int b0,
+                             int count, hipStream_t s);
+hipError_t launch_apply_inv(int n, int batch, const double* Hinv, const double* f, double* gP, hipStream_t s);
 // flat battery data on the MFMA pipe (gpad_flatpanel.hip): per-cell skinny GEMMs over panels
 bool flatpanel_supported(int n, int m, int n_u);
 size_t flatpanel_frag_bytes(int n, int m, int n_u);

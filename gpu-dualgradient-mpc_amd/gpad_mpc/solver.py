@@ -179,6 +179,38 @@ class GpadSolver:
         check(self.lib.gpad_sync(self.h), "gpad_sync")
 
     # ---- per-state QP data / closed loop (gpad.m:79-95; include/gpad.h gpad_setup_plant) ---
+    def precompute(self, H, A, f=None, *, shared: bool = True):
+        """acceldualgrad.m:11,20-21 on the device in fp64 (gpad_precompute): returns
+        (ML = inv(H) A', gP = inv(H) f' or None, L = ||H||_F^2).  shared: one H (n x n), A (m x n)
+        and f [batch][n]; else H [batch][n][n], A [batch][m][n], f [batch][n].  numpy in ->
+        numpy out; torch (device, float64) in -> torch out."""
+        dev = _is_torch(H)
+        n = H.shape[-1]
+        m = A.shape[-2]
+        batch = (f.shape[0] if f is not None and f.ndim == 2 else 1) if shared else H.shape[0]
+        nmat = 1 if shared else batch
+        if dev:
+            import torch
+            H = H.to(torch.float64).contiguous()
+            A = A.to(torch.float64).contiguous()
+            f = None if f is None else f.to(torch.float64).contiguous()
+            ML = torch.empty((nmat, n, m) if not shared else (n, m), dtype=torch.float64, device=H.device)
+            gP = None if f is None else torch.empty_like(f)
+            L = torch.empty(nmat, dtype=torch.float64, device=H.device)
+            mem = _lib.MEM_DEVICE
+        else:
+            H = np.ascontiguousarray(H, np.float64)
+            A = np.ascontiguousarray(A, np.float64)
+            f = None if f is None else np.ascontiguousarray(f, np.float64)
+            ML = np.empty((nmat, n, m) if not shared else (n, m))
+            gP = None if f is None else np.empty_like(f)
+            L = np.empty(nmat)
+            mem = _lib.MEM_HOST
+        opt = lambda a: _ptr(a) if a is not None else None  # noqa: E731
+        check(self.lib.gpad_precompute(self.h, n, m, batch, 1 if shared else 0, mem, _ptr(H), _ptr(A), opt(f),
+                                       _ptr(ML), opt(gP), _ptr(L)), "gpad_precompute")
+        return ML, gP, (float(L[0]) if shared else L)
+
     def setup_plant(self, PM, Pg, *, M0=None, g0=None, A=None, B=None) -> None:
         """Bind M(x) = M0 + PM x, g(x) = g0 + Pg x and (optionally) x+ = A x + B u.
         Same dtype / memory kind as the preceding ``setup``."""

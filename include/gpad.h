@@ -126,6 +126,19 @@ int gpad_run(gpad_handle_t h, void* z0, void* y0, const void* M, const void* g, 
 int gpad_run_scaled(gpad_handle_t h, void* z0, void* y0, const void* gP, const void* pD, int N,
                     double tol, const void* theta, const void* beta, gpad_stats_t* st);
 
+/* ---- one-time QP precompute on the device ---------------------------
+ * acceldualgrad.m:11,20-21 in fp64:  L = ||H||_F^2,  ML = inv(H) A' (n x m),  gP = inv(H) f' (n).
+ * Replaces the MATLAB-side precompute (and the off-line data-file generator) that the reference
+ * runs before main.cu:29-67 reads M_G, g_P.  shared = 1: one H (n x n) and one A (m x n) for the
+ * whole batch (LTI) -> one ML, one L, and gP for each of the batch rows of f; shared = 0: H
+ * [batch][n][n], A [batch][m][n] -> ML [batch][n][m], L [batch], gP [batch][n].  f (and gP) may
+ * be NULL.  One workgroup per elimination of [H | A' | f'] (shared: [H | A' | I], then
+ * gP = inv(H) f' row by row); H must be symmetric positive definite (no pivoting).  memory =
+ * GPAD_MEM_HOST or GPAD_MEM_DEVICE for every pointer (device: on the handle's stream).
+ * Synchronous.  The outputs feed gpad_setup (ML, A as G, L) and gpad_run (gP as M). */
+int gpad_precompute(gpad_handle_t h, int n, int m, int batch, int shared, int memory, const double* H,
+                    const double* A, const double* f, double* ML, double* gP, double* L);
+
 /* ---- per-state QP data and closed-loop MPC -------------------
  * For an LTI plant the state-dependent QP data are affine in the state x (nx):
  *   M(x) = M0 + PM x   (n;  PM = H^-1 F': the reference forms f = x0'F, gpad.m:81, and
