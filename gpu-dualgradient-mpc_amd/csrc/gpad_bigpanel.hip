@@ -87,27 +87,56 @@ __device__ __forceinline__ float4 bas_float4(__attribute__((ext_vector_type(4)))
 }
 
 // acc = sum over k-blocks b < nkb (the last one only its kq 4-steps) of A[b][t] x B[b]:
-// A by buffer loads (byte offset (b * Tr + t) KiB + lane 16 B), two k-blocks in flight; B from LDS.
+// A by buffer loads (byte offset (b * Tr + t) KiB + lane 16 B) two k-blocks ahead, B from LDS
+// one block ahead.  Unrolled by two with fixed register roles and unconditional (clamped) loads
+// so that each block waits only for its own operands (see panel_gemm_rt in gpad_panel.hip).
+__device__ __forceinline__ void big_blk(bf32x4& acc, const float4& a, const float4& b, int steps) {
+    __builtin_amdgcn_sched_barrier(0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc, 0, 0, 0);
+    if (steps > 1) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc, 0, 0, 0);
+    if (steps > 2) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc, 0, 0, 0);
+    if (steps > 3) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+}
+__device__ __forceinline__ void big_blk2(bf32x4& acc0, bf32x4& acc1, const float4& a, const float4& c,
+                                         const float4& b, int steps) {
+    __builtin_amdgcn_sched_barrier(0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(c.x, b.x, acc1, 0, 0, 0);
+    if (steps > 1) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(c.y, b.y, acc1, 0, 0, 0);
+    }
+    if (steps > 2) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(c.z, b.z, acc1, 0, 0, 0);
+    }
+    if (steps > 3) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(c.w, b.w, acc1, 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 __device__ __forceinline__ bf32x4 big_gemm(__amdgpu_buffer_rsrc_t PA, const float4* B, int t, int Tr, int nkb,
                                            int kq, int lane) {
     bf32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-    const int voff = t * 1024 + lane * 16, stride = Tr * 1024;
-    float4 a0 = bas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, 0, 0));
-    float4 a1 = nkb > 1 ? bas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, stride, 0)) : a0;
-    float4 b0 = B[lane];
-    for (int kb = 0; kb < nkb; ++kb) {
-        const float4 ak = a0, bk = b0;
-        a0 = a1;
-        if (kb + 2 < nkb) a1 = bas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb + 2) * stride, 0));
-        if (kb + 1 < nkb) b0 = B[(kb + 1) * 64 + lane];
-        const int steps = kb + 1 < nkb ? 4 : kq;
-        __builtin_amdgcn_sched_barrier(0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, bk.x, acc, 0, 0, 0);
-        if (steps > 1) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, bk.y, acc, 0, 0, 0);
-        if (steps > 2) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, bk.z, acc, 0, 0, 0);
-        if (steps > 3) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, bk.w, acc, 0, 0, 0);
-        asm volatile("" : "+v"(acc)::"memory");
+    const int voff = t * 1024 + lane * 16, stride = Tr * 1024, last = nkb - 1;
+    auto lda = [&](int kb) -> float4 {
+        return bas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb < last ? kb : last) * stride, 0));
+    };
+    float4 a0 = lda(0), a1 = lda(1), b0 = B[lane], b1;
+    for (int kb = 0;; kb += 2) {
+        b1 = B[(kb + 1 < last ? kb + 1 : last) * 64 + lane];
+        big_blk(acc, a0, b0, kb < last ? 4 : kq);
+        a0 = lda(kb + 2);
+        if (kb + 1 > last) break;
+        b0 = B[(kb + 2 < last ? kb + 2 : last) * 64 + lane];
+        big_blk(acc, a1, b1, kb + 1 < last ? 4 : kq);
+        a1 = lda(kb + 3);
+        if (kb + 2 > last) break;
     }
+    asm volatile("" : "+v"(acc)::"memory");
     return acc;
 }
 
@@ -117,42 +146,24 @@ __device__ __forceinline__ void big_gemm2(__amdgpu_buffer_rsrc_t PA, const float
                                           int nkb, int kq, int lane, bf32x4& acc0, bf32x4& acc1) {
     acc0 = bf32x4{0.0f, 0.0f, 0.0f, 0.0f};
     acc1 = bf32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    const int v0 = t0 * 1024 + lane * 16, v1 = t1 * 1024 + lane * 16, stride = Tr * 1024;
-    float4 a0 = bas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, v0, 0, 0));
-    float4 c0 = bas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, v1, 0, 0));
-    float4 a1 = a0, c1 = c0;
-    if (nkb > 1) {
-        a1 = bas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, v0, stride, 0));
-        c1 = bas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, v1, stride, 0));
+    const int v0 = t0 * 1024 + lane * 16, v1 = t1 * 1024 + lane * 16, stride = Tr * 1024, last = nkb - 1;
+    auto lda = [&](int voff, int kb) -> float4 {
+        return bas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb < last ? kb : last) * stride, 0));
+    };
+    float4 a0 = lda(v0, 0), c0 = lda(v1, 0), a1 = lda(v0, 1), c1 = lda(v1, 1), b0 = B[lane], b1;
+    for (int kb = 0;; kb += 2) {
+        b1 = B[(kb + 1 < last ? kb + 1 : last) * 64 + lane];
+        big_blk2(acc0, acc1, a0, c0, b0, kb < last ? 4 : kq);
+        a0 = lda(v0, kb + 2);
+        c0 = lda(v1, kb + 2);
+        if (kb + 1 > last) break;
+        b0 = B[(kb + 2 < last ? kb + 2 : last) * 64 + lane];
+        big_blk2(acc0, acc1, a1, c1, b1, kb + 1 < last ? 4 : kq);
+        a1 = lda(v0, kb + 3);
+        c1 = lda(v1, kb + 3);
+        if (kb + 2 > last) break;
     }
-    float4 b0 = B[lane];
-    for (int kb = 0; kb < nkb; ++kb) {
-        const float4 ak = a0, ck = c0, bk = b0;
-        a0 = a1;
-        c0 = c1;
-        if (kb + 2 < nkb) {
-            a1 = bas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, v0, (kb + 2) * stride, 0));
-            c1 = bas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, v1, (kb + 2) * stride, 0));
-        }
-        if (kb + 1 < nkb) b0 = B[(kb + 1) * 64 + lane];
-        const int steps = kb + 1 < nkb ? 4 : kq;
-        __builtin_amdgcn_sched_barrier(0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, bk.x, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ck.x, bk.x, acc1, 0, 0, 0);
-        if (steps > 1) {
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, bk.y, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ck.y, bk.y, acc1, 0, 0, 0);
-        }
-        if (steps > 2) {
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, bk.z, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ck.z, bk.z, acc1, 0, 0, 0);
-        }
-        if (steps > 3) {
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, bk.w, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ck.w, bk.w, acc1, 0, 0, 0);
-        }
-        asm volatile("" : "+v"(acc0), "+v"(acc1)::"memory");
-    }
+    asm volatile("" : "+v"(acc0), "+v"(acc1)::"memory");
 }
 
 template <int NT1, int NT2>

@@ -220,32 +220,46 @@ __device__ __forceinline__ FpPre fp_pre(__amdgpu_buffer_rsrc_t PA, const float4*
     f.a1 = nkb > 1 ? fp_lda<ALDS>(PA, As, voff, stride) : f.a0;
     return f;
 }
-// one unit's chain over nkb k-blocks (the last only its kq 4-steps); A blocks RING ahead (the
-// first two prefetched by fp_pre), B block b from Ba (b < kbs) or Bb (b >= kbs)
-template <bool ALDS, int RING>
+// one unit's chain over nkb k-blocks (the last only its kq 4-steps): A two blocks ahead (the
+// first two prefetched by fp_pre), B one block ahead, block b of B from Ba (b < kbs) or Bb.
+// Unrolled by two with fixed register roles and every load unconditional (indices clamped to
+// the last block): the waitcnt for a block's operands then counts only the loads issued after
+// them, instead of draining the queue at every conditional load or register rotation.
+template <bool ALDS>
 __device__ __forceinline__ ff32x4 fp_chain(__amdgpu_buffer_rsrc_t PA, const float4* As, FpPre f, int voff, int stride,
                                            int nkb, int kq, const float4* Ba, int kbs, const float4* Bb, int lane) {
     ff32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-    float4 ar[RING];
-    ar[0] = f.a0;
-    ar[1] = f.a1;
-#pragma unroll
-    for (int i = 2; i < RING; ++i) ar[i] = i < nkb ? fp_lda<ALDS>(PA, As, voff, i * stride) : f.a0;
-    float4 b0 = kbs > 0 ? Ba[lane] : Bb[lane];
-    for (int kb = 0; kb < nkb; ++kb) {
-        const float4 ak = ar[0], bk = b0;
-#pragma unroll
-        for (int i = 0; i + 1 < RING; ++i) ar[i] = ar[i + 1];
-        if (kb + RING < nkb) ar[RING - 1] = fp_lda<ALDS>(PA, As, voff, (kb + RING) * stride);
-        if (kb + 1 < nkb) b0 = kb + 1 < kbs ? Ba[(kb + 1) * 64 + lane] : Bb[(kb + 1 - kbs) * 64 + lane];
-        const int steps = kb + 1 < nkb ? 4 : kq;
-        __builtin_amdgcn_sched_barrier(0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, bk.x, acc, 0, 0, 0);
-        if (steps > 1) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, bk.y, acc, 0, 0, 0);
-        if (steps > 2) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, bk.z, acc, 0, 0, 0);
-        if (steps > 3) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, bk.w, acc, 0, 0, 0);
-        asm volatile("" : "+v"(acc)::"memory");
+    const int last = nkb - 1;
+    auto ldb = [&](int kb) -> float4 { return kb < kbs ? Ba[kb * 64 + lane] : Bb[(kb - kbs) * 64 + lane]; };
+    float4 a0 = f.a0, a1 = f.a1;
+    float4 b0 = ldb(0), b1;
+    for (int kb = 0;; kb += 2) {
+        b1 = ldb(kb + 1 < last ? kb + 1 : last);
+        {
+            const int steps = kb < last ? 4 : kq;
+            __builtin_amdgcn_sched_barrier(0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, b0.x, acc, 0, 0, 0);
+            if (steps > 1) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, b0.y, acc, 0, 0, 0);
+            if (steps > 2) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, b0.z, acc, 0, 0, 0);
+            if (steps > 3) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, b0.w, acc, 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        a0 = fp_lda<ALDS>(PA, As, voff, (kb + 2 < last ? kb + 2 : last) * stride);
+        if (kb + 1 > last) break;
+        b0 = ldb(kb + 2 < last ? kb + 2 : last);
+        {
+            const int steps = kb + 1 < last ? 4 : kq;
+            __builtin_amdgcn_sched_barrier(0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, b1.x, acc, 0, 0, 0);
+            if (steps > 1) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, b1.y, acc, 0, 0, 0);
+            if (steps > 2) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, b1.z, acc, 0, 0, 0);
+            if (steps > 3) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, b1.w, acc, 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        a1 = fp_lda<ALDS>(PA, As, voff, (kb + 3 < last ? kb + 3 : last) * stride);
+        if (kb + 2 > last) break;
     }
+    asm volatile("" : "+v"(acc)::"memory");
     return acc;
 }
 
@@ -287,7 +301,6 @@ __device__ __forceinline__ int fp_voff2(const FlatGeom& g, FpU2 x, int lane) {
 
 template <int NU1, int NU2, bool ALDS>
 __global__ __launch_bounds__(64 * kFlatPanelWaves) void gpad_flatpanel_kernel(SolveArgs<float> a, FlatGeom g) {
-    constexpr int RING = 2;  // a 3-block A ring measured no faster at N = 50 (r01_flatpanel_v2.jsonl)
     extern __shared__ __attribute__((aligned(16))) float4 fp_lds[];
     constexpr int W = kFlatPanelWaves;
     const int P = g.P;
@@ -386,7 +399,7 @@ __global__ __launch_bounds__(64 * kFlatPanelWaves) void gpad_flatpanel_kernel(So
                     const float4* L = fp_lds + x.pp * PBf;
                     const int voff = fp_voff2(g, x, lane), stride = (cp ? g.KBe : g.KBc) * 1024;
                     const int nkb = cp ? g.KB3 : g.T1;
-                    const ff32x4 cz = fp_chain<ALDS, RING>(PA, As, fp_pre<ALDS>(PA, As, voff, stride, nkb), voff, stride, nkb,
+                    const ff32x4 cz = fp_chain<ALDS>(PA, As, fp_pre<ALDS>(PA, As, voff, stride, nkb), voff, stride, nkb,
                                                cp ? g.kq3 : g.kq2, cp ? L + oZn : L + oZc + x.cell * g.T1 * 64,
                                                nkb, L + oZn, lane);
 #pragma unroll
@@ -431,7 +444,7 @@ __global__ __launch_bounds__(64 * kFlatPanelWaves) void gpad_flatpanel_kernel(So
                     float4* L = fp_lds + x.pp * PBf;
                     const int voff = fp_voff1(g, x, lane);
                     const FpPre f = q == 0 ? pre1 : fp_pre<ALDS>(PA, As, voff, g.T1 * 1024, g.KB1);
-                    const ff32x4 acc = fp_chain<ALDS, RING>(PA, As, f, voff, g.T1 * 1024, g.KB1, g.kq1, L + x.j * g.KBc * 64, g.KBc,
+                    const ff32x4 acc = fp_chain<ALDS>(PA, As, f, voff, g.T1 * 1024, g.KB1, g.kq1, L + x.j * g.KBc * 64, g.KBc,
                                                 L + oWe, lane);
                     float zh[4];
 #pragma unroll
@@ -470,7 +483,7 @@ __global__ __launch_bounds__(64 * kFlatPanelWaves) void gpad_flatpanel_kernel(So
                     const int voff = fp_voff2(g, x, lane), stride = (cp ? g.KBe : g.KBc) * 1024;
                     const int nkb = cp ? g.KB3 : g.T1;
                     const FpPre f = q == 0 ? pre2 : fp_pre<ALDS>(PA, As, voff, stride, nkb);
-                    const ff32x4 acc = fp_chain<ALDS, RING>(PA, As, f, voff, stride, nkb, cp ? g.kq3 : g.kq2,
+                    const ff32x4 acc = fp_chain<ALDS>(PA, As, f, voff, stride, nkb, cp ? g.kq3 : g.kq2,
                                                 cp ? L + oZn : L + oZc + x.cell * g.T1 * 64, nkb, L + oZn, lane);
                     float4* wp = L + (cp ? oWe + x.t * 64 : (x.cell * g.KBc + x.t) * 64) + lane;
                     const float4 w4 = *wp;

@@ -455,30 +455,23 @@ __device__ __forceinline__ void panel_gemm3(__amdgpu_buffer_rsrc_t PA, const flo
 }
 
 // Runtime-length variant for a GEMM whose K spans fewer k-blocks than the tile count
-// (n != m: e.g. the battery's n = 40 against m = 180 -> 3 of 12 blocks).  A plain loop with the
-// A/B rings rotated by register moves; soffset in an SGPR, so no per-block address VGPRs.
+// (n != m: e.g. the battery's n = 40 against m = 180 -> 3 of 12 blocks).  Unrolled by two with
+// fixed register roles (even blocks in a0, odd in a1) and every load unconditional (indices
+// clamped to the last block), so each block's waitcnt counts only the loads issued after its
+// operands -- a rotated ring with conditional loads made the compiler drain both counters at
+// every block.  A is PD (1 or 2) blocks ahead, B one block ahead; soffset in an SGPR.
 template <int T, bool DUAL, int PD>
 __device__ __forceinline__ void panel_gemm_rt(__amdgpu_buffer_rsrc_t PA, const float4* B0, const float4* B1,
                                               int voff, int lane, f32x4& acc0, f32x4& acc1,
                                               const float4 (&ap)[PD], int nkb, int kq) {
+    static_assert(PD == 1 || PD == 2, "A ring depth 1 or 2");
     acc0 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     acc1 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    float4 a[PD + 1];
-#pragma unroll
-    for (int p = 0; p < PD; ++p) a[p] = ap[p];
-    float4 b0 = B0[lane], b1 = DUAL ? B1[lane] : b0;
-    for (int kb = 0; kb < nkb; ++kb) {
-        const float4 ak = a[0];
-#pragma unroll
-        for (int p = 0; p < PD; ++p) a[p] = a[p + 1];
-        if (kb + PD < nkb)
-            a[PD - 1] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb + PD) * T * 1024, 0));
-        const float4 bk0 = b0, bk1 = b1;
-        if (kb + 1 < nkb) {
-            b0 = B0[(kb + 1) * 64 + lane];
-            if constexpr (DUAL) b1 = B1[(kb + 1) * 64 + lane];
-        }
-        const int steps = kb + 1 < nkb ? 4 : kq;
+    const int last = nkb - 1;
+    auto lda = [&](int kb) -> float4 {
+        return as_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb < last ? kb : last) * T * 1024, 0));
+    };
+    auto blk = [&](const float4& ak, const float4& bk0, const float4& bk1, int steps) {
         __builtin_amdgcn_sched_barrier(0);
         acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, bk0.x, acc0, 0, 0, 0);
         if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, bk1.x, acc1, 0, 0, 0);
@@ -494,9 +487,27 @@ __device__ __forceinline__ void panel_gemm_rt(__amdgpu_buffer_rsrc_t PA, const f
             acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, bk0.w, acc0, 0, 0, 0);
             if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, bk1.w, acc1, 0, 0, 0);
         }
-        if constexpr (DUAL) asm volatile("" : "+v"(acc0), "+v"(acc1)::"memory");
-        else asm volatile("" : "+v"(acc0)::"memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    float4 a0 = ap[0], a1 = PD == 2 ? ap[PD - 1] : ap[0];
+    float4 e0 = B0[lane], f0 = DUAL ? B1[lane] : e0, e1, f1;
+    for (int kb = 0;; kb += 2) {
+        const int k1 = kb + 1 < last ? kb + 1 : last, k2 = kb + 2 < last ? kb + 2 : last;
+        if constexpr (PD == 1) a1 = lda(kb + 1);
+        e1 = B0[k1 * 64 + lane];
+        if constexpr (DUAL) f1 = B1[k1 * 64 + lane];
+        blk(a0, e0, f0, kb < last ? 4 : kq);
+        if constexpr (PD == 2) a0 = lda(kb + 2);
+        if (kb + 1 > last) break;
+        if constexpr (PD == 1) a0 = lda(kb + 2);
+        e0 = B0[k2 * 64 + lane];
+        if constexpr (DUAL) f0 = B1[k2 * 64 + lane];
+        blk(a1, e1, f1, kb + 1 < last ? 4 : kq);
+        if constexpr (PD == 2) a1 = lda(kb + 3);
+        if (kb + 2 > last) break;
     }
+    if constexpr (DUAL) asm volatile("" : "+v"(acc0), "+v"(acc1)::"memory");
+    else asm volatile("" : "+v"(acc0)::"memory");
 }
 
 template <int T>
