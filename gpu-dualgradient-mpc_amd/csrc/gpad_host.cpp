@@ -334,7 +334,7 @@ int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* d, int n_u, const float*
     }
     h->frag.release();
     h->frag_tiles = 0;
-    if (d->batch > 16) {  // MFMA panels over the flat data (gpad_flatpanel.hip)
+    {  // MFMA panels over the flat data (gpad_flatpanel.hip)
         const size_t fb = gpad::flatpanel_frag_bytes(d->n, m, n_u);
         if (fb) {
             if ((rc = h->frag.ensure(fb))) return rc;
@@ -504,8 +504,12 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
     if constexpr (sizeof(T) == sizeof(float)) {
         if (h->flat) {  // structure-exploiting battery path (gpad_setup_flat)
             a.n_u = h->n_u;
+            // flat panels from 8 instances per CU when the register-resident flat chains exist
+            // (their per-CU cost grows with the batch, a panel's does not until every CU holds
+            // one: crossover ~2048 at C1, tools/fp_cross.py); always when only the LDS flat
+            // kernel would be left (several times slower at any batch)
             const char* fpe = std::getenv("GPAD_FLAT_PANEL_MIN");  // tuning knob
-            const int fpm = fpe ? std::atoi(fpe) : 4 * h->num_cus;
+            const int fpm = fpe ? std::atoi(fpe) : (h->GLx.p ? 8 * h->num_cus : 0);
             if (h->frag.p && (kernel == GPAD_KERNEL_PANEL || (kernel == GPAD_KERNEL_AUTO && batch >= fpm))) {
                 e = gpad::launch_flatpanel(a, h->stream);
             } else if (h->GLx.p && kernel != GPAD_KERNEL_STREAM) {  // register-resident flat chains

@@ -166,7 +166,8 @@ def test_flat_batch_bitexact(gpu, oracle, tol, N, kernel, cells):
 @pytest.mark.parametrize("tol,N", [(0.0, 120), (1e-4, 4000)])
 @pytest.mark.parametrize("cells,B,P", [((4, 10), 40, 1), ((3, 17), 33, 1), ((5, 6), 16 * 3 + 1, 1),
                                        ((4, 50), 24, 1), ((2, 30), 20, 1), ((4, 10), 16 * 5 + 3, 4),
-                                       ((4, 10), 16 * 3 + 7, 2), ((3, 17), 16 * 4 + 9, 3), ((5, 6), 16 * 2 + 1, 4)])
+                                       ((4, 10), 16 * 3 + 7, 2), ((3, 17), 16 * 4 + 9, 3), ((5, 6), 16 * 2 + 1, 4),
+                                       ((4, 50), 1, 1), ((3, 17), 5, 1)])
 def test_flat_panel_bitexact(gpu, oracle, monkeypatch, tol, N, cells, B, P):
     """The flat MFMA panel kernel (gpad_flatpanel.hip, forced with KERNEL_PANEL): per-cell
     skinny GEMMs over 16-instance panels, P panels per workgroup (ragged last panel, partly

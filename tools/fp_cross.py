@@ -1,0 +1,51 @@
+"""Flat battery: MFMA flat panels vs per-instance flat chains by batch (AUTO crossover).
+GPU box: python tools/fp_cross.py"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def one(n_u, Nh, batch, N):
+    sys.path.insert(0, os.path.join(ROOT, "gpu-dualgradient-mpc_amd"))
+    import torch
+
+    import gpad_mpc
+    from gpad_mpc import problems
+    dev = torch.device("cuda:0")
+    qp = problems.battery_scenarios(n_u, Nh, batch, seed=9)
+    MGf, GLf, L = problems.flatten_battery(qp, n_u, Nh)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a, np.float64).astype(np.float32))).to(dev)  # noqa: E731
+    L32 = float(np.float32(L))
+    GP = t(qp.M).reshape(batch, -1)
+    PD = (t(qp.g).reshape(batch, -1) * np.float32(-1.0 / np.float64(np.float32(L)))).contiguous()
+    s = gpad_mpc.GpadSolver(0)
+    s.setup_flat(t(MGf), t(GLf), L32, n_u=n_u, batch=batch)
+    Z = torch.zeros(batch, qp.n, device=dev)
+    Y = torch.zeros(batch, qp.m, device=dev)
+    s.run(Z, Y, GP, PD, N, 0.0, scaled=True)
+    best = min(s.run(Z.zero_(), Y.zero_(), GP, PD, N, 0.0, scaled=True)["kernel_ms"] for _ in range(3))
+    print(json.dumps({"n_u": n_u, "N": Nh, "batch": batch, "path": os.environ.get("FP_PATH"),
+                      "us_per_iter": round(best * 1e3 / N, 3), "iters_per_s": batch * N / (best / 1e3)}),
+          flush=True)
+
+
+def main():
+    if len(sys.argv) > 1:
+        one(*(int(x) for x in sys.argv[1:5]))
+        return
+    for Nh in (10, 30):
+        for batch in (512, 1024, 2048, 3072, 4096):
+            for path, thr in (("panel", "0"), ("chains", "1000000000")):
+                env = {k: v for k, v in os.environ.items() if not k.startswith("GPAD_")}
+                env["GPAD_FLAT_PANEL_MIN"] = thr
+                env["FP_PATH"] = path
+                subprocess.run([sys.executable, __file__, "4", str(Nh), str(batch), "200"], env=env, check=True)
+
+
+if __name__ == "__main__":
+    main()
