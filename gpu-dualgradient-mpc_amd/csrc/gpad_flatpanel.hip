@@ -37,7 +37,8 @@ struct FlatGeom {  // sizes in tiles / k-blocks of 16 rows; image offsets in flo
     int kq2;                 // 8d per cell: T2 = KBc row tiles, KB2 = T1 k-blocks
     int KB3, kq3;            // 8d coupling: KBe row tiles, K = n
     int U1, U2;              // units (sub-GEMM, row tile) of the two phases
-    int off2, off3, total;   // images [n_u][KB1][T1], [n_u][T1][KBc], [KB3][KBe] of 64 float4
+    int off1c, off2, off3, total;  // images [n_u][KBc][T1] + [KBe][T1] (the coupling blocks, shared
+                                   // by every cell's chain), [n_u][T1][KBc], [KB3][KBe] of 64 float4
     int PB;                  // LDS blocks per panel
     int P;                   // panels per workgroup (set by the launcher)
     // unit descriptors (set by the launcher): pp << 16 | (cell + 1) << 8 | t
@@ -66,7 +67,8 @@ __host__ __device__ inline FlatGeom flat_geom(int n, int m, int n_u) {
     g.kq3 = fp_kq(n, g.KB3);
     g.U1 = n_u * g.T1;
     g.U2 = g.KBe + n_u * g.KBc;
-    g.off2 = n_u * g.KB1 * g.T1 * 64;
+    g.off1c = n_u * g.KBc * g.T1 * 64;
+    g.off2 = g.off1c + g.KBe * g.T1 * 64;
     g.off3 = g.off2 + n_u * g.T1 * g.KBc * 64;
     g.total = g.off3 + g.KB3 * g.KBe * 64;
     g.PB = n_u * (g.KBc + g.T1) + g.KBe + g.KB3;
@@ -114,9 +116,14 @@ __global__ void pack_flatpanel_kernel(FlatGeom g, const float* __restrict__ MGf,
     const int lane = idx & 63;
     const int rrow = fp_pi16(lane & 15);  // row inside the tile (fragment-order permutation)
     float v[4];
-    if (idx < g.off2) {  // [n_u][KB1][T1]
+    if (idx < g.off1c) {  // [n_u][KBc][T1]: the cell blocks of each cell's 8b chains
         const int blk = idx >> 6;
-        const int t = blk % g.T1, b = (blk / g.T1) % g.KB1, j = blk / (g.T1 * g.KB1);
+        const int t = blk % g.T1, b = (blk / g.T1) % g.KBc, j = blk / (g.T1 * g.KBc);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = flat_a1(g, MGf, j, 16 * t + rrow, 16 * b + 4 * q + (lane >> 4));
+    } else if (idx < g.off2) {  // [KBe][T1]: the coupling blocks (the same for every cell)
+        const int blk = (idx - g.off1c) >> 6;
+        const int t = blk % g.T1, b = g.KBc + blk / g.T1, j = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = flat_a1(g, MGf, j, 16 * t + rrow, 16 * b + 4 * q + (lane >> 4));
     } else if (idx < g.off3) {  // [n_u][T1 k-blocks][KBc tiles]
@@ -213,11 +220,17 @@ __device__ __forceinline__ float4 fp_lda(__amdgpu_buffer_rsrc_t PA, const float4
     if constexpr (ALDS) return As[(voff + off) >> 4];
     else return fas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, off, 0));
 }
+// A block kb of a chain sits at byte offset voff + kb * stride (+ ajump from block akbs on: the
+// 8b chains continue in the shared coupling image)
+__device__ __forceinline__ int fp_aoff(int kb, int stride, int akbs, int ajump) {
+    return kb * stride + (kb >= akbs ? ajump : 0);
+}
 template <bool ALDS>
-__device__ __forceinline__ FpPre fp_pre(__amdgpu_buffer_rsrc_t PA, const float4* As, int voff, int stride, int nkb) {
+__device__ __forceinline__ FpPre fp_pre(__amdgpu_buffer_rsrc_t PA, const float4* As, int voff, int stride, int nkb,
+                                        int akbs = 1 << 30, int ajump = 0) {
     FpPre f;
-    f.a0 = fp_lda<ALDS>(PA, As, voff, 0);
-    f.a1 = nkb > 1 ? fp_lda<ALDS>(PA, As, voff, stride) : f.a0;
+    f.a0 = fp_lda<ALDS>(PA, As, voff, fp_aoff(0, stride, akbs, ajump));
+    f.a1 = fp_lda<ALDS>(PA, As, voff, fp_aoff(nkb > 1 ? 1 : 0, stride, akbs, ajump));
     return f;
 }
 // one unit's chain over nkb k-blocks (the last only its kq 4-steps): A two blocks ahead (the
@@ -227,7 +240,8 @@ __device__ __forceinline__ FpPre fp_pre(__amdgpu_buffer_rsrc_t PA, const float4*
 // them, instead of draining the queue at every conditional load or register rotation.
 template <bool ALDS>
 __device__ __forceinline__ ff32x4 fp_chain(__amdgpu_buffer_rsrc_t PA, const float4* As, FpPre f, int voff, int stride,
-                                           int nkb, int kq, const float4* Ba, int kbs, const float4* Bb, int lane) {
+                                           int nkb, int kq, const float4* Ba, int kbs, const float4* Bb, int lane,
+                                           int akbs = 1 << 30, int ajump = 0) {
     ff32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
     const int last = nkb - 1;
     auto ldb = [&](int kb) -> float4 { return kb < kbs ? Ba[kb * 64 + lane] : Bb[(kb - kbs) * 64 + lane]; };
@@ -244,7 +258,7 @@ __device__ __forceinline__ ff32x4 fp_chain(__amdgpu_buffer_rsrc_t PA, const floa
             if (steps > 3) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, b0.w, acc, 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
         }
-        a0 = fp_lda<ALDS>(PA, As, voff, (kb + 2 < last ? kb + 2 : last) * stride);
+        a0 = fp_lda<ALDS>(PA, As, voff, fp_aoff(kb + 2 < last ? kb + 2 : last, stride, akbs, ajump));
         if (kb + 1 > last) break;
         b0 = ldb(kb + 2 < last ? kb + 2 : last);
         {
@@ -256,7 +270,7 @@ __device__ __forceinline__ ff32x4 fp_chain(__amdgpu_buffer_rsrc_t PA, const floa
             if (steps > 3) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, b1.w, acc, 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
         }
-        a1 = fp_lda<ALDS>(PA, As, voff, (kb + 3 < last ? kb + 3 : last) * stride);
+        a1 = fp_lda<ALDS>(PA, As, voff, fp_aoff(kb + 3 < last ? kb + 3 : last, stride, akbs, ajump));
         if (kb + 2 > last) break;
     }
     asm volatile("" : "+v"(acc)::"memory");
@@ -293,7 +307,10 @@ __device__ __forceinline__ FpU2 fp_u2(const FlatGeom& g, int un) {
     return x;
 }
 __device__ __forceinline__ int fp_voff1(const FlatGeom& g, FpU1 x, int lane) {
-    return (x.j * g.KB1 * g.T1 + x.t) * 1024 + lane * 16;
+    return (x.j * g.KBc * g.T1 + x.t) * 1024 + lane * 16;
+}
+__device__ __forceinline__ int fp_ajump1(const FlatGeom& g, FpU1 x) {  // cell image -> coupling image
+    return g.off1c * 16 - (x.j + 1) * g.KBc * g.T1 * 1024;
 }
 __device__ __forceinline__ int fp_voff2(const FlatGeom& g, FpU2 x, int lane) {
     return (x.cell < 0 ? g.off3 + x.t * 64 : g.off2 + (x.cell * g.T1 * g.KBc + x.t) * 64) * 16 + lane * 16;
@@ -413,7 +430,7 @@ __global__ __launch_bounds__(64 * kFlatPanelWaves) void gpad_flatpanel_kernel(So
         FpPre pre1{}, pre2{};
         if (w < nu1) {
             const FpU1 x = fp_u1(g, w);
-            pre1 = fp_pre<ALDS>(PA, As, fp_voff1(g, x, lane), g.T1 * 1024, g.KB1);
+            pre1 = fp_pre<ALDS>(PA, As, fp_voff1(g, x, lane), g.T1 * 1024, g.KB1, g.KBc, fp_ajump1(g, x));
         }
         int v = 0;
         float th = a.theta[0], bn = a.beta[1];
@@ -443,9 +460,10 @@ __global__ __launch_bounds__(64 * kFlatPanelWaves) void gpad_flatpanel_kernel(So
                     const bool act = (live >> (16 * x.pp + c)) & 1ull;
                     float4* L = fp_lds + x.pp * PBf;
                     const int voff = fp_voff1(g, x, lane);
-                    const FpPre f = q == 0 ? pre1 : fp_pre<ALDS>(PA, As, voff, g.T1 * 1024, g.KB1);
+                    const int ajump = fp_ajump1(g, x);
+                    const FpPre f = q == 0 ? pre1 : fp_pre<ALDS>(PA, As, voff, g.T1 * 1024, g.KB1, g.KBc, ajump);
                     const ff32x4 acc = fp_chain<ALDS>(PA, As, f, voff, g.T1 * 1024, g.KB1, g.kq1, L + x.j * g.KBc * 64, g.KBc,
-                                                L + oWe, lane);
+                                                      L + oWe, lane, g.KBc, ajump);
                     float zh[4];
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
@@ -531,7 +549,7 @@ __global__ __launch_bounds__(64 * kFlatPanelWaves) void gpad_flatpanel_kernel(So
             }
             if (w < nu1) {
                 const FpU1 x = fp_u1(g, w);
-                pre1 = fp_pre<ALDS>(PA, As, fp_voff1(g, x, lane), g.T1 * 1024, g.KB1);
+                pre1 = fp_pre<ALDS>(PA, As, fp_voff1(g, x, lane), g.T1 * 1024, g.KB1, g.KBc, fp_ajump1(g, x));
             }
             th = th_next;
             bn = bn_next;
