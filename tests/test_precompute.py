@@ -32,6 +32,9 @@ def test_precompute_shared_vs_numpy(gpu, n, m, batch):
     assert _rel(ML, Hi @ A.T) < 1e-11
     assert _rel(gP, (Hi @ f.T).T) < 1e-11
     assert abs(L - np.linalg.norm(H, "fro") ** 2) <= 1e-13 * L
+    ML2, gP2, L2 = s.precompute(H, A)  # no f: ML and L only
+    assert gP2 is None and L2 == L
+    np.testing.assert_array_equal(ML2, ML)
 
 
 @pytest.mark.gpu
