@@ -247,32 +247,35 @@ __device__ __forceinline__ ff32x4 fp_chain(__amdgpu_buffer_rsrc_t PA, const floa
     auto ldb = [&](int kb) -> float4 { return kb < kbs ? Ba[kb * 64 + lane] : Bb[(kb - kbs) * 64 + lane]; };
     float4 a0 = f.a0, a1 = f.a1;
     float4 b0 = ldb(0), b1;
-    for (int kb = 0;; kb += 2) {
-        b1 = ldb(kb + 1 < last ? kb + 1 : last);
-        {
-            const int steps = kb < last ? 4 : kq;
-            __builtin_amdgcn_sched_barrier(0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, b0.x, acc, 0, 0, 0);
-            if (steps > 1) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, b0.y, acc, 0, 0, 0);
-            if (steps > 2) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, b0.z, acc, 0, 0, 0);
-            if (steps > 3) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, b0.w, acc, 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        a0 = fp_lda<ALDS>(PA, As, voff, fp_aoff(kb + 2 < last ? kb + 2 : last, stride, akbs, ajump));
-        if (kb + 1 > last) break;
-        b0 = ldb(kb + 2 < last ? kb + 2 : last);
-        {
-            const int steps = kb + 1 < last ? 4 : kq;
-            __builtin_amdgcn_sched_barrier(0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, b1.x, acc, 0, 0, 0);
-            if (steps > 1) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, b1.y, acc, 0, 0, 0);
-            if (steps > 2) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, b1.z, acc, 0, 0, 0);
-            if (steps > 3) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, b1.w, acc, 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-        }
+    auto full = [&](const float4& ak, const float4& bk) {
+        __builtin_amdgcn_sched_barrier(0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, bk.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, bk.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, bk.z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, bk.w, acc, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // pairs of full blocks (four MFMA steps each, no branch in between), then the rest: the last
+    // block alone (its kq steps), or one full block and the last
+    int kb = 0;
+    for (; kb + 2 <= last; kb += 2) {
+        b1 = ldb(kb + 1);
+        full(a0, b0);
+        a0 = fp_lda<ALDS>(PA, As, voff, fp_aoff(kb + 2, stride, akbs, ajump));
+        b0 = ldb(kb + 2);
+        full(a1, b1);
         a1 = fp_lda<ALDS>(PA, As, voff, fp_aoff(kb + 3 < last ? kb + 3 : last, stride, akbs, ajump));
-        if (kb + 2 > last) break;
     }
+    if (kb < last) {
+        b1 = ldb(last);
+        full(a0, b0);
+        a0 = a1;
+        b0 = b1;
+    }
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, b0.x, acc, 0, 0, 0);
+    if (kq > 1) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, b0.y, acc, 0, 0, 0);
+    if (kq > 2) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, b0.z, acc, 0, 0, 0);
+    if (kq > 3) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, b0.w, acc, 0, 0, 0);
     asm volatile("" : "+v"(acc)::"memory");
     return acc;
 }
