@@ -126,16 +126,22 @@ __device__ __forceinline__ bf32x4 big_gemm(__amdgpu_buffer_rsrc_t PA, const floa
         return bas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb < last ? kb : last) * stride, 0));
     };
     float4 a0 = lda(0), a1 = lda(1), b0 = B[lane], b1;
-    for (int kb = 0;; kb += 2) {
-        b1 = B[(kb + 1 < last ? kb + 1 : last) * 64 + lane];
-        big_blk(acc, a0, b0, kb < last ? 4 : kq);
+    int kb = 0;  // pairs of full blocks, then the rest (the last block with its kq steps)
+    for (; kb + 2 <= last; kb += 2) {
+        b1 = B[(kb + 1) * 64 + lane];
+        big_blk(acc, a0, b0, 4);
         a0 = lda(kb + 2);
-        if (kb + 1 > last) break;
-        b0 = B[(kb + 2 < last ? kb + 2 : last) * 64 + lane];
-        big_blk(acc, a1, b1, kb + 1 < last ? 4 : kq);
+        b0 = B[(kb + 2) * 64 + lane];
+        big_blk(acc, a1, b1, 4);
         a1 = lda(kb + 3);
-        if (kb + 2 > last) break;
     }
+    if (kb < last) {
+        b1 = B[last * 64 + lane];
+        big_blk(acc, a0, b0, 4);
+        a0 = a1;
+        b0 = b1;
+    }
+    big_blk(acc, a0, b0, kq);
     asm volatile("" : "+v"(acc)::"memory");
     return acc;
 }
@@ -151,18 +157,25 @@ __device__ __forceinline__ void big_gemm2(__amdgpu_buffer_rsrc_t PA, const float
         return bas_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb < last ? kb : last) * stride, 0));
     };
     float4 a0 = lda(v0, 0), c0 = lda(v1, 0), a1 = lda(v0, 1), c1 = lda(v1, 1), b0 = B[lane], b1;
-    for (int kb = 0;; kb += 2) {
-        b1 = B[(kb + 1 < last ? kb + 1 : last) * 64 + lane];
-        big_blk2(acc0, acc1, a0, c0, b0, kb < last ? 4 : kq);
+    int kb = 0;  // pairs of full blocks, then the rest (the last block with its kq steps)
+    for (; kb + 2 <= last; kb += 2) {
+        b1 = B[(kb + 1) * 64 + lane];
+        big_blk2(acc0, acc1, a0, c0, b0, 4);
         a0 = lda(v0, kb + 2);
         c0 = lda(v1, kb + 2);
-        if (kb + 1 > last) break;
-        b0 = B[(kb + 2 < last ? kb + 2 : last) * 64 + lane];
-        big_blk2(acc0, acc1, a1, c1, b1, kb + 1 < last ? 4 : kq);
+        b0 = B[(kb + 2) * 64 + lane];
+        big_blk2(acc0, acc1, a1, c1, b1, 4);
         a1 = lda(v0, kb + 3);
         c1 = lda(v1, kb + 3);
-        if (kb + 2 > last) break;
     }
+    if (kb < last) {
+        b1 = B[last * 64 + lane];
+        big_blk2(acc0, acc1, a0, c0, b0, 4);
+        a0 = a1;
+        c0 = c1;
+        b0 = b1;
+    }
+    big_blk2(acc0, acc1, a0, c0, b0, kq);
     asm volatile("" : "+v"(acc0), "+v"(acc1)::"memory");
 }
 
