@@ -1,5 +1,5 @@
-"""Per-phase cycle split of the flat panel kernel (build with -DFP_TIMING into tools/ab/fptime.so):
-GPAD_LIB=tools/ab/fptime.so python tools/fp_time.py N_u N batch iters"""
+"""Per-phase cycle split of the flat panel kernel (build with -DFP_TIMING into tools/fpt/fptime.so):
+GPAD_LIB=tools/fpt/fptime.so python tools/fp_time.py N_u N batch iters"""
 import os
 import sys
 
