@@ -14,9 +14,10 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 run() {  # name, rocprofv3 args...
   local name=$1; shift
-  timeout -k 10 300 rocprofv3 "$@" --output-format csv -d $OUT/$name -o run -- python3 bench.py $ARGS \
+  timeout -k 10 300 rocprofv3 "$@" --output-format csv -d $OUT/$name -o run -- python3 $SCRIPT $ARGS \
       > $OUT/$name.log 2>&1
 }
+SCRIPT=${PROFILE_SCRIPT:-bench.py}  # e.g. PROFILE_SCRIPT=tools/c5_run.py for the C5 stream leg alone
 run kt --kernel-trace --stats
 run fetch --pmc FETCH_SIZE
 run write --pmc WRITE_SIZE
