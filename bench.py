@@ -282,7 +282,7 @@ def flat_leg(dev, batch=8192, N=100, horizon=10):
     return out
 
 
-def closed_loop_leg(dev, batch=8192, steps=20, N=100, cpu=True):
+def closed_loop_leg(dev, batch=8192, steps=20, N=100, cpu=True, flat=False):
     """gpad.m:79-95 closed loop on the device for a batch of battery
     packs (C1 plant: n_u = 4 cells, horizon 10 -> n = 40, m = 180), each MPC step = per-state
     QP data + 100 GPAD iterations (acceldualgrad's fixed count) + plant update.  MPC steps/s
@@ -297,7 +297,11 @@ def closed_loop_leg(dev, batch=8192, steps=20, N=100, cpu=True):
     L32 = float(np.float32(qp.L))
     X0 = (np.random.default_rng(3).random((batch, 4)) - 0.5).astype(np.float32)
     with gpad_mpc.GpadSolver(dev.index or 0, stream=torch.cuda.current_stream(dev).cuda_stream) as s:
-        s.setup(f32(qp.ML), f32(qp.G), L32, n=qp.n, m=qp.m, batch=batch)
+        if flat:  # the same packs on the reference's flat data (equal cells; §8f row 4)
+            MGf, GLf, Lf = problems.flatten_battery(qp, 4, 10)
+            s.setup_flat(f32(MGf), f32(GLf), float(np.float32(Lf)), n_u=4, batch=batch)
+        else:
+            s.setup(f32(qp.ML), f32(qp.G), L32, n=qp.n, m=qp.m, batch=batch)
         s.setup_plant(f32(pl.PM), f32(pl.Pg), g0=f32(pl.g0), A=f32(pl.A), B=f32(pl.B))
         X = torch.from_numpy(X0).to(dev)
         Z = torch.zeros(batch, qp.n, device=dev)
@@ -314,6 +318,8 @@ def closed_loop_leg(dev, batch=8192, steps=20, N=100, cpu=True):
                      f"x {N} GPAD iterations, cold start (gpad.m)", "kernel": st["kernel"],
            "mpc_steps_per_s": batch * steps / wall, "iters_per_s": st["total_iterations"] / wall,
            "device_ms": st["kernel_ms"], "wall_ms": wall * 1e3}
+    if flat:
+        out["config"] += ", flat battery data (gpad_setup_flat)"
     if cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import pyoracle
@@ -466,6 +472,7 @@ def main():
             extra["distinct_c2_batch"] = distinct_leg(dev, n, m)
             extra["c3_batch4096"] = c3_leg(dev, n, m)
             extra["closed_loop_battery"] = closed_loop_leg(dev, cpu=not args.no_cpu)
+            extra["closed_loop_battery_flat"] = closed_loop_leg(dev, cpu=False, flat=True)
             extra["flat_battery_c1"] = flat_leg(dev)
             extra["battery_n50"] = flat_leg(dev, horizon=50, N=50)
         out = {

@@ -234,3 +234,55 @@ def test_flat_datafile_run(gpu, oracle):
                                          100, np.float32(d.L), theta=d.theta, beta=d.beta)
     np.testing.assert_array_equal(z, zo)
     np.testing.assert_array_equal(y, yo)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", [0, 3])  # AUTO (register flat chains at this batch) / forced flat panels
+@pytest.mark.parametrize("tol", [0.0, 1e-4])
+def test_flat_closed_loop_bitexact(gpu, oracle, kernel, tol):
+    """gpad.m:79-95 on flat battery data: gpad_setup_flat + gpad_setup_plant + gpad_closed_loop
+    (per-state g_P, b on the device, the flat solve, x+ = A x + B u), cold start, 3 MPC steps,
+    vs the oracle composed step by step (affine maps, flat solve, plant update) per pack."""
+    import gpad_mpc
+    from gpad_mpc import problems
+    n_u, Nh, B, steps, N = 4, 10, 20, 3, 100
+    qp, pl = problems.battery_plant(n_u, Nh)
+    MGf, GLf, L = problems.flatten_battery(qp, n_u, Nh)
+    c = lambda a: np.ascontiguousarray(np.asarray(a, np.float64).astype(np.float32))  # noqa: E731
+    MGf32, GLf32, L32 = c(MGf), c(GLf), np.float32(L)
+    PM, Pg, g0, A, Bm = c(pl.PM), c(pl.Pg), c(pl.g0), c(pl.A), c(pl.B)
+    X0 = c(np.random.default_rng(7).random((B, n_u)) - 0.5)
+    s = gpad_mpc.GpadSolver(0)
+    s.setup_flat(MGf32, GLf32, float(L32), n_u=n_u, batch=B, kernel=kernel)
+    s.setup_plant(PM, Pg, g0=g0, A=A, B=Bm)
+    X = X0.copy()
+    Z = np.zeros((B, qp.n), np.float32)
+    Y = np.zeros((B, qp.m), np.float32)
+    xs = np.zeros((steps, B, n_u), np.float32)
+    us = np.zeros((steps, B, n_u), np.float32)
+    it = np.zeros(steps * B, np.int32)
+    s.closed_loop(X, Z, Y, steps, N, tol, xs=xs, us=us, iters=it)
+    ninv = -1.0 / np.float64(L32)
+    for b in range(B):
+        x = X0[b].copy()
+        for t in range(steps):
+            gP = oracle.affine(PM, None, x)
+            g = oracle.affine(Pg, g0, x)
+            pD = (ninv * g.astype(np.float64)).astype(np.float32)
+            z, y, its, _ = oracle.solve_flat_f32(np.zeros(qp.n), np.zeros(qp.m), MGf32, gP, GLf32, pD, n_u, N,
+                                                 L32, tol)
+            np.testing.assert_array_equal(xs[t, b], x, err_msg=f"x[{t}][{b}]")
+            np.testing.assert_array_equal(us[t, b], z[:n_u], err_msg=f"u[{t}][{b}]")
+            assert it[t * B + b] == its, (t, b)
+            xn = np.zeros(n_u, np.float32)
+            oracle.lib.orc_plant_step_f32(*(a.ctypes.data_as(oracle_fp()) for a in (A, Bm, x, z[:n_u].copy(), xn)),
+                                          n_u, n_u)
+            x = xn
+        np.testing.assert_array_equal(X[b], x, err_msg=f"x_T[{b}]")
+        np.testing.assert_array_equal(Z[b], z, err_msg=f"z[{b}]")
+        np.testing.assert_array_equal(Y[b], y, err_msg=f"y[{b}]")
+
+
+def oracle_fp():
+    import ctypes
+    return ctypes.POINTER(ctypes.c_float)
