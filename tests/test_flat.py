@@ -286,3 +286,33 @@ def test_flat_closed_loop_bitexact(gpu, oracle, kernel, tol):
 def oracle_fp():
     import ctypes
     return ctypes.POINTER(ctypes.c_float)
+
+
+@pytest.mark.gpu
+def test_flat_panel_grid_stride_large_batch(gpu, oracle):
+    """40000 C1 packs on the flat panels (AUTO: 4 panels per workgroup, more groups than
+    workgroups, so each workgroup loops over groups reusing its LDS), ragged last group; a
+    sample of instances vs the oracle's flat solve, bit for bit."""
+    import torch
+
+    import gpad_mpc
+    from gpad_mpc import problems
+    n_u, Nh, B, N = 4, 10, 40000 + 7, 60
+    qp = problems.battery_scenarios(n_u, Nh, B, seed=21)
+    MGf, GLf, L = problems.flatten_battery(qp, n_u, Nh)
+    f32 = lambda a: np.ascontiguousarray(np.asarray(a, np.float64).astype(np.float32))  # noqa: E731
+    L32 = np.float32(L)
+    MGf32, GLf32, GP = f32(MGf), f32(GLf), f32(qp.M)
+    PD = np.ascontiguousarray(oracle.scale_vec(f32(qp.g), L32))
+    t = lambda a: torch.from_numpy(a).to(gpu)  # noqa: E731
+    s = gpad_mpc.GpadSolver(0)
+    s.setup_flat(t(MGf32), t(GLf32), float(L32), n_u=n_u, batch=B)
+    Z = torch.zeros(B, qp.n, device=gpu)
+    Y = torch.zeros(B, qp.m, device=gpu)
+    st = s.run(Z, Y, t(GP), t(PD), N, 0.0, scaled=True)
+    assert st["kernel"] == "flat"
+    Zc, Yc = Z.cpu().numpy(), Y.cpu().numpy()
+    for b in list(range(0, B, 2311)) + [B - 1, B - 7]:
+        z, y, _, _ = oracle.solve_flat_f32(np.zeros(qp.n), np.zeros(qp.m), MGf32, GP[b], GLf32, PD[b], n_u, N, L32)
+        np.testing.assert_array_equal(Zc[b], z, err_msg=f"z[{b}]")
+        np.testing.assert_array_equal(Yc[b], y, err_msg=f"y[{b}]")
