@@ -319,10 +319,9 @@ __device__ __forceinline__ int fp_voff2(const FlatGeom& g, FpU2 x, int lane) {
     return (x.cell < 0 ? g.off3 + x.t * 64 : g.off2 + (x.cell * g.T1 * g.KBc + x.t) * 64) * 16 + lane * 16;
 }
 
-template <int NU1, int NU2, bool ALDS>
-__global__ __launch_bounds__(64 * kFlatPanelWaves) void gpad_flatpanel_kernel(SolveArgs<float> a, FlatGeom g) {
+template <int NU1, int NU2, bool ALDS, int W>
+__global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<float> a, FlatGeom g) {
     extern __shared__ __attribute__((aligned(16))) float4 fp_lds[];
-    constexpr int W = kFlatPanelWaves;
     const int P = g.P;
     // per panel pp at fp_lds + pp * PB * 64:  Wc [n_u][KBc] | We [KBe] | Zc [n_u][T1] | Zn [KB3]
     const int oWe = g.n_u * g.KBc * 64, oZc = oWe + g.KBe * 64, oZn = oZc + g.n_u * g.T1 * 64;
@@ -631,25 +630,62 @@ __global__ __launch_bounds__(64 * kFlatPanelWaves) void gpad_flatpanel_kernel(So
     }
 }
 
-template <int NU1, int NU2, bool ALDS>
+template <int NU1, int NU2, bool ALDS, int W>
 static hipError_t launch_fp_k(const SolveArgs<float>& a, const FlatGeom& g, size_t lds, int grid, hipStream_t s) {
     if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute((const void*)gpad_flatpanel_kernel<NU1, NU2, ALDS>,
+        hipError_t e = hipFuncSetAttribute((const void*)gpad_flatpanel_kernel<NU1, NU2, ALDS, W>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((gpad_flatpanel_kernel<NU1, NU2, ALDS>), dim3(grid), dim3(64 * kFlatPanelWaves), lds, s, a, g);
+    hipLaunchKernelGGL((gpad_flatpanel_kernel<NU1, NU2, ALDS, W>), dim3(grid), dim3(64 * W), lds, s, a, g);
     return hipGetLastError();
 }
-template <int NU1, int NU2>
+template <int NU1, int NU2, int W = kFlatPanelWaves>
 static hipError_t launch_fp_nt(const SolveArgs<float>& a, const FlatGeom& g, size_t lds, bool alds, int grid,
                                hipStream_t s) {
-    return alds ? launch_fp_k<NU1, NU2, true>(a, g, lds, grid, s) : launch_fp_k<NU1, NU2, false>(a, g, lds, grid, s);
+    return alds ? launch_fp_k<NU1, NU2, true, W>(a, g, lds, grid, s)
+                : launch_fp_k<NU1, NU2, false, W>(a, g, lds, grid, s);
 }
 
-static int fp_nt(int units) {
-    const int q = (units + kFlatPanelWaves - 1) / kFlatPanelWaves;
+static int fp_nt(int units, int W = kFlatPanelWaves) {
+    const int q = (units + W - 1) / W;
     return q <= 1 ? 1 : (q <= 2 ? 2 : 4);
+}
+
+// 8-wave workgroups, two per CU: the same waves per CU as one 16-wave workgroup, but two
+// independent barrier domains, so one workgroup's barrier waits overlap the other's chains.
+// Only for shapes whose units fit (phase 1 one per wave, phase 2 at most four per wave) with
+// the LDS of two workgroups; chosen with GPAD_FLAT_WAVES=8 or by the default rule below.
+static hipError_t launch_flatpanel_w8(const SolveArgs<float>& a, FlatGeom g, int panels, hipStream_t s,
+                                      bool force, bool* taken) {
+    *taken = false;
+    int P = 0;
+    for (int q = 2; q >= 1 && !P; --q)
+        if (q * g.U1 <= 8 && q * g.U2 <= 32 && 2 * flatpanel_lds_bytes(g, q) <= 160 * 1024 &&
+            (force ? q == 1 || (panels + q - 1) / q >= 2 * a.num_cus : q == 2 && (panels + q - 1) / q >= 2 * a.num_cus))
+            P = q;
+    if (!P) return hipSuccess;
+    g.P = P;
+    for (int un = 0; un < 4 * kFlatPanelWavesMax; ++un) {
+        const int pp = un / g.U1, uu = un % g.U1;
+        g.d1[un] = un < P * g.U1 ? (pp << 16) | ((uu / g.T1 + 1) << 8) | (uu % g.T1) : 0;
+        const int qq = un / g.U2, vv = un % g.U2;
+        const int cell = vv < g.KBe ? -1 : (vv - g.KBe) / g.KBc;
+        const int t = vv < g.KBe ? vv : (vv - g.KBe) % g.KBc;
+        g.d2[un] = un < P * g.U2 ? (qq << 16) | ((cell + 1) << 8) | t : 0;
+    }
+    size_t lds = flatpanel_lds_bytes(g, P);
+    const size_t abytes = (size_t)g.total * 16;
+    const bool alds = 2 * (lds + abytes) <= 160 * 1024 && !std::getenv("GPAD_FLAT_NO_ALDS");
+    if (alds) lds += abytes;
+    const int groups = (panels + P - 1) / P;
+    const int grid = std::min(groups, 2 * a.num_cus);
+    *taken = true;
+    switch (fp_nt(P * g.U2, 8)) {
+        case 1: return launch_fp_nt<1, 1, 8>(a, g, lds, alds, grid, s);
+        case 2: return launch_fp_nt<1, 2, 8>(a, g, lds, alds, grid, s);
+        default: return launch_fp_nt<1, 4, 8>(a, g, lds, alds, grid, s);
+    }
 }
 
 // whole-batch solve (one launch, no phased compaction); a.frag = the flat fragment images.
@@ -659,6 +695,18 @@ hipError_t launch_flatpanel(const SolveArgs<float>& a, hipStream_t s) {
     if (!flatpanel_supported(a.n, a.m, a.n_u) || !a.frag) return hipErrorInvalidValue;
     FlatGeom g = flat_geom(a.n, a.m, a.n_u);
     const int panels = (a.batch + 15) / 16;
+    if (const char* we = std::getenv("GPAD_FLAT_WAVES"); we && std::atoi(we) == 8) {  // A/B knob
+        bool taken = false;
+        const hipError_t e = launch_flatpanel_w8(a, g, panels, s, true, &taken);
+        if (taken || e != hipSuccess) return e;
+    } else if (!std::getenv("GPAD_FLAT_WAVES")) {
+        // default: two 8-wave workgroups per CU when each can hold two panels (C1 packs from 16384:
+        // 5.41 -> 5.23 us per batch-iteration); at one panel each they lose to one 16-wave
+        // workgroup of two panels (8192: 3.03 vs 3.28 us)
+        bool taken = false;
+        const hipError_t e = launch_flatpanel_w8(a, g, panels, s, false, &taken);
+        if (taken || e != hipSuccess) return e;
+    }
     int P = 1;
     for (int q = 4; q > 1; --q) {
         if (q * g.U1 <= kFlatPanelWaves && q * g.U2 <= 4 * kFlatPanelWaves &&
