@@ -338,8 +338,8 @@ def closed_loop_leg(dev, batch=8192, steps=20, N=100, cpu=True, flat=False):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=8192, help="instances per GPU")
     ap.add_argument("--horizon", type=int, default=50)
     ap.add_argument("--nu", type=int, default=4)
