@@ -431,6 +431,17 @@ static int collect_stats(gpad_handle_t h, gpad_stats_t* st) {
     return GPAD_OK;
 }
 
+int gpad_accumulate_iterations(gpad_handle_t h, long long* acc) {
+    if (!h || !acc) return fail(GPAD_ERR_INVALID, "gpad_accumulate_iterations: null argument");
+    if (h->last_batch <= 0) return fail(GPAD_ERR_NOT_SETUP, "gpad_accumulate_iterations: no run yet");
+    HIP_TRY(hipSetDevice(h->device));
+    // counters: [steps][iters[batch] | conv[batch]]; each solve's iteration block in turn
+    for (int t = 0; t < h->last_steps; ++t)
+        HIP_TRY(gpad::launch_accumulate_iters((const int*)h->counters.p + (size_t)2 * h->last_batch * t,
+                                              h->last_batch, acc, h->stream));
+    return GPAD_OK;
+}
+
 int gpad_last_stats(gpad_handle_t h, gpad_stats_t* st) {
     if (!h || !st) return fail(GPAD_ERR_INVALID, "gpad_last_stats: null argument");
     if (h->last_batch <= 0) return fail(GPAD_ERR_NOT_SETUP, "gpad_last_stats: no run yet");

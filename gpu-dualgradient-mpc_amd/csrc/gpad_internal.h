@@ -118,6 +118,7 @@ hipError_t launch_precompute(int n, int m, int nf, const double* H, long long sH
                              const double* f, long long sF, double* work, double* ML, double* gP, double* L, int b0,
                              int count, hipStream_t s);
 hipError_t launch_apply_inv(int n, int batch, const double* Hinv, const double* f, double* gP, hipStream_t s);
+hipError_t launch_accumulate_iters(const int* iters, long long count, long long* acc, hipStream_t s);
 // flat battery data on the MFMA pipe (gpad_flatpanel.hip): per-cell skinny GEMMs over panels
 bool flatpanel_supported(int n, int m, int n_u);
 size_t flatpanel_frag_bytes(int n, int m, int n_u);

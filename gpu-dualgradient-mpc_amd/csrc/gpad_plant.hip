@@ -115,4 +115,17 @@ template hipError_t launch_plant_step<double>(const double*, const double*, cons
                                               long long, double*, int, int, int, double*, double*,
                                               hipStream_t);
 
+// acc += sum of per-instance iteration counts (one workgroup; wave sums then one atomic per wave)
+__global__ void accumulate_iters_kernel(const int* __restrict__ iters, long long count, long long* acc) {
+    long long sum = 0;
+    for (long long i = threadIdx.x; i < count; i += blockDim.x) sum += iters[i];
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    if ((threadIdx.x & 63) == 0) atomicAdd(reinterpret_cast<unsigned long long*>(acc), (unsigned long long)sum);
+}
+
+hipError_t launch_accumulate_iters(const int* iters, long long count, long long* acc, hipStream_t s) {
+    hipLaunchKernelGGL(accumulate_iters_kernel, dim3(1), dim3(1024), 0, s, iters, count, acc);
+    return hipGetLastError();
+}
+
 }  // namespace gpad

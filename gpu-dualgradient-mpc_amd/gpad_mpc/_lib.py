@@ -31,6 +31,7 @@ EXPORTS = [
     "gpad_setup_plant", "gpad_run_state", "gpad_closed_loop",
     "gpad_datafile_read", "gpad_datafile_write", "gpad_datafile_free",
     "gpad_setup_flat", "gpad_step2_primal_flat", "gpad_step4_project_flat", "gpad_precompute",
+    "gpad_accumulate_iterations",
 ]
 
 FILE_ROWMAJOR, FILE_FLIPPED, FILE_FLAT = 0, 1, 2
@@ -109,6 +110,7 @@ def load(path: str | None = None) -> C.CDLL:
     L.gpad_datafile_free.restype = None
     L.gpad_setup_flat.argtypes = [vp, C.POINTER(Dims), i, cvp, cvp, d]
     L.gpad_precompute.argtypes = [vp, i, i, i, i, i, cvp, cvp, cvp, vp, vp, vp]
+    L.gpad_accumulate_iterations.argtypes = [vp, vp]
     L.gpad_step2_primal_flat.argtypes = [vp, vp, vp, vp, vp, i, i, i]
     L.gpad_step4_project_flat.argtypes = [vp, vp, vp, vp, vp, vp, i, i, i]
     for name in ["gpad_create", "gpad_destroy", "gpad_set_stream", "gpad_sync", "gpad_setup",

@@ -179,6 +179,11 @@ class GpadSolver:
         check(self.lib.gpad_sync(self.h), "gpad_sync")
 
     # ---- per-state QP data / closed loop (gpad.m:79-95; include/gpad.h gpad_setup_plant) ---
+    def accumulate_iterations(self, acc) -> None:
+        """Enqueue acc += sum of the last run's per-instance iteration counts (acc: a 1-element
+        int64 device tensor); no host synchronisation."""
+        check(self.lib.gpad_accumulate_iterations(self.h, _ptr(acc)), "gpad_accumulate_iterations")
+
     def precompute(self, H, A, f=None, *, shared: bool = True):
         """acceldualgrad.m:11,20-21 on the device in fp64 (gpad_precompute): returns
         (ML = inv(H) A', gP = inv(H) f' or None, L = ||H||_F^2).  shared: one H (n x n), A (m x n)

@@ -200,6 +200,11 @@ void gpad_datafile_free(gpad_datafile_t* f);
 /* Per-instance iteration counts / convergence flags of the last run (device work finished). */
 int gpad_last_stats(gpad_handle_t h, gpad_stats_t* st);
 
+/* Enqueue, on the handle's stream, acc[0] += the sum of the last run's per-instance iteration
+ * counts (acc: one device int64).  Lets a caller count the work of back-to-back asynchronous
+ * runs without a host synchronisation per run (bench.py's timed loop). */
+int gpad_accumulate_iterations(gpad_handle_t h, long long* acc);
+
 /* Diagnostics (no reference counterpart): the phase plan the next phased panel solve of this
  * handle will follow, made from the previous solve's iteration counts by gpad_last_stats / a
  * stats-collecting run.  Writes up to cap phase ends (iterations; the last is N) and finisher
