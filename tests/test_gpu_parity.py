@@ -456,3 +456,28 @@ def test_acceldualgrad_mirror(gpu):
     gd = load_golden("battery_10x4")
     u, z, y = gpad_mpc.acceldualgrad(gd["H"], gd["q"], gd["G"], gd["g"], None, None, 10)
     assert np.allclose(u, gd["matlab_z_100"][:10], rtol=1e-12, atol=1e-14)
+
+
+@pytest.mark.gpu
+def test_accumulate_iterations_matches_stats(gpu):
+    """gpad_accumulate_iterations (bench.py's sync-free work count) equals the per-instance counts
+    the stats path reports, summed over back-to-back asynchronous runs (phased panel solves)."""
+    import torch
+
+    import bench
+    import gpad_mpc
+    n, m, B = 200, 200, 1500
+    ML, G, L, M, g = bench.make_shard(n, m, B, 0)
+    f32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(gpu)  # noqa: E731
+    dML, dG, dM, dg = f32(ML), f32(G), f32(M), f32(g)
+    z = torch.zeros(B, n, device=gpu)
+    y = torch.zeros(B, m, device=gpu)
+    s = gpad_mpc.GpadSolver(0)
+    s.setup(dML, dG, float(np.float32(L)), n=n, m=m, batch=B, shared=True)
+    acc = torch.zeros(1, dtype=torch.int64, device=gpu)
+    for _ in range(3):
+        s.run(z.zero_(), y.zero_(), dM, dg, 5000, 1e-4, stats=False)
+        s.accumulate_iterations(acc)
+    it = np.zeros(B, np.int32)
+    st = s.last_stats(iters=it)
+    assert int(acc.item()) == 3 * int(it.sum()) == 3 * st["total_iterations"]
