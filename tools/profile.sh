@@ -8,7 +8,7 @@
 set -e
 TAG=${1:-r01}
 shift || true
-ARGS=${@:---steps 3 --warmup 1 --no-cpu --no-extra}  # C4 solves only: the legs launch the same kernels
+ARGS=${@:---steps 12 --warmup 1 --no-cpu --no-extra}  # C4 solves only: the legs launch the same kernels
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
