@@ -59,46 +59,98 @@ def make_shard(n, m, batch, start, seed=0):
     return base.ML, G, base.L, M, Bv
 
 
-def cpu_baseline(n, m, ML, G, L, M, g, iters_per_instance, budget_s=12.0):
-    """The reference's own seq_functions.cpp (oracle/_ref, -O3 -march=x86-64-v3) in main.cu
-    loop order on this host: instance-iterations/s over a bounded sample, all host cores."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import pyoracle
-    O = pyoracle.Oracle()
-    kind = "reference"
-    path = pyoracle.REF_O3 if os.path.exists(pyoracle.REF_O3) else pyoracle.REF
-    if os.path.exists(path):
-        R = pyoracle.RefSeq(path)
-    else:
-        R, kind = None, "port"
-    ML32, G32, L32 = ML.astype(np.float32), G.astype(np.float32), np.float32(L)
-    MGneg, GL, _ = O.scale(ML32, G32, g[0].astype(np.float32), L32)
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    cores = max(1, min(cores, 16))
-    N = max(1, int(round(iters_per_instance)))
-    th, be = O.schedule_f32(N)
+def host_info():
+    """The host this run's CPU numbers come from: CPU model, the cores in this process's
+    affinity mask, the cgroup CPU quota (the GPU box grants a share of a larger machine) and
+    the thread count the CPU legs use = the quota when one is set, else the affinity count."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    threads = min(aff, quota) if quota else aff
+    return {"cpu_model": model, "nproc_affinity": aff, "cgroup_cpu_quota": quota, "threads": threads}
 
-    def run(count, threads):
-        GP = M[:count].astype(np.float32)
-        PD = O.scale_vec(g[:count], L32)
+
+class CpuRef:
+    """The reference's own seq_functions.cpp (oracle/_ref/libref_seq_o3.so: -O3 -march=x86-64-v3,
+    the timing build) in main.cu:160-175 loop order, OpenMP over instances (oracle/ref_driver.c);
+    the oracle's C port when the reference build is absent.  Test/measurement infrastructure:
+    only this CPU leg uses it, never the timed GPU region."""
+
+    def __init__(self):
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle
+        self.O = pyoracle.Oracle()
+        path = pyoracle.REF_O3 if os.path.exists(pyoracle.REF_O3) else pyoracle.REF
+        self.R = pyoracle.RefSeq(path) if os.path.exists(path) else None
+        self.kind = "reference" if self.R is not None else "port"
+        self.info = host_info()
+
+    def _run(self, MGneg, GP, GL, PD, N, shared, threads):
+        th, be = self.O.schedule_f32(N)
+        count, n = GP.shape
+        m = PD.shape[1]
         Z = np.zeros((count, n), np.float32)
         Y = np.zeros((count, m), np.float32)
         t0 = time.perf_counter()
-        if R is not None:
-            R.solve_batch_c(Z, Y, MGneg, GP, GL, PD, th, be, N, shared=True, threads=threads)
+        if self.R is not None:
+            self.R.solve_batch_c(Z, Y, MGneg, GP, GL, PD, th, be, N, shared=shared, threads=threads)
         else:
-            O.solve_batch_f32(Z, Y, MGneg, GP, GL, PD, N, L32, 0.0, threads=threads)
+            self.O.solve_batch_f32(Z, Y, MGneg, GP, GL, PD, N, 1.0, 0.0, shared=shared, threads=threads)
         return time.perf_counter() - t0
 
-    probe = run(cores, cores)  # one instance per core, to size the sample
-    count = int(max(cores, min(len(M), cores * max(1, int(budget_s / max(probe, 1e-6))))))
-    count = (count // cores) * cores
-    dt = run(count, cores)
-    t1 = run(1, 1)
-    return {"value": count * N / dt, "unit": "GPAD iterations/s", "cores": cores, "kind": kind,
-            "sample": f"{count} C4 instances x {N} iterations (fixed, = mean GPU iterations to "
-                      f"eps), shared ML/G, fp32, OpenMP over instances",
-            "single_thread_value": N / t1, "seconds": round(dt, 2)}
+    def rate(self, MGneg, GP, GL, PD, N, shared=True, threads=None, budget_s=3.0, what=""):
+        """Instance-iterations/s of N fixed iterations over a bounded sample: instances are taken
+        cyclically from the given ones (shared: GP/PD rows; distinct: whole instances) until the
+        sample costs about ``budget_s``."""
+        threads = threads or self.info["threads"]
+        pool = GP.shape[0]
+
+        def take(k):
+            idx = np.arange(k) % pool
+            if shared:
+                return MGneg, GP[idx], GL, PD[idx]
+            return MGneg[idx], GP[idx], GL[idx], PD[idx]
+
+        k0 = max(1, min(threads, 64))
+        probe = self._run(*take(k0), N, shared, threads)
+        per = probe / k0 * min(threads, k0)  # seconds per instance on one thread
+        count = int(max(threads, min(1 << 20, budget_s * threads / max(per, 1e-9))))
+        count = max(threads, (count // threads) * threads) if threads > 1 else max(1, count)
+        dt = self._run(*take(count), N, shared, threads)
+        return {"value": count * N / dt, "unit": "GPAD iterations/s", "cores": threads, "kind": self.kind,
+                "sample": f"{count} instances x {N} iterations{', ' + what if what else ''}, fp32, "
+                          f"{'OpenMP over instances' if threads > 1 else 'one thread'}",
+                "seconds": round(dt, 3), **{k: v for k, v in self.info.items() if k != "threads"}}
+
+
+def cpu_baseline(n, m, ML, G, L, M, g, iters_per_instance, budget_s=12.0, ref=None):
+    """Headline CPU baseline: the C4 workload (shared ML/G, this rank's q/b draws) for the mean
+    GPU iteration count to eps, all granted host cores; plus the single-thread rate."""
+    ref = ref or CpuRef()
+    O = ref.O
+    ML32, G32, L32 = ML.astype(np.float32), G.astype(np.float32), np.float32(L)
+    MGneg, GL, _ = O.scale(ML32, G32, g[0].astype(np.float32), L32)
+    N = max(1, int(round(iters_per_instance)))
+    GP = M.astype(np.float32)
+    PD = O.scale_vec(g.astype(np.float32), L32)
+    out = ref.rate(MGneg, GP, GL, PD, N, shared=True, budget_s=budget_s,
+                   what=f"C4 instances (shared ML/G), N = mean GPU iterations to eps")
+    one = ref.rate(MGneg, GP[:64], GL, PD[:64], N, shared=True, threads=1, budget_s=1.5)
+    out["single_thread_value"] = one["value"]
+    return out
 
 
 def phase_schedule(N, K=10, plan=None, fin=512):
@@ -169,7 +221,7 @@ def traffic_from_profile(kernel_name):
     return v["hbm_bytes_total"] / solves, os.path.relpath(path, ROOT)
 
 
-def hbm_leg(dev, batch=1024, n=800, m=800, N=20):
+def hbm_leg(dev, batch=1024, n=800, m=800, N=20, ref=None):
     """C5: long horizon (N = 200 -> n = 800), m = 800, 1024 instances with DISTINCT matrices:
     the matrices cannot stay on chip, so every iteration streams 5.1 MB per instance from HBM
     (stream kernel).  Returns achieved algorithmic GB/s vs the 8 TB/s roofline."""
@@ -198,13 +250,22 @@ def hbm_leg(dev, batch=1024, n=800, m=800, N=20):
             best = min(best, st["kernel_ms"])
     per_it = 4 * (2 * n * m + 4 * m + 3 * n)
     gbs = batch * N * per_it / (best / 1e3) / 1e9
-    return {"config": f"C5: {batch} distinct instances, N=200 (n={n}), m={m}, {N} iterations",
-            "kernel": st["kernel"], "iters_per_s": batch * N / (best / 1e3),
-            "achieved_GBs": gbs, "peak_GBs": HBM_PEAK_GBS, "frac": gbs / HBM_PEAK_GBS,
-            "bytes_per_instance_iter": per_it}
+    out = {"config": f"C5: {batch} distinct instances, N=200 (n={n}), m={m}, {N} iterations",
+           "kernel": st["kernel"], "iters_per_s": batch * N / (best / 1e3),
+           "achieved_GBs": gbs, "peak_GBs": HBM_PEAK_GBS, "frac": gbs / HBM_PEAK_GBS,
+           "bytes_per_instance_iter": per_it}
+    if ref is not None:  # the reference's CPU steps on a pool of these distinct instances
+        k = min(batch, 2 * ref.info["threads"])
+        L32 = np.float32(L)
+        MGneg = (-ML[:k]).cpu().numpy()
+        GL = (G[:k].double() * (1.0 / float(L32))).float().cpu().numpy()
+        PD = (gv[:k].double() * (-1.0 / float(L32))).float().cpu().numpy()
+        out["cpu_baseline"] = ref.rate(MGneg, M[:k].cpu().numpy(), GL, PD, N, shared=False,
+                                       what=f"C5 distinct 800x800 instances (pool of {k})")
+    return out
 
 
-def distinct_leg(dev, n, m, batch=8192, N=100):
+def distinct_leg(dev, n, m, batch=8192, N=100, ref=None):
     """C2-shape instances with distinct matrices, register-resident (resident kernel)."""
     import torch
 
@@ -220,11 +281,18 @@ def distinct_leg(dev, n, m, batch=8192, N=100):
         s.setup(ML, G, 10.0, n=n, m=m, batch=batch, shared=False)
         s.run(z, y, M, gv, N, 0.0)
         st = s.run(z.zero_(), y.zero_(), M, gv, N, 0.0)
-    return {"config": f"{batch} distinct {n}x{m} instances, {N} iterations", "kernel": st["kernel"],
-            "iters_per_s": batch * N / (st["kernel_ms"] / 1e3)}
+    out = {"config": f"{batch} distinct {n}x{m} instances, {N} iterations", "kernel": st["kernel"],
+           "iters_per_s": batch * N / (st["kernel_ms"] / 1e3)}
+    if ref is not None:
+        k = min(batch, 4 * ref.info["threads"])
+        GL = (G[:k].double() * 0.1).float().cpu().numpy()
+        PD = (gv[:k].double() * -0.1).float().cpu().numpy()
+        out["cpu_baseline"] = ref.rate((-ML[:k]).cpu().numpy(), M[:k].cpu().numpy(), GL, PD, N, shared=False,
+                                       what=f"distinct {n}x{m} instances (pool of {k})")
+    return out
 
 
-def c3_leg(dev, n=200, m=200, batch=4096, reps=3, max_iters=5000, tol=1e-4):
+def c3_leg(dev, n=200, m=200, batch=4096, reps=3, max_iters=5000, tol=1e-4, ref=None):
     """BASELINE config C3: 4096 instances sharing ML/G (N = 50: n = 200), m = 200, solved to
     eps = 1e-4 (Algorithm 1, K = 10) on the panel kernels -- the same generator as the headline
     shard, half its size (one panel per workgroup instead of pairs: 256 panels = 256 CUs)."""
@@ -243,12 +311,22 @@ def c3_leg(dev, n=200, m=200, batch=4096, reps=3, max_iters=5000, tol=1e-4):
             r = s.run(z.zero_(), y.zero_(), dM, dg, max_iters, tol)
             if r["kernel_ms"] < best:
                 best, st = r["kernel_ms"], r
-    return {"config": f"C3: {batch} instances sharing ML/G, n={n}, m={m}, eps={tol}", "kernel": st["kernel"],
-            "iters_per_s": st["total_iterations"] / (best / 1e3), "qp_solves_per_s": batch / (best / 1e3),
-            "mean_iters_to_eps": st["total_iterations"] / batch, "solve_ms": best}
+    out = {"config": f"C3: {batch} instances sharing ML/G, n={n}, m={m}, eps={tol}", "kernel": st["kernel"],
+           "iters_per_s": st["total_iterations"] / (best / 1e3), "qp_solves_per_s": batch / (best / 1e3),
+           "mean_iters_to_eps": st["total_iterations"] / batch, "solve_ms": best}
+    if ref is not None:
+        N = max(1, int(round(st["total_iterations"] / batch)))
+        O = ref.O
+        L32 = np.float32(L)
+        MGneg, GL, _ = O.scale(ML.astype(np.float32), G.astype(np.float32), g[0].astype(np.float32), L32)
+        c = ref.rate(MGneg, M.astype(np.float32), GL, O.scale_vec(g.astype(np.float32), L32), N, shared=True,
+                     what="C3 instances (shared ML/G), N = mean GPU iterations to eps")
+        c["qp_solves_per_s"] = c["value"] / N
+        out["cpu_baseline"] = c
+    return out
 
 
-def flat_leg(dev, batch=8192, N=100, horizon=10):
+def flat_leg(dev, batch=8192, N=100, horizon=10, ref=None):
     """the flat (equal-cell) battery path vs the full-matrix path on the
     same battery packs (n_u = 4; horizon 10: n = 40, m = 180 = C1; horizon 50: n = 200, m = 900,
     the full path then on the big-panel kernel), fixed N iterations, fp32."""
@@ -279,6 +357,20 @@ def flat_leg(dev, batch=8192, N=100, horizon=10):
                 st = s.run(Z.zero_(), Y.zero_(), GP, PD, N, 0.0, scaled=True)
                 best = min(best, st["kernel_ms"])
         out[name] = {"kernel": st["kernel"], "iters_per_s": batch * N / (best / 1e3)}
+    if ref is not None and ref.R is not None:  # the reference's own flat steps, one thread
+        th, be = ref.O.schedule_f32(N)
+        MGf32 = np.ascontiguousarray(np.asarray(MGf, np.float64).astype(np.float32))
+        GLf32 = np.ascontiguousarray(np.asarray(GLf, np.float64).astype(np.float32))
+        GPh, PDh = GP.cpu().numpy(), PD.cpu().numpy()
+        k, t0 = 0, time.perf_counter()
+        while k < batch and time.perf_counter() - t0 < 2.0:
+            ref.R.solve_flat_c(np.zeros(qp.n, np.float32), np.zeros(qp.m, np.float32), MGf32, GPh[k], GLf32,
+                               PDh[k], 4, th, be, N)
+            k += 1
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": k * N / dt, "unit": "GPAD iterations/s", "cores": 1, "kind": "reference",
+                               "sample": f"{k} packs x {N} iterations, the reference's flat steps "
+                                         "(StepTwo/FourGPADFlatSequential), one thread"}
     return out
 
 
@@ -335,6 +427,25 @@ def closed_loop_leg(dev, batch=8192, steps=20, N=100, cpu=True, flat=False):
     return out
 
 
+def make_stream(n, m, batch, count, rank, seed=0):
+    """``count`` independent draws of this rank's shard for the timed steps: every step solves
+    NEW problems (q, b of the SURVEY §8d generator, fresh per instance and per step), so the
+    phase plan and the finisher's longest-first queue -- both built from the previous solve's
+    iteration counts -- predict from a different problem, as in an MPC stream.  Vectorised
+    numpy draws (one generator per rank and step), shared matrices from ``seed``."""
+    from gpad_mpc import problems
+    base = problems.synthetic_qp(n, m, batch=1, seed=seed)
+    G, Hinv = base.G, np.linalg.inv(base.H)
+    out = []
+    for k in range(count):
+        rng = np.random.default_rng([seed, 7919, rank, k])
+        zf = rng.uniform(-0.5, 0.5, size=(batch, n))
+        Bv = zf @ G.T + rng.uniform(0.1, 1.0, size=(batch, m))
+        M = rng.normal(0.0, 1.0, size=(batch, n)) @ Hinv.T
+        out.append((M, Bv))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -349,6 +460,9 @@ def main():
     ap.add_argument("--kernel", default="auto", choices=["auto", "stream", "resident", "panel"])
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C2/C5 side legs")
+    ap.add_argument("--repeat-inputs", action="store_true",
+                    help="headline on the SAME inputs every step (the planner then sees its own future); "
+                         "default: fresh inputs per step, the repeated-input rate reported beside it")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) for real runs; gloo to rehearse ranks sharing one GPU")
     args = ap.parse_args()
@@ -379,6 +493,8 @@ def main():
     ML, G, L, M, g = make_shard(n, m, B, rank * B)
     f32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)  # noqa: E731
     dML, dG, dM, dg = f32(ML), f32(G), f32(M), f32(g)
+    # fresh problems for every warm-up and timed step, resident in HBM before timing
+    fresh = [(f32(a), f32(b)) for a, b in make_stream(n, m, B, args.warmup + args.steps, rank)]
     z = torch.zeros(B, n, device=dev)
     y = torch.zeros(B, m, device=dev)
     kern = {"auto": _lib.KERNEL_AUTO, "stream": _lib.KERNEL_STREAM, "resident": _lib.KERNEL_RESIDENT,
@@ -390,99 +506,128 @@ def main():
     packed = torch.empty(B, n + m, device=dev)
     counts = [B] * world
 
-    def step():
+    def step(Mv, gv):
         z.zero_()
         y.zero_()
-        solver.run(z, y, dM, dg, args.max_iters, args.tol, stats=False)
+        solver.run(z, y, Mv, gv, args.max_iters, args.tol, stats=False)
         if world > 1:  # one RCCL gather of (z*, y*) to rank 0
             packed[:, :n] = z
             packed[:, n:] = y
             parallel.gather_rows(packed.to(comm_dev), world, rank, counts)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    iters_host = np.zeros(B, np.int32)
-    st0 = solver.last_stats(iters=iters_host)
-    util = phase_util(iters_host, args.max_iters, 10, solver.phase_plan())
+    def timed(inputs):
+        """W warm-up steps, then K timed steps enqueued back to back with no host
+        synchronisation: each step's work (the sum of its per-instance iteration counts) is
+        accumulated on the device after its solve; HIP events on the solve stream bracket the
+        K steps (device time of the solves plus the z/y resets, a few us per step).
+        inputs(k) -> (M, g) of step k (k < W: warm-up)."""
+        for k in range(args.warmup):
+            step(*inputs(k))
+        torch.cuda.synchronize(dev)
+        acc = torch.zeros(1, dtype=torch.int64, device=dev)
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for k in range(args.steps):
+            step(*inputs(args.warmup + k))
+            solver.accumulate_iterations(acc)
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        kern_ms = ev0.elapsed_time(ev1)
+        total_iters = int(acc.item())
+        iters_host = np.zeros(B, np.int32)
+        st = solver.last_stats(iters=iters_host)  # the last step's counters, outside the timed region
+        # max time over ranks, sum of work over ranks
+        stats = torch.tensor([dt, float(total_iters), kern_ms, float(st["converged"])], dtype=torch.float64,
+                             device=comm_dev)
+        if world > 1:
+            tmax = stats[0:1].clone()
+            dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+            work = stats[1:4].clone()
+            dist.all_reduce(work, op=dist.ReduceOp.SUM)
+            dt_all, iters_all, conv_all = float(tmax.item()), float(work[0].item()), float(work[2].item())
+        else:
+            dt_all, iters_all, conv_all = dt, float(total_iters), float(st["converged"])
+        return dict(dt=dt_all, iters_all=iters_all, converged_all=conv_all, total_iters=total_iters,
+                    kern_ms=kern_ms, st=st, iters_host=iters_host, plan=solver.phase_plan())
 
-    # The K steps are enqueued back to back with no host synchronisation: each step's work (the
-    # sum of its per-instance iteration counts) is accumulated on the device after its solve,
-    # and HIP events on the solve stream bracket the K steps (device time of the solves plus the
-    # z/y resets, a few us per step).
-    acc = torch.zeros(1, dtype=torch.int64, device=dev)
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-        solver.accumulate_iterations(acc)
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1)
-    total_iters = int(acc.item())
-    st = solver.last_stats()  # the last step's counters (converged count), outside the timed region
-    # max time over ranks, sum of work over ranks
-    stats = torch.tensor([dt, float(total_iters), kern_ms, float(st["converged"])], dtype=torch.float64,
-                         device=comm_dev)
-    if world > 1:
-        tmax = stats[0:1].clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        work = stats[1:4].clone()
-        dist.all_reduce(work, op=dist.ReduceOp.SUM)
-        dt = float(tmax.item())
-        total_iters_all = float(work[0].item())
-        converged_all = float(work[2].item())
-    else:
-        total_iters_all = float(total_iters)
-        converged_all = float(st["converged"])
+    fresh_run = timed(lambda k: fresh[k])
+    repeat_run = timed(lambda k: (dM, dg))
+    head = repeat_run if args.repeat_inputs else fresh_run
+    side = fresh_run if args.repeat_inputs else repeat_run
+
+    # CPU reference on rank 0 (all ranks' timed regions are over: the barrier above)
+    ref = None
+    if rank == 0 and not args.no_cpu:
+        ref = CpuRef()
 
     if rank == 0:
+        dt, st, total_iters, kern_ms = head["dt"], head["st"], head["total_iters"], head["kern_ms"]
         ms_per_step = dt / args.steps * 1e3
-        value = total_iters_all / dt
+        value = head["iters_all"] / dt
         solves = B * world * args.steps / dt
         avg_kernel_s = kern_ms / args.steps / 1e3
         iters_per_launch = total_iters / args.steps
         F = flops_per_iter(n, m)
         achieved_tf = iters_per_launch * F / avg_kernel_s / 1e12
         mean_iters = iters_per_launch / B
-        # C2 single instance (config 1): latency kernel, fixed 1000 iterations
-        one = dict()
+        util = phase_util(head["iters_host"], args.max_iters, 10, head["plan"])
         T = (max(n, m) + 15) // 16
         kname = (f"gpad::gpad_panel2_kernel<{T}>" if T > 8 else f"gpad::gpad_panel_kernel<{T}>") \
             if st["kernel"] == "panel" else f"gpad::gpad_{st['kernel']}_kernel"
         traffic, traffic_src = traffic_from_profile(kname)
         launches = util["launches_per_solve"] if st["kernel"] == "panel" else 1
-        with gpad_mpc.GpadSolver(dev.index, stream=stream.cuda_stream) as s1:
-            s1.setup(dML, dG, L32, n=n, m=m, batch=1)
-            z1 = torch.zeros(1, n, device=dev)
-            y1 = torch.zeros(1, m, device=dev)
-            s1.run(z1, y1, dM[:1], dg[:1], 1000, 0.0)
-            t = []
-            for _ in range(3):
-                st1 = s1.run(z1.zero_(), y1.zero_(), dM[:1], dg[:1], 1000, 0.0)
-                t.append(st1["kernel_ms"])
-            one = {"config": "C2 single instance n=200 m=200", "kernel": st1["kernel"],
-                   "iters_per_s": 1000 / (min(t) / 1e3)}
+        # single instances (configs C1 and C2): latency kernels, fixed iteration counts
+        singles = {}
+        from gpad_mpc import problems
+        qp1 = problems.battery_mpc(4, 10, seed=0)
+        c1 = [np.ascontiguousarray(np.asarray(a, np.float64).astype(np.float32))
+              for a in (qp1.ML, qp1.G, qp1.M, qp1.g)]
+        for name, (mML, mG, mM, mg_, mL, iters) in {
+                "c2": (dML, dG, dM[:1], dg[:1], L32, 1000),
+                "c1": (*[f32(a) for a in c1[:2]], f32(c1[2]).reshape(1, -1), f32(c1[3]).reshape(1, -1),
+                       float(np.float32(qp1.L)), 1000)}.items():
+            nn, mm = mML.shape
+            with gpad_mpc.GpadSolver(dev.index, stream=stream.cuda_stream) as s1:
+                s1.setup(mML, mG, mL, n=nn, m=mm, batch=1)
+                z1 = torch.zeros(1, nn, device=dev)
+                y1 = torch.zeros(1, mm, device=dev)
+                s1.run(z1, y1, mM, mg_, iters, 0.0)
+                t = []
+                for _ in range(3):
+                    st1 = s1.run(z1.zero_(), y1.zero_(), mM, mg_, iters, 0.0)
+                    t.append(st1["kernel_ms"])
+            singles[name] = {"config": ("C2 single instance n=200 m=200" if name == "c2" else
+                                        f"C1 single instance: battery n_u=4, N=10 (n={nn}, m={mm})"),
+                             "kernel": st1["kernel"], "iters_per_s": iters / (min(t) / 1e3)}
+            if ref is not None:  # the reference's CPU steps on the same instance, one thread
+                O = ref.O
+                hm = [a.cpu().numpy() for a in (mML, mG, mM, mg_)]
+                MGneg, GLh, _ = O.scale(hm[0], hm[1], hm[3][0], np.float32(mL))
+                singles[name]["cpu_baseline"] = ref.rate(
+                    MGneg, hm[2], GLh, O.scale_vec(hm[3], np.float32(mL)), iters,
+                    shared=True, threads=1, budget_s=1.5, what=singles[name]["config"])
         cpu = None
-        if not args.no_cpu and world == 1:
-            cpu = cpu_baseline(n, m, ML, G, L, M, g, mean_iters)
+        if ref is not None:
+            cpu = cpu_baseline(n, m, ML, G, L, M, g, mean_iters, ref=ref)
+            cpu["qp_solves_per_s"] = cpu["value"] / max(1, int(round(mean_iters)))
         extra = {}
         if not args.no_extra and world == 1:
-            extra["hbm_bound_c5"] = hbm_leg(dev)
-            extra["distinct_c2_batch"] = distinct_leg(dev, n, m)
-            extra["c3_batch4096"] = c3_leg(dev, n, m)
+            extra["hbm_bound_c5"] = hbm_leg(dev, ref=ref)
+            extra["distinct_c2_batch"] = distinct_leg(dev, n, m, ref=ref)
+            extra["c3_batch4096"] = c3_leg(dev, n, m, ref=ref)
             extra["closed_loop_battery"] = closed_loop_leg(dev, cpu=not args.no_cpu)
             extra["closed_loop_battery_flat"] = closed_loop_leg(dev, cpu=False, flat=True)
-            extra["flat_battery_c1"] = flat_leg(dev)
-            extra["battery_n50"] = flat_leg(dev, horizon=50, N=50)
+            extra["flat_battery_c1"] = flat_leg(dev, ref=ref)
+            extra["battery_n50"] = flat_leg(dev, horizon=50, N=50, ref=ref)
+        side_value = side["iters_all"] / side["dt"]
         out = {
             "metric": "GPAD iterations/s (instance-iterations, solve to eps=1e-4)",
             "value": value,
@@ -495,17 +640,25 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded SURVEY.md §8d generator; shared ML/G, per-instance q/b)",
+            "data": ("synthetic (seeded SURVEY.md §8d generator; shared ML/G, per-instance q/b; "
+                     + ("the same q/b every step" if args.repeat_inputs else
+                        "FRESH q/b draws every step, resident in HBM before timing") + ")"),
             "config": {"workload": f"C4 shard: {B} instances/GPU, N={args.horizon} (n={n}), m={m}, "
                                    f"shared ML/G, Algorithm 1 eps={args.tol}, K=10",
                        "batch_per_gpu": B, "global_batch": B * world, "n": n, "m": m,
+                       "inputs": "repeated" if args.repeat_inputs else "fresh per step",
                        "parallelism": f"instance-sharded x{world}, RCCL gather"},
             "qp_solves_per_s": solves,
             "mean_iters_to_eps": mean_iters,
+            ("value_fresh_inputs" if args.repeat_inputs else "value_repeated_inputs"): side_value,
+            "repeated_inputs_note": "the same q/b every step: the phase plan and the finisher's "
+                                    "longest-first queue are built from the previous solve's exact "
+                                    "per-instance counts, i.e. perfect foresight",
             "batching": util,
-            "converged": int(converged_all),
+            "converged": int(head["converged_all"]),
             "kernel": st["kernel"],
-            "single_instance": one,
+            "single_instance": singles["c2"],
+            "single_instance_c1": singles["c1"],
             "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved_tf / FP32_PEAK_TFLOPS,
                          "traffic": traffic, "traffic_source": traffic_src,

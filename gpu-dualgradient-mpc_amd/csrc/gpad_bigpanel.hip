@@ -300,11 +300,7 @@ __global__ __launch_bounds__(64 * kBigWaves) void gpad_bigpanel_kernel(SolveArgs
                 const int t = w + kBigWaves * q;
                 // tiles q, q + 1 of this wave in one interleaved pass (acc of q + 1 kept for the next q)
                 bf32x4 acc;
-#ifndef BIG_NOPAIR
                 constexpr bool kPair = NT2 > 1;
-#else
-                constexpr bool kPair = false;
-#endif
                 if constexpr (kPair) {
                     if ((q & 1) == 0) {
                         if (t + kBigWaves < T2) {

@@ -436,19 +436,7 @@ __global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<flo
         }
         int v = 0;
         float th = a.theta[0], bn = a.beta[1];
-#ifdef FP_TIMING
-        unsigned long long tm[5] = {0, 0, 0, 0, 0}, tlast = __builtin_amdgcn_s_memtime();
-#define FP_T(i)                                                \
-    {                                                          \
-        const unsigned long long tt_ = __builtin_amdgcn_s_memtime(); \
-        tm[(i) - 1] += tt_ - tlast;                             \
-        tlast = tt_;                                           \
-    }
-#else
-#define FP_T(i)
-#endif
         while (true) {
-            FP_T(5);
             const float th_next = a.theta[v + 1], bn_next = a.beta[v + 2];
             ++v;
             const bool chk = use_tol && (v % K) == 0;
@@ -488,9 +476,7 @@ __global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<flo
                 pre2 = fp_pre<ALDS>(PA, As, fp_voff2(g, x, lane), (x.cell < 0 ? g.KBe : g.KBc) * 1024,
                               x.cell < 0 ? g.KB3 : g.T1);
             }
-            FP_T(1);
             __syncthreads();
-            FP_T(2);
             // ---- 8d + next 8a: cell and coupling chains; w back to LDS; test partials per unit -------
 #pragma unroll
             for (int q = 0; q < NU2; ++q) {
@@ -555,9 +541,7 @@ __global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<flo
             }
             th = th_next;
             bn = bn_next;
-            FP_T(3);
             __syncthreads();
-            FP_T(4);
             if (!chk && v < N) continue;
 
             unsigned long long m1 = 0ull, m2 = 0ull;
@@ -624,9 +608,6 @@ __global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<flo
             if (live == 0ull) break;
         }
         __syncthreads();  // the next group reuses the LDS arrays
-#ifdef FP_TIMING
-        if (blockIdx.x == 0 && lane == 0 && grp == 0) printf("fpt w%d v%d p1 %llu b1 %llu p2 %llu b2 %llu chk %llu\n", w, v, tm[0], tm[1], tm[2], tm[3], tm[4]);
-#endif
     }
 }
 
@@ -676,7 +657,7 @@ static hipError_t launch_flatpanel_w8(const SolveArgs<float>& a, FlatGeom g, int
     }
     size_t lds = flatpanel_lds_bytes(g, P);
     const size_t abytes = (size_t)g.total * 16;
-    const bool alds = 2 * (lds + abytes) <= 160 * 1024 && !std::getenv("GPAD_FLAT_NO_ALDS");
+    const bool alds = 2 * (lds + abytes) <= 160 * 1024 && (!a.tune || a.tune->flat_a_lds);
     if (alds) lds += abytes;
     const int groups = (panels + P - 1) / P;
     const int grid = std::min(groups, 2 * a.num_cus);
@@ -695,11 +676,12 @@ hipError_t launch_flatpanel(const SolveArgs<float>& a, hipStream_t s) {
     if (!flatpanel_supported(a.n, a.m, a.n_u) || !a.frag) return hipErrorInvalidValue;
     FlatGeom g = flat_geom(a.n, a.m, a.n_u);
     const int panels = (a.batch + 15) / 16;
-    if (const char* we = std::getenv("GPAD_FLAT_WAVES"); we && std::atoi(we) == 8) {  // A/B knob
+    const Tuning tn = a.tune ? *a.tune : Tuning{};
+    if (tn.flat_waves == 8) {  // forced 8-wave workgroups
         bool taken = false;
         const hipError_t e = launch_flatpanel_w8(a, g, panels, s, true, &taken);
         if (taken || e != hipSuccess) return e;
-    } else if (!std::getenv("GPAD_FLAT_WAVES")) {
+    } else if (tn.flat_waves == 0) {
         // default: two 8-wave workgroups per CU when each can hold two panels (C1 packs from 16384:
         // 5.41 -> 5.23 us per batch-iteration); at one panel each they lose to one 16-wave
         // workgroup of two panels (8192: 3.03 vs 3.28 us)
@@ -715,7 +697,7 @@ hipError_t launch_flatpanel(const SolveArgs<float>& a, hipStream_t s) {
             break;
         }
     }
-    if (const char* e = std::getenv("GPAD_FLAT_PANELS")) P = std::max(1, std::min(4, std::atoi(e)));  // A/B knob
+    if (tn.flat_panels > 0) P = std::min(4, tn.flat_panels);
     while (P > 1 && (P * g.U1 > 4 * kFlatPanelWaves || P * g.U2 > 4 * kFlatPanelWaves ||
                      flatpanel_lds_bytes(g, P) > 160 * 1024))
         --P;
@@ -730,7 +712,7 @@ hipError_t launch_flatpanel(const SolveArgs<float>& a, hipStream_t s) {
     }
     size_t lds = flatpanel_lds_bytes(g, P);
     const size_t abytes = (size_t)g.total * 16;
-    const bool alds = lds + abytes <= 160 * 1024 && !std::getenv("GPAD_FLAT_NO_ALDS");  // A image in LDS
+    const bool alds = lds + abytes <= 160 * 1024 && tn.flat_a_lds;  // A image in LDS
     if (alds) lds += abytes;
     const int groups = (panels + P - 1) / P;
     int grid = a.num_cus * (lds * 2 <= 160 * 1024 ? 2 : 1);

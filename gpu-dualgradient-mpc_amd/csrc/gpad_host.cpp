@@ -96,6 +96,14 @@ struct gpad_handle_s {
     bool scaled = false;
     int ldn = 0, ldm = 0;
     DevBuf MGt, GLt, frag, stage;
+    bool frag_ok = false;      // frag holds the fragment image of the bound matrices
+    bool keep_stage = false;   // gpad_solve's cached handle keeps its staging buffer
+    // gpad_solve: host copy of the last bound (ML, G, L, dims) so a repeated one-shot call on
+    // the same host matrices skips the H2D copy and repack
+    std::vector<unsigned char> shadow;
+    gpad_dims_t shadow_dims{};
+    double shadow_L = 0.0;
+    bool shadow_ok = false;
     DevBuf GLx;  // flat path: flat G_L expanded to the full k-major image (flat resident kernel)
     int frag_tiles = 0;
     DevBuf theta, beta;
@@ -118,6 +126,7 @@ struct gpad_handle_s {
     DevBuf state;                       // per-state workspaces (M(x), g(x), x ping-pong, ...)
     int num_cus = 256;
     bool timed = false;
+    gpad::Tuning tune;                  // gpad_set_option
 };
 
 extern "C" {
@@ -191,6 +200,40 @@ int gpad_set_stream(gpad_handle_t h, void* stream) {
     return GPAD_OK;
 }
 
+int gpad_set_option(gpad_handle_t h, int option, int value) {
+    if (!h) return fail(GPAD_ERR_INVALID, "gpad_set_option: null handle");
+    gpad::Tuning& t = h->tune;
+    const gpad::Tuning def{};
+    auto set = [&](int& field, int lo, int hi, int dflt) -> int {
+        if (value == GPAD_OPT_DEFAULT) {
+            field = dflt;
+            return GPAD_OK;
+        }
+        if (value < lo || value > hi) return fail(GPAD_ERR_INVALID, "gpad_set_option: value out of range");
+        field = value;
+        return GPAD_OK;
+    };
+    const int big = 1 << 30;
+    switch (option) {
+        case GPAD_OPT_PHASE_LEN: return set(t.phase_len, 0, big, def.phase_len);
+        case GPAD_OPT_FINISH_THRESH: return set(t.finish_thresh, 0, big, def.finish_thresh);
+        case GPAD_OPT_PLAN: h->plan.nph = 0; h->plan_key = 0; return set(t.plan, 0, 1, def.plan);
+        case GPAD_OPT_PHASED: return set(t.phased, 0, 1, def.phased);
+        case GPAD_OPT_FINISHER: return set(t.finisher, 0, 1, def.finisher);
+        case GPAD_OPT_LPT: return set(t.lpt, 0, 1, def.lpt);
+        case GPAD_OPT_PANEL_MAX_GRID: return set(t.panel_max_grid, 0, big, def.panel_max_grid);
+        case GPAD_OPT_DUO_MAX_GRID: return set(t.duo_max_grid, 0, big, def.duo_max_grid);
+        case GPAD_OPT_FLAT_PANEL_MIN: return set(t.flat_panel_min, 0, big, def.flat_panel_min);
+        case GPAD_OPT_FLAT_PANELS: return set(t.flat_panels, 0, 4, def.flat_panels);
+        case GPAD_OPT_FLAT_WAVES:
+            if (value != GPAD_OPT_DEFAULT && value != 0 && value != 8 && value != 16)
+                return fail(GPAD_ERR_INVALID, "gpad_set_option: flat waves must be 0, 8 or 16");
+            return set(t.flat_waves, 0, 16, def.flat_waves);
+        case GPAD_OPT_FLAT_A_LDS: return set(t.flat_a_lds, 0, 1, def.flat_a_lds);
+        default: return fail(GPAD_ERR_INVALID, "gpad_set_option: unknown option");
+    }
+}
+
 int gpad_sync(gpad_handle_t h) {
     if (!h) return fail(GPAD_ERR_INVALID, "gpad_sync: null handle");
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -228,7 +271,9 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
     HIP_TRY(hipSetDevice(h->device));
     h->ready = false;
     h->flat = false;
+    h->shadow_ok = false;
     h->plan.nph = 0;
+    h->last_phased = false;
     h->dims = *d;
     if (h->dims.check_every <= 0) h->dims.check_every = 10;
     h->L = L;
@@ -266,8 +311,9 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
         HIP_TRY(gpad::launch_pack_kmajor<double>((const double*)dB, (double*)h->GLt.p, m, n, h->ldm, sb,
                                                  nmats, in_stride, (long long)b_elems, h->stream));
     }
-    // fragment image for the MFMA panel kernel (shared f32 matrices only)
-    h->frag.release();
+    // fragment image for the MFMA panel kernel (shared f32 matrices only); the buffer is kept
+    // across setups and only grows
+    h->frag_ok = false;
     h->frag_tiles = 0;
     if (d->shared && d->dtype == GPAD_DTYPE_F32) {
         const size_t fb = gpad::panel_frag_bytes(n, m, d->batch);
@@ -276,10 +322,11 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
             HIP_TRY(gpad::launch_pack_panel((const float*)dA, (const float*)dB, n, m, d->batch,
                                             (float)sa, sb, h->frag.p, h->stream));
             h->frag_tiles = gpad::panel_tiles(n, m, d->batch);
+            h->frag_ok = true;
         }
     }
     HIP_TRY(hipStreamSynchronize(h->stream));
-    if (d->memory == GPAD_MEM_HOST) h->stage.release();
+    if (d->memory == GPAD_MEM_HOST && !h->keep_stage) h->stage.release();
     h->ready = true;
     return GPAD_OK;
 }
@@ -307,7 +354,9 @@ int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* d, int n_u, const float*
     HIP_TRY(hipSetDevice(h->device));
     h->ready = false;
     h->flat = false;
+    h->shadow_ok = false;
     h->plan.nph = 0;
+    h->last_phased = false;
     h->dims = *d;
     if (h->dims.check_every <= 0) h->dims.check_every = 10;
     h->L = L;
@@ -333,7 +382,7 @@ int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* d, int n_u, const float*
         HIP_TRY(gpad::launch_expand_flat_gl((const float*)dG, (float*)h->GLx.p, Nh, n_u, m, h->ldm,
                                             h->stream));
     }
-    h->frag.release();
+    h->frag_ok = false;
     h->frag_tiles = 0;
     {  // MFMA panels over the flat data (gpad_flatpanel.hip)
         const size_t fb = gpad::flatpanel_frag_bytes(d->n, m, n_u);
@@ -341,10 +390,11 @@ int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* d, int n_u, const float*
             if ((rc = h->frag.ensure(fb))) return rc;
             HIP_TRY(gpad::launch_pack_flatpanel((const float*)h->MGt.p, (const float*)h->GLt.p, d->n, m, n_u,
                                                 h->frag.p, h->stream));
+            h->frag_ok = true;
         }
     }
     HIP_TRY(hipStreamSynchronize(h->stream));
-    if (d->memory == GPAD_MEM_HOST) h->stage.release();
+    if (d->memory == GPAD_MEM_HOST && !h->keep_stage) h->stage.release();
     h->n_u = n_u;
     h->flat = true;
     h->ready = true;
@@ -420,7 +470,7 @@ static int collect_stats(gpad_handle_t h, gpad_stats_t* st) {
         for (int b = 0; b < batch; ++b) key = (key ^ (unsigned)h->h_counts[b]) * 1099511628211ull;
         if (key != h->plan_key || h->plan.nph == 0) {
             gpad::panel_plan(h->h_counts.data(), batch, h->dims.n, h->dims.m, h->last_N, h->dims.check_every,
-                             h->num_cus, &h->plan);
+                             h->num_cus, &h->tune, &h->plan);
             h->plan_key = key;
         }
     }
@@ -465,7 +515,7 @@ int gpad_plan_phases(const int* iters, int batch, int n, int m, int N, int check
     if (!iters || batch <= 0 || n <= 0 || m <= 0 || N <= 0 || num_cus <= 0)
         return fail(GPAD_ERR_INVALID, "gpad_plan_phases: bad argument");
     gpad::PanelPlan p;
-    gpad::panel_plan(iters, batch, n, m, N, check_every, num_cus, &p);
+    gpad::panel_plan(iters, batch, n, m, N, check_every, num_cus, nullptr, &p);
     for (int i = 0; i < p.nph && i < cap; ++i) {
         if (ends) ends[i] = p.ends[i];
         if (fins) fins[i] = p.fins[i];
@@ -488,7 +538,7 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
     a.GLt = (const T*)h->GLt.p;
     a.strideA = d.shared ? 0 : (long long)m * h->ldn;
     a.strideB = d.shared ? 0 : (long long)n * h->ldm;
-    a.frag = h->frag.p;
+    a.frag = h->frag_ok ? h->frag.p : nullptr;
     a.frag_tiles = h->frag_tiles;
     a.gP = dM;
     a.g = dg;
@@ -511,7 +561,10 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
     a.iters = iters;
     a.conv = conv;
     a.num_cus = h->num_cus;
+    a.tune = &h->tune;
     int kernel = d.kernel;
+    h->last_phased = false;  // set again below when this launch is a phased panel solve
+    h->last_N = N;
     hipError_t e = hipSuccess;
     bool ok = false;
     if (N == 0) {  // nothing to iterate: outputs are the inputs, zero counts
@@ -527,9 +580,8 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
             // (their per-CU cost grows with the batch, a panel's does not until every CU holds
             // one: crossover ~2048 at C1, tools/fp_cross.py); always when only the LDS flat
             // kernel would be left (several times slower at any batch)
-            const char* fpe = std::getenv("GPAD_FLAT_PANEL_MIN");  // tuning knob
-            const int fpm = fpe ? std::atoi(fpe) : (h->GLx.p ? 8 * h->num_cus : 0);
-            if (h->frag.p && (kernel == GPAD_KERNEL_PANEL || (kernel == GPAD_KERNEL_AUTO && batch >= fpm))) {
+            const int fpm = h->tune.flat_panel_min >= 0 ? h->tune.flat_panel_min : (h->GLx.p ? 8 * h->num_cus : 0);
+            if (h->frag_ok && (kernel == GPAD_KERNEL_PANEL || (kernel == GPAD_KERNEL_AUTO && batch >= fpm))) {
                 e = gpad::launch_flatpanel(a, h->stream);
             } else if (h->GLx.p && kernel != GPAD_KERNEL_STREAM) {  // register-resident flat chains
                 a.GLt = (const T*)h->GLx.p;
@@ -548,7 +600,7 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
         // run at ~one round (4 per CU: 4 x its 1/6-panel iteration time < one panel iteration)
         const int panel_min = gpad::resident_supported(n, m) ? 4 * h->num_cus : 64;
         if (kernel == GPAD_KERNEL_PANEL || (kernel == GPAD_KERNEL_AUTO && d.shared && batch > panel_min)) {
-            if (tol > 0.0 && h->frag.p) {  // phased compaction workspace (gpad_panel.hip)
+            if (tol > 0.0 && h->frag_ok) {  // phased compaction workspace (gpad_panel.hip)
                 int rc = h->pwork.ensure(gpad::panel_work_bytes(m, batch));
                 if (rc) return rc;
                 a.pwork = h->pwork.p;
@@ -584,7 +636,6 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
     }
     *kernel_out = kernel;
     h->last_phased = kernel == GPAD_KERNEL_PANEL && a.pwork != nullptr;
-    h->last_N = N;
     return GPAD_OK;
 }
 
@@ -663,6 +714,9 @@ int gpad_run_scaled(gpad_handle_t h, void* z0, void* y0, const void* gP, const v
 
 int gpad_solve(void* z0, void* y0, const void* ML, const void* M, const void* G, const void* g, int N,
                double L, double tol, const gpad_dims_t* dims, gpad_stats_t* st) {
+    // One handle per thread and device, kept between calls: a per-MPC-step caller (gpad.m:90)
+    // pays the handle, the workspaces and -- when the host matrices are unchanged -- the H2D
+    // copy and repack of ML/G once, not per call.
     struct Cache {
         gpad_handle_t h = nullptr;
         int device = -1;
@@ -671,21 +725,41 @@ int gpad_solve(void* z0, void* y0, const void* ML, const void* M, const void* G,
         }
     };
     thread_local Cache cache;
+    int rc = validate_dims(dims);
+    if (rc) return rc;
+    if (!ML || !G) return fail(GPAD_ERR_INVALID, "gpad_solve: null matrix");
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
     if (!cache.h || cache.device != dev) {
         if (cache.h) gpad_destroy(cache.h);
         cache.h = nullptr;
-        int rc = gpad_create(&cache.h, dev, nullptr);
-        if (rc) return rc;
+        if ((rc = gpad_create(&cache.h, dev, nullptr))) return rc;
         cache.device = dev;
+        cache.h->keep_stage = true;
     }
-    int rc = gpad_setup(cache.h, dims, ML, G, L);
-    if (rc) return rc;
-    gpad_stats_t local{};
-    rc = gpad_run(cache.h, z0, y0, M, g, N, tol, st ? st : &local);
-    if (rc) return rc;
-    return gpad_sync(cache.h);
+    gpad_handle_t h = cache.h;
+    // host matrices: reuse the bound problem when (dims, L, ML, G) equal the last call's; the
+    // comparison is the full contents (a caller may rewrite its buffers in place).  Device
+    // matrices are always repacked (two stream-ordered pack kernels, no copy).
+    const bool host = dims->memory == GPAD_MEM_HOST;
+    const size_t bytes = (size_t)dims->n * dims->m * esize(dims->dtype) * (dims->shared ? 1 : dims->batch);
+    bool same = false;
+    if (host && h->ready && h->shadow_ok && L == h->shadow_L &&
+        std::memcmp(&h->shadow_dims, dims, sizeof(gpad_dims_t)) == 0 && h->shadow.size() == 2 * bytes)
+        same = std::memcmp(h->shadow.data(), ML, bytes) == 0 && std::memcmp(h->shadow.data() + bytes, G, bytes) == 0;
+    if (!same) {
+        if ((rc = gpad_setup(h, dims, ML, G, L))) return rc;
+        if (host) {
+            h->shadow.resize(2 * bytes);
+            std::memcpy(h->shadow.data(), ML, bytes);
+            std::memcpy(h->shadow.data() + bytes, G, bytes);
+            h->shadow_dims = *dims;
+            h->shadow_L = L;
+            h->shadow_ok = true;
+        }
+    }
+    if ((rc = gpad_run(h, z0, y0, M, g, N, tol, st))) return rc;
+    return gpad_sync(h);
 }
 
 // ---- per-state QP data and closed-loop MPC (gpad.m:79-95) --------

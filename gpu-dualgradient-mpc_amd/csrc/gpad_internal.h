@@ -12,6 +12,24 @@ namespace gpad {
 // gpad_last_error() detail for the calling thread; returns code (gpad_host.cpp)
 int set_last_error(int code, const std::string& msg);
 
+// Schedule / launch tuning of a handle (gpad_set_option, include/gpad.h GPAD_OPT_*): for tests,
+// diagnostics and A/B tools.  None of these changes results -- only launch boundaries, grid
+// sizes, work-queue order and where operands are staged.
+struct Tuning {
+    int phase_len = 0;        // GPAD_OPT_PHASE_LEN: panel phase length, iterations (0: 4 tests)
+    int finish_thresh = -1;   // GPAD_OPT_FINISH_THRESH: finisher takeover (-1: 2 per CU)
+    int plan = 1;             // GPAD_OPT_PLAN: phase plan from the previous solve
+    int phased = 1;           // GPAD_OPT_PHASED: phased compaction of tol > 0 panel solves
+    int finisher = 0;         // GPAD_OPT_FINISHER: 0 = duo work queue, 1 = one instance/workgroup
+    int lpt = 1;              // GPAD_OPT_LPT: longest-predicted-first finisher queue
+    int panel_max_grid = 0;   // GPAD_OPT_PANEL_MAX_GRID: cap on the panel grid (0: none)
+    int duo_max_grid = 0;     // GPAD_OPT_DUO_MAX_GRID: cap on the finisher grid (0: none)
+    int flat_panel_min = -1;  // GPAD_OPT_FLAT_PANEL_MIN: batch from which flat setups use panels
+    int flat_panels = 0;      // GPAD_OPT_FLAT_PANELS: panels per flat-panel workgroup (0: auto)
+    int flat_waves = 0;       // GPAD_OPT_FLAT_WAVES: 0 auto, 8 or 16 waves per workgroup
+    int flat_a_lds = 1;       // GPAD_OPT_FLAT_A_LDS: flat fragment image in LDS when it fits
+};
+
 // Arguments of a fused solve launch (all kernel families).  Every instance b of the batch
 // reads its matrices at MGt + b*strideA / GLt + b*strideB (stride 0 = shared).
 template <typename T>
@@ -52,6 +70,7 @@ struct SolveArgs {
     int n_u;               // flat battery path: cells (n = n_u * horizon), see gpad_flat.hip
     int flat_staged;       // flat path: matrices staged in LDS (set by launch_flat)
     const struct PanelPlan* plan;  // panel phases: host-side plan from the previous solve (or null)
+    const Tuning* tune;    // host-side tuning options (never null on a launch from gpad_host.cpp)
 };
 
 // launchers (return hipError_t of the launch)
@@ -69,8 +88,8 @@ bool resident_supported(int n, int m);
 hipError_t launch_panel(const SolveArgs<float>& a, hipStream_t s, bool* supported);
 size_t panel_frag_bytes(int n, int m, int batch);
 size_t panel_work_bytes(int m, int batch);
-int panel_phase_len(int check_every);
-int panel_fin_thresh(int n, int m, int num_cus);
+int panel_phase_len(int check_every, const Tuning* t);
+int panel_fin_thresh(int n, int m, int num_cus, const Tuning* t);
 // phase plan of a phased panel solve, from the previous solve's iteration counts (panel_plan)
 constexpr int kPanelMaxPhases = 48;
 struct PanelPlan {
@@ -80,7 +99,8 @@ struct PanelPlan {
     int fins[kPanelMaxPhases];    // finisher threshold at the start of phase ph (ph >= 1)
     double cost_us = 0.0;         // modelled solve time
 };
-int panel_plan(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus, PanelPlan* out);
+int panel_plan(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus, const Tuning* t,
+               PanelPlan* out);
 int panel_tiles(int n, int m, int batch);
 // gpad_bigpanel.hip: shared f32 matrices with n or m in (256, 1024]
 bool bigpanel_supported(int n, int m);

@@ -522,12 +522,8 @@ struct Panel2Lds {
 // The work of one wave role, NU = units per wave (2: double, 1: single, 0: idle).  Each role
 // is its own instantiation, so a single wave does not carry a double's registers; every role
 // executes the same sequence of barriers.
-#ifndef PANEL_PD1
-#define PANEL_PD1 2  // A-ring depth of single waves
-#endif
-#ifndef PANEL_PD2
-#define PANEL_PD2 1  // ... and of double waves (2 spills at 128 VGPRs; measured no better)
-#endif
+// A-ring depth: 2 for single waves; 1 for double waves (2 spills at 128 VGPRs, measured no
+// better; deeper rings for singles within +-1 %, tools/ab_mb.sh)
 
 template <int T, int NU>
 __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<T>& L, int t, int p0,
@@ -614,7 +610,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
         }
         __syncthreads();
 
-        constexpr int PD = NU == 2 ? PANEL_PD2 : PANEL_PD1;
+        constexpr int PD = NU == 2 ? 1 : 2;
         float4 ap[PD];  // A blocks of the next GEMM, in flight across the barrier before it
         if constexpr (NU > 0) panel_a_prefetch<T, PD>(PA1, voff, ap);
         int v = a.v_begin;
@@ -830,25 +826,19 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
 }
 
 // schedule parameters shared by the launcher and the host's phase hint
-int panel_phase_len(int check_every) {
+int panel_phase_len(int check_every, const Tuning* t) {
     // a multiple of the test period (phases end right after a test); default four tests
     int len = 4 * check_every;
-    if (const char* pl = std::getenv("GPAD_PANEL_PHASE")) {  // test / tuning knob
-        const int q = std::atoi(pl);
-        if (q > 0) len = q;
-    }
+    if (t && t->phase_len > 0) len = t->phase_len;
     return ((len + check_every - 1) / check_every) * check_every;
 }
 
-int panel_fin_thresh(int n, int m, int num_cus) {
+int panel_fin_thresh(int n, int m, int num_cus, const Tuning* t) {
     // the tail of a phased solve (survivors <= 2 per CU) goes to the latency kernel: one
     // instance per workgroup at ~1/6 of a panel's iteration time (when n, m fit it); measured
     // on C4: 2/CU 5.42e8 it/s, 4/CU 5.35e8, 8/CU 5.35e8, no finisher 5.04e8
     int f = resident_supported(n, m) ? 2 * num_cus : 0;
-    if (const char* ft = std::getenv("GPAD_FINISH_THRESH")) {  // test / tuning knob
-        const int q = std::atoi(ft);
-        if (q >= 0 && f) f = q;
-    }
+    if (t && t->finish_thresh >= 0 && f) f = t->finish_thresh;
     return f;
 }
 
@@ -912,11 +902,12 @@ struct PlanModel {
 };
 }  // namespace
 
-int panel_plan(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus, PanelPlan* out) {
+int panel_plan(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus, const Tuning* t,
+               PanelPlan* out) {
     out->nph = 0;
     out->N = N;
     const int T = panel_tiles_for(n, m);
-    if (!T || batch <= 0 || N <= 0 || std::getenv("GPAD_PANEL_NOPLAN")) return 0;
+    if (!T || batch <= 0 || N <= 0 || (t && !t->plan)) return 0;
     const int K = check_every > 0 ? check_every : 1;
     int maxit = 0;
     for (int b = 0; b < batch; ++b) maxit = iters[b] > maxit ? iters[b] : maxit;
@@ -980,7 +971,7 @@ int panel_plan(const int* iters, int batch, int n, int m, int N, int check_every
         nxt[j] = arg;
     }
     // walk the plan: ends of the panel phases, then the takeover (finisher) or run-out phase
-    const int fin_default = panel_fin_thresh(n, m, num_cus);
+    const int fin_default = panel_fin_thresh(n, m, num_cus, t);
     int j = 0, ph = 0;
     while (j < J && ph < slots) {
         const int k = nxt[j];
@@ -1084,12 +1075,10 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     const int panels = (a.batch + 15) / 16;
     const int resident = (T == 0 || T > 8) ? a.num_cus : a.num_cus * (32 / T);
     int grid = panels < resident ? panels : resident;
-    if (const char* cap = std::getenv("GPAD_PANEL_MAX_GRID")) {  // test knob: grid-stride panels
-        const int c = std::atoi(cap);
-        if (c > 0 && c < grid) grid = c;
-    }
-    const bool phased = a.tol > 0.0 && a.pwork != nullptr && !std::getenv("GPAD_PANEL_NOPHASE");
-    a.fin_thresh = phased ? panel_fin_thresh(a.n, a.m, a.num_cus) : 0;
+    const Tuning tn = a.tune ? *a.tune : Tuning{};
+    if (tn.panel_max_grid > 0 && tn.panel_max_grid < grid) grid = tn.panel_max_grid;  // grid-stride panels
+    const bool phased = a.tol > 0.0 && a.pwork != nullptr && tn.phased;
+    a.fin_thresh = phased ? panel_fin_thresh(a.n, a.m, a.num_cus, &tn) : 0;
     if (!phased) {  // fixed N (or no workspace): one phase, nothing carried
         a.v_begin = 0;
         a.v_end = a.N;
@@ -1110,11 +1099,10 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     // phase length: a multiple of the test period (phases end right after a test); default
     // four tests, doubling after 10 phases so a long tail costs O(log N) launches (a phase with
     // no survivors left costs one empty launch, ~5 us)
-    const int len = panel_phase_len(a.check_every);
+    const int len = panel_phase_len(a.check_every, &tn);
     const PanelPlan* plan = (a.plan && a.plan->nph > 0 && a.plan->N == a.N) ? a.plan : nullptr;
     const int fin_default = a.fin_thresh;
-    const char* fk = std::getenv("GPAD_FINISHER");  // A/B knob: "resident" = one per workgroup
-    const bool duo = !(fk && std::string(fk) == "resident");
+    const bool duo = tn.finisher == 0;  // else one instance per workgroup
     int v0 = 0;
     for (int ph = 0; v0 < a.N; ++ph) {
         int plen = len;
@@ -1136,14 +1124,11 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
         if (ph && a.fin_thresh) {  // few survivors left: the latency kernels take them, run to N
             if (duo) {  // two instances per CU in ping-pong, fed from the survivor list
                 a.qctr = qctrs + ph;
-                if (a.pred && !std::getenv("GPAD_NO_LPT"))  // longest predicted solves first
+                if (a.pred && tn.lpt)  // longest predicted solves first
                     hipLaunchKernelGGL(survivor_sort_kernel, dim3(1), dim3(1024), 0, s, const_cast<int*>(a.idx_in),
                                        a.count_in, a.pred, a.fin_thresh);
                 int g = a.fin_thresh < a.num_cus ? a.fin_thresh : a.num_cus;
-                if (const char* cap = std::getenv("GPAD_DUO_MAX_GRID")) {  // test knob: more claims
-                    const int q = std::atoi(cap);
-                    if (q > 0 && q < g) g = q;
-                }
+                if (tn.duo_max_grid > 0 && tn.duo_max_grid < g) g = tn.duo_max_grid;  // more claims
                 if ((e = launch_duo(a, g, s)) != hipSuccess) return e;
             } else if ((e = launch_resident_finisher(a, a.fin_thresh, s)) != hipSuccess) {
                 return e;  // one instance per workgroup

@@ -31,8 +31,19 @@ EXPORTS = [
     "gpad_setup_plant", "gpad_run_state", "gpad_closed_loop",
     "gpad_datafile_read", "gpad_datafile_write", "gpad_datafile_free",
     "gpad_setup_flat", "gpad_step2_primal_flat", "gpad_step4_project_flat", "gpad_precompute",
-    "gpad_accumulate_iterations",
+    "gpad_accumulate_iterations", "gpad_set_option",
 ]
+
+# gpad_set_option (include/gpad.h GPAD_OPT_*): schedule / launch tuning, never results
+OPT_DEFAULT = -1
+OPT_PHASE_LEN, OPT_FINISH_THRESH, OPT_PLAN, OPT_PHASED, OPT_FINISHER, OPT_LPT = 1, 2, 3, 4, 5, 6
+OPT_PANEL_MAX_GRID, OPT_DUO_MAX_GRID, OPT_FLAT_PANEL_MIN, OPT_FLAT_PANELS = 7, 8, 9, 10
+OPT_FLAT_WAVES, OPT_FLAT_A_LDS = 11, 12
+OPTIONS = {"phase_len": OPT_PHASE_LEN, "finish_thresh": OPT_FINISH_THRESH, "plan": OPT_PLAN,
+           "phased": OPT_PHASED, "finisher": OPT_FINISHER, "lpt": OPT_LPT,
+           "panel_max_grid": OPT_PANEL_MAX_GRID, "duo_max_grid": OPT_DUO_MAX_GRID,
+           "flat_panel_min": OPT_FLAT_PANEL_MIN, "flat_panels": OPT_FLAT_PANELS,
+           "flat_waves": OPT_FLAT_WAVES, "flat_a_lds": OPT_FLAT_A_LDS}
 
 FILE_ROWMAJOR, FILE_FLIPPED, FILE_FLAT = 0, 1, 2
 
@@ -111,6 +122,7 @@ def load(path: str | None = None) -> C.CDLL:
     L.gpad_setup_flat.argtypes = [vp, C.POINTER(Dims), i, cvp, cvp, d]
     L.gpad_precompute.argtypes = [vp, i, i, i, i, i, cvp, cvp, cvp, vp, vp, vp]
     L.gpad_accumulate_iterations.argtypes = [vp, vp]
+    L.gpad_set_option.argtypes = [vp, i, i]
     L.gpad_step2_primal_flat.argtypes = [vp, vp, vp, vp, vp, i, i, i]
     L.gpad_step4_project_flat.argtypes = [vp, vp, vp, vp, vp, vp, i, i, i]
     for name in ["gpad_create", "gpad_destroy", "gpad_set_stream", "gpad_sync", "gpad_setup",
@@ -119,7 +131,8 @@ def load(path: str | None = None) -> C.CDLL:
                  "gpad_step3_average", "gpad_step4_project", "gpad_schedule", "gpad_setup_plant",
                  "gpad_run_state", "gpad_closed_loop", "gpad_datafile_read",
                  "gpad_datafile_write", "gpad_setup_flat", "gpad_step2_primal_flat",
-                 "gpad_step4_project_flat"]:
+                 "gpad_step4_project_flat", "gpad_precompute", "gpad_accumulate_iterations",
+                 "gpad_set_option"]:
         getattr(L, name).restype = i
     _LIB = L
     return L

@@ -57,6 +57,7 @@ class GpadSolver:
             import torch
             stream = torch.cuda.current_stream(device).cuda_stream
         check(self.lib.gpad_create(C.byref(self.h), device, C.c_void_p(stream or 0)), "gpad_create")
+        self._device = device
         self.dims = None
 
     @staticmethod
@@ -83,6 +84,16 @@ class GpadSolver:
 
     def __exit__(self, *exc):
         self.close()
+
+    def set_option(self, name, value: int = _lib.OPT_DEFAULT) -> None:
+        """gpad_set_option: schedule / launch tuning (``name`` in _lib.OPTIONS or a GPAD_OPT_*
+        code); never changes results.  ``value`` -1 restores the default."""
+        code = _lib.OPTIONS[name] if isinstance(name, str) else int(name)
+        check(self.lib.gpad_set_option(self.h, code, int(value)), f"gpad_set_option({name})")
+
+    def set_options(self, **kw) -> None:
+        for k, v in kw.items():
+            self.set_option(k, v)
 
     def set_stream(self, stream) -> None:
         check(self.lib.gpad_set_stream(self.h, C.c_void_p(stream or 0)), "gpad_set_stream")
@@ -123,6 +134,9 @@ class GpadSolver:
             it_arr = iters
             st.iters = it_arr.ctypes.data_as(C.POINTER(C.c_int))
         want = stats or not _is_torch(z)
+        for tab in (theta, beta):  # host tables whatever the memory kind (include/gpad.h)
+            if tab is not None and (_is_torch(tab) or not isinstance(tab, np.ndarray)):
+                raise TypeError("theta/beta must be host numpy arrays (include/gpad.h gpad_run_scaled)")
         if scaled:
             rc = self.lib.gpad_run_scaled(self.h, _ptr(z), _ptr(y), _ptr(M), _ptr(g), int(N),
                                           float(tol), _ptr(theta) if theta is not None else None,
@@ -181,7 +195,12 @@ class GpadSolver:
     # ---- per-state QP data / closed loop (gpad.m:79-95; include/gpad.h gpad_setup_plant) ---
     def accumulate_iterations(self, acc) -> None:
         """Enqueue acc += sum of the last run's per-instance iteration counts (acc: a 1-element
-        int64 device tensor); no host synchronisation."""
+        int64 device tensor on this handle's device); no host synchronisation."""
+        import torch
+        if not (_is_torch(acc) and acc.is_cuda and acc.dtype == torch.int64 and acc.numel() >= 1):
+            raise TypeError("acc must be an int64 CUDA tensor with at least one element")
+        if self._device is not None and acc.device.index != self._device:
+            raise ValueError(f"acc lives on cuda:{acc.device.index}, the handle on cuda:{self._device}")
         check(self.lib.gpad_accumulate_iterations(self.h, _ptr(acc)), "gpad_accumulate_iterations")
 
     def precompute(self, H, A, f=None, *, shared: bool = True):

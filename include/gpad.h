@@ -122,7 +122,8 @@ int gpad_run(gpad_handle_t h, void* z0, void* y0, const void* M, const void* g, 
 
 /* gpad_run for gpad_setup_scaled problems: gP (g_P) and pD (p_D = -g/L) as in the data file,
  * optional per-iteration theta/beta tables (main.cu:61-64; float or double per dtype, length N;
- * NULL -> dims.schedule). */
+ * NULL -> dims.schedule).  theta/beta are HOST arrays whatever dims.memory says (as main.cu:163,
+ * 170 pass them by value per launch); the library copies them to the device. */
 int gpad_run_scaled(gpad_handle_t h, void* z0, void* y0, const void* gP, const void* pD, int N,
                     double tol, const void* theta, const void* beta, gpad_stats_t* st);
 
@@ -245,6 +246,26 @@ int gpad_step4_project_flat(gpad_handle_t h, const float* GLf, float* yp1, const
                             const float* pD, const float* zhat, int N, int n_u, int m);
 /* 8e (host): theta[v], beta[v] for v < N   -- acceldualgrad.m:18,27,55-56 / main.cu:61-64    */
 int gpad_schedule(int N, int kind, double* theta, double* beta);
+
+/* ---- schedule / launch tuning (no reference counterpart) ---------------------------------
+ * Per-handle options for tests, diagnostics and A/B tools.  None changes any result: they move
+ * phase boundaries, cap grids, reorder the finisher's queue or choose where operands are staged.
+ * value GPAD_OPT_DEFAULT restores the default.  Returns GPAD_ERR_INVALID for an unknown option
+ * or an out-of-range value. */
+#define GPAD_OPT_DEFAULT (-1)
+#define GPAD_OPT_PHASE_LEN 1       /* panel phase length in iterations (default 4 * check_every)   */
+#define GPAD_OPT_FINISH_THRESH 2   /* survivors at which the finisher takes over (default 2/CU)    */
+#define GPAD_OPT_PLAN 3            /* 1: plan phases from the previous solve's counts (default)    */
+#define GPAD_OPT_PHASED 4          /* 1: phased compaction of tol > 0 panel solves (default)       */
+#define GPAD_OPT_FINISHER 5        /* 0: two-slot work-queue finisher (default); 1: one per group  */
+#define GPAD_OPT_LPT 6             /* 1: longest-predicted-first finisher queue (default)          */
+#define GPAD_OPT_PANEL_MAX_GRID 7  /* cap on the panel grid, workgroups (0 = none, default)        */
+#define GPAD_OPT_DUO_MAX_GRID 8    /* cap on the finisher grid (0 = none, default)                 */
+#define GPAD_OPT_FLAT_PANEL_MIN 9  /* batch from which flat setups run the flat panels (default 8/CU) */
+#define GPAD_OPT_FLAT_PANELS 10    /* panels per flat-panel workgroup, 1..4 (0 = auto, default)    */
+#define GPAD_OPT_FLAT_WAVES 11     /* flat-panel workgroup waves: 0 auto (default), 8 or 16         */
+#define GPAD_OPT_FLAT_A_LDS 12     /* 1: flat fragment image staged in LDS when it fits (default)  */
+int gpad_set_option(gpad_handle_t h, int option, int value);
 
 /* Synchronise the handle's stream (for callers using device memory + async runs). */
 int gpad_sync(gpad_handle_t h);

@@ -169,16 +169,12 @@ def test_flat_batch_bitexact(gpu, oracle, tol, N, kernel, cells):
                                        ((4, 10), 16 * 3 + 7, 2), ((3, 17), 16 * 4 + 9, 3), ((5, 6), 16 * 2 + 1, 4),
                                        ((4, 50), 1, 1), ((3, 17), 5, 1), ((4, 10), 16 * 3 + 5, 8),
                                        ((3, 17), 16 * 2 + 3, 8), ((5, 6), 16 * 4 + 1, 8)])
-def test_flat_panel_bitexact(gpu, oracle, monkeypatch, tol, N, cells, B, P):
+def test_flat_panel_bitexact(gpu, oracle, tol, N, cells, B, P):
     """The flat MFMA panel kernel (gpad_flatpanel.hip, forced with KERNEL_PANEL): per-cell
     skinny GEMMs over 16-instance panels, P panels per workgroup (ragged last panel, partly
     empty last group), vs the oracle's flat solve."""
     from gpad_mpc import problems
     import gpad_mpc
-    if P == 8:  # 8-wave workgroups, two per CU (GPAD_FLAT_WAVES)
-        monkeypatch.setenv("GPAD_FLAT_WAVES", "8")
-    else:
-        monkeypatch.setenv("GPAD_FLAT_PANELS", str(P))
     n_u, Nh = cells
     qp = problems.battery_scenarios(n_u, Nh, B, seed=11)
     MGf, GLf, L = problems.flatten_battery(qp, n_u, Nh)
@@ -189,6 +185,10 @@ def test_flat_panel_bitexact(gpu, oracle, monkeypatch, tol, N, cells, B, P):
     PD = np.ascontiguousarray(oracle.scale_vec(f32(qp.g), L32))
     s = gpad_mpc.GpadSolver(0)
     s.setup_flat(MGf32, GLf32, float(L32), n_u=n_u, batch=B, kernel=gpad_mpc.KERNEL_PANEL)
+    if P == 8:  # 8-wave workgroups, two per CU
+        s.set_option("flat_waves", 8)
+    else:
+        s.set_option("flat_panels", P)
     Z = np.zeros((B, qp.n), np.float32)
     Y = np.zeros((B, qp.m), np.float32)
     it = np.zeros(B, np.int32)

@@ -24,7 +24,7 @@ def kcode(name):
 
 
 def run_gpu(ML, M, G, g, L, N, tol=0.0, z0=None, y0=None, kernel="auto", shared=True,
-            schedule=0, check_every=10):
+            schedule=0, check_every=10, opts=None):
     import gpad_mpc
     n, m = ML.shape[-2], ML.shape[-1]
     batch = M.shape[0] if M.ndim == 2 else 1
@@ -34,6 +34,7 @@ def run_gpu(ML, M, G, g, L, N, tol=0.0, z0=None, y0=None, kernel="auto", shared=
     with gpad_mpc.GpadSolver(0) as s:
         s.setup(np.ascontiguousarray(ML), np.ascontiguousarray(G), float(L), n=n, m=m, batch=batch,
                 shared=shared, kernel=kcode(kernel), schedule=schedule, check_every=check_every)
+        s.set_options(**(opts or {}))
         st = s.run(z, y, np.ascontiguousarray(M), np.ascontiguousarray(g), N, tol, iters=iters)
     return z, y, st, iters
 
@@ -174,19 +175,14 @@ def test_panel_two_wave_panels_large_batch(gpu, oracle, nm):
                                             (0, 0, None), (0, 10, 24)])
 @pytest.mark.parametrize("tol,N", [(1e-4, 3000), (0.0, 57)])
 @pytest.mark.parametrize("nm,B", [((40, 72), 150), ((150, 130), 40), ((131, 256), 37)])
-def test_panel_phased_compaction_bitexact(gpu, oracle, monkeypatch, grid, phase, fin, tol, N, nm, B):
+def test_panel_phased_compaction_bitexact(gpu, oracle, grid, phase, fin, tol, N, nm, B):
     """Phased compaction + grid-stride panels (+ panel pairs for T > 8 when panels outnumber
     workgroups) + the resident finisher for the tail (fin = its threshold; 0 disables it):
     survivors of each phase are re-packed into new panels (different columns, workgroups,
     pairs and phases) or finished one per workgroup; every instance must still match its own
     oracle solve exactly, including its iteration count."""
     from gpad_mpc import problems
-    if grid:
-        monkeypatch.setenv("GPAD_PANEL_MAX_GRID", str(grid))
-    if phase:
-        monkeypatch.setenv("GPAD_PANEL_PHASE", str(phase))
-    if fin is not None:
-        monkeypatch.setenv("GPAD_FINISH_THRESH", str(fin))
+    opts = dict(panel_max_grid=grid, phase_len=phase, finish_thresh=-1 if fin is None else fin)
     n, m = nm
     qp = problems.synthetic_qp(n, m, batch=B, seed=8)
     ML, G = qp.ML.astype(np.float32), qp.G.astype(np.float32)
@@ -194,7 +190,7 @@ def test_panel_phased_compaction_bitexact(gpu, oracle, monkeypatch, grid, phase,
     L = np.float32(qp.L)
     rng = np.random.default_rng(1)
     z0 = (0.1 * rng.normal(size=(B, n))).astype(np.float32)  # warm starts: exercises the u seed
-    z, y, st, iters = run_gpu(ML, M, G, g, L, N, tol=tol, kernel="panel", z0=z0)
+    z, y, st, iters = run_gpu(ML, M, G, g, L, N, tol=tol, kernel="panel", z0=z0, opts=opts)
     assert st["kernel"] == "panel"
     for b in range(B):
         zo, yo, it, _ = oracle.solve_f32(z0[b], np.zeros(m), ML, M[b], G, g[b], N, L, tol)
@@ -206,15 +202,12 @@ def test_panel_phased_compaction_bitexact(gpu, oracle, monkeypatch, grid, phase,
 @pytest.mark.parametrize("tol,N", [(1e-4, 2000), (0.0, 37)])
 @pytest.mark.parametrize("nm,B", [((200, 900), 40), ((300, 300), 20), ((257, 130), 33), ((520, 600), 17), ((1000, 300), 9)])
 @pytest.mark.parametrize("grid,phase", [(0, 0), (2, 20)])
-def test_bigpanel_bitexact(gpu, oracle, monkeypatch, tol, N, nm, B, grid, phase):
+def test_bigpanel_bitexact(gpu, oracle, tol, N, nm, B, grid, phase):
     """Shared matrices beyond 256 rows on the big-panel MFMA kernel (gpad_bigpanel.hip): GEMMs of
     different tile counts, up to 4 row tiles per wave, grid-stride panels and phases; every
     instance must match its own oracle solve exactly, iteration count included."""
     from gpad_mpc import problems
-    if grid:
-        monkeypatch.setenv("GPAD_PANEL_MAX_GRID", str(grid))
-    if phase:
-        monkeypatch.setenv("GPAD_PANEL_PHASE", str(phase))
+    opts = dict(panel_max_grid=grid, phase_len=phase)
     n, m = nm
     qp = problems.synthetic_qp(n, m, batch=B, seed=17)
     ML, G = qp.ML.astype(np.float32), qp.G.astype(np.float32)
@@ -222,7 +215,7 @@ def test_bigpanel_bitexact(gpu, oracle, monkeypatch, tol, N, nm, B, grid, phase)
     L = np.float32(qp.L)
     rng = np.random.default_rng(3)
     z0 = (0.1 * rng.normal(size=(B, n))).astype(np.float32)
-    z, y, st, iters = run_gpu(ML, M, G, g, L, N, tol=tol, kernel="panel", z0=z0)
+    z, y, st, iters = run_gpu(ML, M, G, g, L, N, tol=tol, kernel="panel", z0=z0, opts=opts)
     assert st["kernel"] == "panel"
     for b in range(B):
         zo, yo, it, _ = oracle.solve_f32(z0[b], np.zeros(m), ML, M[b], G, g[b], N, L, tol)
@@ -233,18 +226,15 @@ def test_bigpanel_bitexact(gpu, oracle, monkeypatch, tol, N, nm, B, grid, phase)
 
 @pytest.mark.parametrize("finisher,grid", [("duo", 1), ("duo", 3), ("duo", 0), ("resident", 0)])
 @pytest.mark.parametrize("nm,B,z0s", [((200, 200), 120, 0.0), ((40, 180), 200, 0.1), ((131, 64), 97, 0.1)])
-def test_finisher_queue_bitexact(gpu, oracle, monkeypatch, finisher, grid, nm, B, z0s):
+def test_finisher_queue_bitexact(gpu, oracle, finisher, grid, nm, B, z0s):
     """The tail of a phased panel solve on the latency kernels: the duo kernel (two instances per
     workgroup in ping-pong, slots refilled from the survivor list through a device counter;
     grid capped to 1 or 3 workgroups to force many claims) or the one-per-workgroup resident
     finisher.  The finisher takes over after the first 10-iteration phase, so nearly the whole
     solve runs there; every instance must match its own oracle solve, iteration count included."""
     from gpad_mpc import problems
-    monkeypatch.setenv("GPAD_FINISHER", finisher)
-    monkeypatch.setenv("GPAD_PANEL_PHASE", "10")
-    monkeypatch.setenv("GPAD_FINISH_THRESH", "100000")
-    if grid:
-        monkeypatch.setenv("GPAD_DUO_MAX_GRID", str(grid))
+    opts = dict(finisher=0 if finisher == "duo" else 1, phase_len=10, finish_thresh=100000,
+                duo_max_grid=grid)
     n, m = nm
     qp = problems.synthetic_qp(n, m, batch=B, seed=12)
     ML, G = qp.ML.astype(np.float32), qp.G.astype(np.float32)
@@ -253,7 +243,7 @@ def test_finisher_queue_bitexact(gpu, oracle, monkeypatch, finisher, grid, nm, B
     rng = np.random.default_rng(2)
     z0 = (z0s * rng.normal(size=(B, n))).astype(np.float32)
     N = 1500
-    z, y, st, iters = run_gpu(ML, M, G, g, L, N, tol=1e-4, kernel="panel", z0=z0)
+    z, y, st, iters = run_gpu(ML, M, G, g, L, N, tol=1e-4, kernel="panel", z0=z0, opts=opts)
     assert st["kernel"] == "panel"
     assert iters.min() > 10  # the finisher ran every instance's tail
     for b in range(B):
@@ -264,15 +254,12 @@ def test_finisher_queue_bitexact(gpu, oracle, monkeypatch, finisher, grid, nm, B
 
 
 @pytest.mark.parametrize("fin", [None, 0])
-def test_panel_phase_plan_reuse_bitexact(gpu, oracle, monkeypatch, fin):
+def test_panel_phase_plan_reuse_bitexact(gpu, oracle, fin):
     """A handle plans its phases from the previous solve's iteration counts (csrc/gpad_panel.hip
     panel_plan); a later solve that needs more (or fewer) iterations than the plan expects must
     still be exact -- the plan moves launch boundaries and the finisher takeover only."""
     import gpad_mpc
     from gpad_mpc import problems
-    if fin is not None:
-        monkeypatch.setenv("GPAD_FINISH_THRESH", str(fin))
-    monkeypatch.setenv("GPAD_PANEL_PHASE", "10")
     n, m, B = 40, 72, 300
     qp = problems.synthetic_qp(n, m, batch=B, seed=31)
     ML, G = qp.ML.astype(np.float32), qp.G.astype(np.float32)
@@ -280,6 +267,7 @@ def test_panel_phase_plan_reuse_bitexact(gpu, oracle, monkeypatch, fin):
     rng = np.random.default_rng(5)
     with gpad_mpc.GpadSolver(0) as s:
         s.setup(ML, G, float(L), n=n, m=m, batch=B, kernel=kcode("panel"))
+        s.set_options(phase_len=10, finish_thresh=-1 if fin is None else fin)
         for scale, tol in ((1.0, 1e-3), (3.0, 1e-5), (1.0, 1e-4)):  # easy, harder, middle
             M = (qp.M * scale).astype(np.float32)
             g = (qp.g + 0.1 * rng.random((B, m))).astype(np.float32)

@@ -23,6 +23,8 @@ def one(args):
     import torch
 
     import gpad_mpc
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import tune_env  # noqa: F401  (legacy GPAD_* env -> gpad_set_option)
     from gpad_mpc import _lib, problems
     dev = torch.device("cuda:0")
     n, m, B, N = args.n, args.m, args.batch, args.N

@@ -15,6 +15,8 @@ def one(n_u, Nh, batch, N):
     import torch
 
     import gpad_mpc
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import tune_env  # noqa: F401  (legacy GPAD_* env -> gpad_set_option)
     from gpad_mpc import problems
     dev = torch.device("cuda:0")
     qp = problems.battery_scenarios(n_u, Nh, batch, seed=9)

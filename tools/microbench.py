@@ -20,6 +20,8 @@ sys.path.insert(0, os.path.join(ROOT, "gpu-dualgradient-mpc_amd"))
 def case(kernel, n, m, batch, N, shared=True, reps=3, tol=0.0, check_every=10):
     import torch
     import gpad_mpc
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import tune_env  # noqa: F401  (legacy GPAD_* env -> gpad_set_option)
     from gpad_mpc import _lib, problems
     dev = torch.device("cuda:0")
     kc = {"stream": _lib.KERNEL_STREAM, "resident": _lib.KERNEL_RESIDENT, "panel": _lib.KERNEL_PANEL,

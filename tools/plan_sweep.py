@@ -23,6 +23,8 @@ def one(reps):
 
     import bench
     import gpad_mpc
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import tune_env  # noqa: F401  (legacy GPAD_* env -> gpad_set_option)
     dev = torch.device("cuda:0")
     n, m, B = 200, 200, 8192
     ML, G, L, M, g = bench.make_shard(n, m, B, 0)

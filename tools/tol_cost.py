@@ -6,6 +6,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, 'gpu-dualgradient-mpc_amd'))
 import torch, bench, gpad_mpc
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import tune_env  # noqa: F401,E402  (legacy GPAD_* env -> gpad_set_option)
 dev = torch.device('cuda:0')
 n = m = 200; B = 8192
 ML, G, L, M, g = bench.make_shard(n, m, B, 0)
