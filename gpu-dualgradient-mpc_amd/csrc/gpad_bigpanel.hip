@@ -51,6 +51,7 @@ __host__ __device__ inline int big_tiles(int x) { return (x + 15) / 16; }
 struct BigSlot {  // per wave: its tiles' partials of the test, per column
     float violz[16], violh[16], wmin[16];
     double gap[16];
+    float magh[16];  // max(|G_L zhat| + |pD|); with violz reused by the verification of test (A)
 };
 
 // LDS: w and p_D per GEMM-2 row tile, zhat per GEMM-1 row tile (1 KiB each), 16 test slots
@@ -292,7 +293,7 @@ __global__ __launch_bounds__(64 * kBigWaves) void gpad_bigpanel_kernel(SolveArgs
             }
             __syncthreads();
             // ---- GEMM 2 + epilogue: y+ (8d), next w (8a), test partials ----------------------------
-            float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY;
+            float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY, magh = 0.0f;
             double gap = 0.0;
             bf32x4 acc_next = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
@@ -332,6 +333,7 @@ __global__ __launch_bounds__(64 * kBigWaves) void gpad_bigpanel_kernel(SolveArgs
                             if (chk && active && (16 * t + 4 * r + j) < m) {
                                 const float tt = cv + pdq[r];
                                 violh = fmaxf(violh, tt);
+                                magh = fmaxf(magh, __builtin_fabsf(cv) + __builtin_fabsf(pdq[r]));
                                 wmin = fminf(wmin, wv[r]);
                                 gap -= (double)wv[r] * (double)tt;
                                 violz = fmaxf(violz, u[q][r] + pdq[r]);
@@ -347,12 +349,14 @@ __global__ __launch_bounds__(64 * kBigWaves) void gpad_bigpanel_kernel(SolveArgs
                 for (int o = 16; o < 64; o <<= 1) {
                     violz = fmaxf(violz, __shfl_xor(violz, o, 64));
                     violh = fmaxf(violh, __shfl_xor(violh, o, 64));
+                    magh = fmaxf(magh, __shfl_xor(magh, o, 64));
                     wmin = fminf(wmin, __shfl_xor(wmin, o, 64));
                     gap += __shfl_xor(gap, o, 64);
                 }
                 if (j == 0) {
                     slots[w].violz[c] = violz;
                     slots[w].violh[c] = violh;
+                    slots[w].magh[c] = magh;
                     slots[w].wmin[c] = wmin;
                     slots[w].gap[c] = gap;
                 }
@@ -364,22 +368,86 @@ __global__ __launch_bounds__(64 * kBigWaves) void gpad_bigpanel_kernel(SolveArgs
 
             // ---- Algorithm 1 test: every wave reduces the wave slots for the 16 columns, ballot ---
             unsigned m1 = 0u, m2 = 0u;
+            bool zh_out = true;  // this iteration's zhat still in Zh (no verification GEMM ran)
             if (chk) {
-                int cd = 0;
+                int st1 = 0;
                 if (lane < 16 && ((live >> lane) & 1u)) {
-                    double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gq = 0.0;
+                    double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gq = 0.0, mh = 0.0;
 #pragma unroll
                     for (int s2 = 0; s2 < kBigWaves; ++s2) {
                         vz = fmax(vz, (double)slots[s2].violz[lane]);
                         vh = fmax(vh, (double)slots[s2].violh[lane]);
+                        mh = fmax(mh, (double)slots[s2].magh[lane]);
                         wm = fmin(wm, (double)slots[s2].wmin[lane]);
                         gq += slots[s2].gap[lane];
                     }
-                    if (vz * a.L <= a.tol) cd = 1;
-                    else if ((vh * a.L <= a.tol) && (wm >= 0.0) && (gq * a.L <= a.tol)) cd = 2;
+                    st1 = (vz * a.L <= a.tol ? 1 : 0) |
+                          ((viol_ok(vh, mh, a.L, a.tol, ViolMargin<float>::value) && (wm >= 0.0) &&
+                            (gq * a.L <= a.tol_gap)) ? 2 : 0);
                 }
-                m1 = (unsigned)__ballot(cd == 1);
-                m2 = (unsigned)__ballot(cd == 2);
+                const unsigned mA = (unsigned)__ballot(st1 & 1);
+                m2 = (unsigned)__ballot(st1 & 2);
+                if (mA) {  // (A) nominated for some column: G_L z for the panel
+                    zh_out = false;
+#pragma unroll
+                    for (int q = 0; q < NT1; ++q) {
+                        const int t = w + kBigWaves * q;
+                        if (t < T1) {
+                            if (active && ((m2 >> c) & 1u)) {  // test (B)'s zhat out before z replaces it
+                                const float4 h4 = Zh[t * 64 + lane];
+                                const float zh[4] = {h4.x, h4.y, h4.z, h4.w};
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) {
+                                    const int i = 16 * t + 4 * r + j;
+                                    if (i < n) a.z[bi * n + i] = zh[r];
+                                }
+                            }
+                            Zh[t * 64 + lane] = make_float4(z[q][0], z[q][1], z[q][2], z[q][3]);
+                        }
+                    }
+                    __syncthreads();
+                    const bool nom = active && ((mA >> c) & 1u);
+                    float vc = -INFINITY, mc = 0.0f;
+#pragma unroll
+                    for (int q = 0; q < NT2; ++q) {
+                        const int t = w + kBigWaves * q;
+                        if (t < T2) {
+                            const bf32x4 cz = big_gemm(PA2, Zh, t, T2, T1, kq2, lane);
+                            const float4 p4 = Pd[t * 64 + lane];
+                            const float pdq[4] = {p4.x, p4.y, p4.z, p4.w};
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                if (nom && (16 * t + 4 * r + j) < m) {
+                                    u[q][r] = cz[r];  // the recursion restarts from the direct value
+                                    vc = fmaxf(vc, cz[r] + pdq[r]);
+                                    mc = fmaxf(mc, __builtin_fabsf(cz[r]) + __builtin_fabsf(pdq[r]));
+                                }
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int o = 16; o < 64; o <<= 1) {
+                        vc = fmaxf(vc, __shfl_xor(vc, o, 64));
+                        mc = fmaxf(mc, __shfl_xor(mc, o, 64));
+                    }
+                    if (j == 0) {  // every wave's stage-1 reads precede the barrier above
+                        slots[w].violz[c] = vc;
+                        slots[w].magh[c] = mc;
+                    }
+                    __syncthreads();
+                    bool ver = false;
+                    if (lane < 16 && ((mA >> lane) & 1u)) {
+                        double vcc = -INFINITY, mcc = 0.0;
+#pragma unroll
+                        for (int s2 = 0; s2 < kBigWaves; ++s2) {
+                            vcc = fmax(vcc, (double)slots[s2].violz[lane]);
+                            mcc = fmax(mcc, (double)slots[s2].magh[lane]);
+                        }
+                        ver = viol_ok(vcc, mcc, a.L, a.tol, ViolMargin<float>::value);
+                    }
+                    m1 = (unsigned)__ballot(ver);
+                    m2 &= ~m1;
+                }
             }
             const int cdc = ((m1 >> c) & 1u) ? 1 : (((m2 >> c) & 1u) ? 2 : 0);
             if (active && (cdc != 0 || v >= N)) {  // finished column: results out
@@ -392,7 +460,7 @@ __global__ __launch_bounds__(64 * kBigWaves) void gpad_bigpanel_kernel(SolveArgs
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             const int i = 16 * t + 4 * r + j;
-                            if (i < n) a.z[bi * n + i] = cdc == 2 ? zh[r] : z[q][r];  // (B): zhat
+                            if (i < n && (cdc != 2 || zh_out)) a.z[bi * n + i] = cdc == 2 ? zh[r] : z[q][r];
                         }
                     }
                 }

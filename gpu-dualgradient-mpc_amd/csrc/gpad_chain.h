@@ -44,14 +44,18 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 // Per-wave partials of the Algorithm-1 test -> LDS slot of the wave.
+//   violz: max(u + pD) (recursive G_L z, nominates test A)   violh: max(G_L zhat + pD)
+//   magh:  max(|G_L zhat| + |pD|) (test B's rounding scale)  wmin, gap: test B's other terms
+// The verification of a nominated test A publishes max(G_L z + pD) in violz and
+// max(|G_L z| + |pD|) in magh of a second slot array.
 struct CheckSlot {
-    double violz, violh, wmin, gap;
+    double violz, violh, wmin, gap, magh;
 };
 
 template <typename T>
 __device__ __forceinline__ void check_publish(CheckSlot* slots, T violz, T violh, T wmin,
-                                              double gap) {
-    const T a = wave_max(violz), b = wave_max(violh), c = wave_min(wmin);
+                                              double gap, T magh) {
+    const T a = wave_max(violz), b = wave_max(violh), c = wave_min(wmin), e = wave_max(magh);
     const double d = wave_sum(gap);
     if ((threadIdx.x & 63) == 0) {
         CheckSlot& s = slots[threadIdx.x >> 6];
@@ -59,25 +63,45 @@ __device__ __forceinline__ void check_publish(CheckSlot* slots, T violz, T violh
         s.violh = (double)b;
         s.wmin = (double)c;
         s.gap = d;
+        s.magh = (double)e;
     }
 }
 
 // Every thread evaluates the decision from the same LDS words -> uniform, no extra barrier.
-// 1: (A) L*max(G_L z + pD) <= tol              -> z certified
-// 2: (B) L*max(G_L zhat + pD) <= tol, w >= 0, -L w't <= tol -> zhat certified (returned as z*)
-__device__ __forceinline__ int check_decide(const CheckSlot* slots, int nwaves, double L,
-                                            double tol) {
-    double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gap = 0.0;
+// Returns bit 1: test (A) nominated by the recursion (L*max(u + pD) <= tol; decided later on
+// the direct G_L z by check_verify), bit 2: test (B) passed
+//   L*max(G_L zhat + pD) + margin L*max(|G_L zhat| + |pD|) <= tol, w >= 0, -L w't <= tol_gap.
+template <typename T>
+__device__ __forceinline__ int check_stage1(const CheckSlot* slots, int nwaves, double L, double tol,
+                                            double tol_gap) {
+    double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gap = 0.0, mh = 0.0;
     for (int i = 0; i < nwaves; ++i) {
         vz = fmax(vz, slots[i].violz);
         vh = fmax(vh, slots[i].violh);
         wm = fmin(wm, slots[i].wmin);
         gap += slots[i].gap;
+        mh = fmax(mh, slots[i].magh);
     }
-    if (vz * L <= tol) return 1;
-    return ((vh * L <= tol) && (wm >= 0.0) && (gap * L <= tol)) ? 2 : 0;
+    const bool a = vz * L <= tol;
+    const bool b = viol_ok(vh, mh, L, tol, ViolMargin<T>::value) && (wm >= 0.0) && (gap * L <= tol_gap);
+    return (a ? 1 : 0) | (b ? 2 : 0);
 }
 
+// Test (A) on the direct chain c = G_L z: slots hold max(c + pD) in violz, max(|c| + |pD|) in magh.
+template <typename T>
+__device__ __forceinline__ bool check_verify(const CheckSlot* slots, int nwaves, double L, double tol) {
+    double vc = -INFINITY, mc = 0.0;
+    for (int i = 0; i < nwaves; ++i) {
+        vc = fmax(vc, slots[i].violz);
+        mc = fmax(mc, slots[i].magh);
+    }
+    return viol_ok(vc, mc, L, tol, ViolMargin<T>::value);
+}
+
+// final code from the two stages: 1 = (A) verified, 2 = (B), 0 = continue
+__device__ __forceinline__ int check_code(int stage1, bool verified) {
+    return ((stage1 & 1) && verified) ? 1 : ((stage1 & 2) ? 2 : 0);
+}
 
 // =========================================================================================
 // register-resident DPP chains (gpad_resident_kernel, gpad_duo_kernel): one matrix row per

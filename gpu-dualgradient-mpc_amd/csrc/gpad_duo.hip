@@ -96,7 +96,7 @@ template <int KA, int KB, int K>
 __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx& c, DuoSlot& sa, DuoSlot& sb,
                                          float* wa_l, float* zha_l, const float* gpa_l, float* wb_l,
                                          const float* zhb_l, float* gpb_l, float* pdb_l, CheckSlot* slots_b,
-                                         int* claim_b, float* z_l, const float (&r)[K]) {
+                                         CheckSlot* vslots, int* claim_b, float* z_l, const float (&r)[K]) {
     const bool runA = sa.pos < c.count && !sa.need8d;
     const bool runB = sb.need8d;
     const bool chk = runB && c.use_tol && ((sb.vs + 1) % c.Kc) == 0;
@@ -112,7 +112,7 @@ __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx
             }
         }
     } else {
-        float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY;
+        float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY, magh = 0.0f;
         double gap = 0.0;
         if (runB) {
             const float th = sb.th, bn = sb.bn;
@@ -125,6 +125,7 @@ __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx
                 if (chk) {
                     const float t = cv + pdi;
                     violh = t;
+                    magh = __builtin_fabsf(cv) + __builtin_fabsf(pdi);
                     wmin = wi;
                     gap = -((double)wi * (double)t);
                     violz = sb.x2 + pdi;
@@ -134,7 +135,7 @@ __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx
                 wb_l[c.row] = sb.x1;
             }
         }
-        if (chk) check_publish<float>(slots_b, violz, violh, wmin, gap);
+        if (chk) check_publish<float>(slots_b, violz, violh, wmin, gap, magh);
     }
     __syncthreads();
     if (runA) sa.need8d = true;
@@ -143,7 +144,28 @@ __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx
         const int v = ++sb.vs;
         sb.th = a.theta[v];  // next iteration's schedule (tables hold N + 2 entries)
         sb.bn = a.beta[v + 1];
-        const int done = chk ? check_decide(slots_b + c.nA, c.nwaves - c.nA, a.L, a.tol) : 0;
+        int done = 0;
+        if (chk) {
+            const int st1 = check_stage1<float>(slots_b + c.nA, c.nwaves - c.nA, a.L, a.tol, a.tol_gap);
+            bool verified = false;
+            if (st1 & 1) {  // (A) nominated: decide on the direct chain G_L z, reset u to it
+                if (c.isA && c.live) z_l[c.row] = sb.x0;
+                __syncthreads();
+                float vc = -INFINITY, mc = 0.0f;
+                if (!c.isA) {
+                    const float cz = chain_regs<KB, K>(r, z_l);
+                    if (c.live) {
+                        sb.x2 = cz;
+                        vc = cz + pdb_l[c.row];
+                        mc = __builtin_fabsf(cz) + __builtin_fabsf(pdb_l[c.row]);
+                    }
+                    check_publish<float>(vslots, vc, vc, vc, 0.0, mc);
+                }
+                __syncthreads();
+                verified = check_verify<float>(vslots + c.nA, c.nwaves - c.nA, a.L, a.tol);
+            }
+            done = check_code(st1, verified);
+        }
         if (done || v >= c.N) {
             const size_t b = (size_t)(a.idx_in ? a.idx_in[sb.pos] : sb.pos);
             if (c.live) {
@@ -169,6 +191,7 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs
     __shared__ float gp_l[2][PB];                               // per slot: g_P of the -ML rows
     __shared__ float pd_l[2][PA];                               //           p_D of the G/L rows
     __shared__ CheckSlot slots[2][kResidentMaxThreads / 64];
+    __shared__ CheckSlot vslots[kResidentMaxThreads / 64];  // verification of a nominated test (A)
     __shared__ int claim_l[2];
 
     DuoCtx c;
@@ -213,9 +236,9 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs
     duo_refill<KB, K>(a, c, s1, blockIdx.x + c.G, w_l[1], gp_l[1], pd_l[1], z_l, r);
     while (s0.pos < c.count || s1.pos < c.count) {
         duo_step<KA, KB, K>(a, c, s0, s1, w_l[0], zh_l[0], gp_l[0], w_l[1], zh_l[1], gp_l[1], pd_l[1], slots[1],
-                            &claim_l[1], z_l, r);
+                            vslots, &claim_l[1], z_l, r);
         duo_step<KA, KB, K>(a, c, s1, s0, w_l[1], zh_l[1], gp_l[1], w_l[0], zh_l[0], gp_l[0], pd_l[0], slots[0],
-                            &claim_l[0], z_l, r);
+                            vslots, &claim_l[0], z_l, r);
     }
 }
 

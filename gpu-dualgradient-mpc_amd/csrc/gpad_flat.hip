@@ -26,6 +26,7 @@
 
 #include <cmath>
 
+#include "gpad_chain.h"
 #include "gpad_internal.h"
 
 namespace gpad {
@@ -33,25 +34,6 @@ namespace gpad {
 constexpr int kFlatBlock = 256;
 constexpr size_t kFlatStageMax = 64 * 1024;  // bytes of flat matrices staged in LDS
 
-struct FlatSlot {
-    double violz, violh, wmin, gap;
-};
-
-__device__ __forceinline__ float fwave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
-}
-__device__ __forceinline__ float fwave_min(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
-    return v;
-}
-__device__ __forceinline__ double fwave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
 
 // primal row r = (i, j): the structural nonzeros of row r of -ML, ascending k
 __device__ __forceinline__ float flat_row2(const float* MG, const float* w, int i, int j, int n_u, int mc,
@@ -91,8 +73,9 @@ __global__ __launch_bounds__(kFlatBlock) void gpad_flat_kernel(SolveArgs<float> 
     float* zh = us + m;                         // [n]
     float* zs = zh + n;                         // [n]
     float* gp = zs + n;                         // [n]
-    FlatSlot* slots = reinterpret_cast<FlatSlot*>(gp + n + ((n & 1) ? 1 : 0));
-    float* stage = reinterpret_cast<float*>(slots + kFlatBlock / 64);
+    // [2][waves]: the test's partials, the verification of a nominated test (A)
+    CheckSlot* slots = reinterpret_cast<CheckSlot*>(gp + n + ((n & 1) ? 1 : 0));
+    float* stage = reinterpret_cast<float*>(slots + 2 * (kFlatBlock / 64));
     const bool staged = a.flat_staged != 0;
     const float* MG = a.MGt;  // flat -ML, Nh x m
     const float* GLT = a.GLt;  // flat G_L, t-major Nh x m
@@ -136,7 +119,7 @@ __global__ __launch_bounds__(kFlatBlock) void gpad_flat_kernel(SolveArgs<float> 
         __syncthreads();
         // ---- 8d + next 8a (StepFourGPADFlatSequential) ----------------------------------
         const bool chk = use_tol && ((v + 1) % a.check_every) == 0;
-        float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY;
+        float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY, magh = 0.0f;
         double gap = 0.0;
         for (int r = tid; r < m; r += kFlatBlock) {
             const float s = flat_row4(GLT, zh, r, Nh, n_u, mc, m);
@@ -149,6 +132,7 @@ __global__ __launch_bounds__(kFlatBlock) void gpad_flat_kernel(SolveArgs<float> 
                 if (chk) {
                     const float t = s + pdi;
                     violh = fmaxf(violh, t);
+                    magh = fmaxf(magh, __builtin_fabsf(s) + __builtin_fabsf(pdi));
                     wmin = fminf(wmin, wi);
                     gap -= (double)wi * (double)t;
                     violz = fmaxf(violz, ui + pdi);
@@ -157,23 +141,26 @@ __global__ __launch_bounds__(kFlatBlock) void gpad_flat_kernel(SolveArgs<float> 
             w[r] = __builtin_fmaf(bnext, yp - yi, yp);
             ys[r] = yp;
         }
-        if (chk) {
-            const float A = fwave_max(violz), B = fwave_max(violh), Cm = fwave_min(wmin);
-            const double D = fwave_sum(gap);
-            if ((tid & 63) == 0) slots[tid >> 6] = FlatSlot{(double)A, (double)B, (double)Cm, D};
-        }
+        constexpr int nw = kFlatBlock / 64;
+        if (chk) check_publish<float>(slots, violz, violh, wmin, gap, magh);
         __syncthreads();
         it = v + 1;
         if (chk) {
-            double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gq = 0.0;
-            for (int q = 0; q < kFlatBlock / 64; ++q) {
-                vz = fmax(vz, slots[q].violz);
-                vh = fmax(vh, slots[q].violh);
-                wm = fmin(wm, slots[q].wmin);
-                gq += slots[q].gap;
+            const int st1 = check_stage1<float>(slots, nw, a.L, a.tol, a.tol_gap);
+            bool verified = false;
+            if (st1 & 1) {  // (A) nominated: decide on the direct flat chain G_L z, reset u to it
+                float vc = -INFINITY, mcz = 0.0f;
+                for (int r = tid; r < m; r += kFlatBlock) {
+                    const float cz = flat_row4(GLT, zs, r, Nh, n_u, mc, m);
+                    us[r] = cz;
+                    vc = fmaxf(vc, cz + pd[r]);
+                    mcz = fmaxf(mcz, __builtin_fabsf(cz) + __builtin_fabsf(pd[r]));
+                }
+                check_publish<float>(slots + nw, vc, vc, vc, 0.0, mcz);
+                __syncthreads();
+                verified = check_verify<float>(slots + nw, nw, a.L, a.tol);
             }
-            if (vz * a.L <= a.tol) done = 1;
-            else if ((vh * a.L <= a.tol) && (wm >= 0.0) && (gq * a.L <= a.tol)) done = 2;
+            done = check_code(st1, verified);
         }
         if (done) break;
     }
@@ -187,7 +174,7 @@ __global__ __launch_bounds__(kFlatBlock) void gpad_flat_kernel(SolveArgs<float> 
 }
 
 static size_t flat_vec_bytes(int n, int m) {
-    return sizeof(float) * (size_t)(4 * m + 3 * n + 1) + sizeof(FlatSlot) * (kFlatBlock / 64) + 16;
+    return sizeof(float) * (size_t)(4 * m + 3 * n + 1) + sizeof(CheckSlot) * 2 * (kFlatBlock / 64) + 16;
 }
 
 hipError_t launch_flat(const SolveArgs<float>& a, hipStream_t s) {

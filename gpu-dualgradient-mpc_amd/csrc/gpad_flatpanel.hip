@@ -85,6 +85,7 @@ __host__ __device__ inline FlatGeom flat_geom(int n, int m, int n_u) {
 struct FlatPanelSlot {
     float violz[16], violh[16], wmin[16];
     double gap[16];
+    float magh[16];  // max(|G_L zhat| + |pD|); with violz reused by the verification of test (A)
 };
 static size_t flatpanel_lds_bytes(const FlatGeom& g, int P) {
     return (size_t)P * g.PB * 1024 + (size_t)P * g.U2 * sizeof(FlatPanelSlot);
@@ -496,7 +497,7 @@ __global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<flo
                     const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
                     const int lim = cp ? g.E : 4 * g.Nh;
                     float wn[4];
-                    float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY;
+                    float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY, magh = 0.0f;
                     double gap = 0.0;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
@@ -509,6 +510,7 @@ __global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<flo
                             if (chk && act && 16 * x.t + 4 * r + jl < lim) {
                                 const float tt = cv + pdi;
                                 violh = fmaxf(violh, tt);
+                                magh = fmaxf(magh, __builtin_fabsf(cv) + __builtin_fabsf(pdi));
                                 wmin = fminf(wmin, wi);
                                 gap -= (double)wi * (double)tt;
                                 violz = fmaxf(violz, u[q][r] + pdi);
@@ -523,12 +525,14 @@ __global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<flo
                         for (int o = 16; o < 64; o <<= 1) {
                             violz = fmaxf(violz, __shfl_xor(violz, o, 64));
                             violh = fmaxf(violh, __shfl_xor(violh, o, 64));
+                            magh = fmaxf(magh, __shfl_xor(magh, o, 64));
                             wmin = fminf(wmin, __shfl_xor(wmin, o, 64));
                             gap += __shfl_xor(gap, o, 64);
                         }
                         if (jl == 0) {
                             slots[un].violz[c] = violz;
                             slots[un].violh[c] = violh;
+                            slots[un].magh[c] = magh;
                             slots[un].wmin[c] = wmin;
                             slots[un].gap[c] = gap;
                         }
@@ -545,22 +549,104 @@ __global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<flo
             if (!chk && v < N) continue;
 
             unsigned long long m1 = 0ull, m2 = 0ull;
+            bool zh_out = true;  // this iteration's zhat still in Zc (no verification chains ran)
             if (chk) {  // lane = (panel lane >> 4, column lane & 15): reduce that panel's unit slots
-                int cd = 0;
+                int st1 = 0;
                 const int pp = lane >> 4;
                 if (pp < P && ((live >> lane) & 1ull)) {
-                    double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gq = 0.0;
+                    double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gq = 0.0, mh = 0.0;
                     for (int s2 = pp * g.U2; s2 < (pp + 1) * g.U2; ++s2) {
                         vz = fmax(vz, (double)slots[s2].violz[c]);
                         vh = fmax(vh, (double)slots[s2].violh[c]);
+                        mh = fmax(mh, (double)slots[s2].magh[c]);
                         wm = fmin(wm, (double)slots[s2].wmin[c]);
                         gq += slots[s2].gap[c];
                     }
-                    if (vz * a.L <= a.tol) cd = 1;
-                    else if ((vh * a.L <= a.tol) && (wm >= 0.0) && (gq * a.L <= a.tol)) cd = 2;
+                    st1 = (vz * a.L <= a.tol ? 1 : 0) |
+                          ((viol_ok(vh, mh, a.L, a.tol, ViolMargin<float>::value) && (wm >= 0.0) &&
+                            (gq * a.L <= a.tol_gap)) ? 2 : 0);
                 }
-                m1 = __ballot(cd == 1);
-                m2 = __ballot(cd == 2);
+                const unsigned long long mA = __ballot(st1 & 1);
+                m2 = __ballot(st1 & 2);
+                if (mA) {  // (A) nominated for some column: the flat G_L z chains of the group
+                    zh_out = false;
+#pragma unroll
+                    for (int q = 0; q < NU1; ++q) {
+                        const int un = w + W * q;
+                        if (un < nu1) {
+                            const FpU1 x = fp_u1(g, un);
+                            const int bit = 16 * x.pp + c;
+                            float4* L = fp_lds + x.pp * PBf;
+                            float4* zc = &L[oZc + (x.j * g.T1 + x.t) * 64 + lane];
+                            if ((m2 >> bit) & 1ull) {  // test (B)'s zhat out before z replaces it
+                                const float4 zh4 = *zc;
+                                const float zhv[4] = {zh4.x, zh4.y, zh4.z, zh4.w};
+                                const size_t bi = (size_t)(k0 + bit);
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) {
+                                    const int i = 16 * x.t + 4 * r + jl;
+                                    if (i < g.Nh) a.z[bi * n + i * g.n_u + x.j] = zhv[r];
+                                }
+                            }
+                            *zc = make_float4(z[q][0], z[q][1], z[q][2], z[q][3]);
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                const int i = 16 * x.t + 4 * r + jl, kk = i * g.n_u + x.j;
+                                if (i < g.Nh)
+                                    reinterpret_cast<float*>(&L[oZn + (kk >> 4) * 64 + (kk & 3) * 16 + c])[(kk >> 2) & 3] =
+                                        z[q][r];
+                            }
+                        }
+                    }
+                    __syncthreads();
+#pragma unroll
+                    for (int q = 0; q < NU2; ++q) {
+                        const int un = w + W * q;
+                        if (un < nu2) {
+                            const FpU2 x = fp_u2(g, un);
+                            const bool nom = (mA >> (16 * x.pp + c)) & 1ull;
+                            const bool cp = x.cell < 0;
+                            const float4* L = fp_lds + x.pp * PBf;
+                            const int voff = fp_voff2(g, x, lane), stride = (cp ? g.KBe : g.KBc) * 1024;
+                            const int nkb = cp ? g.KB3 : g.T1;
+                            const ff32x4 cz = fp_chain<ALDS>(PA, As, fp_pre<ALDS>(PA, As, voff, stride, nkb), voff,
+                                                             stride, nkb, cp ? g.kq3 : g.kq2,
+                                                             cp ? L + oZn : L + oZc + x.cell * g.T1 * 64, nkb,
+                                                             L + oZn, lane);
+                            const int lim = cp ? g.E : 4 * g.Nh;
+                            float vc = -INFINITY, mc = 0.0f;
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                if (nom) u[q][r] = cz[r];  // the recursion restarts from the direct value
+                                if (nom && 16 * x.t + 4 * r + jl < lim) {
+                                    vc = fmaxf(vc, cz[r] + pd[q][r]);
+                                    mc = fmaxf(mc, __builtin_fabsf(cz[r]) + __builtin_fabsf(pd[q][r]));
+                                }
+                            }
+#pragma unroll
+                            for (int o = 16; o < 64; o <<= 1) {
+                                vc = fmaxf(vc, __shfl_xor(vc, o, 64));
+                                mc = fmaxf(mc, __shfl_xor(mc, o, 64));
+                            }
+                            if (jl == 0) {  // every wave's stage-1 reads precede the barrier above
+                                slots[un].violz[c] = vc;
+                                slots[un].magh[c] = mc;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                    bool ver = false;
+                    if (pp < P && ((mA >> lane) & 1ull)) {
+                        double vcc = -INFINITY, mcc = 0.0;
+                        for (int s2 = pp * g.U2; s2 < (pp + 1) * g.U2; ++s2) {
+                            vcc = fmax(vcc, (double)slots[s2].violz[c]);
+                            mcc = fmax(mcc, (double)slots[s2].magh[c]);
+                        }
+                        ver = viol_ok(vcc, mcc, a.L, a.tol, ViolMargin<float>::value);
+                    }
+                    m1 = __ballot(ver);
+                    m2 &= ~m1;
+                }
             }
             const unsigned long long fin = v >= N ? live : (live & (m1 | m2));
             if (fin) {  // finished columns: results out
@@ -570,11 +656,11 @@ __global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<flo
                     if (un < nu1) {
                         const FpU1 x = fp_u1(g, un);
                         const int bit = 16 * x.pp + c;
-                        if ((fin >> bit) & 1ull) {
+                        const bool tb = (m2 >> bit) & 1ull;  // test (B): zhat (pre-written when verified over)
+                        if (((fin >> bit) & 1ull) && (!tb || zh_out)) {
                             const size_t bi = (size_t)(k0 + bit);
                             const float4 zh4 = fp_lds[x.pp * PBf + oZc + (x.j * g.T1 + x.t) * 64 + lane];
                             const float zhv[4] = {zh4.x, zh4.y, zh4.z, zh4.w};
-                            const bool tb = (m2 >> bit) & 1ull && !((m1 >> bit) & 1ull);  // test (B): zhat
 #pragma unroll
                             for (int r = 0; r < 4; ++r) {
                                 const int i = 16 * x.t + 4 * r + jl;

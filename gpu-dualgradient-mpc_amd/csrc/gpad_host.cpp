@@ -258,6 +258,7 @@ static int validate_dims(const gpad_dims_t* d) {
         return fail(GPAD_ERR_INVALID, "dims: bad schedule");
     if (d->kernel < GPAD_KERNEL_AUTO || d->kernel > GPAD_KERNEL_PANEL)
         return fail(GPAD_ERR_INVALID, "dims: bad kernel");
+    if (!std::isfinite(d->tol_gap)) return fail(GPAD_ERR_INVALID, "dims: tol_gap must be finite");
     return GPAD_OK;
 }
 
@@ -555,6 +556,7 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
     a.N = N;
     a.check_every = d.check_every;
     a.tol = tol;
+    a.tol_gap = d.tol_gap > 0.0 ? d.tol_gap : tol;
     a.L = h->L;
     a.theta = (const T*)h->theta.p;
     a.beta = (const T*)h->beta.p;

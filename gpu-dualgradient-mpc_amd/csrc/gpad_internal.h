@@ -30,6 +30,18 @@ struct Tuning {
     int flat_a_lds = 1;       // GPAD_OPT_FLAT_A_LDS: flat fragment image in LDS when it fits
 };
 
+// Rounding margin of the Algorithm 1 decisions, in units of max_i(|chain_i| + |pD_i|): a test
+// passes when L max(chain + pD) + kViolMargin L max(|chain| + |pD|) <= tol (16 units of 2^-24 /
+// 2^-53).  Test (A) is nominated by the recursive u = G_L z and decided on the direct chain
+// G_L z (which then also resets u).  Same constants and arithmetic as oracle/gpad_oracle.h.
+template <typename T> struct ViolMargin;
+template <> struct ViolMargin<float> { static constexpr double value = 0x1p-20; };
+template <> struct ViolMargin<double> { static constexpr double value = 0x1p-49; };
+// the decision itself, one expression everywhere (no contraction: -ffp-contract=off)
+__host__ __device__ inline bool viol_ok(double viol, double mag, double L, double tol, double margin) {
+    return viol * L + margin * mag * L <= tol;
+}
+
 // Arguments of a fused solve launch (all kernel families).  Every instance b of the batch
 // reads its matrices at MGt + b*strideA / GLt + b*strideB (stride 0 = shared).
 template <typename T>
@@ -49,6 +61,7 @@ struct SolveArgs {
     int n, m, ldn, ldm;    // ldn = round_up(n,4), ldm = round_up(m,4)
     int batch, N, check_every;
     double tol, L;         // Algorithm 1: stop when L*viol <= tol (tol <= 0: fixed N)
+    double tol_gap;        // e_V of test (B)'s duality-gap term (set = tol when the caller gives <= 0)
     const T* theta;        // [N+2] theta_v (two zero pads: kernels prefetch ahead)
     const T* beta;         // [N+2] beta_v
     int* iters;            // [batch] iterations executed

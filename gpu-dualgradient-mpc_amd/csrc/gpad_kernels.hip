@@ -56,7 +56,7 @@ __device__ __forceinline__ StreamLds<T> stream_lds(unsigned char* smem, int ldn,
     s.gp = s.ys + ldm;                  // [ldn] g_P
     s.pd = s.gp + ldn;                  // [ldm] p_D
     s.us = s.pd + ldm;                  // [ldm] u = G_L z (termination test, by recursion)
-    s.slots = reinterpret_cast<CheckSlot*>(s.us + ldm);
+    s.slots = reinterpret_cast<CheckSlot*>(s.us + ldm);  // [2][waves]: test, verification of (A)
     return s;
 }
 
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(kStreamBlock) void gpad_stream_kernel(SolveArgs<T> 
         __syncthreads();
         // ---- phase 2: 8d + next 8a, rows of G/L ------------------------------------------
         const bool chk = use_tol && ((v + 1) % a.check_every) == 0;
-        T violz = neg_inf<T>(), violh = neg_inf<T>(), wmin = -neg_inf<T>();
+        T violz = neg_inf<T>(), violh = neg_inf<T>(), wmin = -neg_inf<T>(), magh = T(0);
         double gap = 0.0;
         for (int r0 = 4 * tid; r0 < m; r0 += 4 * kStreamBlock) {
             T c[4] = {T(0), T(0), T(0), T(0)};
@@ -170,6 +170,7 @@ __global__ __launch_bounds__(kStreamBlock) void gpad_stream_kernel(SolveArgs<T> 
                         if (chk) {
                             const T t = c[r] + pdi;
                             violh = fmax(violh, t);
+                            magh = fmax(magh, absd(c[r]) + absd(pdi));
                             wmin = fmin(wmin, wi);
                             gap -= (double)wi * (double)t;
                             violz = fmax(violz, ui + pdi);
@@ -180,10 +181,33 @@ __global__ __launch_bounds__(kStreamBlock) void gpad_stream_kernel(SolveArgs<T> 
                 }
             }
         }
-        if (chk) check_publish<T>(s.slots, violz, violh, wmin, gap);
+        if (chk) check_publish<T>(s.slots, violz, violh, wmin, gap, magh);
         __syncthreads();
         it = v + 1;
-        if (chk) done = check_decide(s.slots, nwaves, a.L, a.tol);
+        if (chk) {
+            const int st1 = check_stage1<T>(s.slots, nwaves, a.L, a.tol, a.tol_gap);
+            bool verified = false;
+            if (st1 & 1) {  // (A) nominated: decide on the direct chain G_L z, reset u to it
+                T vc = neg_inf<T>(), mc = T(0);
+                for (int r0 = 4 * tid; r0 < m; r0 += 4 * kStreamBlock) {
+                    T c[4] = {T(0), T(0), T(0), T(0)};
+                    chain4<T>(GLt, ldm, r0, s.zs, n, c);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int i = r0 + r;
+                        if (i < m) {
+                            s.us[i] = c[r];
+                            vc = fmax(vc, c[r] + s.pd[i]);
+                            mc = fmax(mc, absd(c[r]) + absd(s.pd[i]));
+                        }
+                    }
+                }
+                check_publish<T>(s.slots + nwaves, vc, vc, vc, 0.0, mc);
+                __syncthreads();
+                verified = check_verify<T>(s.slots + nwaves, nwaves, a.L, a.tol);
+            }
+            done = check_code(st1, verified);
+        }
         if (done) break;
     }
     const T* zout = done == 2 ? s.zh : s.zs;  // test (B) certifies zhat
@@ -198,7 +222,7 @@ __global__ __launch_bounds__(kStreamBlock) void gpad_stream_kernel(SolveArgs<T> 
 template <typename T>
 hipError_t launch_stream(const SolveArgs<T>& a, hipStream_t st) {
     const size_t lds = sizeof(T) * (size_t)(3 * a.ldn + 4 * a.ldm) +
-                       sizeof(CheckSlot) * (kStreamBlock / 64);
+                       sizeof(CheckSlot) * 2 * (kStreamBlock / 64);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)gpad_stream_kernel<T>,
@@ -228,7 +252,7 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
     __shared__ __attribute__((aligned(16))) float w_l[FLAT ? kFlatMaxCells * PA : PA];  // w (flat: wP)
     __shared__ __attribute__((aligned(16))) float zh_l[PB];  // zhat, broadcast to G/L rows
     __shared__ __attribute__((aligned(16))) float z_l[PB];   // z_{-1}, to seed u = G_L z
-    __shared__ CheckSlot slots[kResidentMaxThreads / 64];
+    __shared__ CheckSlot slots[2][kResidentMaxThreads / 64];  // test, verification of (A)
 
     const int tid = threadIdx.x;
     // finisher mode (phased panel solves): this block takes survivor blockIdx.x of the list
@@ -330,7 +354,7 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
             }
         }
         __syncthreads();
-        float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY;
+        float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY, magh = 0.0f;
         double gap = 0.0;
         if (!isA) {  // ---- 8d + next 8a ------------------------------------------------
             const float c = chain_regs<KB, K>(r, zh_l);
@@ -347,6 +371,7 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
                 if (chk) {
                     const float t = c + pdi;
                     violh = t;
+                    magh = __builtin_fabsf(c) + __builtin_fabsf(pdi);
                     wmin = wi;
                     gap = -((double)wi * (double)t);
                     violz = ui + pdi;
@@ -356,12 +381,32 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
                 put_w(wi);
             }
         }
-        if (chk) check_publish<float>(slots, violz, violh, wmin, gap);
+        if (chk) check_publish<float>(slots[0], violz, violh, wmin, gap, magh);
         __syncthreads();
         it = v + 1;
         th = th_next;
         bn = bn_next;
-        if (chk) done = check_decide(slots, nwaves, a.L, a.tol);
+        if (chk) {
+            const int st1 = check_stage1<float>(slots[0], nwaves, a.L, a.tol, a.tol_gap);
+            bool verified = false;
+            if (st1 & 1) {  // (A) nominated: decide on the direct chain G_L z, reset u to it
+                if (isA && live) z_l[row] = zi;
+                __syncthreads();
+                float vc = -INFINITY, mc = 0.0f;
+                if (!isA) {
+                    const float cz = chain_regs<KB, K>(r, z_l);
+                    if (live) {
+                        ui = cz;
+                        vc = cz + pdi;
+                        mc = __builtin_fabsf(cz) + __builtin_fabsf(pdi);
+                    }
+                }
+                check_publish<float>(slots[1], vc, vc, vc, 0.0, mc);
+                __syncthreads();
+                verified = check_verify<float>(slots[1], nwaves, a.L, a.tol);
+            }
+            done = check_code(st1, verified);
+        }
         if (done) break;
     }
     if (live) {

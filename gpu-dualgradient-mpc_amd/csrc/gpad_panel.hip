@@ -101,7 +101,10 @@ hipError_t launch_pack_panel(const float* ML, const float* G, int n, int m, int 
 struct PanelSlot {  // per wave (row tile), per instance partials of the Algorithm-1 test
     float violz[16], violh[16], wmin[16];
     double gap[16];
+    float magh[16];  // max(|G_L zhat| + |pD|): test (B)'s rounding scale
 };
+// (A) nominated by the recursive u is decided on the direct G_L z (gpad_internal.h ViolMargin):
+// the verification reuses violz / magh of the slots for max(G_L z + pD) / max(|G_L z| + |pD|).
 
 // acc = A[tile t] (T k-blocks, streamed from L2 one block ahead) x B (LDS, fragment order).
 // The MFMA k-order is ascending (block 0..T-1, step 0..3), i.e. the reference's sequential chain.
@@ -244,7 +247,7 @@ __global__ __launch_bounds__(64 * T) void gpad_panel_kernel(SolveArgs<float> a) 
             }
             __syncthreads();
             // ---- GEMM 2 + epilogue: y+ = [w + G_L zhat + p_D]+ (8d), next w (8a) ----------
-            float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY;
+            float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY, magh = 0.0f;
             double gap = 0.0;
             {
                 const f32x4 acc = panel_gemm<T>(PA2, Zh, voff, lane);
@@ -265,6 +268,7 @@ __global__ __launch_bounds__(64 * T) void gpad_panel_kernel(SolveArgs<float> a) 
                         if (chk && active && (16 * t + 4 * r + j) < m) {
                             const float tt = cv + pd[r];
                             violh = fmaxf(violh, tt);
+                            magh = fmaxf(magh, __builtin_fabsf(cv) + __builtin_fabsf(pd[r]));
                             wmin = fminf(wmin, wv[r]);
                             gap -= (double)wv[r] * (double)tt;
                             violz = fmaxf(violz, u[r] + pd[r]);
@@ -281,42 +285,95 @@ __global__ __launch_bounds__(64 * T) void gpad_panel_kernel(SolveArgs<float> a) 
 
             // ---- Algorithm 1 test, per column: lane groups j, then row tiles through LDS ----
             int code = 0;
+            bool zh_out = true;  // this iteration's zhat still in Zh (no verification GEMM ran)
             if (chk) {
 #pragma unroll
                 for (int o = 16; o < 64; o <<= 1) {
                     violz = fmaxf(violz, __shfl_xor(violz, o, 64));
                     violh = fmaxf(violh, __shfl_xor(violh, o, 64));
+                    magh = fmaxf(magh, __shfl_xor(magh, o, 64));
                     wmin = fminf(wmin, __shfl_xor(wmin, o, 64));
                     gap += __shfl_xor(gap, o, 64);
                 }
                 if (j == 0) {
                     slots[t].violz[c] = violz;
                     slots[t].violh[c] = violh;
+                    slots[t].magh[c] = magh;
                     slots[t].wmin[c] = wmin;
                     slots[t].gap[c] = gap;
                 }
                 __syncthreads();
+                int st1 = 0;
                 if (active) {
-                    double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gq = 0.0;
+                    double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gq = 0.0, mh = 0.0;
 #pragma unroll
                     for (int s2 = 0; s2 < T; ++s2) {
                         vz = fmax(vz, (double)slots[s2].violz[c]);
                         vh = fmax(vh, (double)slots[s2].violh[c]);
+                        mh = fmax(mh, (double)slots[s2].magh[c]);
                         wm = fmin(wm, (double)slots[s2].wmin[c]);
                         gq += slots[s2].gap[c];
                     }
-                    if (vz * a.L <= a.tol) code = 1;
-                    else if ((vh * a.L <= a.tol) && (wm >= 0.0) && (gq * a.L <= a.tol)) code = 2;
+                    st1 = (vz * a.L <= a.tol ? 1 : 0) |
+                          ((viol_ok(vh, mh, a.L, a.tol, ViolMargin<float>::value) && (wm >= 0.0) &&
+                            (gq * a.L <= a.tol_gap)) ? 2 : 0);
                 }
+                bool verified = false;
+                if (__syncthreads_or(st1 & 1)) {  // (A) nominated somewhere: G_L z for the panel
+                    zh_out = false;
+                    if (st1 & 2) {  // test (B)'s result (zhat) out now: Zh is about to hold z
+                        const float4 h4 = Zh4[slot];
+                        const float zh[4] = {h4.x, h4.y, h4.z, h4.w};
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int i = 16 * t + 4 * r + j;
+                            if (i < n) a.z[(size_t)inst * n + i] = zh[r];
+                        }
+                    }
+                    Zh4[slot] = make_float4(z[0], z[1], z[2], z[3]);
+                    __syncthreads();
+                    const f32x4 cz = panel_gemm<T>(PA2, Zh, voff, lane);
+                    const float4 p4 = Pd4[slot];
+                    const float pd[4] = {p4.x, p4.y, p4.z, p4.w};
+                    float vc = -INFINITY, mc = 0.0f;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        if ((st1 & 1) && (16 * t + 4 * r + j) < m) {
+                            u[r] = cz[r];  // the recursion restarts from the direct value
+                            vc = fmaxf(vc, cz[r] + pd[r]);
+                            mc = fmaxf(mc, __builtin_fabsf(cz[r]) + __builtin_fabsf(pd[r]));
+                        }
+                    }
+#pragma unroll
+                    for (int o = 16; o < 64; o <<= 1) {
+                        vc = fmaxf(vc, __shfl_xor(vc, o, 64));
+                        mc = fmaxf(mc, __shfl_xor(mc, o, 64));
+                    }
+                    if (j == 0) {  // every wave finished reading the slots before the barrier above
+                        slots[t].violz[c] = vc;
+                        slots[t].magh[c] = mc;
+                    }
+                    __syncthreads();
+                    if (st1 & 1) {
+                        double vcc = -INFINITY, mcc = 0.0;
+#pragma unroll
+                        for (int s2 = 0; s2 < T; ++s2) {
+                            vcc = fmax(vcc, (double)slots[s2].violz[c]);
+                            mcc = fmax(mcc, (double)slots[s2].magh[c]);
+                        }
+                        verified = viol_ok(vcc, mcc, a.L, a.tol, ViolMargin<float>::value);
+                    }
+                }
+                code = ((st1 & 1) && verified) ? 1 : ((st1 & 2) ? 2 : 0);
             }
             // ---- finished columns: results out ---------------------------------------------
             if (active && (code != 0 || v >= N)) {
-                const float4 h4 = Zh4[slot];  // this iteration's zhat (own slot, not yet overwritten)
+                const float4 h4 = Zh4[slot];  // this iteration's zhat (own slot), unless verified over
                 const float zh[4] = {h4.x, h4.y, h4.z, h4.w};
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int i = 16 * t + 4 * r + j;
-                    if (i < n) a.z[(size_t)inst * n + i] = code == 2 ? zh[r] : z[r];  // (B): zhat
+                    if (i < n && (code != 2 || zh_out)) a.z[(size_t)inst * n + i] = code == 2 ? zh[r] : z[r];
                     if (i < m) a.y[(size_t)inst * m + i] = y[r];
                 }
                 if (t == 0 && j == 0) {
@@ -648,12 +705,13 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             }
             __syncthreads();
             // ---- GEMM 2 + epilogue: y+ = [w + G_L zhat + p_D]+ (8d), next w (8a) ----------
-            float violz[Q], violh[Q], wmin[Q];
+            float violz[Q], violh[Q], wmin[Q], magh[Q];
             double gap[Q];
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
                 violz[q] = violh[q] = -INFINITY;
                 wmin[q] = INFINITY;
+                magh[q] = 0.0f;
                 gap[q] = 0.0;
             }
             if constexpr (NU > 0) {
@@ -686,6 +744,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                             if (chk && act[q] && (16 * t + 4 * r + j) < m) {
                                 const float tt = cv + pd[r];
                                 violh[q] = fmaxf(violh[q], tt);
+                                magh[q] = fmaxf(magh[q], __builtin_fabsf(cv) + __builtin_fabsf(pd[r]));
                                 wmin[q] = fminf(wmin[q], wv[r]);
                                 gap[q] -= (double)wv[r] * (double)tt;
                                 violz[q] = fmaxf(violz[q], u[q][r] + pd[r]);
@@ -699,6 +758,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                         for (int o = 16; o < 64; o <<= 1) {
                             violz[q] = fmaxf(violz[q], __shfl_xor(violz[q], o, 64));
                             violh[q] = fmaxf(violh[q], __shfl_xor(violh[q], o, 64));
+                            magh[q] = fmaxf(magh[q], __shfl_xor(magh[q], o, 64));
                             wmin[q] = fminf(wmin[q], __shfl_xor(wmin[q], o, 64));
                             gap[q] += __shfl_xor(gap[q], o, 64);
                         }
@@ -706,6 +766,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                             PanelSlot& S = L.slots[p0 + q][t];
                             S.violz[c] = violz[q];
                             S.violh[c] = violh[q];
+                            S.magh[c] = magh[q];
                             S.wmin[c] = wmin[q];
                             S.gap[c] = gap[q];
                         }
@@ -721,24 +782,88 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             // item's columns (lane 16 pp + cc <-> panel pp, column cc) and votes by ballot, so the
             // outcome is uniform across the workgroup without a second barrier ---------------------
             unsigned m1 = 0u, m2 = 0u;
+            bool zh_out = true;  // this iteration's zhat still in L.Zh (no verification GEMM ran)
             if (chk) {
-                int cd = 0;
+                int st1 = 0;
                 const int pp = (lane >> 4) & 1, cc = lane & 15;
                 if (lane < 32 && ((live >> lane) & 1u)) {
-                    double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gq = 0.0;
+                    double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gq = 0.0, mh = 0.0;
 #pragma unroll
                     for (int s2 = 0; s2 < T; ++s2) {
                         const PanelSlot& S = L.slots[pp][s2];
                         vz = fmax(vz, (double)S.violz[cc]);
                         vh = fmax(vh, (double)S.violh[cc]);
+                        mh = fmax(mh, (double)S.magh[cc]);
                         wm = fmin(wm, (double)S.wmin[cc]);
                         gq += S.gap[cc];
                     }
-                    if (vz * a.L <= a.tol) cd = 1;
-                    else if ((vh * a.L <= a.tol) && (wm >= 0.0) && (gq * a.L <= a.tol)) cd = 2;
+                    st1 = (vz * a.L <= a.tol ? 1 : 0) |
+                          ((viol_ok(vh, mh, a.L, a.tol, ViolMargin<float>::value) && (wm >= 0.0) &&
+                            (gq * a.L <= a.tol_gap)) ? 2 : 0);
                 }
-                m1 = (unsigned)__ballot(cd == 1);
-                m2 = (unsigned)__ballot(cd == 2);
+                const unsigned mA = (unsigned)__ballot(st1 & 1);
+                m2 = (unsigned)__ballot(st1 & 2);
+                if (mA) {  // (A) nominated for some column of the item: G_L z of both panels
+                    zh_out = false;
+                    if constexpr (NU > 0) {
+#pragma unroll
+                        for (int q = 0; q < Q; ++q) {
+                            const int bit = 16 * (p0 + q) + c;
+                            if (act[q] && ((m2 >> bit) & 1u)) {  // test (B)'s zhat out before z replaces it
+                                const float4 h4 = L.Zh[p0 + q][slot];
+                                const float zh[4] = {h4.x, h4.y, h4.z, h4.w};
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) {
+                                    const int i = 16 * t + 4 * r + j;
+                                    if (i < n) a.z[(size_t)inst[q] * n + i] = zh[r];
+                                }
+                            }
+                            L.Zh[p0 + q][slot] = make_float4(z[q][0], z[q][1], z[q][2], z[q][3]);
+                        }
+                    }
+                    __syncthreads();
+                    if constexpr (NU > 0) {
+                        f32x4 cz[2];
+                        panel_gemm2<T, NU == 2>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, cz[0], cz[1]);
+#pragma unroll
+                        for (int q = 0; q < Q; ++q) {
+                            const bool nom = act[q] && ((mA >> (16 * (p0 + q) + c)) & 1u);
+                            const float4 p4 = L.Pd[p0 + q][slot];
+                            const float pd[4] = {p4.x, p4.y, p4.z, p4.w};
+                            float vc = -INFINITY, mc = 0.0f;
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                if (nom && (16 * t + 4 * r + j) < m) {
+                                    u[q][r] = cz[q][r];  // the recursion restarts from the direct value
+                                    vc = fmaxf(vc, cz[q][r] + pd[r]);
+                                    mc = fmaxf(mc, __builtin_fabsf(cz[q][r]) + __builtin_fabsf(pd[r]));
+                                }
+                            }
+#pragma unroll
+                            for (int o = 16; o < 64; o <<= 1) {
+                                vc = fmaxf(vc, __shfl_xor(vc, o, 64));
+                                mc = fmaxf(mc, __shfl_xor(mc, o, 64));
+                            }
+                            if (j == 0) {  // the stage-1 reads of every wave precede the barrier above
+                                L.slots[p0 + q][t].violz[c] = vc;
+                                L.slots[p0 + q][t].magh[c] = mc;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                    bool ver = false;
+                    if (lane < 32 && ((mA >> lane) & 1u)) {
+                        double vcc = -INFINITY, mcc = 0.0;
+#pragma unroll
+                        for (int s2 = 0; s2 < T; ++s2) {
+                            vcc = fmax(vcc, (double)L.slots[pp][s2].violz[cc]);
+                            mcc = fmax(mcc, (double)L.slots[pp][s2].magh[cc]);
+                        }
+                        ver = viol_ok(vcc, mcc, a.L, a.tol, ViolMargin<float>::value);
+                    }
+                    m1 = (unsigned)__ballot(ver);
+                    m2 &= ~m1;
+                }
             }
             // ---- finished columns: results out ---------------------------------------------
             if constexpr (NU > 0) {
@@ -746,21 +871,19 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 for (int q = 0; q < Q; ++q) {
                     const int bit = 16 * (p0 + q) + c;
                     const int cdq = ((m1 >> bit) & 1u) ? 1 : (((m2 >> bit) & 1u) ? 2 : 0);
-                    int code[Q];
-                    code[q] = cdq;
-                    if (act[q] && (code[q] != 0 || v >= N)) {
+                    if (act[q] && (cdq != 0 || v >= N)) {
                         const float4 h4 = L.Zh[p0 + q][slot];
                         const float zh[4] = {h4.x, h4.y, h4.z, h4.w};
                         const size_t b = (size_t)inst[q];
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             const int i = 16 * t + 4 * r + j;
-                            if (i < n) a.z[b * n + i] = code[q] == 2 ? zh[r] : z[q][r];  // (B): zhat
+                            if (i < n && (cdq != 2 || zh_out)) a.z[b * n + i] = cdq == 2 ? zh[r] : z[q][r];
                             if (i < m) a.y[b * m + i] = y[q][r];
                         }
                         if (t == 0 && j == 0) {
                             a.iters[b] = v;
-                            a.conv[b] = code[q];
+                            a.conv[b] = cdq;
                         }
                         act[q] = false;
                     }

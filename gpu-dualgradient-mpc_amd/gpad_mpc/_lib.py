@@ -51,7 +51,7 @@ FILE_ROWMAJOR, FILE_FLIPPED, FILE_FLAT = 0, 1, 2
 class Dims(C.Structure):
     _fields_ = [("n", C.c_int), ("m", C.c_int), ("batch", C.c_int), ("shared", C.c_int),
                 ("dtype", C.c_int), ("memory", C.c_int), ("schedule", C.c_int),
-                ("check_every", C.c_int), ("kernel", C.c_int)]
+                ("check_every", C.c_int), ("kernel", C.c_int), ("tol_gap", C.c_double)]
 
 
 class Stats(C.Structure):

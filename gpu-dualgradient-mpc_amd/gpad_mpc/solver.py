@@ -100,19 +100,21 @@ class GpadSolver:
 
     def setup(self, ML, G, L: float, *, n: int, m: int, batch: int = 1, shared: bool = True,
               schedule: int = _lib.SCHEDULE_MATLAB, check_every: int = 10,
-              kernel: int = _lib.KERNEL_AUTO, scaled: bool = False) -> None:
-        """Bind (ML, G, L) -- or (MGneg, GL, L) with ``scaled`` (reference data-file form)."""
+              kernel: int = _lib.KERNEL_AUTO, scaled: bool = False, tol_gap: float = 0.0) -> None:
+        """Bind (ML, G, L) -- or (MGneg, GL, L) with ``scaled`` (reference data-file form).
+        ``tol_gap``: e_V of test (B)'s gap term (acceldualgrad.m:13; 0 = the run's tol)."""
         mem = _lib.MEM_DEVICE if _is_torch(ML) else _lib.MEM_HOST
         if _is_torch(ML) and not ML.is_cuda:
             raise ValueError("torch inputs must live on the GPU (use numpy for host memory)")
         self.dims = Dims(n=n, m=m, batch=batch, shared=int(bool(shared)), dtype=_dtype_code(ML),
-                         memory=mem, schedule=schedule, check_every=check_every, kernel=kernel)
+                         memory=mem, schedule=schedule, check_every=check_every, kernel=kernel,
+                         tol_gap=float(tol_gap))
         fn = self.lib.gpad_setup_scaled if scaled else self.lib.gpad_setup
         check(fn(self.h, C.byref(self.dims), _ptr(ML), _ptr(G), float(L)), "gpad_setup")
 
     def setup_flat(self, MGf, GLf, L: float, *, n_u: int, batch: int = 1,
                    schedule: int = _lib.SCHEDULE_MATLAB, check_every: int = 10,
-                   kernel: int = _lib.KERNEL_AUTO) -> None:
+                   kernel: int = _lib.KERNEL_AUTO, tol_gap: float = 0.0) -> None:
         """Bind the reference's flat battery data (seq_functions.cpp:5-43): MGf (N x m) flat
         sign-folded M_G, GLf (m x N) flat G_L; then ``run(..., scaled=True)`` with g_P, p_D.
         kernel=KERNEL_STREAM forces the LDS flat kernel (else the register-resident one when
@@ -120,7 +122,7 @@ class GpadSolver:
         Nh, m = MGf.shape
         mem = _lib.MEM_DEVICE if _is_torch(MGf) else _lib.MEM_HOST
         self.dims = Dims(n=n_u * Nh, m=m, batch=batch, shared=1, dtype=_lib.DTYPE_F32, memory=mem,
-                         schedule=schedule, check_every=check_every, kernel=kernel)
+                         schedule=schedule, check_every=check_every, kernel=kernel, tol_gap=float(tol_gap))
         check(self.lib.gpad_setup_flat(self.h, C.byref(self.dims), int(n_u), _ptr(MGf), _ptr(GLf),
                                        float(L)), "gpad_setup_flat")
 
@@ -311,7 +313,7 @@ def schedule(N: int, kind: int = _lib.SCHEDULE_MATLAB):
 
 def solve(z0, y0, ML, M, G, g, N: int, L: float, tol: float = 0.0, *, shared: bool = True,
           schedule: int = _lib.SCHEDULE_MATLAB, check_every: int = 10,
-          kernel: int = _lib.KERNEL_AUTO, device: int = 0):
+          kernel: int = _lib.KERNEL_AUTO, device: int = 0, tol_gap: float = 0.0):
     """solve(z0, y0, ML, M, G, g, N, L, tol) -> (z*, y*, stats).
 
     Shapes: z0 (n,) or (batch, n); y0 (m,) or (batch, m); ML (n, m) or (batch, n, m); M like z0;
@@ -333,7 +335,7 @@ def solve(z0, y0, ML, M, G, g, N: int, L: float, tol: float = 0.0, *, shared: bo
     shared = shared and ML.ndim == 2
     with GpadSolver(device) as s:
         s.setup(ML, G, L, n=n, m=m, batch=batch, shared=shared, schedule=schedule,
-                check_every=check_every, kernel=kernel)
+                check_every=check_every, kernel=kernel, tol_gap=tol_gap)
         st = s.run(z, y, M, g, N, tol)
     return z, y, st
 

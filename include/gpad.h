@@ -64,6 +64,8 @@ typedef struct gpad_dims {
     int schedule;    /* GPAD_SCHEDULE_*                                                 */
     int check_every; /* termination test period K when tol > 0 (<= 0 -> 10)            */
     int kernel;      /* GPAD_KERNEL_*                                                   */
+    double tol_gap;  /* e_V of acceldualgrad.m:13: tolerance of test (B)'s duality-gap term
+                      * -w'(G zhat - g); <= 0 (e.g. a zeroed struct): the run's tol (= e_g) */
 } gpad_dims_t;
 
 typedef struct gpad_stats {
@@ -114,7 +116,15 @@ int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* dims, int n_u, const flo
  *   g : constraint rhs         [batch][m]   (b_i; p_D = -g/L, acceldualgrad.m:23)
  *   N : max iterations (reference: N_v = 100, main.cu:87)
  *   tol <= 0: exactly N iterations (paper Algorithm 2, main.cu behaviour);
- *   tol  > 0: Algorithm 1 test every check_every iterations (acceldualgrad.m:66-79).
+ *   tol  > 0: Algorithm 1 test every check_every iterations (acceldualgrad.m:66-79), tol = e_g:
+ *     (A) max(G z - g) <= tol                                  -> z* = z,    converged = 1
+ *     (B) max(G zhat - g) <= tol, w >= 0, -w'(G zhat - g) <= e_V -> z* = zhat, converged = 2
+ *     e_V = dims.tol_gap (default tol).  Both violation tests are decided on directly evaluated
+ *     chains (G/L z, G/L zhat) with a rounding margin of 16 units of 2^-24 (f32) / 2^-53 (f64)
+ *     of max_i |(G x)_i| + |g_i| / L, so a reported convergence holds for G z* - g evaluated
+ *     exactly on the returned z*.  The value-function branches of acceldualgrad.m:73,76
+ *     (valuefcn(zhat) e_V/(1+e_V), valuefcn - dualfcn <= e_V max(dualfcn, 1)) need H and q,
+ *     which this surface does not carry: they are not evaluated.
  * Host memory: synchronous.  Device memory: enqueued on the handle's stream; synchronous only
  * when st != NULL (stats need the per-instance counters). */
 int gpad_run(gpad_handle_t h, void* z0, void* y0, const void* M, const void* g, int N, double tol,

@@ -77,12 +77,20 @@ void orc_schedule(int N, int kind, double* theta, double* beta) {
 }
 
 /* Algorithm 1 test (nmpc12-gpad.pdf sec. 4.2; acceldualgrad.m:66-79 restricted to the
- * branches computable from (ML, M, G, g, L)):
+ * branches computable from (ML, M, G, g, L); the value-function branches :73,76 need H and q):
  *   (A) max_i (G z - g)_i <= tol                                   -> stop, return z     (1)
- *   (B) max_i (G zhat - g)_i <= tol, w >= 0, -w'(G zhat - g) <= tol -> stop, return zhat  (2)
- * with G x - g = L (GL x + pD).  GL zhat is the step-4 chain itself; GL z is carried by the
- * same affine recursion as z (8c): u_v = (1-theta_v) u_{v-1} + theta_v (GL zhat_v), u_{-1} =
- * GL z_{-1} -- equal to GL z_v in exact arithmetic, and it costs no extra mat-vec.  The paper
+ *   (B) max_i (G zhat - g)_i <= tol, w >= 0, -w'(G zhat - g) <= tol_gap -> stop, return zhat (2)
+ * with G x - g = L (GL x + pD) (tol = e_g, tol_gap = e_V of acceldualgrad.m:12-13).
+ *
+ * Certified on the constraint itself.  GL zhat is the step-4 chain.  GL z is carried by the
+ * affine recursion of 8c, u_v = (1-theta_v) u_{v-1} + theta_v (GL zhat_v) -- equal to GL z_v
+ * in exact arithmetic, but its f32 rounding drifts from the f32 z (measured: ~10 units of
+ * 2^-24 of max|G z|+|g| after 300 iterations, 400 after 20000).  So the recursion only
+ * NOMINATES: when it passes (A), GL z is evaluated directly (one chain per row, the step-4
+ * chain on z), u is reset to it, and (A) is decided on the direct value.  Both decisions keep a
+ * rounding margin: accept when L max(s) + ORC_MARGIN L max_i(|a_i| + |pD_i|) <= tol, where
+ * s = a + pD and a is the chain (GL z or GL zhat): the f32 chain error measured against fp64
+ * G x - g stays below 3.3 units of 2^-24 of that scale, the margin is 16 units.  The paper
  * (sec. 4.2) returns whichever candidate passed; the commented MATLAB returns z_v in both
  * branches, which for (B) hands back a point that was never certified. */
 static float orc_chain(const float* row, const float* x, int n) {
@@ -91,26 +99,47 @@ static float orc_chain(const float* row, const float* x, int n) {
     return sum;
 }
 
-static int orc_check_f32(const float* u, const float* ch, const float* pD, const float* w, int m,
-                         float L, float tol) {
+/* chain of row i of G_L on x: full rows (row-major m x n) or the flat battery rows */
+typedef float (*orc_row_fn)(const void* ctx, int i, const float* x);
+
+static int orc_check_f32(float* u, const float* ch, const float* pD, const float* w, const float* z,
+                         int m, orc_row_fn rowf, const void* ctx, double L, double tol, double tol_gap) {
     float viol = -INFINITY;
     for (int i = 0; i < m; i++) viol = fmaxf(viol, u[i] + pD[i]);
-    if ((double)viol * (double)L <= (double)tol) return 1;
-    float violh = -INFINITY, wmin = INFINITY;
+    if ((double)viol * L <= tol) {  /* (A) nominated by the recursion: decide on G_L z itself */
+        float vc = -INFINITY, mag = 0.0f;
+        for (int i = 0; i < m; i++) {
+            const float c = rowf(ctx, i, z);
+            u[i] = c;
+            vc = fmaxf(vc, c + pD[i]);
+            mag = fmaxf(mag, fabsf(c) + fabsf(pD[i]));
+        }
+        if ((double)vc * L + ORC_MARGIN_F32 * (double)mag * L <= tol) return 1;
+    }
+    float violh = -INFINITY, magh = 0.0f, wmin = INFINITY;
     double gap = 0.0;
     for (int i = 0; i < m; i++) {
         const float t = ch[i] + pD[i];
         violh = fmaxf(violh, t);
+        magh = fmaxf(magh, fabsf(ch[i]) + fabsf(pD[i]));
         wmin = fminf(wmin, w[i]);
         gap -= (double)w[i] * (double)t;
     }
-    gap *= (double)L;
-    return (((double)violh * (double)L <= (double)tol) && (wmin >= 0.0f) && (gap <= (double)tol)) ? 2 : 0;
+    return (((double)violh * L + ORC_MARGIN_F32 * (double)magh * L <= tol) && (wmin >= 0.0f) &&
+            (gap * L <= tol_gap)) ? 2 : 0;
 }
 
+struct orc_full_rows { const float* GL; int n; };
+static float orc_full_row(const void* ctx, int i, const float* x) {
+    const struct orc_full_rows* c = (const struct orc_full_rows*)ctx;
+    return orc_chain(c->GL + (size_t)i * c->n, x, c->n);
+}
+
+static double orc_tol_gap(double tol, double tol_gap) { return tol_gap > 0.0 ? tol_gap : tol; }
+
 int orc_solve_f32(float* z, float* y, const float* MGneg, const float* gP, const float* GL,
-                  const float* pD, int n, int m, int N, float L, float tol, int check_every,
-                  const float* theta, const float* beta, int* converged) {
+                  const float* pD, int n, int m, int N, float L, double tol, double tol_gap,
+                  int check_every, const float* theta, const float* beta, int* converged) {
     const int mm = m > 0 ? m : 1;
     float* base = (float*)malloc(sizeof(float) * (size_t)mm * 6);
     float* ycur = base;
@@ -123,7 +152,9 @@ int orc_solve_f32(float* z, float* y, const float* MGneg, const float* gP, const
     if (check_every <= 0) check_every = 10;
     memcpy(ycur, y, sizeof(float) * m);
     memcpy(yprev, y, sizeof(float) * m); /* acceldualgrad.m:16: y_0 = y_{-1} */
-    const int use_tol = tol > 0.0f;
+    const int use_tol = tol > 0.0;
+    const double tgap = orc_tol_gap(tol, tol_gap);
+    const struct orc_full_rows rows = {GL, n};
     if (use_tol)
         for (int i = 0; i < m; i++) u[i] = orc_chain(GL + (size_t)i * n, z, n);
     int it = 0, conv = 0;
@@ -141,7 +172,7 @@ int orc_solve_f32(float* z, float* y, const float* MGneg, const float* gP, const
                 u[i] = fmaf(omt, u[i], th * ch[i]);
             }
             if ((it % check_every) == 0) {
-                const int c = orc_check_f32(u, ch, pD, w, m, L, tol);
+                const int c = orc_check_f32(u, ch, pD, w, z, m, orc_full_row, &rows, (double)L, tol, tgap);
                 if (c) {
                     if (c == 2) memcpy(z, zhat, sizeof(float) * n);
                     conv = c;
@@ -158,24 +189,36 @@ int orc_solve_f32(float* z, float* y, const float* MGneg, const float* gP, const
 }
 
 /* ---- fp64, acceldualgrad.m operation order ------------------------------------- */
-static int orc_check_f64(const double* u, const double* ch, const double* pD, const double* w,
-                         int m, double L, double tol) {
+/* the fp64 twin of orc_check_f32 (margin ORC_MARGIN_F64 = 16 units of 2^-53) */
+static int orc_check_f64(double* u, const double* ch, const double* pD, const double* w, const double* z,
+                         const double* GL, int n, int m, double L, double tol, double tol_gap) {
     double viol = -INFINITY;
     for (int i = 0; i < m; i++) viol = fmax(viol, u[i] + pD[i]);
-    if (viol * L <= tol) return 1;
-    double violh = -INFINITY, wmin = INFINITY, gap = 0.0;
+    if (viol * L <= tol) {
+        double vc = -INFINITY, mag = 0.0;
+        for (int i = 0; i < m; i++) {
+            double c = 0.0;
+            for (int j = 0; j < n; j++) c = fma(GL[(size_t)i * n + j], z[j], c);
+            u[i] = c;
+            vc = fmax(vc, c + pD[i]);
+            mag = fmax(mag, fabs(c) + fabs(pD[i]));
+        }
+        if (vc * L + ORC_MARGIN_F64 * mag * L <= tol) return 1;
+    }
+    double violh = -INFINITY, magh = 0.0, wmin = INFINITY, gap = 0.0;
     for (int i = 0; i < m; i++) {
         const double t = ch[i] + pD[i];
         violh = fmax(violh, t);
+        magh = fmax(magh, fabs(ch[i]) + fabs(pD[i]));
         wmin = fmin(wmin, w[i]);
         gap -= w[i] * t;
     }
-    return ((violh * L <= tol) && (wmin >= 0.0) && (gap * L <= tol)) ? 2 : 0;
+    return ((violh * L + ORC_MARGIN_F64 * magh * L <= tol) && (wmin >= 0.0) && (gap * L <= tol_gap)) ? 2 : 0;
 }
 
 int orc_solve_f64(double* z, double* y, const double* ML, const double* gP, const double* G,
-                  const double* g, int n, int m, int N, double L, double tol, int check_every,
-                  int schedule, int* converged) {
+                  const double* g, int n, int m, int N, double L, double tol, double tol_gap,
+                  int check_every, int schedule, int* converged) {
     const size_t nm = (size_t)n * m;
     double* GL = (double*)malloc(sizeof(double) * (nm + 1));
     double* pD = (double*)malloc(sizeof(double) * (m + 1));
@@ -222,7 +265,7 @@ int orc_solve_f64(double* z, double* y, const double* ML, const double* gP, cons
         double* t = yvm1; yvm1 = yv; yv = yp1; yp1 = t;                               /* :60-64 */
         it = v + 1;
         if (use_tol && (it % check_every) == 0) {
-            const int c = orc_check_f64(u, ch, pD, w, m, L, tol);
+            const int c = orc_check_f64(u, ch, pD, w, z, GL, n, m, L, tol, orc_tol_gap(tol, tol_gap));
             if (c) {
                 if (c == 2) memcpy(z, zhat, sizeof(double) * n);
                 conv = c;
@@ -239,7 +282,7 @@ int orc_solve_f64(double* z, double* y, const double* ML, const double* gP, cons
 
 long long orc_solve_batch_f32(float* z, float* y, const float* MGneg, const float* gP,
                               const float* GL, const float* pD, int n, int m, int batch,
-                              int shared, int N, float L, float tol, int check_every,
+                              int shared, int N, float L, double tol, double tol_gap, int check_every,
                               const float* theta, const float* beta, int* iters, int threads) {
     long long total = 0;
     const size_t nm = (size_t)n * m;
@@ -252,7 +295,7 @@ long long orc_solve_batch_f32(float* z, float* y, const float* MGneg, const floa
         const float* gl = shared ? GL : GL + (size_t)b * nm;
         int conv = 0;
         int it = orc_solve_f32(z + (size_t)b * n, y + (size_t)b * m, mg, gP + (size_t)b * n, gl,
-                               pD + (size_t)b * m, n, m, N, L, tol, check_every, theta, beta, &conv);
+                               pD + (size_t)b * m, n, m, N, L, tol, tol_gap, check_every, theta, beta, &conv);
         if (iters) iters[b] = it;
         total += it;
     }
@@ -282,8 +325,8 @@ void orc_plant_step_f32(const float* A, const float* B, const float* x, const fl
 long long orc_closed_loop_f32(float* x, float* z, float* y, const float* MGneg, const float* GL,
                               float L, int n, int m, const float* PM, const float* M0,
                               const float* Pg, const float* g0, const float* A, const float* B,
-                              int nx, int nu, int steps, int N, float tol, int check_every,
-                              const float* theta, const float* beta, int warm, float* xs,
+                              int nx, int nu, int steps, int N, double tol, double tol_gap,
+                              int check_every, const float* theta, const float* beta, int warm, float* xs,
                               float* us, int* iters) {
     float* gP = (float*)malloc(sizeof(float) * (n + 1));
     float* g = (float*)malloc(sizeof(float) * (m + 1));
@@ -300,7 +343,7 @@ long long orc_closed_loop_f32(float* x, float* z, float* y, const float* MGneg, 
             memset(y, 0, sizeof(float) * m);
         }
         int conv = 0;
-        const int it = orc_solve_f32(z, y, MGneg, gP, GL, pD, n, m, N, L, tol, check_every, theta,
+        const int it = orc_solve_f32(z, y, MGneg, gP, GL, pD, n, m, N, L, tol, tol_gap, check_every, theta,
                                      beta, &conv);
         total += it;
         if (iters) iters[t] = it;
@@ -351,8 +394,14 @@ void orc_step4_flat_f32(const float* GLf, float* yp1, const float* w, const floa
     }
 }
 
+struct orc_flat_rows { const float* GLf; int Nh, n_u, mc; };
+static float orc_flat_row(const void* ctx, int i, const float* x) {
+    const struct orc_flat_rows* c = (const struct orc_flat_rows*)ctx;
+    return orc_flat_row4(c->GLf, x, i, c->Nh, c->n_u, c->mc);
+}
+
 int orc_solve_flat_f32(float* z, float* y, const float* MGf, const float* gP, const float* GLf,
-                       const float* pD, int Nh, int n_u, int m, int N, float L, float tol,
+                       const float* pD, int Nh, int n_u, int m, int N, float L, double tol, double tol_gap,
                        int check_every, const float* theta, const float* beta, int* converged) {
     const int n = n_u * Nh, mc = 4 * n_u * Nh;
     const int mm = m > 0 ? m : 1;
@@ -367,7 +416,9 @@ int orc_solve_flat_f32(float* z, float* y, const float* MGf, const float* gP, co
     if (check_every <= 0) check_every = 10;
     memcpy(ycur, y, sizeof(float) * m);
     memcpy(yprev, y, sizeof(float) * m);
-    const int use_tol = tol > 0.0f;
+    const int use_tol = tol > 0.0;
+    const double tgap = orc_tol_gap(tol, tol_gap);
+    const struct orc_flat_rows rows = {GLf, Nh, n_u, mc};
     if (use_tol)
         for (int r = 0; r < m; r++) u[r] = orc_flat_row4(GLf, z, r, Nh, n_u, mc);
     int it = 0, conv = 0;
@@ -385,7 +436,7 @@ int orc_solve_flat_f32(float* z, float* y, const float* MGf, const float* gP, co
                 u[r] = fmaf(omt, u[r], th * ch[r]);
             }
             if ((it % check_every) == 0) {
-                const int c = orc_check_f32(u, ch, pD, w, m, L, tol);
+                const int c = orc_check_f32(u, ch, pD, w, z, m, orc_flat_row, &rows, (double)L, tol, tgap);
                 if (c) {
                     if (c == 2) memcpy(z, zhat, sizeof(float) * n);
                     conv = c;

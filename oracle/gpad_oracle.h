@@ -51,26 +51,33 @@ void orc_scale_f32(const float* ML, const float* G, const float* g, float L, int
 /* theta[v] multiplies zhat in iteration v, beta[v] extrapolates w in iteration v (fp64). */
 void orc_schedule(int N, int kind, double* theta, double* beta);
 
+/* Rounding margin of the Algorithm 1 decisions (see orc_check_f32 in gpad_oracle.c): a test
+ * passes when L max(chain + pD) + MARGIN L max(|chain| + |pD|) <= tol; 16 units of the f32
+ * (2^-24) / f64 (2^-53) rounding unit.  The kernels use the same constants (gpad_internal.h). */
+#define ORC_MARGIN_F32 0x1p-20
+#define ORC_MARGIN_F64 0x1p-49
+
 /* Full solve in main.cu:160-175 order.  z: in z_{-1}, out z*; y: in y0 (= y_{-1}), out y*.
  * tol <= 0: exactly N iterations (Algorithm 2).  tol > 0: Algorithm 1 check every
  * check_every iterations (acceldualgrad.m:66-79; test (A) certifies z, test (B) certifies
- * zhat, which is then returned as z*).  theta/beta: fp32 schedule tables of length N.
+ * zhat, which is then returned as z*); tol = e_g (constraint violation), tol_gap = e_V (the
+ * duality-gap term of (B); <= 0: = tol).  theta/beta: fp32 schedule tables of length N.
  * Returns the number of iterations executed; *converged = 0 (no), 1 (test A), 2 (test B). */
 int orc_solve_f32(float* z, float* y, const float* MGneg, const float* gP, const float* GL,
-                  const float* pD, int n, int m, int N, float L, float tol, int check_every,
-                  const float* theta, const float* beta, int* converged);
+                  const float* pD, int n, int m, int N, float L, double tol, double tol_gap,
+                  int check_every, const float* theta, const float* beta, int* converged);
 
 /* fp64 solve in acceldualgrad.m:43-64 order: inputs are ML (+H^-1 G^T), gP, G, g, L. */
 int orc_solve_f64(double* z, double* y, const double* ML, const double* gP, const double* G,
-                  const double* g, int n, int m, int N, double L, double tol, int check_every,
-                  int schedule, int* converged);
+                  const double* g, int n, int m, int N, double L, double tol, double tol_gap,
+                  int check_every, int schedule, int* converged);
 
 /* Batch of independent instances (shared ML/G when shared != 0), `threads` OpenMP
  * threads (<= 0: all).  Per-instance vectors are packed [batch][n] / [batch][m].
  * iters (optional) receives per-instance iteration counts.  Returns total iterations. */
 long long orc_solve_batch_f32(float* z, float* y, const float* MGneg, const float* gP,
                               const float* GL, const float* pD, int n, int m, int batch,
-                              int shared, int N, float L, float tol, int check_every,
+                              int shared, int N, float L, double tol, double tol_gap, int check_every,
                               const float* theta, const float* beta, int* iters, int threads);
 
 /* ---- "flat" battery steps (equal cell capacities; seq_functions.cpp:5-43) --------------
@@ -86,7 +93,7 @@ void orc_step4_flat_f32(const float* GLf, float* yp1, const float* w, const floa
                         const float* zhat, int Nh, int n_u, int m);
 /* main_prof.cu flat loop order (steps 1, 2-flat, 3, 4-flat) + the same Algorithm 1 test. */
 int orc_solve_flat_f32(float* z, float* y, const float* MGf, const float* gP, const float* GLf,
-                       const float* pD, int Nh, int n_u, int m, int N, float L, float tol,
+                       const float* pD, int Nh, int n_u, int m, int N, float L, double tol, double tol_gap,
                        int check_every, const float* theta, const float* beta, int* converged);
 
 /* ---- per-state data and closed loop (gpad_setup_plant / gpad_closed_loop) ----------
@@ -104,8 +111,8 @@ void orc_plant_step_f32(const float* A, const float* B, const float* x, const fl
 long long orc_closed_loop_f32(float* x, float* z, float* y, const float* MGneg, const float* GL,
                               float L, int n, int m, const float* PM, const float* M0,
                               const float* Pg, const float* g0, const float* A, const float* B,
-                              int nx, int nu, int steps, int N, float tol, int check_every,
-                              const float* theta, const float* beta, int warm, float* xs,
+                              int nx, int nu, int steps, int N, double tol, double tol_gap,
+                              int check_every, const float* theta, const float* beta, int warm, float* xs,
                               float* us, int* iters);
 
 #ifdef __cplusplus

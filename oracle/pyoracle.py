@@ -55,24 +55,25 @@ class Oracle:
         L.orc_scale_f32.argtypes = [_f, _f, _f, C.c_float, C.c_int, C.c_int, _f, _f, _f]
         L.orc_schedule.argtypes = [C.c_int, C.c_int, _d, _d]
         L.orc_solve_f32.argtypes = [_f, _f, _f, _f, _f, _f, C.c_int, C.c_int, C.c_int, C.c_float,
-                                    C.c_float, C.c_int, _f, _f, _i]
+                                    C.c_double, C.c_double, C.c_int, _f, _f, _i]
         L.orc_solve_f32.restype = C.c_int
         L.orc_solve_f64.argtypes = [_d, _d, _d, _d, _d, _d, C.c_int, C.c_int, C.c_int, C.c_double,
-                                    C.c_double, C.c_int, C.c_int, _i]
+                                    C.c_double, C.c_double, C.c_int, C.c_int, _i]
         L.orc_solve_f64.restype = C.c_int
         L.orc_solve_batch_f32.argtypes = [_f, _f, _f, _f, _f, _f, C.c_int, C.c_int, C.c_int, C.c_int,
-                                          C.c_int, C.c_float, C.c_float, C.c_int, _f, _f, _i, C.c_int]
+                                          C.c_int, C.c_float, C.c_double, C.c_double, C.c_int, _f, _f, _i,
+                                          C.c_int]
         L.orc_solve_batch_f32.restype = C.c_longlong
         L.orc_affine_f32.argtypes = [_f, _f, _f, _f, C.c_int, C.c_int]
         L.orc_plant_step_f32.argtypes = [_f, _f, _f, _f, _f, C.c_int, C.c_int]
         L.orc_closed_loop_f32.argtypes = [_f, _f, _f, _f, _f, C.c_float, C.c_int, C.c_int, _f, _f, _f,
-                                          _f, _f, _f, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float,
-                                          C.c_int, _f, _f, C.c_int, _f, _f, _i]
+                                          _f, _f, _f, C.c_int, C.c_int, C.c_int, C.c_int, C.c_double,
+                                          C.c_double, C.c_int, _f, _f, C.c_int, _f, _f, _i]
         L.orc_closed_loop_f32.restype = C.c_longlong
         L.orc_step2_flat_f32.argtypes = [_f, _f, _f, _f, C.c_int, C.c_int, C.c_int]
         L.orc_step4_flat_f32.argtypes = [_f, _f, _f, _f, _f, C.c_int, C.c_int, C.c_int]
         L.orc_solve_flat_f32.argtypes = [_f, _f, _f, _f, _f, _f, C.c_int, C.c_int, C.c_int, C.c_int,
-                                         C.c_float, C.c_float, C.c_int, _f, _f, _i]
+                                         C.c_float, C.c_double, C.c_double, C.c_int, _f, _f, _i]
         L.orc_solve_flat_f32.restype = C.c_int
         self.lib = L
 
@@ -130,13 +131,15 @@ class Oracle:
 
     # -- solves -----------------------------------------------------------------
     def solve_f32(self, z0, y0, ML, M, G, g, N, L, tol=0.0, check_every=10,
-                  schedule=SCHEDULE_MATLAB):
-        """solve(z0, y0, ML, M, G, g, N, L, tol) restated on the CPU in fp32."""
+                  schedule=SCHEDULE_MATLAB, tol_gap=0.0):
+        """solve(z0, y0, ML, M, G, g, N, L, tol) restated on the CPU in fp32 (tol = e_g,
+        tol_gap = e_V; <= 0: = tol)."""
         MGneg, GL, pD = self.scale(ML, G, g, L)
-        return self.solve_scaled_f32(z0, y0, MGneg, M, GL, pD, N, L, tol, check_every, schedule)
+        return self.solve_scaled_f32(z0, y0, MGneg, M, GL, pD, N, L, tol, check_every, schedule,
+                                     tol_gap=tol_gap)
 
     def solve_scaled_f32(self, z0, y0, MGneg, gP, GL, pD, N, L, tol=0.0, check_every=10,
-                         schedule=SCHEDULE_MATLAB, theta=None, beta=None):
+                         schedule=SCHEDULE_MATLAB, theta=None, beta=None, tol_gap=0.0):
         n, m = MGneg.shape
         z = np.array(z0, np.float32, copy=True).reshape(n)
         y = np.array(y0, np.float32, copy=True).reshape(m)
@@ -148,12 +151,12 @@ class Oracle:
                                     _fp(np.ascontiguousarray(gP, np.float32)),
                                     _fp(np.ascontiguousarray(GL, np.float32)),
                                     _fp(np.ascontiguousarray(pD, np.float32)), n, m, N,
-                                    np.float32(L), np.float32(tol), check_every, _fp(theta),
+                                    np.float32(L), float(tol), float(tol_gap), check_every, _fp(theta),
                                     _fp(beta), C.byref(conv))
         return z, y, it, bool(conv.value)
 
     def solve_f64(self, z0, y0, ML, M, G, g, N, L, tol=0.0, check_every=10,
-                  schedule=SCHEDULE_MATLAB):
+                  schedule=SCHEDULE_MATLAB, tol_gap=0.0):
         ML = np.ascontiguousarray(ML, np.float64); n, m = ML.shape
         z = np.array(z0, np.float64, copy=True).reshape(n)
         y = np.array(y0, np.float64, copy=True).reshape(m)
@@ -161,11 +164,11 @@ class Oracle:
         it = self.lib.orc_solve_f64(_dp(z), _dp(y), _dp(ML), _dp(np.ascontiguousarray(M, np.float64)),
                                     _dp(np.ascontiguousarray(G, np.float64)),
                                     _dp(np.ascontiguousarray(g, np.float64)), n, m, N, float(L),
-                                    float(tol), check_every, schedule, C.byref(conv))
+                                    float(tol), float(tol_gap), check_every, schedule, C.byref(conv))
         return z, y, it, bool(conv.value)
 
     def solve_batch_f32(self, Z0, Y0, MGneg, GP, GL, PD, N, L, tol=0.0, check_every=10,
-                        shared=True, threads=1, schedule=SCHEDULE_MATLAB):
+                        shared=True, threads=1, schedule=SCHEDULE_MATLAB, tol_gap=0.0):
         """Batch of instances; per-instance vectors packed [batch][n] / [batch][m]."""
         Z = np.array(Z0, np.float32, copy=True); Y = np.array(Y0, np.float32, copy=True)
         batch, n = Z.shape
@@ -176,7 +179,7 @@ class Oracle:
             _fp(Z), _fp(Y), _fp(np.ascontiguousarray(MGneg, np.float32)),
             _fp(np.ascontiguousarray(GP, np.float32)), _fp(np.ascontiguousarray(GL, np.float32)),
             _fp(np.ascontiguousarray(PD, np.float32)), n, m, batch, int(bool(shared)), N,
-            np.float32(L), np.float32(tol), check_every, _fp(theta), _fp(beta),
+            np.float32(L), float(tol), float(tol_gap), check_every, _fp(theta), _fp(beta),
             iters.ctypes.data_as(_i), threads)
         return Z, Y, iters, int(total)
 
@@ -198,7 +201,7 @@ class Oracle:
         return yp
 
     def solve_flat_f32(self, z0, y0, MGf, gP, GLf, pD, n_u, N, L, tol=0.0, check_every=10,
-                       schedule=SCHEDULE_MATLAB, theta=None, beta=None):
+                       schedule=SCHEDULE_MATLAB, theta=None, beta=None, tol_gap=0.0):
         MGf = np.ascontiguousarray(MGf, np.float32); Nh, m = MGf.shape
         n = Nh * n_u
         z = np.array(z0, np.float32, copy=True).reshape(n)
@@ -209,7 +212,7 @@ class Oracle:
         it = self.lib.orc_solve_flat_f32(_fp(z), _fp(y), _fp(MGf), _fp(np.ascontiguousarray(gP, np.float32)),
                                          _fp(np.ascontiguousarray(GLf, np.float32)),
                                          _fp(np.ascontiguousarray(pD, np.float32)), Nh, n_u, m, N,
-                                         np.float32(L), np.float32(tol), check_every,
+                                         np.float32(L), float(tol), float(tol_gap), check_every,
                                          _fp(np.ascontiguousarray(theta, np.float32)),
                                          _fp(np.ascontiguousarray(beta, np.float32)), C.byref(conv))
         return z, y, it, conv.value
@@ -223,7 +226,7 @@ class Oracle:
         return out
 
     def closed_loop_f32(self, x0, MGneg, GL, L, PM, Pg, A, B, steps, N, tol=0.0, M0=None, g0=None,
-                        check_every=10, warm=False, z0=None, y0=None, schedule=SCHEDULE_MATLAB):
+                        check_every=10, warm=False, z0=None, y0=None, schedule=SCHEDULE_MATLAB, tol_gap=0.0):
         """One instance: returns (x_T, z, y, xs [steps][nx], us [steps][nu], iters [steps])."""
         MGneg = np.ascontiguousarray(MGneg, np.float32); n, m = MGneg.shape
         c = lambda a: np.ascontiguousarray(a, np.float32)  # noqa: E731
@@ -238,7 +241,7 @@ class Oracle:
         opt = lambda a: None if a is None else _fp(c(a))  # noqa: E731
         self.lib.orc_closed_loop_f32(
             _fp(x), _fp(z), _fp(y), _fp(MGneg), _fp(c(GL)), np.float32(L), n, m, _fp(PM), opt(M0),
-            _fp(Pg), opt(g0), _fp(A), _fp(B), nx, nu, steps, N, np.float32(tol), check_every,
+            _fp(Pg), opt(g0), _fp(A), _fp(B), nx, nu, steps, N, float(tol), float(tol_gap), check_every,
             _fp(theta), _fp(beta), int(bool(warm)), _fp(xs), _fp(us), iters.ctypes.data_as(_i))
         return x, z, y, xs, us, iters
 

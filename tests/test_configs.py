@@ -36,3 +36,37 @@ def test_c5_batch1024_distinct_800x800_bitexact(gpu, oracle):
         assert it == N
         np.testing.assert_array_equal(Z[b], zo, err_msg=f"z[{b}]")
         np.testing.assert_array_equal(Y[b], yo, err_msg=f"y[{b}]")
+
+
+def test_c4_shard_certified_on_the_constraint(gpu, oracle):
+    """C4 shard (bench.py's workload: 8192 instances sharing ML/G, eps = 1e-4, phased panel
+    solve + finisher): every instance reported converged satisfies max(G z* - g) <= 1e-4
+    evaluated exactly (fp64) on the returned z* and the caller's f32 G, g; iteration counts
+    of a spread sample equal the oracle's."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    import torch
+
+    import gpad_mpc
+    n = m = 200
+    B, tol, N = 8192, 1e-4, 5000
+    ML, G, L, M, g = bench.make_shard(n, m, B, 0)
+    f32 = np.float32
+    ML32, G32, M32, g32, L32 = ML.astype(f32), G.astype(f32), M.astype(f32), g.astype(f32), f32(L)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)  # noqa: E731
+    z = torch.zeros(B, n, device=gpu)
+    y = torch.zeros(B, m, device=gpu)
+    it = np.zeros(B, np.int32)
+    with gpad_mpc.GpadSolver(0) as s:
+        s.setup(t(ML32), t(G32), float(L32), n=n, m=m, batch=B, check_every=10)
+        st = s.run(z, y, t(M32), t(g32), N, tol, iters=it)
+    assert st["kernel"] == "panel" and st["converged"] == B
+    Z = z.cpu().numpy().astype(np.float64)
+    viol = (Z @ G32.astype(np.float64).T - g32.astype(np.float64)).max(axis=1)
+    assert viol.max() <= tol, (viol.max(), int(viol.argmax()))
+    for b in range(0, B, 257):
+        zo, yo, ito, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), ML32, M32[b], G32, g32[b], N, L32, tol)
+        assert it[b] == ito, b
+        np.testing.assert_array_equal(Z[b].astype(np.float32), zo)

@@ -24,7 +24,7 @@ def kcode(name):
 
 
 def run_gpu(ML, M, G, g, L, N, tol=0.0, z0=None, y0=None, kernel="auto", shared=True,
-            schedule=0, check_every=10, opts=None):
+            schedule=0, check_every=10, opts=None, tol_gap=0.0):
     import gpad_mpc
     n, m = ML.shape[-2], ML.shape[-1]
     batch = M.shape[0] if M.ndim == 2 else 1
@@ -33,7 +33,8 @@ def run_gpu(ML, M, G, g, L, N, tol=0.0, z0=None, y0=None, kernel="auto", shared=
     iters = np.zeros(batch, np.int32)
     with gpad_mpc.GpadSolver(0) as s:
         s.setup(np.ascontiguousarray(ML), np.ascontiguousarray(G), float(L), n=n, m=m, batch=batch,
-                shared=shared, kernel=kcode(kernel), schedule=schedule, check_every=check_every)
+                shared=shared, kernel=kcode(kernel), schedule=schedule, check_every=check_every,
+                tol_gap=tol_gap)
         s.set_options(**(opts or {}))
         st = s.run(z, y, np.ascontiguousarray(M), np.ascontiguousarray(g), N, tol, iters=iters)
     return z, y, st, iters
@@ -469,3 +470,25 @@ def test_accumulate_iterations_matches_stats(gpu):
     it = np.zeros(B, np.int32)
     st = s.last_stats(iters=it)
     assert int(acc.item()) == 3 * int(it.sum()) == 3 * st["total_iterations"]
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("tol,tol_gap", [(1e-4, 1e-2), (1e-3, 1e-7)])
+def test_separate_gap_tolerance_bitexact(gpu, oracle, kernel, tol, tol_gap):
+    """e_g and e_V (acceldualgrad.m:12-13) as separate tolerances: tol bounds the constraint
+    violation of both tests, tol_gap the duality-gap term of test (B); every kernel family
+    stops at the oracle's iteration with the oracle's z*, y* and convergence code."""
+    from gpad_mpc import problems
+    B = 300 if kernel == "panel" else 24
+    qp = problems.synthetic_qp(64, 96, batch=B, seed=21)
+    ML, G = qp.ML.astype(np.float32), qp.G.astype(np.float32)
+    M, g = qp.M.astype(np.float32), qp.g.astype(np.float32)
+    L = np.float32(qp.L)
+    z, y, st, iters = run_gpu(ML, M, G, g, L, 4000, tol=tol, kernel=kernel, tol_gap=tol_gap)
+    assert st["kernel"] == kernel
+    for b in range(0, B, 7 if kernel == "panel" else 1):
+        zo, yo, it, _ = oracle.solve_f32(np.zeros(64), np.zeros(96), ML, M[b], G, g[b], 4000, L, tol,
+                                         tol_gap=tol_gap)
+        assert iters[b] == it, b
+        assert_bitexact(z[b], zo, f"{b} z")
+        assert_bitexact(y[b], yo, f"{b} y")
