@@ -28,6 +28,8 @@ struct Tuning {
     int flat_panels = 0;      // GPAD_OPT_FLAT_PANELS: panels per flat-panel workgroup (0: auto)
     int flat_waves = 0;       // GPAD_OPT_FLAT_WAVES: 0 auto, 8 or 16 waves per workgroup
     int flat_a_lds = 1;       // GPAD_OPT_FLAT_A_LDS: flat fragment image in LDS when it fits
+    int finish_solo = -1;     // GPAD_OPT_FINISH_SOLO: duo workgroups running one instance each
+                              // (the longest-predicted survivors; -1: default)
 };
 
 // Rounding margin of the Algorithm 1 decisions, in units of max_i(|chain_i| + |pD_i|): a test
@@ -78,6 +80,8 @@ struct SolveArgs {
     float* uc;             // carried u = G_L z [batch][m]
     int fin_thresh;        // survivors <= this: the resident finisher takes them (0: none)
     int* qctr;             // duo kernel: zeroed device counter of its work-list claims
+    int fin_solo;          // duo kernel: workgroups that run the list's first (longest) entries
+                           // one per CU (their second slot stays empty)
     const int* pred;       // phased solves: per-instance iteration counts predicted from the
                            // previous solve (or null); orders the finisher's queue longest first
     int n_u;               // flat battery path: cells (n = n_u * horizon), see gpad_flat.hip

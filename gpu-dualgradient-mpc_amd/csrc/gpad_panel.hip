@@ -1134,6 +1134,9 @@ size_t panel_work_bytes(int m, int batch) {
 // The order inside a bin is arbitrary -- results never depend on it, only the schedule.
 // A no-op when the list is not the finisher's (count > thresh) or longer than kSortMax.
 constexpr int kSortMax = 8192;
+// default solo workgroups of the duo finisher (GPAD_OPT_FINISH_SOLO): 0 -- measured on fresh
+// inputs (tools/tl_solo.sh) 16 or 48 solo CUs gave no tail gain beyond run-to-run noise
+constexpr int kFinishSolo = 0;
 constexpr int kSortBins = 4096;
 __global__ __launch_bounds__(1024) void survivor_sort_kernel(int* idx, const int* count_p, const int* pred,
                                                              int thresh) {
@@ -1252,6 +1255,7 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
                                        a.count_in, a.pred, a.fin_thresh);
                 int g = a.fin_thresh < a.num_cus ? a.fin_thresh : a.num_cus;
                 if (tn.duo_max_grid > 0 && tn.duo_max_grid < g) g = tn.duo_max_grid;  // more claims
+                a.fin_solo = tn.finish_solo >= 0 ? tn.finish_solo : kFinishSolo;
                 if ((e = launch_duo(a, g, s)) != hipSuccess) return e;
             } else if ((e = launch_resident_finisher(a, a.fin_thresh, s)) != hipSuccess) {
                 return e;  // one instance per workgroup

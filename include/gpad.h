@@ -275,6 +275,7 @@ int gpad_schedule(int N, int kind, double* theta, double* beta);
 #define GPAD_OPT_FLAT_PANELS 10    /* panels per flat-panel workgroup, 1..4 (0 = auto, default)    */
 #define GPAD_OPT_FLAT_WAVES 11     /* flat-panel workgroup waves: 0 auto (default), 8 or 16         */
 #define GPAD_OPT_FLAT_A_LDS 12     /* 1: flat fragment image staged in LDS when it fits (default)  */
+#define GPAD_OPT_FINISH_SOLO 13    /* finisher CUs that run one (the longest) survivor each         */
 int gpad_set_option(gpad_handle_t h, int option, int value);
 
 /* Synchronise the handle's stream (for callers using device memory + async runs). */

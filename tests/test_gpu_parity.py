@@ -225,9 +225,10 @@ def test_bigpanel_bitexact(gpu, oracle, tol, N, nm, B, grid, phase):
         assert_bitexact(y[b], yo, f"instance {b} y")
 
 
-@pytest.mark.parametrize("finisher,grid", [("duo", 1), ("duo", 3), ("duo", 0), ("resident", 0)])
+@pytest.mark.parametrize("finisher,grid,solo", [("duo", 1, 0), ("duo", 3, 0), ("duo", 0, 0), ("resident", 0, 0),
+                                                ("duo", 5, 2), ("duo", 0, 40), ("duo", 3, 7)])
 @pytest.mark.parametrize("nm,B,z0s", [((200, 200), 120, 0.0), ((40, 180), 200, 0.1), ((131, 64), 97, 0.1)])
-def test_finisher_queue_bitexact(gpu, oracle, finisher, grid, nm, B, z0s):
+def test_finisher_queue_bitexact(gpu, oracle, finisher, grid, solo, nm, B, z0s):
     """The tail of a phased panel solve on the latency kernels: the duo kernel (two instances per
     workgroup in ping-pong, slots refilled from the survivor list through a device counter;
     grid capped to 1 or 3 workgroups to force many claims) or the one-per-workgroup resident
@@ -235,7 +236,7 @@ def test_finisher_queue_bitexact(gpu, oracle, finisher, grid, nm, B, z0s):
     solve runs there; every instance must match its own oracle solve, iteration count included."""
     from gpad_mpc import problems
     opts = dict(finisher=0 if finisher == "duo" else 1, phase_len=10, finish_thresh=100000,
-                duo_max_grid=grid)
+                duo_max_grid=grid, finish_solo=solo)  # solo: workgroups with one slot (longest first)
     n, m = nm
     qp = problems.synthetic_qp(n, m, batch=B, seed=12)
     ML, G = qp.ML.astype(np.float32), qp.G.astype(np.float32)

@@ -27,23 +27,30 @@ def run(args):
 
     import bench
     import gpad_mpc
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import tune_env  # noqa: F401  (GPAD_* env -> gpad_set_option)
     dev = torch.device("cuda:0")
     n, m, B = 200, 200, args.batch
     ML, G, L, M, g = bench.make_shard(n, m, B, 0)
     f32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)  # noqa: E731
     dML, dG, dM, dg = f32(ML), f32(G), f32(M), f32(g)
+    fresh = [(f32(a), f32(b)) for a, b in bench.make_stream(n, m, B, args.reps, 0)] if args.fresh else None
     z = torch.zeros(B, n, device=dev)
     y = torch.zeros(B, m, device=dev)
     s = gpad_mpc.GpadSolver(0)
     s.setup(dML, dG, float(np.float32(L)), n=n, m=m, batch=B, shared=True, check_every=10)
     it = np.zeros(B, np.int32)
-    for _ in range(args.reps):
+    prev = np.zeros(B, np.int32)
+    for r in range(args.reps):
         z.zero_()
         y.zero_()
-        s.run(z, y, dM, dg, 5000, 1e-4, stats=False)
+        Mv, gv = fresh[r] if fresh else (dM, dg)
+        prev[:] = it
+        s.run(z, y, Mv, gv, 5000, 1e-4, stats=False)
         st = s.last_stats(iters=it)
     torch.cuda.synchronize()
     np.save(args.out, it)
+    np.save(args.out.replace(".npy", "_prev.npy"), prev)
     print(f"kernel {st['kernel']} kernel_ms {st['kernel_ms']:.4f} mean_iters {it.mean():.1f} "
           f"min {it.min()} max {it.max()}")
 
@@ -93,6 +100,7 @@ def main():
     a.add_argument("--reps", type=int, default=5)
     a.add_argument("--batch", type=int, default=8192)
     a.add_argument("--out", default="gpurun_out/tl_iters.npy")
+    a.add_argument("--fresh", action="store_true", help="new q/b draws every solve (bench default)")
     b = sub.add_parser("parse")
     b.add_argument("dir")
     b.add_argument("--iters", default="gpurun_out/tl_iters.npy")
