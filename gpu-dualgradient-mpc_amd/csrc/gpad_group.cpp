@@ -1,0 +1,399 @@
+// gpad_group.cpp -- several devices from one C caller: instance-sharded solves with an RCCL
+// scatter/gather (north_star: "partition across the 8 GPUs of one node by
+// sharding independent MPC problem instances with a single RCCL gather of solutions").
+//
+// A group owns one libgpad handle and one HIP stream per device and, when the devices are
+// distinct, one RCCL communicator clique over them (ncclCommInitAll: single process, one rank
+// per device -- the reference's caller is a single C process, main.cu:79-203).  The batch is
+// split into contiguous shards (sizes differ by at most one, larger first, as
+// gpad_mpc/parallel.shard_range).  Per run there is no communication between the shards'
+// solves; the data movement is:
+//   host memory   : each device copies its own shard in and its solution out (no collective)
+//   device memory : the caller's buffers live on devices[0] (the root); one grouped
+//                   ncclSend/ncclRecv moves every non-root shard of (M, g, z0, y0) out, and one
+//                   more brings (z*, y*) back into the caller's root buffers.  Shared matrices are
+//                   broadcast once at setup (ncclBroadcast), per-instance matrices sent per shard.
+// A device listed twice (one GPU standing in for several, e.g. the 1-GPU test box) has no RCCL
+// clique (RCCL refuses duplicate devices): the same moves are then peer copies
+// (hipMemcpyPeerAsync), ordered by events exactly where the RCCL calls are.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gpad.h"
+#include "gpad_internal.h"
+
+namespace {
+
+int gfail(int code, const std::string& msg) { return gpad::set_last_error(code, msg); }
+
+#define G_HIP(expr)                                                                                   \
+    do {                                                                                              \
+        hipError_t _e = (expr);                                                                       \
+        if (_e != hipSuccess)                                                                         \
+            return gfail(_e == hipErrorOutOfMemory ? GPAD_ERR_NOMEM : GPAD_ERR_HIP,                   \
+                         std::string(#expr) + ": " + hipGetErrorString(_e));                          \
+    } while (0)
+#define G_NCCL(expr)                                                                                  \
+    do {                                                                                              \
+        ncclResult_t _r = (expr);                                                                     \
+        if (_r != ncclSuccess)                                                                        \
+            return gfail(GPAD_ERR_HIP, std::string(#expr) + ": " + ncclGetErrorString(_r));            \
+    } while (0)
+
+size_t esz(int dtype) { return dtype == GPAD_DTYPE_F64 ? sizeof(double) : sizeof(float); }
+
+}  // namespace
+
+struct gpad_group_s {
+    int ndev = 0;
+    std::vector<int> dev;
+    std::vector<gpad_handle_t> h;
+    std::vector<hipStream_t> st;
+    std::vector<hipEvent_t> ev;      // one per device: ordering of the peer-copy transport
+    std::vector<ncclComm_t> comm;    // empty: peer-copy transport (a device listed twice)
+    gpad_dims_t dims{};              // the whole batch
+    double L = 0.0;
+    bool ready = false;
+    std::vector<int> start, count;   // shard of device d: [start, start + count)
+    std::vector<void*> vec;          // per device: M | g | z | y of its shard (device memory)
+    std::vector<size_t> vec_bytes;
+    std::vector<void*> mat;          // per device: raw ML | G before packing
+    std::vector<size_t> mat_bytes;
+};
+
+namespace {
+
+int release(gpad_group_s* g) {
+    for (int d = 0; d < g->ndev; ++d) {
+        (void)hipSetDevice(g->dev[d]);
+        if (d < (int)g->st.size() && g->st[d]) (void)hipStreamSynchronize(g->st[d]);
+        if (d < (int)g->h.size() && g->h[d]) gpad_destroy(g->h[d]);
+        if (d < (int)g->vec.size() && g->vec[d]) (void)hipFree(g->vec[d]);
+        if (d < (int)g->mat.size() && g->mat[d]) (void)hipFree(g->mat[d]);
+        if (d < (int)g->ev.size() && g->ev[d]) (void)hipEventDestroy(g->ev[d]);
+        if (d < (int)g->st.size() && g->st[d]) (void)hipStreamDestroy(g->st[d]);
+    }
+    for (ncclComm_t c : g->comm) (void)ncclCommDestroy(c);
+    delete g;
+    return GPAD_OK;
+}
+
+int ensure(gpad_group_s* g, std::vector<void*>& bufs, std::vector<size_t>& sizes, int d, size_t want) {
+    if (sizes[d] >= want && bufs[d]) return GPAD_OK;
+    G_HIP(hipSetDevice(g->dev[d]));
+    if (bufs[d]) (void)hipFree(bufs[d]);
+    bufs[d] = nullptr;
+    sizes[d] = 0;
+    if (want == 0) return GPAD_OK;
+    G_HIP(hipMalloc(&bufs[d], want));
+    sizes[d] = want;
+    return GPAD_OK;
+}
+
+// Root -> device d moves: (dst on device d, src on the root) pairs, all in one RCCL group (or
+// peer copies on the root stream, with every destination stream waiting on it).
+struct Move {
+    int d;
+    void* dst;
+    const void* src;
+    size_t bytes;
+};
+
+int scatter(gpad_group_s* g, const std::vector<Move>& mv) {
+    if (mv.empty()) return GPAD_OK;
+    if (!g->comm.empty()) {
+        G_NCCL(ncclGroupStart());
+        for (const Move& x : mv) {
+            G_NCCL(ncclSend(x.src, x.bytes, ncclChar, x.d, g->comm[0], g->st[0]));
+            G_NCCL(ncclRecv(x.dst, x.bytes, ncclChar, 0, g->comm[x.d], g->st[x.d]));
+        }
+        G_NCCL(ncclGroupEnd());
+        return GPAD_OK;
+    }
+    G_HIP(hipSetDevice(g->dev[0]));
+    for (const Move& x : mv)
+        G_HIP(hipMemcpyPeerAsync(x.dst, g->dev[x.d], x.src, g->dev[0], x.bytes, g->st[0]));
+    G_HIP(hipEventRecord(g->ev[0], g->st[0]));
+    for (int d = 1; d < g->ndev; ++d) {
+        G_HIP(hipSetDevice(g->dev[d]));
+        G_HIP(hipStreamWaitEvent(g->st[d], g->ev[0], 0));
+    }
+    return GPAD_OK;
+}
+
+// Device d -> root moves (dst on the root, src on device d): the gather of the solutions.
+int gather(gpad_group_s* g, const std::vector<Move>& mv) {
+    if (mv.empty()) return GPAD_OK;
+    if (!g->comm.empty()) {
+        G_NCCL(ncclGroupStart());
+        for (const Move& x : mv) {
+            G_NCCL(ncclSend(x.src, x.bytes, ncclChar, 0, g->comm[x.d], g->st[x.d]));
+            G_NCCL(ncclRecv(x.dst, x.bytes, ncclChar, x.d, g->comm[0], g->st[0]));
+        }
+        G_NCCL(ncclGroupEnd());
+        return GPAD_OK;
+    }
+    for (int d = 1; d < g->ndev; ++d) {  // the root copies once every shard's solve is done
+        G_HIP(hipSetDevice(g->dev[d]));
+        G_HIP(hipEventRecord(g->ev[d], g->st[d]));
+        G_HIP(hipSetDevice(g->dev[0]));
+        G_HIP(hipStreamWaitEvent(g->st[0], g->ev[d], 0));
+    }
+    G_HIP(hipSetDevice(g->dev[0]));
+    for (const Move& x : mv)
+        G_HIP(hipMemcpyPeerAsync(x.dst, g->dev[0], x.src, g->dev[x.d], x.bytes, g->st[0]));
+    return GPAD_OK;
+}
+
+int sync_all(gpad_group_s* g) {
+    for (int d = 0; d < g->ndev; ++d) {
+        G_HIP(hipSetDevice(g->dev[d]));
+        G_HIP(hipStreamSynchronize(g->st[d]));
+    }
+    return GPAD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gpad_group_create(gpad_group_t* out, int ndev, const int* devices) {
+    if (!out || ndev <= 0 || !devices) return gfail(GPAD_ERR_INVALID, "gpad_group_create: bad arguments");
+    *out = nullptr;
+    int visible = 0;
+    if (hipGetDeviceCount(&visible) != hipSuccess || visible <= 0)
+        return gfail(GPAD_ERR_NO_DEVICE, "gpad_group_create: no HIP device visible");
+    for (int d = 0; d < ndev; ++d)
+        if (devices[d] < 0 || devices[d] >= visible)
+            return gfail(GPAD_ERR_INVALID, "gpad_group_create: bad device index");
+    auto* g = new gpad_group_s;
+    g->ndev = ndev;
+    g->dev.assign(devices, devices + ndev);
+    g->h.assign(ndev, nullptr);
+    g->st.assign(ndev, nullptr);
+    g->ev.assign(ndev, nullptr);
+    g->vec.assign(ndev, nullptr);
+    g->vec_bytes.assign(ndev, 0);
+    g->mat.assign(ndev, nullptr);
+    g->mat_bytes.assign(ndev, 0);
+    for (int d = 0; d < ndev; ++d) {
+        int rc;
+        if (hipSetDevice(g->dev[d]) != hipSuccess || hipStreamCreateWithFlags(&g->st[d], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&g->ev[d], hipEventDisableTiming) != hipSuccess) {
+            release(g);
+            return gfail(GPAD_ERR_HIP, "gpad_group_create: stream/event creation failed");
+        }
+        if ((rc = gpad_create(&g->h[d], g->dev[d], g->st[d]))) {
+            release(g);
+            return rc;
+        }
+    }
+    std::vector<int> sorted(g->dev);
+    std::sort(sorted.begin(), sorted.end());
+    const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+    if (distinct) {  // one RCCL clique, rank d on devices[d]
+        g->comm.assign(ndev, nullptr);
+        const ncclResult_t r = ncclCommInitAll(g->comm.data(), ndev, g->dev.data());
+        if (r != ncclSuccess) {
+            g->comm.clear();
+            release(g);
+            return gfail(GPAD_ERR_HIP, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+        }
+    }
+    *out = g;
+    return GPAD_OK;
+}
+
+int gpad_group_destroy(gpad_group_t g) {
+    if (!g) return GPAD_OK;
+    return release(g);
+}
+
+int gpad_group_transport(gpad_group_t g) {
+    if (!g) return gfail(GPAD_ERR_INVALID, "gpad_group_transport: null group");
+    return g->comm.empty() ? GPAD_GROUP_PEER : GPAD_GROUP_RCCL;
+}
+
+int gpad_group_setup(gpad_group_t g, const gpad_dims_t* dims, const void* ML, const void* G, double L) {
+    if (!g || !dims || !ML || !G) return gfail(GPAD_ERR_INVALID, "gpad_group_setup: bad arguments");
+    if (dims->batch < 1 || dims->n <= 0 || dims->m <= 0)
+        return gfail(GPAD_ERR_INVALID, "gpad_group_setup: dims: n, m, batch must be positive");
+    g->ready = false;
+    const int nd = g->ndev, B = dims->batch;
+    g->start.assign(nd, 0);
+    g->count.assign(nd, 0);
+    for (int d = 0, s = 0; d < nd; ++d) {  // contiguous shards, larger first
+        g->count[d] = B / nd + (d < B % nd ? 1 : 0);
+        g->start[d] = s;
+        s += g->count[d];
+    }
+    const bool host = dims->memory == GPAD_MEM_HOST;
+    const size_t es = esz(dims->dtype), nm = (size_t)dims->n * dims->m * es;
+    std::vector<Move> mv;
+    std::vector<const void*> mlp(nd), gp(nd);
+    int rc;
+    for (int d = 0; d < nd; ++d) {
+        const int c = std::max(g->count[d], 1);
+        const size_t per = dims->shared ? nm : nm * (size_t)c;  // each of ML and G
+        const size_t off = dims->shared ? 0 : nm * (size_t)g->start[d];
+        if (g->count[d] == 0 && !dims->shared) {  // more devices than instances: an idle shard
+            if ((rc = ensure(g, g->mat, g->mat_bytes, d, 2 * per))) return rc;
+            G_HIP(hipSetDevice(g->dev[d]));
+            G_HIP(hipMemsetAsync(g->mat[d], 0, 2 * per, g->st[d]));
+            mlp[d] = g->mat[d];
+            gp[d] = (char*)g->mat[d] + per;
+            continue;
+        }
+        if (!host && d == 0) {  // the root's shard reads the caller's buffers in place
+            mlp[d] = (const char*)ML + off;
+            gp[d] = (const char*)G + off;
+            continue;
+        }
+        if ((rc = ensure(g, g->mat, g->mat_bytes, d, 2 * per))) return rc;
+        void* dml = g->mat[d];
+        void* dg = (char*)g->mat[d] + per;
+        mlp[d] = dml;
+        gp[d] = dg;
+        if (host) {
+            G_HIP(hipSetDevice(g->dev[d]));
+            G_HIP(hipMemcpyAsync(dml, (const char*)ML + off, per, hipMemcpyHostToDevice, g->st[d]));
+            G_HIP(hipMemcpyAsync(dg, (const char*)G + off, per, hipMemcpyHostToDevice, g->st[d]));
+        } else if (!dims->shared || g->comm.empty()) {
+            mv.push_back({d, dml, (const char*)ML + off, per});
+            mv.push_back({d, dg, (const char*)G + off, per});
+        }
+    }
+    if (!host && dims->shared && !g->comm.empty() && nd > 1) {  // shared matrices: one broadcast each
+        G_NCCL(ncclGroupStart());
+        for (int d = 0; d < nd; ++d) {
+            G_NCCL(ncclBroadcast(d == 0 ? ML : nullptr, const_cast<void*>(mlp[d]), nm, ncclChar, 0, g->comm[d], g->st[d]));
+            G_NCCL(ncclBroadcast(d == 0 ? G : nullptr, const_cast<void*>(gp[d]), nm, ncclChar, 0, g->comm[d], g->st[d]));
+        }
+        G_NCCL(ncclGroupEnd());
+    }
+    if ((rc = scatter(g, mv))) return rc;
+    for (int d = 0; d < nd; ++d) {  // pack on every device (each handle orders on its stream)
+        gpad_dims_t dd = *dims;
+        dd.batch = std::max(g->count[d], 1);
+        dd.memory = GPAD_MEM_DEVICE;
+        if ((rc = gpad_setup(g->h[d], &dd, mlp[d], gp[d], L))) return rc;
+    }
+    if ((rc = sync_all(g))) return rc;
+    g->dims = *dims;
+    g->L = L;
+    g->ready = true;
+    return GPAD_OK;
+}
+
+int gpad_group_run(gpad_group_t g, void* z0, void* y0, const void* M, const void* gv, int N, double tol,
+                   gpad_stats_t* st) {
+    if (!g) return gfail(GPAD_ERR_INVALID, "gpad_group_run: null group");
+    if (!g->ready) return gfail(GPAD_ERR_NOT_SETUP, "gpad_group_run: call gpad_group_setup first");
+    if (!z0 || !y0 || !M || !gv) return gfail(GPAD_ERR_INVALID, "gpad_group_run: null vector");
+    const gpad_dims_t& D = g->dims;
+    const bool host = D.memory == GPAD_MEM_HOST;
+    const size_t es = esz(D.dtype), nb = (size_t)D.n * es, mb = (size_t)D.m * es;
+    const int nd = g->ndev;
+    std::vector<char*> Mp(nd), gp(nd), zp(nd), yp(nd);
+    std::vector<Move> in, out;
+    int rc;
+    for (int d = 0; d < nd; ++d) {
+        const size_t c = (size_t)g->count[d], s0 = (size_t)g->start[d];
+        if (!host && d == 0) {  // root shard in place
+            Mp[d] = (char*)M;
+            gp[d] = (char*)gv;
+            zp[d] = (char*)z0;
+            yp[d] = (char*)y0;
+            continue;
+        }
+        if ((rc = ensure(g, g->vec, g->vec_bytes, d, std::max<size_t>(1, 2 * c * (nb + mb))))) return rc;
+        Mp[d] = (char*)g->vec[d];
+        gp[d] = Mp[d] + c * nb;
+        zp[d] = gp[d] + c * mb;
+        yp[d] = zp[d] + c * nb;
+        if (c == 0) continue;
+        if (host) {
+            G_HIP(hipSetDevice(g->dev[d]));
+            G_HIP(hipMemcpyAsync(Mp[d], (const char*)M + s0 * nb, c * nb, hipMemcpyHostToDevice, g->st[d]));
+            G_HIP(hipMemcpyAsync(gp[d], (const char*)gv + s0 * mb, c * mb, hipMemcpyHostToDevice, g->st[d]));
+            G_HIP(hipMemcpyAsync(zp[d], (const char*)z0 + s0 * nb, c * nb, hipMemcpyHostToDevice, g->st[d]));
+            G_HIP(hipMemcpyAsync(yp[d], (const char*)y0 + s0 * mb, c * mb, hipMemcpyHostToDevice, g->st[d]));
+        } else {
+            in.push_back({d, Mp[d], (const char*)M + s0 * nb, c * nb});
+            in.push_back({d, gp[d], (const char*)gv + s0 * mb, c * mb});
+            in.push_back({d, zp[d], (const char*)z0 + s0 * nb, c * nb});
+            in.push_back({d, yp[d], (const char*)y0 + s0 * mb, c * mb});
+            out.push_back({d, (char*)z0 + s0 * nb, zp[d], c * nb});
+            out.push_back({d, (char*)y0 + s0 * mb, yp[d], c * mb});
+        }
+    }
+    if ((rc = scatter(g, in))) return rc;
+    for (int d = 0; d < nd; ++d) {  // every shard's solve, asynchronous on its device's stream
+        if (g->count[d] == 0) continue;
+        if ((rc = gpad_run(g->h[d], zp[d], yp[d], Mp[d], gp[d], N, tol, nullptr))) return rc;
+    }
+    if ((rc = gather(g, out))) return rc;
+    if (host) {
+        for (int d = 0; d < nd; ++d) {
+            const size_t c = (size_t)g->count[d], s0 = (size_t)g->start[d];
+            if (c == 0) continue;
+            G_HIP(hipSetDevice(g->dev[d]));
+            G_HIP(hipMemcpyAsync((char*)z0 + s0 * nb, zp[d], c * nb, hipMemcpyDeviceToHost, g->st[d]));
+            G_HIP(hipMemcpyAsync((char*)y0 + s0 * mb, yp[d], c * mb, hipMemcpyDeviceToHost, g->st[d]));
+        }
+    }
+    if ((rc = sync_all(g))) return rc;
+    if (st) {  // per-shard counters (host copies), aggregated; st->iters [batch] in global order
+        gpad_stats_t tot{};
+        tot.iters = nullptr;
+        for (int d = 0; d < nd; ++d) {
+            if (g->count[d] == 0) continue;
+            gpad_stats_t sd{};
+            sd.iters = st->iters ? st->iters + g->start[d] : nullptr;
+            if ((rc = gpad_last_stats(g->h[d], &sd))) return rc;
+            tot.iterations = std::max(tot.iterations, sd.iterations);
+            tot.converged += sd.converged;
+            tot.total_iterations += sd.total_iterations;
+            tot.kernel = sd.kernel;
+            tot.kernel_ms = std::max(tot.kernel_ms, sd.kernel_ms);
+        }
+        int* keep = st->iters;
+        *st = tot;
+        st->iters = keep;
+    }
+    return GPAD_OK;
+}
+
+int gpad_solve_sharded(int ndev, const int* devices, void* z0, void* y0, const void* ML, const void* M,
+                       const void* G, const void* g, int N, double L, double tol, const gpad_dims_t* dims,
+                       gpad_stats_t* st) {
+    // one group per thread and device list, kept between calls (communicator set-up is the
+    // expensive part); the matrices are re-bound every call
+    struct Cache {
+        gpad_group_t grp = nullptr;
+        std::vector<int> devs;
+        ~Cache() {
+            if (grp) gpad_group_destroy(grp);
+        }
+    };
+    thread_local Cache cache;
+    if (ndev <= 0 || !devices) return gfail(GPAD_ERR_INVALID, "gpad_solve_sharded: bad device list");
+    std::vector<int> want(devices, devices + ndev);
+    if (!cache.grp || cache.devs != want) {
+        if (cache.grp) gpad_group_destroy(cache.grp);
+        cache.grp = nullptr;
+        int rc = gpad_group_create(&cache.grp, ndev, devices);
+        if (rc) return rc;
+        cache.devs = want;
+    }
+    int rc = gpad_group_setup(cache.grp, dims, ML, G, L);
+    if (rc) return rc;
+    return gpad_group_run(cache.grp, z0, y0, M, g, N, tol, st);
+}
+
+}  // extern "C"

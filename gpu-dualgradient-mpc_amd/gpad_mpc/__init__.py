@@ -8,10 +8,10 @@ from . import datafile, problems
 from ._lib import (DTYPE_F32, DTYPE_F64, KERNEL_AUTO, KERNEL_PANEL, KERNEL_RESIDENT,
                    KERNEL_STREAM, MEM_DEVICE, MEM_HOST, SCHEDULE_MATLAB, SCHEDULE_PAPER, GpadError,
                    load)
-from .solver import GpadSolver, acceldualgrad, schedule, solve
+from .solver import GpadGroup, GpadSolver, acceldualgrad, schedule, solve
 
 __all__ = [
-    "problems", "datafile", "load", "GpadSolver", "GpadError", "solve", "acceldualgrad", "schedule",
+    "problems", "datafile", "load", "GpadSolver", "GpadGroup", "GpadError", "solve", "acceldualgrad", "schedule",
     "DTYPE_F32", "DTYPE_F64", "KERNEL_AUTO", "KERNEL_STREAM", "KERNEL_RESIDENT", "KERNEL_PANEL",
     "MEM_HOST", "MEM_DEVICE", "SCHEDULE_MATLAB", "SCHEDULE_PAPER",
 ]

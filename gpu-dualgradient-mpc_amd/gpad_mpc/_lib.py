@@ -32,7 +32,10 @@ EXPORTS = [
     "gpad_datafile_read", "gpad_datafile_write", "gpad_datafile_free",
     "gpad_setup_flat", "gpad_step2_primal_flat", "gpad_step4_project_flat", "gpad_precompute",
     "gpad_accumulate_iterations", "gpad_set_option",
+    "gpad_group_create", "gpad_group_destroy", "gpad_group_transport", "gpad_group_setup", "gpad_group_run",
+    "gpad_solve_sharded",
 ]
+GROUP_RCCL, GROUP_PEER = 1, 2
 
 # gpad_set_option (include/gpad.h GPAD_OPT_*): schedule / launch tuning, never results
 OPT_DEFAULT = -1
@@ -123,6 +126,13 @@ def load(path: str | None = None) -> C.CDLL:
     L.gpad_precompute.argtypes = [vp, i, i, i, i, i, cvp, cvp, cvp, vp, vp, vp]
     L.gpad_accumulate_iterations.argtypes = [vp, vp]
     L.gpad_set_option.argtypes = [vp, i, i]
+    ip = C.POINTER(C.c_int)
+    L.gpad_group_create.argtypes = [C.POINTER(vp), i, ip]
+    L.gpad_group_destroy.argtypes = [vp]
+    L.gpad_group_transport.argtypes = [vp]
+    L.gpad_group_setup.argtypes = [vp, C.POINTER(Dims), cvp, cvp, d]
+    L.gpad_group_run.argtypes = [vp, vp, vp, cvp, cvp, i, d, C.POINTER(Stats)]
+    L.gpad_solve_sharded.argtypes = [i, ip, vp, vp, cvp, cvp, cvp, cvp, i, d, d, C.POINTER(Dims), C.POINTER(Stats)]
     L.gpad_step2_primal_flat.argtypes = [vp, vp, vp, vp, vp, i, i, i]
     L.gpad_step4_project_flat.argtypes = [vp, vp, vp, vp, vp, vp, i, i, i]
     for name in ["gpad_create", "gpad_destroy", "gpad_set_stream", "gpad_sync", "gpad_setup",
@@ -132,7 +142,8 @@ def load(path: str | None = None) -> C.CDLL:
                  "gpad_run_state", "gpad_closed_loop", "gpad_datafile_read",
                  "gpad_datafile_write", "gpad_setup_flat", "gpad_step2_primal_flat",
                  "gpad_step4_project_flat", "gpad_precompute", "gpad_accumulate_iterations",
-                 "gpad_set_option"]:
+                 "gpad_set_option", "gpad_group_create", "gpad_group_destroy", "gpad_group_transport",
+                 "gpad_group_setup", "gpad_group_run", "gpad_solve_sharded"]:
         getattr(L, name).restype = i
     _LIB = L
     return L

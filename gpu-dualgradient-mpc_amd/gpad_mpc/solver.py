@@ -301,6 +301,59 @@ class GpadSolver:
                                           _ptr(zhat), n, m), "gpad_step4")
 
 
+class GpadGroup:
+    """Several devices from one process (include/gpad.h gpad_group_*): contiguous instance shards,
+    RCCL scatter/gather to devices[0] for device memory (peer copies when a device repeats)."""
+
+    def __init__(self, devices):
+        self.lib = _lib.load()
+        self.devices = list(devices)
+        arr = (C.c_int * len(self.devices))(*self.devices)
+        self.g = C.c_void_p()
+        check(self.lib.gpad_group_create(C.byref(self.g), len(self.devices), arr), "gpad_group_create")
+        self.dims = None
+
+    @property
+    def transport(self) -> str:
+        t = self.lib.gpad_group_transport(self.g)
+        check(min(t, 0), "gpad_group_transport")
+        return "rccl" if t == _lib.GROUP_RCCL else "peer"
+
+    def close(self):
+        if self.g:
+            self.lib.gpad_group_destroy(self.g)
+            self.g = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def setup(self, ML, G, L: float, *, n: int, m: int, batch: int, shared: bool = True,
+              schedule: int = _lib.SCHEDULE_MATLAB, check_every: int = 10, kernel: int = _lib.KERNEL_AUTO,
+              tol_gap: float = 0.0) -> None:
+        mem = _lib.MEM_DEVICE if _is_torch(ML) else _lib.MEM_HOST
+        self.dims = Dims(n=n, m=m, batch=batch, shared=int(bool(shared)), dtype=_dtype_code(ML), memory=mem,
+                         schedule=schedule, check_every=check_every, kernel=kernel, tol_gap=float(tol_gap))
+        check(self.lib.gpad_group_setup(self.g, C.byref(self.dims), _ptr(ML), _ptr(G), float(L)),
+              "gpad_group_setup")
+
+    def run(self, z, y, M, g, N: int, tol: float = 0.0, *, iters=None) -> dict:
+        st = Stats()
+        if iters is not None:
+            st.iters = iters.ctypes.data_as(C.POINTER(C.c_int))
+        check(self.lib.gpad_group_run(self.g, _ptr(z), _ptr(y), _ptr(M), _ptr(g), int(N), float(tol),
+                                      C.byref(st)), "gpad_group_run")
+        return GpadSolver._stats_dict(st)
+
+
 def schedule(N: int, kind: int = _lib.SCHEDULE_MATLAB):
     """theta[v], beta[v] (acceldualgrad.m:18,27,55-56) from the library's host routine."""
     lib = _lib.load()

@@ -231,6 +231,35 @@ int gpad_plan_phases(const int* iters, int batch, int n, int m, int N, int check
 int gpad_solve(void* z0, void* y0, const void* ML, const void* M, const void* G, const void* g,
                int N, double L, double tol, const gpad_dims_t* dims, gpad_stats_t* st);
 
+/* ---- multi-device: instance shards, RCCL scatter/gather ------------------
+ * A group drives several devices from ONE C process (the reference's caller is a single C
+ * program, main.cu:79-203; north_star: "partition across the 8 GPUs of one node by sharding
+ * independent MPC problem instances with a single RCCL gather of solutions").  One handle and
+ * HIP stream per device; the batch splits into contiguous shards (sizes differ by at most one,
+ * larger first) solved with no communication.  dims.memory == GPAD_MEM_DEVICE: every pointer is
+ * device memory on devices[0] (the root); shared ML/G are broadcast at setup (ncclBroadcast),
+ * per-instance matrices and each non-root shard of M, g, z0, y0 go out by one grouped
+ * ncclSend/ncclRecv, and (z*, y*) come back into the root buffers by another.  GPAD_MEM_HOST:
+ * every device copies its own shard in and out.  With distinct devices the group holds one RCCL
+ * clique (ncclCommInitAll); a device listed twice (one GPU standing in for several) moves the
+ * same bytes by peer copies instead (gpad_group_transport tells which). */
+typedef struct gpad_group_s* gpad_group_t;
+#define GPAD_GROUP_RCCL 1
+#define GPAD_GROUP_PEER 2
+int gpad_group_create(gpad_group_t* g, int ndev, const int* devices);
+int gpad_group_destroy(gpad_group_t g);
+int gpad_group_transport(gpad_group_t g); /* GPAD_GROUP_RCCL or GPAD_GROUP_PEER */
+/* dims.batch is the WHOLE batch (as for gpad_setup); ML, G as gpad_setup's. */
+int gpad_group_setup(gpad_group_t g, const gpad_dims_t* dims, const void* ML, const void* G, double L);
+/* The whole batch's vectors (gpad_run's meaning).  Synchronous.  st aggregates every shard
+ * (kernel_ms: the slowest shard's device time); st->iters, when given, receives [batch] counts. */
+int gpad_group_run(gpad_group_t g, void* z0, void* y0, const void* M, const void* g_rhs, int N, double tol,
+                   gpad_stats_t* st);
+/* One-shot solve(...) over several devices (the group is cached per thread and device list). */
+int gpad_solve_sharded(int ndev, const int* devices, void* z0, void* y0, const void* ML, const void* M,
+                       const void* G, const void* g, int N, double L, double tol, const gpad_dims_t* dims,
+                       gpad_stats_t* st);
+
 /* ---- per-step device entry points (float, device pointers, handle stream) ---------------
  * Mirror the reference kernels of kernel_functions.h:9-41 one for one, with the CPU
  * semantics of seq_functions.h:4-17 (row-major matrices).  For integration and per-step

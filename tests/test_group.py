@@ -1,0 +1,100 @@
+"""Multi-device C-ABI (include/gpad.h gpad_group_*, gpad_solve_sharded): instance shards over
+several devices of one process, RCCL scatter/gather to the root for device memory.
+
+On the 1-GPU box: devices [0] is a one-rank RCCL clique (every code path of the RCCL transport
+but the sends, which a single rank does not need); devices [0, 0, 0] stand three shards on one
+GPU with the peer-copy transport (the same scatter/gather moves, by hipMemcpyPeerAsync).  Every
+shard layout must give exactly the single-handle (oracle-pinned) results -- the 8-GPU timing is
+the driver's SCALE run.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _qp(n, m, B, seed, shared=True):
+    from gpad_mpc import problems
+    qp = problems.synthetic_qp(n, m, batch=B, seed=seed)
+    f = lambda a: np.ascontiguousarray(np.asarray(a, np.float64).astype(np.float32))  # noqa: E731
+    ML, G = f(qp.ML), f(qp.G)
+    if not shared:
+        rng = np.random.default_rng(seed)
+        ML = f(ML[None] * (1 + 0.02 * rng.random((B, 1, 1))))
+        G = f(G[None] * (1 + 0.02 * rng.random((B, 1, 1))))
+    return ML, f(qp.M).reshape(B, n), G, f(qp.g).reshape(B, m), np.float32(qp.L)
+
+
+def _single(ML, M, G, g, L, N, tol, shared):
+    import gpad_mpc
+    B, n = M.shape
+    m = g.shape[1]
+    z = np.zeros((B, n), np.float32)
+    y = np.zeros((B, m), np.float32)
+    it = np.zeros(B, np.int32)
+    with gpad_mpc.GpadSolver(0) as s:
+        s.setup(ML, G, float(L), n=n, m=m, batch=B, shared=shared)
+        s.run(z, y, M, g, N, tol, iters=it)
+    return z, y, it
+
+
+@pytest.mark.parametrize("devices,transport", [([0], "rccl"), ([0, 0, 0], "peer"), ([0, 0], "peer")])
+@pytest.mark.parametrize("memory", ["host", "device"])
+@pytest.mark.parametrize("shared,B,N,tol", [(True, 300, 3000, 1e-4), (True, 37, 60, 0.0), (False, 7, 2000, 1e-4),
+                                            (True, 2, 500, 1e-4)])
+def test_group_shards_equal_single_handle(gpu, devices, transport, memory, shared, B, N, tol):
+    import torch
+
+    import gpad_mpc
+    n, m = 40, 72
+    ML, M, G, g, L = _qp(n, m, B, seed=B + 3, shared=shared)
+    zr, yr, itr = _single(ML, M, G, g, L, N, tol, shared)
+    Z = np.zeros((B, n), np.float32)
+    Y = np.zeros((B, m), np.float32)
+    it = np.zeros(B, np.int32)
+    with gpad_mpc.GpadGroup(devices) as grp:
+        assert grp.transport == transport
+        if memory == "device":
+            t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)  # noqa: E731
+            dZ, dY = t(Z), t(Y)
+            grp.setup(t(ML), t(G), float(L), n=n, m=m, batch=B, shared=shared)
+            st = grp.run(dZ, dY, t(M), t(g), N, tol, iters=it)
+            Z, Y = dZ.cpu().numpy(), dY.cpu().numpy()
+        else:
+            grp.setup(ML, G, float(L), n=n, m=m, batch=B, shared=shared)
+            st = grp.run(Z, Y, M, g, N, tol, iters=it)
+    np.testing.assert_array_equal(it, itr)
+    np.testing.assert_array_equal(Z, zr)
+    np.testing.assert_array_equal(Y, yr)
+    assert st["total_iterations"] == int(itr.sum()) and st["iterations"] == int(itr.max())
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0, 0]])
+def test_solve_sharded_one_shot(gpu, oracle, devices):
+    """gpad_solve_sharded(ndev, devices, z0, y0, ML, M, G, g, N, L, tol, dims, stats) through ctypes,
+    called twice (the cached group re-binds the matrices) -- bit-exact vs the oracle."""
+    from gpad_mpc import _lib
+    lib = _lib.load()
+    n, m, B, N, tol = 64, 96, 50, 3000, 1e-4
+    for seed in (1, 2):
+        ML, M, G, g, L = _qp(n, m, B, seed)
+        Z = np.zeros((B, n), np.float32)
+        Y = np.zeros((B, m), np.float32)
+        it = np.zeros(B, np.int32)
+        d = _lib.Dims(n=n, m=m, batch=B, shared=1, dtype=_lib.DTYPE_F32, memory=_lib.MEM_HOST,
+                      schedule=_lib.SCHEDULE_MATLAB, check_every=10, kernel=_lib.KERNEL_AUTO)
+        st = _lib.Stats()
+        st.iters = it.ctypes.data_as(C.POINTER(C.c_int))
+        devs = (C.c_int * len(devices))(*devices)
+        p = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
+        _lib.check(lib.gpad_solve_sharded(len(devices), devs, p(Z), p(Y), p(ML), p(M), p(G), p(g), N, float(L), tol,
+                                          C.byref(d), C.byref(st)), "gpad_solve_sharded")
+        for b in range(0, B, 5):
+            zo, yo, ito, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), ML, M[b], G, g[b], N, L, tol)
+            assert it[b] == ito
+            np.testing.assert_array_equal(Z[b], zo)
+            np.testing.assert_array_equal(Y[b], yo)
