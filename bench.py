@@ -601,7 +601,7 @@ def main():
                 y1 = torch.zeros(1, mm, device=dev)
                 s1.run(z1, y1, mM, mg_, iters, 0.0)
                 t = []
-                for _ in range(3):
+                for _ in range(5):
                     st1 = s1.run(z1.zero_(), y1.zero_(), mM, mg_, iters, 0.0)
                     t.append(st1["kernel_ms"])
             singles[name] = {"config": ("C2 single instance n=200 m=200" if name == "c2" else
