@@ -201,18 +201,18 @@ def phase_util(iters, N, K=10, plan=None, fin=512):
 
 def traffic_from_profile(kernel_name):
     """HBM bytes per solve of the dominant kernel from the committed PMC profile of this same
-    bench command (tools/profile.sh -> profiles/r01_bench_summary.json; FETCH_SIZE x2 +
+    bench command (tools/profile.sh -> profiles/r02_bench_summary.json; FETCH_SIZE x2 +
     WRITE_SIZE, MI355X_MICROARCH.md §HBM): the kernel's bytes summed over every launch of the
-    profiled run / the C4 solves that run made (its --warmup + --steps; the side legs launch other
-    kernel instantiations).  None when absent."""
-    path = os.path.join(ROOT, "profiles", "r01_bench_summary.json")
+    profiled run / the C4 solves that run made (2 x (--warmup + --steps): the fresh-input and the
+    repeated-input loops; the side legs launch other kernel instantiations).  None when absent."""
+    path = os.path.join(ROOT, "profiles", "r02_bench_summary.json")
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
         return None, None
     args = d.get("bench_args", "").split()
     try:
-        solves = int(args[args.index("--steps") + 1]) + int(args[args.index("--warmup") + 1])
+        solves = 2 * (int(args[args.index("--steps") + 1]) + int(args[args.index("--warmup") + 1]))
     except (ValueError, IndexError):
         return None, None
     v = d.get("pmc_per_launch", {}).get(kernel_name)

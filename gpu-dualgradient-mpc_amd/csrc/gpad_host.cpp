@@ -117,6 +117,14 @@ struct gpad_handle_s {
     int last_N = 0;
     gpad::PanelPlan plan;
     unsigned long long plan_key = 0;    // fingerprint of the counts the plan was built from
+    // asynchronous runs (no stats): the counts of each phased solve are copied to pinned host
+    // memory behind it; the next run re-plans from them once that copy has landed, so a pipeline
+    // of back-to-back solves plans from its most recent completed solve without a host sync
+    int* plan_pin = nullptr;
+    size_t plan_pin_cap = 0;
+    hipEvent_t plan_ev = nullptr;
+    bool plan_pending = false;
+    int plan_pending_N = 0, plan_pending_batch = 0;
     // plant binding (gpad_setup_plant): affine state maps and dynamics, device copies
     int nx = 0, nu = 0;
     bool plant_ready = false, plant_dyn = false;
@@ -188,6 +196,8 @@ int gpad_destroy(gpad_handle_t h) {
     h->state.release();
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
+    if (h->plan_ev) (void)hipEventDestroy(h->plan_ev);
+    if (h->plan_pin) (void)hipHostFree(h->plan_pin);
     delete h;
     return GPAD_OK;
 }
@@ -275,6 +285,7 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
     h->flat = false;
     h->shadow_ok = false;
     h->plan.nph = 0;
+    h->plan_pending = false;
     h->last_phased = false;
     h->dims = *d;
     if (h->dims.check_every <= 0) h->dims.check_every = 10;
@@ -358,6 +369,7 @@ int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* d, int n_u, const float*
     h->flat = false;
     h->shadow_ok = false;
     h->plan.nph = 0;
+    h->plan_pending = false;
     h->last_phased = false;
     h->dims = *d;
     if (h->dims.check_every <= 0) h->dims.check_every = 10;
@@ -444,6 +456,18 @@ static int ensure_schedule(gpad_handle_t h, int N, const void* theta_in, const v
     return GPAD_OK;
 }
 
+// The phase plan is a pure function of the per-instance counts (and the shape): rebuild it only
+// when they changed (repeated solves of one batch skip the DP).
+static void update_plan(gpad_handle_t h, const int* counts, int batch, int N) {
+    unsigned long long key = 1469598103934665603ull ^ (unsigned long long)N;
+    for (int b = 0; b < batch; ++b) key = (key ^ (unsigned)counts[b]) * 1099511628211ull;
+    if (key != h->plan_key || h->plan.nph == 0) {
+        gpad::panel_plan(counts, batch, h->dims.n, h->dims.m, N, h->dims.check_every, h->num_cus, &h->tune,
+                         &h->plan);
+        h->plan_key = key;
+    }
+}
+
 // Counters are laid out [steps][iters[batch] | conv[batch]].
 static int collect_stats(gpad_handle_t h, gpad_stats_t* st) {
     const int batch = h->last_batch;
@@ -466,15 +490,8 @@ static int collect_stats(gpad_handle_t h, gpad_stats_t* st) {
         }
     }
     if (h->last_phased && h->last_steps == 1) {
-        // the plan is a pure function of the per-instance counts (and the shape): rebuild it only
-        // when they changed (repeated solves of one batch skip the DP)
-        unsigned long long key = 1469598103934665603ull ^ (unsigned long long)h->last_N;
-        for (int b = 0; b < batch; ++b) key = (key ^ (unsigned)h->h_counts[b]) * 1099511628211ull;
-        if (key != h->plan_key || h->plan.nph == 0) {
-            gpad::panel_plan(h->h_counts.data(), batch, h->dims.n, h->dims.m, h->last_N, h->dims.check_every,
-                             h->num_cus, &h->tune, &h->plan);
-            h->plan_key = key;
-        }
+        update_plan(h, h->h_counts.data(), batch, h->last_N);
+        h->plan_pending = false;  // these counts are at least as recent as any copy in flight
     }
     st->kernel = h->last_kernel;
     float ms = 0.0f;
@@ -670,6 +687,10 @@ static int run_typed(gpad_handle_t h, T* z, T* y, const T* M, const T* g, int N,
     }
     int* iters = (int*)h->counters.p;
     int kernel = 0;
+    if (h->plan_pending && hipEventQuery(h->plan_ev) == hipSuccess) {  // a previous solve's counts landed
+        if (h->plan_pending_batch == batch) update_plan(h, h->plan_pin, batch, h->plan_pending_N);
+        h->plan_pending = false;
+    }
     HIP_TRY(hipEventRecord(h->ev0, h->stream));
     if ((rc = launch_solve<T>(h, dz, dy, dM, dg, N, tol, scaled_vec, iters, iters + batch, &kernel)))
         return rc;
@@ -678,6 +699,22 @@ static int run_typed(gpad_handle_t h, T* z, T* y, const T* M, const T* g, int N,
     h->last_kernel = kernel;
     h->last_batch = batch;
     h->last_steps = 1;
+    if (!st && h->last_phased && h->tune.plan) {  // asynchronous run: counts to the host behind it
+        const size_t want = sizeof(int) * (size_t)batch;
+        if (h->plan_pin_cap < want) {
+            if (h->plan_pin) (void)hipHostFree(h->plan_pin);
+            h->plan_pin = nullptr;
+            h->plan_pin_cap = 0;
+            HIP_TRY(hipHostMalloc((void**)&h->plan_pin, want, hipHostMallocDefault));
+            h->plan_pin_cap = want;
+        }
+        if (!h->plan_ev) HIP_TRY(hipEventCreateWithFlags(&h->plan_ev, hipEventDisableTiming));
+        HIP_TRY(hipMemcpyAsync(h->plan_pin, iters, want, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipEventRecord(h->plan_ev, h->stream));
+        h->plan_pending = true;
+        h->plan_pending_N = N;
+        h->plan_pending_batch = batch;
+    }
     if (d.memory == GPAD_MEM_HOST) {
         HIP_TRY(hipMemcpyAsync(z, dz, zb, hipMemcpyDeviceToHost, h->stream));
         HIP_TRY(hipMemcpyAsync(y, dy, yb, hipMemcpyDeviceToHost, h->stream));

@@ -288,6 +288,42 @@ def test_panel_phase_plan_reuse_bitexact(gpu, oracle, fin):
                 assert_bitexact(y[b], yo, f"{scale} y[{b}]")
 
 
+def test_async_runs_plan_from_previous_solve(gpu, oracle):
+    """Asynchronous solves (device tensors, stats=False) never sync for counts: each phased solve
+    copies its counts to pinned host memory behind it and the next run plans from them once they
+    landed (csrc/gpad_host.cpp run_typed).  The plan appears without any stats call, and the
+    planned solve of a different batch is still exact."""
+    import torch
+    import gpad_mpc
+    from gpad_mpc import problems
+    n, m, B, N, tol = 40, 72, 300, 4000, 1e-4
+    qp = problems.synthetic_qp(n, m, batch=B, seed=33)
+    ML, G = qp.ML.astype(np.float32), qp.G.astype(np.float32)
+    L = np.float32(qp.L)
+    rng = np.random.default_rng(9)
+    with gpad_mpc.GpadSolver(0) as s:
+        s.setup(torch.from_numpy(ML).to(gpu), torch.from_numpy(G).to(gpu), float(L), n=n, m=m, batch=B,
+                kernel=kcode("panel"))
+        s.set_options(phase_len=10)
+        assert s.phase_plan()["ends"] == []
+        for k in range(3):
+            M = (qp.M * (1.0 + 0.5 * k)).astype(np.float32)
+            g = (qp.g + 0.1 * rng.random((B, m))).astype(np.float32)
+            dz = torch.zeros((B, n), device=gpu)
+            dy = torch.zeros((B, m), device=gpu)
+            assert s.run(dz, dy, torch.from_numpy(M).to(gpu), torch.from_numpy(g).to(gpu), N, tol,
+                         stats=False) is None
+            plan = s.phase_plan()
+            if k > 0:  # the previous solve finished (synchronised below) -> its counts planned this one
+                assert plan["ends"] and plan["ends"][-1] == N, plan
+            torch.cuda.synchronize()
+            z, y = dz.cpu().numpy(), dy.cpu().numpy()
+            for b in range(0, B, 11):
+                zo, yo, _, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), ML, M[b], G, g[b], N, L, tol)
+                assert_bitexact(z[b], zo, f"{k} z[{b}]")
+                assert_bitexact(y[b], yo, f"{k} y[{b}]")
+
+
 def test_paper_schedule_bitexact(gpu, oracle):
     gd = load_golden("battery_c1")
     ML, M, G, g, L = f32_inputs(gd)

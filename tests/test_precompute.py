@@ -80,3 +80,32 @@ def test_precompute_feeds_gpad_battery(gpu, oracle):
     zo, yo, _, _ = oracle.solve_f32(np.zeros(qp.n), np.zeros(qp.m), f32(qp.ML), f32(qp.M), f32(qp.G), f32(qp.g),
                                     100, np.float32(qp.L))
     assert _rel(z, zo) < 1e-6 and _rel(y, yo) < 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shared", [True, False])
+def test_precompute_c5_size_800(gpu, shared):
+    """BASELINE C5's shape (N = 200: n = 800, m = 800): the device Gauss-Jordan at the size
+    DESIGN.md times, shared (one H, a batch of f rows) and per-instance (3 distinct H, A)."""
+    import gpad_mpc
+    rng = np.random.default_rng(800)
+    n = m = 800
+    s = gpad_mpc.GpadSolver(0)
+    if shared:
+        H, A, f = _spd(n, rng), rng.standard_normal((m, n)), rng.standard_normal((4, n))
+        ML, gP, L = s.precompute(H, A, f)
+        Hi = np.linalg.inv(H)
+        assert _rel(ML, Hi @ A.T) < 1e-10
+        assert _rel(gP, (Hi @ f.T).T) < 1e-10
+        assert abs(L - np.linalg.norm(H, "fro") ** 2) <= 1e-12 * L
+    else:
+        B = 3
+        H = np.stack([_spd(n, rng) for _ in range(B)])
+        A = rng.standard_normal((B, m, n))
+        f = rng.standard_normal((B, n))
+        ML, gP, L = s.precompute(H, A, f, shared=False)
+        for b in range(B):
+            Hi = np.linalg.inv(H[b])
+            assert _rel(ML[b], Hi @ A[b].T) < 1e-10, b
+            assert _rel(gP[b], Hi @ f[b]) < 1e-10, b
+            assert abs(L[b] - np.linalg.norm(H[b], "fro") ** 2) <= 1e-12 * L[b]
