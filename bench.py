@@ -595,18 +595,30 @@ def main():
                 "c1": (*[f32(a) for a in c1[:2]], f32(c1[2]).reshape(1, -1), f32(c1[3]).reshape(1, -1),
                        float(np.float32(qp1.L)), 1000)}.items():
             nn, mm = mML.shape
-            with gpad_mpc.GpadSolver(dev.index, stream=stream.cuda_stream) as s1:
-                s1.setup(mML, mG, mL, n=nn, m=mm, batch=1)
-                z1 = torch.zeros(1, nn, device=dev)
-                y1 = torch.zeros(1, mm, device=dev)
-                s1.run(z1, y1, mM, mg_, iters, 0.0)
-                t = []
-                for _ in range(5):
-                    st1 = s1.run(z1.zero_(), y1.zero_(), mM, mg_, iters, 0.0)
-                    t.append(st1["kernel_ms"])
+            res = {}
+            for kk in (_lib.KERNEL_AUTO, _lib.KERNEL_CONDENSED):
+                with gpad_mpc.GpadSolver(dev.index, stream=stream.cuda_stream) as s1:
+                    s1.setup(mML, mG, mL, n=nn, m=mm, batch=1, kernel=kk)
+                    z1 = torch.zeros(1, nn, device=dev)
+                    y1 = torch.zeros(1, mm, device=dev)
+                    s1.run(z1, y1, mM, mg_, iters, 0.0)
+                    t = []
+                    for _ in range(5):
+                        st1 = s1.run(z1.zero_(), y1.zero_(), mM, mg_, iters, 0.0)
+                        t.append(st1["kernel_ms"])
+                res[kk] = (st1["kernel"], iters / (min(t) / 1e3), z1.double().cpu(), y1.double().cpu())
+            kb, kc = res[_lib.KERNEL_AUTO], res[_lib.KERNEL_CONDENSED]
+            rel = lambda a, b: float((a - b).norm() / b.norm())  # noqa: E731
             singles[name] = {"config": ("C2 single instance n=200 m=200" if name == "c2" else
                                         f"C1 single instance: battery n_u=4, N=10 (n={nn}, m={mm})"),
-                             "kernel": st1["kernel"], "iters_per_s": iters / (min(t) / 1e3)}
+                             "kernel": kb[0], "iters_per_s": kb[1],
+                             "condensed": {
+                                 "kernel": kc[0], "iters_per_s": kc[1],
+                                 "rel_dev_z": rel(kc[2], kb[2]), "rel_dev_y": rel(kc[3], kb[3]),
+                                 "note": "opt-in GPAD_KERNEL_CONDENSED (one m-long chain per iteration, "
+                                         "not bit-exact); rel_dev_* = norm-wise distance from the bit-exact "
+                                         "kernel's z/y after the same iterations (tests/test_condensed.py "
+                                         "bounds it by the reference's own fp32-vs-fp64 spread at N<=100)"}}
             if ref is not None:  # the reference's CPU steps on the same instance, one thread
                 O = ref.O
                 hm = [a.cpu().numpy() for a in (mML, mG, mM, mg_)]

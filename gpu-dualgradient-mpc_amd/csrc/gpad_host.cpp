@@ -96,6 +96,8 @@ struct gpad_handle_s {
     bool scaled = false;
     int ldn = 0, ldm = 0;
     DevBuf MGt, GLt, frag, stage;
+    DevBuf Hc;                 // GPAD_KERNEL_CONDENSED: H = G_L (-ML) images (gpad_condensed.hip)
+    bool Hc_ok = false;
     bool frag_ok = false;      // frag holds the fragment image of the bound matrices
     bool keep_stage = false;   // gpad_solve's cached handle keeps its staging buffer
     // gpad_solve: host copy of the last bound (ML, G, L, dims) so a repeated one-shot call on
@@ -184,6 +186,7 @@ int gpad_destroy(gpad_handle_t h) {
     (void)hipStreamSynchronize(h->stream);
     h->MGt.release();
     h->GLt.release();
+    h->Hc.release();
     h->GLx.release();
     h->frag.release();
     h->stage.release();
@@ -267,8 +270,10 @@ static int validate_dims(const gpad_dims_t* d) {
         return fail(GPAD_ERR_INVALID, "dims: bad memory kind");
     if (d->schedule != GPAD_SCHEDULE_MATLAB && d->schedule != GPAD_SCHEDULE_PAPER)
         return fail(GPAD_ERR_INVALID, "dims: bad schedule");
-    if (d->kernel < GPAD_KERNEL_AUTO || d->kernel > GPAD_KERNEL_PANEL)
+    if ((d->kernel < GPAD_KERNEL_AUTO || d->kernel > GPAD_KERNEL_PANEL) && d->kernel != GPAD_KERNEL_CONDENSED)
         return fail(GPAD_ERR_INVALID, "dims: bad kernel");
+    if (d->kernel == GPAD_KERNEL_CONDENSED && (d->dtype != GPAD_DTYPE_F32 || !gpad::condensed_supported(d->n, d->m)))
+        return fail(GPAD_ERR_UNSUPPORTED, "dims: the condensed kernel needs f32, m <= 208, n <= 256");
     if (!std::isfinite(d->tol_gap)) return fail(GPAD_ERR_INVALID, "dims: tol_gap must be finite");
     return GPAD_OK;
 }
@@ -324,6 +329,15 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
         HIP_TRY(gpad::launch_pack_kmajor<double>((const double*)dB, (double*)h->GLt.p, m, n, h->ldm, sb,
                                                  nmats, in_stride, (long long)b_elems, h->stream));
     }
+    // condensed operator H = G_L (-ML) (GPAD_KERNEL_CONDENSED only)
+    h->Hc_ok = false;
+    if (d->kernel == GPAD_KERNEL_CONDENSED) {
+        if ((rc = h->Hc.ensure(sizeof(float) * (size_t)m * h->ldm * nmats))) return rc;
+        HIP_TRY(gpad::launch_condense((const float*)h->GLt.p, (const float*)h->MGt.p, n, m, h->ldn, h->ldm, nmats,
+                                      d->shared ? 0 : (long long)a_elems, d->shared ? 0 : (long long)b_elems,
+                                      (float*)h->Hc.p, h->stream));
+        h->Hc_ok = true;
+    }
     // fragment image for the MFMA panel kernel (shared f32 matrices only); the buffer is kept
     // across setups and only grows
     h->frag_ok = false;
@@ -362,6 +376,8 @@ int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* d, int n_u, const float*
     if (!(L > 0.0) || !std::isfinite(L)) return fail(GPAD_ERR_INVALID, "gpad_setup_flat: L must be > 0");
     if (d->dtype != GPAD_DTYPE_F32 || !d->shared)
         return fail(GPAD_ERR_UNSUPPORTED, "gpad_setup_flat: f32 and shared matrices only");
+    if (d->kernel == GPAD_KERNEL_CONDENSED)
+        return fail(GPAD_ERR_UNSUPPORTED, "gpad_setup_flat: no condensed kernel on the flat path");
     if (n_u <= 0 || d->n % n_u != 0 || d->m < 4 * d->n)
         return fail(GPAD_ERR_INVALID, "gpad_setup_flat: need n = n_u*N and m >= 4 n_u N");
     HIP_TRY(hipSetDevice(h->device));
@@ -582,6 +598,8 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
     a.conv = conv;
     a.num_cus = h->num_cus;
     a.tune = &h->tune;
+    a.Hc = h->Hc_ok ? (const float*)h->Hc.p : nullptr;
+    a.strideH = d.shared ? 0 : (long long)m * h->ldm;
     int kernel = d.kernel;
     h->last_phased = false;  // set again below when this launch is a phased panel solve
     h->last_N = N;
@@ -614,6 +632,13 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
                 return fail(e == hipErrorInvalidValue ? GPAD_ERR_UNSUPPORTED : GPAD_ERR_HIP,
                             std::string("flat kernel: ") + hipGetErrorString(e));
             *kernel_out = GPAD_KERNEL_FLAT;
+            return GPAD_OK;
+        }
+        if (kernel == GPAD_KERNEL_CONDENSED) {  // opt-in condensed operator (gpad_condensed.hip)
+            e = gpad::launch_condensed(a, h->stream, &ok);
+            if (e != hipSuccess) return fail(GPAD_ERR_HIP, std::string("condensed: ") + hipGetErrorString(e));
+            if (!ok) return fail(GPAD_ERR_UNSUPPORTED, "condensed kernel: bind with dims.kernel = CONDENSED");
+            *kernel_out = kernel;
             return GPAD_OK;
         }
         // shared matrices: panels once there are more instances than the latency kernel can
@@ -734,6 +759,8 @@ static int run_impl(gpad_handle_t h, void* z0, void* y0, const void* M, const vo
     if (!z0 || !y0 || !M || !g) return fail(GPAD_ERR_INVALID, "gpad_run: null vector");
     if (N < 0) return fail(GPAD_ERR_INVALID, "gpad_run: N < 0");
     if (!(tol <= 0.0) && !std::isfinite(tol)) return fail(GPAD_ERR_INVALID, "gpad_run: bad tol");
+    if (h->dims.kernel == GPAD_KERNEL_CONDENSED && theta && N > 0 && ((const float*)theta)[0] != 1.0f)
+        return fail(GPAD_ERR_UNSUPPORTED, "gpad_run_scaled: the condensed kernel needs theta[0] = 1");
     HIP_TRY(hipSetDevice(h->device));
     if (h->dims.dtype == GPAD_DTYPE_F64)
         return run_typed<double>(h, (double*)z0, (double*)y0, (const double*)M, (const double*)g, N,

@@ -88,6 +88,8 @@ struct SolveArgs {
     int flat_staged;       // flat path: matrices staged in LDS (set by launch_flat)
     const struct PanelPlan* plan;  // panel phases: host-side plan from the previous solve (or null)
     const Tuning* tune;    // host-side tuning options (never null on a launch from gpad_host.cpp)
+    const float* Hc;       // condensed operator H = G_L (-ML), k-major [m][ldm] (gpad_condensed.hip)
+    long long strideH;     // elements between consecutive instances' H images (0 = shared)
 };
 
 // launchers (return hipError_t of the launch)
@@ -102,6 +104,12 @@ hipError_t launch_resident_finisher(const SolveArgs<float>& a, int grid, hipStre
 // zeroed a.qctr.  Persistent grid of `grid` workgroups (one per CU).
 hipError_t launch_duo(const SolveArgs<float>& a, int grid, hipStream_t s);
 bool resident_supported(int n, int m);
+// GPAD_KERNEL_CONDENSED (gpad_condensed.hip): H = G_L (-ML) images for nmats matrix pairs, then
+// the one-chain-per-iteration latency kernel (m <= 208, n <= 256)
+bool condensed_supported(int n, int m);
+hipError_t launch_condense(const float* GLt, const float* MGt, int n, int m, int ldn, int ldm, int nmats,
+                           long long strideA, long long strideB, float* Ht, hipStream_t s);
+hipError_t launch_condensed(const SolveArgs<float>& a, hipStream_t s, bool* supported);
 hipError_t launch_panel(const SolveArgs<float>& a, hipStream_t s, bool* supported);
 size_t panel_frag_bytes(int n, int m, int batch);
 size_t panel_work_bytes(int m, int batch);

@@ -18,8 +18,9 @@ SCHEDULE_MATLAB, SCHEDULE_PAPER = 0, 1
 MEM_HOST, MEM_DEVICE = 0, 1
 DTYPE_F32, DTYPE_F64 = 0, 1
 KERNEL_AUTO, KERNEL_STREAM, KERNEL_RESIDENT, KERNEL_PANEL, KERNEL_FLAT = 0, 1, 2, 3, 4
+KERNEL_CONDENSED = 5  # opt-in, not bit-exact: the condensed operator (include/gpad.h)
 KERNEL_NAMES = {KERNEL_AUTO: "auto", KERNEL_STREAM: "stream", KERNEL_RESIDENT: "resident",
-                KERNEL_PANEL: "panel", KERNEL_FLAT: "flat"}
+                KERNEL_PANEL: "panel", KERNEL_FLAT: "flat", KERNEL_CONDENSED: "condensed"}
 
 # every symbol include/gpad.h declares (checked by tests/test_abi.py)
 EXPORTS = [

@@ -53,6 +53,15 @@ extern "C" {
 #define GPAD_KERNEL_RESIDENT 2 /* matrix rows held in VGPRs; one workgroup/instance; n,m <= 208  */
 #define GPAD_KERNEL_PANEL 3    /* shared ML/G, f32 MFMA 16x16x4 panels; one wave per 16 instances */
 #define GPAD_KERNEL_FLAT 4     /* reported only: the flat battery path bound by gpad_setup_flat      */
+/* Opt-in, NOT bit-exact with the reference: the condensed operator.  G_L zhat = H w + c with
+ * H = G_L (-ML) (m x m, formed once per gpad_setup from an fp64 product) and c = -G_L gP, and
+ * z = (-ML) wbar - gP with wbar the theta-averaged dual point -- one m-long chain per iteration
+ * instead of the reference's m-long (8b) and n-long (8d) chains (C2 latency ~halved).  A
+ * reassociation of the same iteration: z* and y* stay within the reference's own fp32-vs-MATLAB
+ * spread (tests/test_condensed.py); Algorithm 1 is still decided on direct G_L z of the returned
+ * point.  f32, one workgroup per instance, m <= 208, n <= 256; requires theta_0 = 1 (both
+ * built-in schedules); custom theta tables of gpad_run_scaled must keep it. */
+#define GPAD_KERNEL_CONDENSED 5
 
 typedef struct gpad_dims {
     int n;           /* primal variables, n = n_u * N                                   */
