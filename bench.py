@@ -374,6 +374,74 @@ def flat_leg(dev, batch=8192, N=100, horizon=10, ref=None):
     return out
 
 
+def flat_phase_schedule(N, K=10, base=0, vpred=0):
+    """csrc/gpad_flatpanel.hip flat_phase_len: 2K, then a quarter of the iterations done; past
+    the previous solve's last iteration vpred one phase to N."""
+    out, v0 = [], 0
+    while v0 < N:
+        plen = max(base or 2 * K, (v0 // 4) // K * K)
+        if vpred and v0 >= vpred:
+            plen = N
+        v1 = N if N - v0 <= plen else v0 + plen
+        out.append((v0, v1))
+        v0 = v1
+    return out
+
+
+def flat_util(iters, N, width, phased=True, K=10, vpred=0):
+    """Column utilisation of the flat panels: useful instance-iterations / column-iterations
+    issued.  A group of `width` columns runs until the phase end or its last column's end;
+    phased=False: one phase (a group runs until its slowest column)."""
+    it = iters.astype(np.int64)
+    phases = flat_phase_schedule(N, K, vpred=vpred) if phased else [(0, N)]
+    executed = 0
+    for v0, v1 in phases:
+        surv = it[it > v0]
+        for i in range(0, surv.size, width):
+            executed += width * (min(v1, int(surv[i:i + width].max())) - v0)
+    return float(it.sum() / executed) if executed else None, len(phases)
+
+
+def flat_tol_leg(dev, batch=8192, horizon=10, tol=1e-4, N=5000):
+    """§8 f4 in tol mode: the flat panels with phased compaction vs one launch (groups run to
+    their slowest column); column utilisation estimated from the per-instance counts.  The
+    timed solves repeat one batch, so the phase schedule's end (the previous solve's last
+    iteration) is exact here."""
+    import torch
+
+    import gpad_mpc
+    from gpad_mpc import problems
+    qp = problems.battery_scenarios(4, horizon, batch, seed=9)
+    MGf, GLf, L = problems.flatten_battery(qp, 4, horizon)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a, np.float64).astype(np.float32))).to(dev)  # noqa: E731
+    L32 = float(np.float32(L))
+    GP, G = t(qp.M), t(qp.g)
+    PD = (G * np.float32(-1.0 / np.float64(np.float32(L)))).contiguous()
+    out = {"config": f"{batch} battery packs (n_u=4, N={horizon}: n={qp.n}, m={qp.m}), flat data, eps={tol}"}
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    for phased in (2, 0):  # forced phases / one launch (the default picks phases from 4 panels per CU)
+        with gpad_mpc.GpadSolver(dev.index or 0, stream=stream) as s:
+            s.setup_flat(t(MGf), t(GLf), L32, n_u=4, batch=batch)
+            s.set_option("phased", phased)
+            Z = torch.zeros(batch, qp.n, device=dev)
+            Y = torch.zeros(batch, qp.m, device=dev)
+            it = np.zeros(batch, np.int32)
+            s.run(Z, Y, GP, PD, N, tol, scaled=True)
+            best = 1e30
+            for _ in range(3):
+                st = s.run(Z.zero_(), Y.zero_(), GP, PD, N, tol, scaled=True, iters=it)
+                best = min(best, st["kernel_ms"])
+        vp = int(it.max())  # the timed solves re-solve the same batch: predicted = last max
+        u16, launches = flat_util(it, N, 16, bool(phased), vpred=vp)
+        u32, _ = flat_util(it, N, 32, bool(phased), vpred=vp)
+        out["phased" if phased else "one_launch"] = {
+            "kernel": st["kernel"], "iters_per_s": float(it.sum()) / (best / 1e3),
+            "qp_solves_per_s": batch / (best / 1e3), "solve_ms": best, "converged": st["converged"],
+            "mean_iters": float(it.mean()), "max_iters": int(it.max()),
+            "column_util_est": {"P1_16_columns": u16, "P2_32_columns": u32}, "launches": launches}
+    return out
+
+
 def closed_loop_leg(dev, batch=8192, steps=20, N=100, cpu=True, flat=False):
     """gpad.m:79-95 closed loop on the device for a batch of battery
     packs (C1 plant: n_u = 4 cells, horizon 10 -> n = 40, m = 180), each MPC step = per-state
@@ -639,6 +707,8 @@ def main():
             extra["closed_loop_battery_flat"] = closed_loop_leg(dev, cpu=False, flat=True)
             extra["flat_battery_c1"] = flat_leg(dev, ref=ref)
             extra["battery_n50"] = flat_leg(dev, horizon=50, N=50, ref=ref)
+            extra["flat_tol_c1"] = flat_tol_leg(dev, batch=65536)
+            extra["flat_tol_n50"] = flat_tol_leg(dev, horizon=50, tol=1e-3, batch=16384)
         side_value = side["iters_all"] / side["dt"]
         out = {
             "metric": "GPAD iterations/s (instance-iterations, solve to eps=1e-4)",

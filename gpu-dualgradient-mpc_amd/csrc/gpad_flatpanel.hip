@@ -337,7 +337,11 @@ __global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<flo
     const __amdgpu_buffer_rsrc_t PA =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.frag), 0, g.total * 16, 0x00020000);
     const bool use_tol = a.tol > 0.0;
-    const int count = a.batch;
+    // phased compaction (as gpad_panel.hip): a phase runs iterations [v_begin, v_end) over the
+    // instances idx_in[0 .. *count_in) (null: all), parks the survivors and lists them
+    const bool fresh = a.v_begin == 0;
+    const bool carry = a.v_end < N;
+    const int count = a.count_in ? __builtin_amdgcn_readfirstlane(*a.count_in) : a.batch;
     const int groups = (count + 16 * P - 1) / (16 * P);
     const int nu1 = P * g.U1, nu2 = P * g.U2;
     if constexpr (ALDS) {
@@ -351,6 +355,11 @@ __global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<flo
 
     for (int grp = blockIdx.x; grp < groups; grp += gridDim.x) {
         const int k0 = 16 * P * grp;  // first column of the group; column (pp, c) = k0 + 16 pp + c
+        // the instance of column `bit` (= 16 pp + c) of this group
+        auto inst_of = [&](int bit) -> size_t {
+            const int k = k0 + bit;
+            return (size_t)(a.idx_in ? a.idx_in[k] : k);
+        };
         unsigned long long live = 0ull;
         for (int pp = 0; pp < P; ++pp) {
             const int left = count - k0 - 16 * pp;
@@ -366,7 +375,7 @@ __global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<flo
             const FpU1 x = fp_u1(g, un < nu1 ? un : 0);
             const int col = k0 + 16 * x.pp + c;
             const bool act = un < nu1 && col < count;
-            const size_t bi = (size_t)(act ? col : 0);
+            const size_t bi = act ? inst_of(16 * x.pp + c) : 0;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int i = 16 * x.t + 4 * r + jl;
@@ -374,7 +383,7 @@ __global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<flo
                 z[q][r] = ok ? a.z[bi * n + i * g.n_u + x.j] : 0.0f;
                 gp[q][r] = ok ? a.gP[bi * a.ld_gP + i * g.n_u + x.j] : 0.0f;
             }
-            if (un < nu1 && use_tol) {  // z_{-1} as the B operand of u = G_L z_{-1}
+            if (un < nu1 && use_tol && fresh) {  // z_{-1} as the B operand of u = G_L z_{-1}
                 float4* L = fp_lds + x.pp * PBf;
                 L[oZc + (x.j * g.T1 + x.t) * 64 + lane] = make_float4(z[q][0], z[q][1], z[q][2], z[q][3]);
 #pragma unroll
@@ -391,7 +400,7 @@ __global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<flo
             const FpU2 x = fp_u2(g, un < nu2 ? un : 0);
             const int col = k0 + 16 * x.pp + c;
             const bool act = un < nu2 && col < count;
-            const size_t bi = (size_t)(act ? col : 0);
+            const size_t bi = act ? inst_of(16 * x.pp + c) : 0;
             float wv[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -399,8 +408,13 @@ __global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<flo
                 const bool ok = row >= 0 && act;
                 y[q][r] = ok ? a.y[bi * m + row] : 0.0f;
                 pd[q][r] = ok ? (float)(a.gscale * (double)a.g[bi * a.ld_g + row]) : 0.0f;
-                u[q][r] = 0.0f;
-                wv[r] = __builtin_fmaf(a.beta[0], y[q][r] - y[q][r], y[q][r]);
+                if (fresh) {  // w_0 = y_0 + beta_0 (y_0 - y_{-1}), y_{-1} = y_0; u below
+                    u[q][r] = 0.0f;
+                    wv[r] = __builtin_fmaf(a.beta[0], y[q][r] - y[q][r], y[q][r]);
+                } else {  // carried from the previous phase
+                    u[q][r] = ok && use_tol ? a.uc[bi * m + row] : 0.0f;
+                    wv[r] = ok ? a.wc[bi * m + row] : 0.0f;
+                }
             }
             if (un < nu2) {
                 float4* L = fp_lds + x.pp * PBf;
@@ -409,7 +423,7 @@ __global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<flo
             }
         }
         __syncthreads();
-        if (use_tol) {  // u = G_L z_{-1}
+        if (use_tol && fresh) {  // u = G_L z_{-1}
 #pragma unroll
             for (int q = 0; q < NU2; ++q) {
                 const int un = w + W * q;
@@ -435,8 +449,8 @@ __global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<flo
             const FpU1 x = fp_u1(g, w);
             pre1 = fp_pre<ALDS>(PA, As, fp_voff1(g, x, lane), g.T1 * 1024, g.KB1, g.KBc, fp_ajump1(g, x));
         }
-        int v = 0;
-        float th = a.theta[0], bn = a.beta[1];
+        int v = a.v_begin;
+        float th = a.theta[v], bn = a.beta[v + 1];
         while (true) {
             const float th_next = a.theta[v + 1], bn_next = a.beta[v + 2];
             ++v;
@@ -546,7 +560,7 @@ __global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<flo
             th = th_next;
             bn = bn_next;
             __syncthreads();
-            if (!chk && v < N) continue;
+            if (!chk && v < a.v_end) continue;
 
             unsigned long long m1 = 0ull, m2 = 0ull;
             bool zh_out = true;  // this iteration's zhat still in Zc (no verification chains ran)
@@ -581,7 +595,7 @@ __global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<flo
                             if ((m2 >> bit) & 1ull) {  // test (B)'s zhat out before z replaces it
                                 const float4 zh4 = *zc;
                                 const float zhv[4] = {zh4.x, zh4.y, zh4.z, zh4.w};
-                                const size_t bi = (size_t)(k0 + bit);
+                                const size_t bi = inst_of(bit);
 #pragma unroll
                                 for (int r = 0; r < 4; ++r) {
                                     const int i = 16 * x.t + 4 * r + jl;
@@ -658,7 +672,7 @@ __global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<flo
                         const int bit = 16 * x.pp + c;
                         const bool tb = (m2 >> bit) & 1ull;  // test (B): zhat (pre-written when verified over)
                         if (((fin >> bit) & 1ull) && (!tb || zh_out)) {
-                            const size_t bi = (size_t)(k0 + bit);
+                            const size_t bi = inst_of(bit);
                             const float4 zh4 = fp_lds[x.pp * PBf + oZc + (x.j * g.T1 + x.t) * 64 + lane];
                             const float zhv[4] = {zh4.x, zh4.y, zh4.z, zh4.w};
 #pragma unroll
@@ -676,7 +690,7 @@ __global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<flo
                         const FpU2 x = fp_u2(g, un);
                         const int bit = 16 * x.pp + c;
                         if ((fin >> bit) & 1ull) {
-                            const size_t bi = (size_t)(k0 + bit);
+                            const size_t bi = inst_of(bit);
 #pragma unroll
                             for (int r = 0; r < 4; ++r) {
                                 const int row = fp_row2(g, FpUnit2{x.cell, x.t}, 16 * x.t + 4 * r + jl);
@@ -686,12 +700,62 @@ __global__ __launch_bounds__(64 * W, 4) void gpad_flatpanel_kernel(SolveArgs<flo
                     }
                 }
                 if (w == 0 && ((fin >> lane) & 1ull)) {
-                    a.iters[k0 + lane] = v;
-                    a.conv[k0 + lane] = (m1 >> lane) & 1ull ? 1 : ((m2 >> lane) & 1ull ? 2 : 0);
+                    const size_t bi = inst_of(lane);
+                    a.iters[bi] = v;
+                    a.conv[bi] = (m1 >> lane) & 1ull ? 1 : ((m2 >> lane) & 1ull ? 2 : 0);
                 }
             }
             live &= ~fin;
-            if (live == 0ull) break;
+            if (live == 0ull || v >= a.v_end) break;
+        }
+        // ---- phase end: park the survivors (z, y in place; w, u carried) and list them ------------
+        if (carry && live) {
+#pragma unroll
+            for (int q = 0; q < NU1; ++q) {
+                const int un = w + W * q;
+                if (un < nu1) {
+                    const FpU1 x = fp_u1(g, un);
+                    const int bit = 16 * x.pp + c;
+                    if ((live >> bit) & 1ull) {
+                        const size_t bi = inst_of(bit);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int i = 16 * x.t + 4 * r + jl;
+                            if (i < g.Nh) a.z[bi * n + i * g.n_u + x.j] = z[q][r];
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < NU2; ++q) {
+                const int un = w + W * q;
+                if (un < nu2) {
+                    const FpU2 x = fp_u2(g, un);
+                    const int bit = 16 * x.pp + c;
+                    if ((live >> bit) & 1ull) {
+                        const size_t bi = inst_of(bit);
+                        const float4 w4 = fp_lds[x.pp * PBf + (x.cell < 0 ? oWe + x.t * 64 : (x.cell * g.KBc + x.t) * 64) +
+                                                 lane];  // w of iteration v (this unit's own rows)
+                        const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int row = fp_row2(g, FpUnit2{x.cell, x.t}, 16 * x.t + 4 * r + jl);
+                            if (row >= 0) {
+                                a.y[bi * m + row] = y[q][r];
+                                a.wc[bi * m + row] = wv[r];
+                                if (use_tol) a.uc[bi * m + row] = u[q][r];
+                            }
+                        }
+                    }
+                }
+            }
+            if (w == 0) {  // lanes 0 .. 16 P - 1 speak for the group's columns
+                const bool mine = (live >> lane) & 1ull;
+                int base = 0;
+                if (lane == 0) base = atomicAdd(a.count_out, (int)__popcll(live));
+                base = __shfl(base, 0, 64);
+                if (mine) a.idx_out[base + (int)__popcll(live & ((1ull << lane) - 1ull))] = (int)inst_of(lane);
+            }
         }
         __syncthreads();  // the next group reuses the LDS arrays
     }
@@ -755,10 +819,11 @@ static hipError_t launch_flatpanel_w8(const SolveArgs<float>& a, FlatGeom g, int
     }
 }
 
-// whole-batch solve (one launch, no phased compaction); a.frag = the flat fragment images.
+// one launch over a.batch instances, or over the phase's list (a.count_in; the geometry and grid
+// are sized for a.batch, extra workgroups find no group); a.frag = the flat fragment images.
 // P panels per workgroup: as many as keep every CU busy (groups >= CUs), the phase-1 units within
 // one per wave and the phase-2 units within 4 per wave, and the LDS within 160 KiB.
-hipError_t launch_flatpanel(const SolveArgs<float>& a, hipStream_t s) {
+static hipError_t launch_flatpanel_once(const SolveArgs<float>& a, hipStream_t s) {
     if (!flatpanel_supported(a.n, a.m, a.n_u) || !a.frag) return hipErrorInvalidValue;
     FlatGeom g = flat_geom(a.n, a.m, a.n_u);
     const int panels = (a.batch + 15) / 16;
@@ -813,6 +878,61 @@ hipError_t launch_flatpanel(const SolveArgs<float>& a, hipStream_t s) {
         default: return launch_fp_nt<4, 4>(a, g, lds, alds, grid, s);
     }
 #undef FP_CASE
+}
+
+// Phase schedule of a phased flat solve: 2K iterations, then a quarter of the iterations done so
+// far (rounded to the test period K), so phases stay short while most columns are alive and grow
+// geometrically in a long tail (O(log N) launches); past the previous solve's last iteration
+// (v_pred) one phase runs to N, so an unused tail costs no empty launches.  Estimated on battery
+// tol-mode batches of 8192: column utilisation ~0.9-0.96 vs 0.61-0.70 in one launch.
+int flat_phase_len(int v0, int check_every, const Tuning* t) {
+    const int K = check_every > 0 ? check_every : 10;
+    const int base = (t && t->phase_len > 0) ? t->phase_len : 2 * K;
+    const int grow = (v0 / 4) / K * K;
+    return grow > base ? grow : base;
+}
+
+hipError_t launch_flatpanel(const SolveArgs<float>& a0, hipStream_t s) {
+    if (!flatpanel_supported(a0.n, a0.m, a0.n_u) || !a0.frag) return hipErrorInvalidValue;
+    SolveArgs<float> a = a0;
+    const Tuning tn = a.tune ? *a.tune : Tuning{};
+    a.v_begin = 0;
+    a.v_end = a.N;
+    a.idx_in = nullptr;
+    a.count_in = nullptr;
+    // phases pay when the batch is several resident rounds of groups (the time of a resident round
+    // is its slowest column either way; compaction shortens the queue of rounds): measured on
+    // battery packs, eps mode, phased vs one launch -- C1 8192: 1.91 vs 1.63 ms, 65536: 8.8 vs
+    // 10.0 ms; N = 50 4096: 25.1 vs 23.9 ms, 16384: 67.7 vs 87.2 ms (profiles/r02_flat_phased.txt).
+    // GPAD_OPT_PHASED: 0 never, 1 (default) from 4 panels per CU, 2 always.
+    const int panels = (a.batch + 15) / 16;
+    const bool phased = a.tol > 0.0 && a.pwork != nullptr &&
+                        (tn.phased == 2 || (tn.phased == 1 && panels >= 4 * a.num_cus));
+    if (!phased) return launch_flatpanel_once(a, s);
+    // workspace as the panel path's (panel_work_bytes): idx ping-pong, phase counts, carried w, u
+    int* idx0 = reinterpret_cast<int*>(a.pwork);
+    int* idx1 = idx0 + a.batch;
+    int* counts = idx1 + a.batch;
+    float* wc = reinterpret_cast<float*>(counts + 2 * kPanelMaxPhases);
+    a.wc = wc;
+    a.uc = wc + (size_t)a.batch * a.m;
+    hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * kPanelMaxPhases, s);
+    if (e != hipSuccess) return e;
+    int v0 = 0;
+    for (int ph = 0; v0 < a.N; ++ph) {
+        int plen = ph >= kPanelMaxPhases - 1 ? a.N : flat_phase_len(v0, a.check_every, &tn);
+        if (a0.v_pred > 0 && v0 >= a0.v_pred) plen = a.N;  // beyond the prediction: one last phase
+        const int v1 = (a.N - v0 <= plen) ? a.N : v0 + plen;
+        a.v_begin = v0;
+        a.v_end = v1;
+        a.idx_in = ph ? ((ph & 1) ? idx0 : idx1) : nullptr;
+        a.count_in = ph ? counts + ph - 1 : nullptr;
+        a.idx_out = (ph & 1) ? idx1 : idx0;
+        a.count_out = counts + ph;
+        if ((e = launch_flatpanel_once(a, s)) != hipSuccess) return e;
+        v0 = v1;
+    }
+    return hipSuccess;
 }
 
 }  // namespace gpad

@@ -119,6 +119,7 @@ struct gpad_handle_s {
     int last_N = 0;
     gpad::PanelPlan plan;
     unsigned long long plan_key = 0;    // fingerprint of the counts the plan was built from
+    int flat_vpred = 0;                 // flat panels: last iteration of the previous phased solve
     // asynchronous runs (no stats): the counts of each phased solve are copied to pinned host
     // memory behind it; the next run re-plans from them once that copy has landed, so a pipeline
     // of back-to-back solves plans from its most recent completed solve without a host sync
@@ -231,7 +232,7 @@ int gpad_set_option(gpad_handle_t h, int option, int value) {
         case GPAD_OPT_PHASE_LEN: return set(t.phase_len, 0, big, def.phase_len);
         case GPAD_OPT_FINISH_THRESH: return set(t.finish_thresh, 0, big, def.finish_thresh);
         case GPAD_OPT_PLAN: h->plan.nph = 0; h->plan_key = 0; return set(t.plan, 0, 1, def.plan);
-        case GPAD_OPT_PHASED: return set(t.phased, 0, 1, def.phased);
+        case GPAD_OPT_PHASED: return set(t.phased, 0, 2, def.phased);
         case GPAD_OPT_FINISHER: return set(t.finisher, 0, 1, def.finisher);
         case GPAD_OPT_LPT: return set(t.lpt, 0, 1, def.lpt);
         case GPAD_OPT_PANEL_MAX_GRID: return set(t.panel_max_grid, 0, big, def.panel_max_grid);
@@ -290,6 +291,7 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
     h->flat = false;
     h->shadow_ok = false;
     h->plan.nph = 0;
+    h->flat_vpred = 0;
     h->plan_pending = false;
     h->last_phased = false;
     h->dims = *d;
@@ -385,6 +387,7 @@ int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* d, int n_u, const float*
     h->flat = false;
     h->shadow_ok = false;
     h->plan.nph = 0;
+    h->flat_vpred = 0;
     h->plan_pending = false;
     h->last_phased = false;
     h->dims = *d;
@@ -475,6 +478,12 @@ static int ensure_schedule(gpad_handle_t h, int N, const void* theta_in, const v
 // The phase plan is a pure function of the per-instance counts (and the shape): rebuild it only
 // when they changed (repeated solves of one batch skip the DP).
 static void update_plan(gpad_handle_t h, const int* counts, int batch, int N) {
+    if (h->flat) {  // the flat panels' phases run to the previous solve's last iteration
+        int mx = 0;
+        for (int b = 0; b < batch; ++b) mx = std::max(mx, counts[b]);
+        h->flat_vpred = mx;
+        return;
+    }
     unsigned long long key = 1469598103934665603ull ^ (unsigned long long)N;
     for (int b = 0; b < batch; ++b) key = (key ^ (unsigned)counts[b]) * 1099511628211ull;
     if (key != h->plan_key || h->plan.nph == 0) {
@@ -601,6 +610,7 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
     a.Hc = h->Hc_ok ? (const float*)h->Hc.p : nullptr;
     a.strideH = d.shared ? 0 : (long long)m * h->ldm;
     int kernel = d.kernel;
+    const bool prev_phased = h->last_phased;  // the previous launch's counts are still in `iters`
     h->last_phased = false;  // set again below when this launch is a phased panel solve
     h->last_N = N;
     hipError_t e = hipSuccess;
@@ -620,7 +630,14 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
             // kernel would be left (several times slower at any batch)
             const int fpm = h->tune.flat_panel_min >= 0 ? h->tune.flat_panel_min : (h->GLx.p ? 8 * h->num_cus : 0);
             if (h->frag_ok && (kernel == GPAD_KERNEL_PANEL || (kernel == GPAD_KERNEL_AUTO && batch >= fpm))) {
+                if (tol > 0.0) {  // phased compaction workspace (gpad_flatpanel.hip)
+                    int rc = h->pwork.ensure(gpad::panel_work_bytes(m, batch));
+                    if (rc) return rc;
+                    a.pwork = h->pwork.p;
+                    a.v_pred = h->flat_vpred;  // the previous solve's last iteration (0: unknown)
+                }
                 e = gpad::launch_flatpanel(a, h->stream);
+                h->last_phased = a.pwork != nullptr;
             } else if (h->GLx.p && kernel != GPAD_KERNEL_STREAM) {  // register-resident flat chains
                 a.GLt = (const T*)h->GLx.p;
                 a.strideA = a.strideB = 0;
@@ -652,7 +669,7 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
                 a.plan = &h->plan;
                 // the previous phased solve's counts are still in `iters` for every instance this
                 // solve has not finished yet: the finisher orders its queue by them
-                if (h->last_phased && h->last_batch == batch && h->last_steps == 1) a.pred = iters;
+                if (prev_phased && h->last_batch == batch && h->last_steps == 1) a.pred = iters;
             }
             e = gpad::launch_panel(a, h->stream, &ok);
             if (e != hipSuccess) return fail(GPAD_ERR_HIP, std::string("panel: ") + hipGetErrorString(e));

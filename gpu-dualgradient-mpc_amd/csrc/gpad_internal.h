@@ -72,6 +72,7 @@ struct SolveArgs {
     // panel kernel, phased compaction (set by launch_panel; see gpad_panel.hip)
     void* pwork;           // workspace of panel_work_bytes(m, batch) bytes, or null (one phase)
     int v_begin, v_end;    // iterations [v_begin, v_end) of this phase
+    int v_pred;            // flat panels: predicted last iteration (previous solve), 0 = unknown
     const int* idx_in;     // instances of this phase (null: 0..batch-1)
     const int* count_in;   // their number (device; null: batch)
     int* idx_out;          // survivors appended here ...
@@ -169,7 +170,9 @@ bool flatpanel_supported(int n, int m, int n_u);
 size_t flatpanel_frag_bytes(int n, int m, int n_u);
 hipError_t launch_pack_flatpanel(const float* MGf, const float* GLT, int n, int m, int n_u, void* frag,
                                  hipStream_t s);
+// tol > 0 with a.pwork (panel_work_bytes): phased compaction, phases of flat_phase_len iterations
 hipError_t launch_flatpanel(const SolveArgs<float>& a, hipStream_t s);
+int flat_phase_len(int v0, int check_every, const Tuning* t);
 // flat G_L (m x Nh) -> full k-major image out[k*ld + r] (k < n), zero off the structure
 hipError_t launch_expand_flat_gl(const float* GLf, float* out, int Nh, int n_u, int m, int ld, hipStream_t s);
 hipError_t launch_step2_flat(const float* MGf, const float* w, const float* gP, float* zhat, int Nh, int n_u,

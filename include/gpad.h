@@ -304,7 +304,8 @@ int gpad_schedule(int N, int kind, double* theta, double* beta);
 #define GPAD_OPT_PHASE_LEN 1       /* panel phase length in iterations (default 4 * check_every)   */
 #define GPAD_OPT_FINISH_THRESH 2   /* survivors at which the finisher takes over (default 2/CU)    */
 #define GPAD_OPT_PLAN 3            /* 1: plan phases from the previous solve's counts (default)    */
-#define GPAD_OPT_PHASED 4          /* 1: phased compaction of tol > 0 panel solves (default)       */
+#define GPAD_OPT_PHASED 4          /* 1: phased compaction of tol > 0 panel solves (default; flat
+                                    * panels: from 4 panels per CU), 2: always, 0: one launch       */
 #define GPAD_OPT_FINISHER 5        /* 0: two-slot work-queue finisher (default); 1: one per group  */
 #define GPAD_OPT_LPT 6             /* 1: longest-predicted-first finisher queue (default)          */
 #define GPAD_OPT_PANEL_MAX_GRID 7  /* cap on the panel grid, workgroups (0 = none, default)        */

@@ -203,6 +203,48 @@ def test_flat_panel_bitexact(gpu, oracle, tol, N, cells, B, P):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("phase_len,phased,P", [(10, 2, 1), (30, 2, 2), (0, 2, 4), (0, 0, 1), (10, 2, 8),
+                                                 (20, 2, 3)])
+@pytest.mark.parametrize("cells,B", [((4, 10), 16 * 6 + 5), ((3, 17), 16 * 4 + 9)])
+def test_flat_panel_phased_bitexact(gpu, oracle, phase_len, phased, P, cells, B):
+    """Phased compaction on the flat panels (tol mode): survivors of each phase are parked
+    (z, y in place; w, u carried) and re-packed into new groups (other columns, panels and
+    workgroups) for the next phase; warm-started y.  Every instance must equal its own oracle
+    flat solve, iteration count included.  phased=2 forces phases at this small batch (the
+    default starts at 4 panels per CU); phased=0: one launch, groups run to their last column."""
+    from gpad_mpc import problems
+    import gpad_mpc
+    n_u, Nh = cells
+    qp = problems.battery_scenarios(n_u, Nh, B, seed=13)
+    MGf, GLf, L = problems.flatten_battery(qp, n_u, Nh)
+    f32 = lambda a: np.ascontiguousarray(np.asarray(a, np.float64).astype(np.float32))  # noqa: E731
+    L32 = np.float32(L)
+    MGf32, GLf32, GP = f32(MGf), f32(GLf), f32(qp.M)
+    PD = np.ascontiguousarray(oracle.scale_vec(f32(qp.g), L32))
+    Y0 = (0.02 * np.random.default_rng(3).random((B, qp.m))).astype(np.float32)
+    s = gpad_mpc.GpadSolver(0)
+    s.setup_flat(MGf32, GLf32, float(L32), n_u=n_u, batch=B, kernel=gpad_mpc.KERNEL_PANEL)
+    if P == 8:
+        s.set_option("flat_waves", 8)
+    else:
+        s.set_option("flat_panels", P)
+    s.set_options(phase_len=phase_len, phased=phased)
+    for rnd, tol in enumerate((1e-3, 1e-4)):  # the second solve's phases end at the first's last iteration
+        Z = np.zeros((B, qp.n), np.float32)
+        Y = Y0.copy()
+        it = np.zeros(B, np.int32)
+        st = s.run(Z, Y, GP, PD, 4000, tol, scaled=True, iters=it)
+        assert st["kernel"] == "flat" and st["converged"] == B
+        assert it.max() > it.min() + 40  # the batch spans several phases
+        for b in range(B):
+            z, y, its, _ = oracle.solve_flat_f32(np.zeros(qp.n), Y0[b], MGf32, GP[b], GLf32, PD[b], n_u, 4000,
+                                                 L32, tol)
+            assert it[b] == its, (rnd, b)
+            np.testing.assert_array_equal(Z[b], z, err_msg=f"{rnd} z[{b}]")
+            np.testing.assert_array_equal(Y[b], y, err_msg=f"{rnd} y[{b}]")
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name", FLAT_SETS)
 def test_flat_step_entry_points(gpu, name):
     """gpad_step2_primal_flat / gpad_step4_project_flat vs the reference's flat step KATs."""
