@@ -570,18 +570,36 @@ def main():
     solver = gpad_mpc.GpadSolver(dev.index, stream=stream.cuda_stream)
     L32 = float(np.float32(L))
     solver.setup(dML, dG, L32, n=n, m=m, batch=B, shared=True, check_every=10, kernel=kern)
-    from gpad_mpc import parallel
-    packed = torch.empty(B, n + m, device=dev)
-    counts = [B] * world
+    # one gather of (z*, y*) to rank 0 per step, asynchronous and double buffered: the gather of
+    # step k (RCCL on its own stream, ordered after the copy into its buffer) may overlap the
+    # solve of step k + 1; a buffer is reused only after its gather two steps back completed,
+    # and every gather is waited for inside the timed region (drain)
+    slots = []
+    if world > 1:
+        for _ in range(2):
+            pk = torch.empty(B, n + m, device=comm_dev)
+            slots.append({"packed": pk, "work": None,
+                          "gl": [torch.empty_like(pk) for _ in range(world)] if rank == 0 else None})
+    nstep = [0]
 
     def step(Mv, gv):
         z.zero_()
         y.zero_()
         solver.run(z, y, Mv, gv, args.max_iters, args.tol, stats=False)
-        if world > 1:  # one RCCL gather of (z*, y*) to rank 0
-            packed[:, :n] = z
-            packed[:, n:] = y
-            parallel.gather_rows(packed.to(comm_dev), world, rank, counts)
+        if world > 1:
+            sl = slots[nstep[0] % 2]
+            nstep[0] += 1
+            if sl["work"] is not None:
+                sl["work"].wait()
+            sl["packed"][:, :n] = z
+            sl["packed"][:, n:] = y
+            sl["work"] = dist.gather(sl["packed"], sl["gl"], dst=0, async_op=True)
+
+    def drain():
+        for sl in slots:
+            if sl["work"] is not None:
+                sl["work"].wait()
+                sl["work"] = None
 
     def timed(inputs):
         """W warm-up steps, then K timed steps enqueued back to back with no host
@@ -591,6 +609,7 @@ def main():
         inputs(k) -> (M, g) of step k (k < W: warm-up)."""
         for k in range(args.warmup):
             step(*inputs(k))
+        drain()
         torch.cuda.synchronize(dev)
         acc = torch.zeros(1, dtype=torch.int64, device=dev)
         ev0 = torch.cuda.Event(enable_timing=True)
@@ -603,6 +622,7 @@ def main():
         for k in range(args.steps):
             step(*inputs(args.warmup + k))
             solver.accumulate_iterations(acc)
+        drain()
         ev1.record(stream)
         torch.cuda.synchronize(dev)
         if world > 1:
