@@ -326,6 +326,42 @@ def c3_leg(dev, n=200, m=200, batch=4096, reps=3, max_iters=5000, tol=1e-4, ref=
     return out
 
 
+def condensed_leg(dev, n=200, m=200, batch=8192, reps=3, max_iters=5000, tol=1e-4):
+    """The headline C4 shard on the opt-in condensed operator (GPAD_KERNEL_CONDENSED: one H GEMM
+    per iteration on the MFMA panels, gpad_cpanel.hip; NOT the reference's arithmetic) beside the
+    bit-exact panels on the same inputs: rate, the norm-wise distance of z* from the bit-exact z*,
+    and the fp64 constraint violation of the returned z* (Algorithm 1 decides on direct G_L z)."""
+    import torch
+
+    import gpad_mpc
+    from gpad_mpc import _lib
+    ML, G, L, M, g = make_shard(n, m, batch, 0)
+    f32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)  # noqa: E731
+    dML, dG, dM, dg = f32(ML), f32(G), f32(M), f32(g)
+    out = {"config": f"C4 shard: {batch} instances sharing ML/G, n={n}, m={m}, eps={tol}"}
+    zs = {}
+    for name, kern in (("condensed", _lib.KERNEL_CONDENSED), ("bit_exact", _lib.KERNEL_AUTO)):
+        z = torch.zeros(batch, n, device=dev)
+        y = torch.zeros(batch, m, device=dev)
+        with gpad_mpc.GpadSolver(dev.index or 0, stream=torch.cuda.current_stream(dev).cuda_stream) as s:
+            s.setup(dML, dG, float(np.float32(L)), n=n, m=m, batch=batch, shared=True, check_every=10, kernel=kern)
+            best, st = 1e30, None
+            for _ in range(reps + 2):
+                r = s.run(z.zero_(), y.zero_(), dM, dg, max_iters, tol)
+                if r["kernel_ms"] < best:
+                    best, st = r["kernel_ms"], r
+        zs[name] = z.double()
+        out[name] = {"kernel": st["kernel"], "iters_per_s": st["total_iterations"] / (best / 1e3),
+                     "qp_solves_per_s": batch / (best / 1e3), "mean_iters_to_eps": st["total_iterations"] / batch,
+                     "solve_ms": best, "converged": st["converged"]}
+    zc, zb = zs["condensed"], zs["bit_exact"]
+    out["condensed"]["rel_dev_z_vs_bit_exact"] = float((zc - zb).norm() / zb.norm())
+    Gd, gd = dG.double(), dg.double()
+    out["condensed"]["max_constraint_violation"] = float((zc @ Gd.T - gd).max())
+    out["speedup"] = out["condensed"]["iters_per_s"] / out["bit_exact"]["iters_per_s"]
+    return out
+
+
 def flat_leg(dev, batch=8192, N=100, horizon=10, ref=None):
     """the flat (equal-cell) battery path vs the full-matrix path on the
     same battery packs (n_u = 4; horizon 10: n = 40, m = 180 = C1; horizon 50: n = 200, m = 900,
@@ -723,6 +759,7 @@ def main():
             extra["hbm_bound_c5"] = hbm_leg(dev, ref=ref)
             extra["distinct_c2_batch"] = distinct_leg(dev, n, m, ref=ref)
             extra["c3_batch4096"] = c3_leg(dev, n, m, ref=ref)
+            extra["c4_condensed"] = condensed_leg(dev, n, m, batch=B)
             extra["closed_loop_battery"] = closed_loop_leg(dev, cpu=not args.no_cpu)
             extra["closed_loop_battery_flat"] = closed_loop_leg(dev, cpu=False, flat=True)
             extra["flat_battery_c1"] = flat_leg(dev, ref=ref)

@@ -1,0 +1,498 @@
+// gpad_cpanel.hip -- GPAD_KERNEL_CONDENSED for shared-matrix batches: the condensed operator on
+// the f32 MFMA pipe (opt-in; NOT the reference's arithmetic, see gpad_condensed.hip / gpad.h).
+//
+// The panel kernels (gpad_panel.hip) run the reference's two skinny GEMMs per iteration,
+// Zhat = (-ML) W and Y' = G_L Zhat.  With zhat eliminated (G_L zhat = H w + c, H = G_L (-ML),
+// m x m) an iteration is ONE GEMM  S[m x 16] = H W[m x 16]  plus the 8d/8c epilogue on the dual
+// side (wbar = theta-average of w, so z = -ML wbar - g_P is formed only when Algorithm 1 decides
+// and at the end): half the MFMA work at n = m, one barrier per iteration.
+//
+// Layout: an 8-wave workgroup owns a group of two panels (32 instances) at a time, grid-stride
+// over groups.  Row tile t of BOTH panels belongs to wave t mod 8 (one A stream feeds two
+// interleaved MFMA chains; T = 13: 4, 3, 3, 3 tiles per SIMD), its row state (y, u, c of 16 rows x
+// 32 columns) in the wave's registers (256 VGPRs at 2 waves per SIMD), p_D and wbar in LDS.  W is double buffered in LDS in
+// MFMA B-fragment order (the accumulator layout of the fragment-permuted A images equals the
+// next B fragment, see gpad_panel.hip), so an iteration reads W[v & 1] and writes W[(v+1) & 1].
+// The direct GEMMs of a decided test -- X = (-ML) V (V = wbar for test A, w for test B) and
+// G_L X -- reuse the panel kernels' packed -ML / G_L images; the H image is packed the same way.
+// Bit-exact against oracle/gpad_oracle.c orc_solve_condensed_f32 (each output row one
+// ascending-k fmaf chain, as the MFMA computes it).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "gpad_internal.h"
+
+namespace gpad {
+
+typedef float cf32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned cu32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kCpWaves = 8;   // 2 per SIMD: 256 VGPRs each (no spills)
+constexpr int kCpPanels = 2;  // panels per group (32 instances)
+
+__device__ __forceinline__ int cp_pi16(int rho) { return 4 * (rho & 3) + (rho >> 2); }
+
+// H image from the k-major Ht (Ht[k][ldm] = H[i][k]): PH[b][t][lane][q] = H[16t + pi(lane&15)][16b + 4q + (lane>>4)]
+__global__ void pack_cpanel_kernel(const float* __restrict__ Ht, int m, int ldm, int T, float4* __restrict__ dst) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= T * T * 64) return;
+    const int lane = idx & 63, t = (idx >> 6) % T, b = (idx >> 6) / T;
+    const int row = 16 * t + cp_pi16(lane & 15);
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int col = 16 * b + 4 * q + (lane >> 4);
+        v[q] = (row < m && col < m) ? Ht[(size_t)col * ldm + row] : 0.0f;
+    }
+    dst[idx] = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+__device__ __forceinline__ float4 cp_f4(cu32x4 v) {
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+
+// acc = A[tile] (T k-blocks from L2, one block ahead) x B (LDS fragment order), ascending k
+template <int T>
+__device__ __forceinline__ cf32x4 cp_gemm(__amdgpu_buffer_rsrc_t PA, const float4* B, int voff, int lane) {
+    cf32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    float4 a[2], b[2];
+    a[0] = cp_f4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, 0, 0));
+    b[0] = B[lane];
+#pragma unroll
+    for (int kb = 0; kb < T; ++kb) {
+        const int cur = kb & 1, nxt = cur ^ 1;
+        if (kb + 1 < T) {
+            a[nxt] = cp_f4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb + 1) * T * 1024, 0));
+            b[nxt] = B[(kb + 1) * 64 + lane];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].x, b[cur].x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].y, b[cur].y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].z, b[cur].z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].w, b[cur].w, acc, 0, 0, 0);
+        asm volatile("" ::: "memory");
+    }
+    return acc;
+}
+
+// two accumulators sharing every A fragment (the same tile of both panels), MFMAs interleaved
+template <int T>
+__device__ __forceinline__ void cp_gemm_dual(__amdgpu_buffer_rsrc_t PA, const float4* B0, const float4* B1, int voff,
+                                             int lane, cf32x4& acc0, cf32x4& acc1) {
+    acc0 = cf32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    acc1 = cf32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    float4 a[2], b0[2], b1[2];
+    a[0] = cp_f4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, 0, 0));
+    b0[0] = B0[lane];
+    b1[0] = B1[lane];
+#pragma unroll
+    for (int kb = 0; kb < T; ++kb) {
+        const int cur = kb & 1, nxt = cur ^ 1;
+        if (kb + 1 < T) {
+            a[nxt] = cp_f4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb + 1) * T * 1024, 0));
+            b0[nxt] = B0[(kb + 1) * 64 + lane];
+            b1[nxt] = B1[(kb + 1) * 64 + lane];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].x, b0[cur].x, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].x, b1[cur].x, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].y, b0[cur].y, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].y, b1[cur].y, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].z, b0[cur].z, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].z, b1[cur].z, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].w, b0[cur].w, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].w, b1[cur].w, acc1, 0, 0, 0);
+        asm volatile("" ::: "memory");
+    }
+}
+
+struct CpSlot {  // per unit: per column partials of the Algorithm-1 test
+    float violz[16], violh[16], wmin[16], magh[16];
+    double gap[16];
+};
+
+template <int T>
+struct CpLds {
+    float4 W[kCpPanels][2][T * 64];  // w, double buffered (B of the H GEMM)
+    float4 WB[kCpPanels][T * 64];    // wbar (B of test A's direct GEMM and of the final z)
+    float4 Z[kCpPanels][T * 64];     // X = -ML V - g_P (B of the direct G_L GEMM); g_P at group start
+    float4 PD[kCpPanels][T * 64];    // p_D of the unit rows (parked in LDS, not VGPRs)
+    CpSlot slots[kCpPanels * T];
+};
+constexpr int kCpMaxTiles = 14;  // LDS: 6 T KiB per panel + slots <= 160 KiB
+
+template <int T>
+__global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<float> a) {
+    constexpr int NU = (T + kCpWaves - 1) / kCpWaves;  // tiles per wave (each for both panels)
+    extern __shared__ __attribute__((aligned(16))) float4 cp_lds[];
+    CpLds<T>* Lp = reinterpret_cast<CpLds<T>*>(cp_lds);
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int j = lane >> 4, c = lane & 15;
+    const int n = a.n, m = a.m, N = a.N, K = a.check_every;
+    const int abytes = T * T * 1024;
+    const __amdgpu_buffer_rsrc_t PA1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.frag), 0, abytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t PA2 =
+        __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)a.frag + abytes), 0, abytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t PH = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.hfrag), 0, abytes, 0x00020000);
+    const bool use_tol = a.tol > 0.0;
+    const int count = a.batch;
+    const int groups = (count + 16 * kCpPanels - 1) / (16 * kCpPanels);
+    auto tile = [&](int q) { return w + kCpWaves * q; };  // tile of unit q (valid when < T)
+    // acc[pp] = A (tile of unit q) x B_pp, both panels sharing each A fragment
+    auto gemm = [&](int q, __amdgpu_buffer_rsrc_t PA, const float4* B0, const float4* B1, cf32x4 (&acc)[2]) {
+        cp_gemm_dual<T>(PA, B0, B1, tile(q) * 1024 + lane * 16, lane, acc[0], acc[1]);
+    };
+
+    for (int grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+        const int k0 = 16 * kCpPanels * grp;
+        unsigned live = 0u;  // bit 16 pp + c: column c of panel pp holds an unfinished instance
+        for (int pp = 0; pp < kCpPanels; ++pp) {
+            const int left = count - k0 - 16 * pp;
+            live |= (left >= 16 ? 0xFFFFu : (left > 0 ? (1u << left) - 1u : 0u)) << (16 * pp);
+        }
+        // ---- unit state (y, u, c in registers; p_D, wbar, w in LDS); g_P into Z -----------------
+        float y[NU][2][4], u[NU][2][4], cv[NU][2][4];
+#pragma unroll
+        for (int q = 0; q < NU; ++q) {
+            const int t = tile(q), fo = t * 64 + lane;
+#pragma unroll
+            for (int pp = 0; pp < kCpPanels; ++pp) {
+                const int col = k0 + 16 * pp + c;
+                const bool act = t < T && col < count;
+                float gp[4], wv[4], pdv[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 16 * t + 4 * r + j;
+                    const bool okm = act && i < m, okn = act && i < n;
+                    y[q][pp][r] = okm ? a.y[(size_t)col * m + i] : 0.0f;
+                    pdv[r] = okm ? (float)(a.gscale * (double)a.g[(size_t)col * a.ld_g + i]) : 0.0f;
+                    gp[r] = okn ? a.gP[(size_t)col * a.ld_gP + i] : 0.0f;
+                    wv[r] = __builtin_fmaf(a.beta[0], y[q][pp][r] - y[q][pp][r], y[q][pp][r]);
+                    u[q][pp][r] = 0.0f;  // theta_0 = 1: u_0 = s whatever the seed
+                }
+                if (t < T) {
+                    Lp->Z[pp][fo] = make_float4(gp[0], gp[1], gp[2], gp[3]);
+                    Lp->W[pp][0][fo] = make_float4(wv[0], wv[1], wv[2], wv[3]);
+                    Lp->WB[pp][fo] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                    Lp->PD[pp][fo] = make_float4(pdv[0], pdv[1], pdv[2], pdv[3]);
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < NU; ++q) {  // c = -G_L g_P (one chain per row, as orc_chain)
+            cf32x4 acc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+            if (tile(q) < T) gemm(q, PA2, Lp->Z[0], Lp->Z[1], acc);
+#pragma unroll
+            for (int pp = 0; pp < kCpPanels; ++pp)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) cv[q][pp][r] = -acc[pp][r];
+        }
+        __syncthreads();  // Z is rewritten by the tests
+
+        // X = -ML V - g_P (V: B0 / B1, fragment order) into Z; all threads call it (barrier after);
+        // the caller then runs G_L X per unit (gemm(q, PA2, Z...)) and reads X back from Z
+        auto direct_x = [&](const float4* B0, const float4* B1) {
+#pragma unroll
+            for (int q = 0; q < NU; ++q) {
+                const int t = tile(q);
+                if (t < T) {
+                    cf32x4 acc[2];
+                    gemm(q, PA1, B0, B1, acc);
+#pragma unroll
+                    for (int pp = 0; pp < kCpPanels; ++pp) {
+                        const int col = k0 + 16 * pp + c;
+                        float xo[4];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int i = 16 * t + 4 * r + j;
+                            const float gpi = (i < n && col < count) ? a.gP[(size_t)col * a.ld_gP + i] : 0.0f;
+                            xo[r] = i < n ? acc[pp][r] - gpi : 0.0f;  // seq_functions.cpp:61-62 order
+                        }
+                        Lp->Z[pp][t * 64 + lane] = make_float4(xo[0], xo[1], xo[2], xo[3]);
+                    }
+                }
+            }
+            __syncthreads();
+        };
+        // per-column reduction of a panel's tile slots (lane = 16 pp + c, lane < 32)
+        auto reduce = [&](double& vz, double& vh, double& mh, double& wm, double& gq) {
+            vz = -INFINITY;
+            vh = -INFINITY;
+            mh = 0.0;
+            wm = INFINITY;
+            gq = 0.0;
+            const int pp = lane >> 4;
+            if (pp < kCpPanels)
+                for (int s2 = pp * T; s2 < (pp + 1) * T; ++s2) {
+                    vz = fmax(vz, (double)Lp->slots[s2].violz[c]);
+                    vh = fmax(vh, (double)Lp->slots[s2].violh[c]);
+                    mh = fmax(mh, (double)Lp->slots[s2].magh[c]);
+                    wm = fmin(wm, (double)Lp->slots[s2].wmin[c]);
+                    gq += Lp->slots[s2].gap[c];
+                }
+        };
+        auto publish = [&](int pp, int t, float vz, float vh, float mh, float wm, double gp) {
+#pragma unroll
+            for (int o = 16; o < 64; o <<= 1) {
+                vz = fmaxf(vz, __shfl_xor(vz, o, 64));
+                vh = fmaxf(vh, __shfl_xor(vh, o, 64));
+                mh = fmaxf(mh, __shfl_xor(mh, o, 64));
+                wm = fminf(wm, __shfl_xor(wm, o, 64));
+                gp += __shfl_xor(gp, o, 64);
+            }
+            if (j == 0) {
+                CpSlot& sl = Lp->slots[pp * T + t];
+                sl.violz[c] = vz;
+                sl.violh[c] = vh;
+                sl.magh[c] = mh;
+                sl.wmin[c] = wm;
+                sl.gap[c] = gp;
+            }
+        };
+        // results of the columns in `done`: z rows from Z (the last direct_x), y from the registers
+        auto put_out = [&](unsigned done, int v, int code) {
+#pragma unroll
+            for (int q = 0; q < NU; ++q) {
+                const int t = tile(q);
+                if (t < T) {
+#pragma unroll
+                    for (int pp = 0; pp < kCpPanels; ++pp) {
+                        const int bit = 16 * pp + c;
+                        if ((done >> bit) & 1u) {
+                            const size_t col = (size_t)(k0 + bit);
+                            const float4 x4 = Lp->Z[pp][t * 64 + lane];
+                            const float xo[4] = {x4.x, x4.y, x4.z, x4.w};
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                const int i = 16 * t + 4 * r + j;
+                                if (i < n) a.z[col * n + i] = xo[r];
+                                if (i < m) a.y[col * m + i] = y[q][pp][r];
+                            }
+                        }
+                    }
+                }
+            }
+            if (w == 0 && lane < 32 && ((done >> lane) & 1u)) {
+                a.iters[k0 + lane] = v;
+                a.conv[k0 + lane] = code;
+            }
+        };
+
+        int v = 0;
+        float th = a.theta[0], bn = a.beta[1];
+        while (true) {
+            const float th_next = a.theta[v + 1], bn_next = a.beta[v + 2];
+            const int rb = v & 1;
+            ++v;
+            const bool chk = use_tol && (v % K) == 0;
+            const float omt = 1.0f - th;
+            {
+#pragma unroll
+                for (int q = 0; q < NU; ++q) {
+                    const int t = tile(q), fo = t * 64 + lane;
+                    if (t < T) {
+                        cf32x4 acc[2];
+                        gemm(q, PH, Lp->W[0][rb], Lp->W[1][rb], acc);
+#pragma unroll
+                        for (int pp = 0; pp < kCpPanels; ++pp) {
+                            const bool act = (live >> (16 * pp + c)) & 1u;
+                            const float4 w4 = Lp->W[pp][rb][fo], b4 = Lp->WB[pp][fo], p4 = Lp->PD[pp][fo];
+                            const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+                            const float wbv[4] = {b4.x, b4.y, b4.z, b4.w};
+                            const float pdv[4] = {p4.x, p4.y, p4.z, p4.w};
+                            float wn[4], wbn[4];
+                            float vz = -INFINITY, vh = -INFINITY, mh = 0.0f, wm = INFINITY;
+                            double gp = 0.0;
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                const float sc = acc[pp][r] + cv[q][pp][r];  // G_L zhat, condensed
+                                wbn[r] = __builtin_fmaf(omt, wbv[r], th * wv[r]);
+                                const float sv = (wv[r] + pdv[r]) + sc;
+                                const float yp = (__builtin_fabsf(sv) + sv) * 0.5f;
+                                const float un2 = __builtin_fmaf(omt, u[q][pp][r], th * sc);
+                                wn[r] = __builtin_fmaf(bn, yp - y[q][pp][r], yp);
+                                if (act) {
+                                    if (use_tol) u[q][pp][r] = un2;
+                                    y[q][pp][r] = yp;
+                                }
+                                if (chk && act && 16 * t + 4 * r + j < m) {
+                                    const float tt = sc + pdv[r];
+                                    vz = fmaxf(vz, u[q][pp][r] + pdv[r]);
+                                    vh = fmaxf(vh, tt);
+                                    mh = fmaxf(mh, __builtin_fabsf(sc) + __builtin_fabsf(pdv[r]));
+                                    wm = fminf(wm, wv[r]);
+                                    gp -= (double)wv[r] * (double)tt;
+                                }
+                            }
+                            if (act) {
+                                Lp->W[pp][rb ^ 1][fo] = make_float4(wn[0], wn[1], wn[2], wn[3]);
+                                Lp->WB[pp][fo] = make_float4(wbn[0], wbn[1], wbn[2], wbn[3]);
+                            } else {
+                                Lp->W[pp][rb ^ 1][fo] = w4;
+                            }
+                            if (chk) publish(pp, t, vz, vh, mh, wm, gp);
+                        }
+                    }
+                }
+            }
+            th = th_next;
+            bn = bn_next;
+            __syncthreads();
+            if (!chk && v < N) continue;
+
+            if (chk) {
+                double vz, vh, mh, wm, gq;
+                reduce(vz, vh, mh, wm, gq);
+                const bool mine = lane < 16 * kCpPanels && ((live >> (lane & 31)) & 1u);
+                const bool nomA = mine && vz * a.L <= a.tol;
+                const bool nomB = mine && viol_ok(vh, mh, a.L, a.tol, ViolMargin<float>::value) && wm >= 0.0 &&
+                                  gq * a.L <= a.tol_gap;
+                const unsigned mA = (unsigned)__ballot(nomA);
+                const unsigned mB = (unsigned)__ballot(nomB);
+                __syncthreads();  // every wave's slot reads precede the rewrites below
+                if (mA) {  // (A): decide on G_L z of z = -ML wbar - g_P, u reset to it
+                    direct_x(Lp->WB[0], Lp->WB[1]);
+#pragma unroll
+                    for (int q = 0; q < NU; ++q) {
+                        const int t = tile(q);
+                        if (t < T) {
+                            cf32x4 gz[2];
+                            gemm(q, PA2, Lp->Z[0], Lp->Z[1], gz);
+#pragma unroll
+                            for (int pp = 0; pp < kCpPanels; ++pp) {
+                                const bool nom = (mA >> (16 * pp + c)) & 1u;
+                                const float4 p4 = Lp->PD[pp][t * 64 + lane];
+                                const float pdv[4] = {p4.x, p4.y, p4.z, p4.w};
+                                float vc = -INFINITY, mc = 0.0f;
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) {
+                                    if (nom) u[q][pp][r] = gz[pp][r];
+                                    if (nom && 16 * t + 4 * r + j < m) {
+                                        vc = fmaxf(vc, gz[pp][r] + pdv[r]);
+                                        mc = fmaxf(mc, __builtin_fabsf(gz[pp][r]) + __builtin_fabsf(pdv[r]));
+                                    }
+                                }
+                                publish(pp, t, vc, -INFINITY, mc, INFINITY, 0.0);
+                            }
+                        }
+                    }
+                    __syncthreads();
+                    reduce(vz, vh, mh, wm, gq);
+                    const unsigned m1 = (unsigned)__ballot(lane < 32 && ((mA >> (lane & 31)) & 1u) &&
+                                                           viol_ok(vz, mh, a.L, a.tol, ViolMargin<float>::value)) &
+                                        live;
+                    if (m1) put_out(m1, v, 1);
+                    live &= ~m1;
+                    __syncthreads();  // slot reads before the (B) rewrites
+                }
+                const unsigned mBv = mB & live;
+                if (mBv) {  // (B): decide on G_L zhat of zhat = -ML w - g_P (w: W[rb], intact)
+                    direct_x(Lp->W[0][rb], Lp->W[1][rb]);
+#pragma unroll
+                    for (int q = 0; q < NU; ++q) {
+                        const int t = tile(q);
+                        if (t < T) {
+                            cf32x4 gh[2];
+                            gemm(q, PA2, Lp->Z[0], Lp->Z[1], gh);
+#pragma unroll
+                            for (int pp = 0; pp < kCpPanels; ++pp) {
+                                const bool nom = (mBv >> (16 * pp + c)) & 1u;
+                                const float4 w4 = Lp->W[pp][rb][t * 64 + lane], p4 = Lp->PD[pp][t * 64 + lane];
+                                const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+                                const float pdv[4] = {p4.x, p4.y, p4.z, p4.w};
+                                float vh2 = -INFINITY, mh2 = 0.0f, wm2 = INFINITY;
+                                double gp2 = 0.0;
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) {
+                                    if (nom && 16 * t + 4 * r + j < m) {
+                                        const float tt = gh[pp][r] + pdv[r];
+                                        vh2 = fmaxf(vh2, tt);
+                                        mh2 = fmaxf(mh2, __builtin_fabsf(gh[pp][r]) + __builtin_fabsf(pdv[r]));
+                                        wm2 = fminf(wm2, wv[r]);
+                                        gp2 -= (double)wv[r] * (double)tt;
+                                    }
+                                }
+                                publish(pp, t, -INFINITY, vh2, mh2, wm2, gp2);
+                            }
+                        }
+                    }
+                    __syncthreads();
+                    reduce(vz, vh, mh, wm, gq);
+                    const unsigned m2 = (unsigned)__ballot(lane < 32 && ((mBv >> (lane & 31)) & 1u) &&
+                                                           viol_ok(vh, mh, a.L, a.tol, ViolMargin<float>::value) &&
+                                                           wm >= 0.0 && gq * a.L <= a.tol_gap) &
+                                        live;
+                    if (m2) put_out(m2, v, 2);
+                    live &= ~m2;
+                }
+            }
+            if (v >= N && live) {  // the rest ran out of iterations: z = -ML wbar - g_P
+                __syncthreads();
+                direct_x(Lp->WB[0], Lp->WB[1]);
+                put_out(live, v, 0);
+                live = 0u;
+            }
+            if (live == 0u) break;
+            if (chk) __syncthreads();  // the tests' LDS traffic precedes the next iteration
+        }
+        __syncthreads();  // the next group reuses the LDS arrays
+    }
+}
+
+bool cpanel_supported(int n, int m) {
+    const int T = ((n > m ? n : m) + 15) / 16;
+    return T >= 1 && T <= kCpMaxTiles;
+}
+
+size_t cpanel_frag_bytes(int n, int m) {
+    const int T = ((n > m ? n : m) + 15) / 16;
+    return (size_t)T * T * 1024;
+}
+
+hipError_t launch_pack_cpanel(const float* Ht, int n, int m, int ldm, void* hfrag, hipStream_t s) {
+    const int T = ((n > m ? n : m) + 15) / 16;
+    const int tot = T * T * 64;
+    hipLaunchKernelGGL(pack_cpanel_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, Ht, m, ldm, T,
+                       reinterpret_cast<float4*>(hfrag));
+    return hipGetLastError();
+}
+
+template <int T>
+static hipError_t launch_cp_t(const SolveArgs<float>& a, hipStream_t s) {
+    const size_t lds = sizeof(CpLds<T>);
+    hipError_t e = hipFuncSetAttribute((const void*)gpad_cpanel_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+    const int groups = (a.batch + 16 * kCpPanels - 1) / (16 * kCpPanels);
+    const int grid = groups < a.num_cus ? groups : a.num_cus;
+    hipLaunchKernelGGL((gpad_cpanel_kernel<T>), dim3(grid), dim3(64 * kCpWaves), lds, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_cpanel(const SolveArgs<float>& a, hipStream_t s, bool* supported) {
+    const int T = ((a.n > a.m ? a.n : a.m) + 15) / 16;
+    *supported = cpanel_supported(a.n, a.m) && a.frag && a.hfrag && a.frag_tiles == T && a.strideA == 0 &&
+                 a.strideB == 0;
+    if (!*supported) return hipSuccess;
+    switch (T) {
+        case 1: return launch_cp_t<1>(a, s);
+        case 2: return launch_cp_t<2>(a, s);
+        case 3: return launch_cp_t<3>(a, s);
+        case 4: return launch_cp_t<4>(a, s);
+        case 5: return launch_cp_t<5>(a, s);
+        case 6: return launch_cp_t<6>(a, s);
+        case 7: return launch_cp_t<7>(a, s);
+        case 8: return launch_cp_t<8>(a, s);
+        case 9: return launch_cp_t<9>(a, s);
+        case 10: return launch_cp_t<10>(a, s);
+        case 11: return launch_cp_t<11>(a, s);
+        case 12: return launch_cp_t<12>(a, s);
+        case 13: return launch_cp_t<13>(a, s);
+        default: return launch_cp_t<14>(a, s);
+    }
+}
+
+}  // namespace gpad

@@ -98,6 +98,8 @@ struct gpad_handle_s {
     DevBuf MGt, GLt, frag, stage;
     DevBuf Hc;                 // GPAD_KERNEL_CONDENSED: H = G_L (-ML) images (gpad_condensed.hip)
     bool Hc_ok = false;
+    DevBuf Hfrag;              // ... H in the panel fragment layout (gpad_cpanel.hip), shared f32
+    bool Hfrag_ok = false;
     bool frag_ok = false;      // frag holds the fragment image of the bound matrices
     bool keep_stage = false;   // gpad_solve's cached handle keeps its staging buffer
     // gpad_solve: host copy of the last bound (ML, G, L, dims) so a repeated one-shot call on
@@ -188,6 +190,7 @@ int gpad_destroy(gpad_handle_t h) {
     h->MGt.release();
     h->GLt.release();
     h->Hc.release();
+    h->Hfrag.release();
     h->GLx.release();
     h->frag.release();
     h->stage.release();
@@ -245,6 +248,7 @@ int gpad_set_option(gpad_handle_t h, int option, int value) {
             return set(t.flat_waves, 0, 16, def.flat_waves);
         case GPAD_OPT_FLAT_A_LDS: return set(t.flat_a_lds, 0, 1, def.flat_a_lds);
         case GPAD_OPT_FINISH_SOLO: return set(t.finish_solo, 0, big, def.finish_solo);
+        case GPAD_OPT_CONDENSED_PANEL: return set(t.cpanel, 0, 1, def.cpanel);
         default: return fail(GPAD_ERR_INVALID, "gpad_set_option: unknown option");
     }
 }
@@ -340,6 +344,7 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
                                       (float*)h->Hc.p, h->stream));
         h->Hc_ok = true;
     }
+    h->Hfrag_ok = false;
     // fragment image for the MFMA panel kernel (shared f32 matrices only); the buffer is kept
     // across setups and only grows
     h->frag_ok = false;
@@ -352,6 +357,11 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
                                             (float)sa, sb, h->frag.p, h->stream));
             h->frag_tiles = gpad::panel_tiles(n, m, d->batch);
             h->frag_ok = true;
+        }
+        if (h->Hc_ok && h->frag_ok && gpad::cpanel_supported(n, m)) {  // condensed batches on the MFMA pipe
+            if ((rc = h->Hfrag.ensure(gpad::cpanel_frag_bytes(n, m)))) return rc;
+            HIP_TRY(gpad::launch_pack_cpanel((const float*)h->Hc.p, n, m, h->ldm, h->Hfrag.p, h->stream));
+            h->Hfrag_ok = true;
         }
     }
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -608,6 +618,7 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
     a.num_cus = h->num_cus;
     a.tune = &h->tune;
     a.Hc = h->Hc_ok ? (const float*)h->Hc.p : nullptr;
+    a.hfrag = h->Hfrag_ok ? h->Hfrag.p : nullptr;
     a.strideH = d.shared ? 0 : (long long)m * h->ldm;
     int kernel = d.kernel;
     const bool prev_phased = h->last_phased;  // the previous launch's counts are still in `iters`
@@ -652,6 +663,16 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
             return GPAD_OK;
         }
         if (kernel == GPAD_KERNEL_CONDENSED) {  // opt-in condensed operator (gpad_condensed.hip)
+            // shared-matrix batches beyond ~2 per CU on the MFMA pipe (gpad_cpanel.hip), else one
+            // workgroup per instance
+            if (d.shared && batch > 2 * h->num_cus && h->tune.cpanel) {
+                e = gpad::launch_cpanel(a, h->stream, &ok);
+                if (e != hipSuccess) return fail(GPAD_ERR_HIP, std::string("condensed panel: ") + hipGetErrorString(e));
+                if (ok) {
+                    *kernel_out = kernel;
+                    return GPAD_OK;
+                }
+            }
             e = gpad::launch_condensed(a, h->stream, &ok);
             if (e != hipSuccess) return fail(GPAD_ERR_HIP, std::string("condensed: ") + hipGetErrorString(e));
             if (!ok) return fail(GPAD_ERR_UNSUPPORTED, "condensed kernel: bind with dims.kernel = CONDENSED");

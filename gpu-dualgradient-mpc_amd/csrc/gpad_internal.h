@@ -30,6 +30,7 @@ struct Tuning {
     int flat_a_lds = 1;       // GPAD_OPT_FLAT_A_LDS: flat fragment image in LDS when it fits
     int finish_solo = -1;     // GPAD_OPT_FINISH_SOLO: duo workgroups running one instance each
                               // (the longest-predicted survivors; -1: default)
+    int cpanel = 1;           // GPAD_OPT_CONDENSED_PANEL: condensed batches on the MFMA panels
 };
 
 // Rounding margin of the Algorithm 1 decisions, in units of max_i(|chain_i| + |pD_i|): a test
@@ -90,6 +91,7 @@ struct SolveArgs {
     const struct PanelPlan* plan;  // panel phases: host-side plan from the previous solve (or null)
     const Tuning* tune;    // host-side tuning options (never null on a launch from gpad_host.cpp)
     const float* Hc;       // condensed operator H = G_L (-ML), k-major [m][ldm] (gpad_condensed.hip)
+    const void* hfrag;     // H in the panel fragment layout (gpad_cpanel.hip), or null
     long long strideH;     // elements between consecutive instances' H images (0 = shared)
 };
 
@@ -111,6 +113,12 @@ bool condensed_supported(int n, int m);
 hipError_t launch_condense(const float* GLt, const float* MGt, int n, int m, int ldn, int ldm, int nmats,
                            long long strideA, long long strideB, float* Ht, hipStream_t s);
 hipError_t launch_condensed(const SolveArgs<float>& a, hipStream_t s, bool* supported);
+// ... and on the MFMA pipe for shared-matrix batches (gpad_cpanel.hip; T = ceil(max(n,m)/16) <= 16,
+// needs the panel fragment images and the H image)
+bool cpanel_supported(int n, int m);
+size_t cpanel_frag_bytes(int n, int m);
+hipError_t launch_pack_cpanel(const float* Ht, int n, int m, int ldm, void* hfrag, hipStream_t s);
+hipError_t launch_cpanel(const SolveArgs<float>& a, hipStream_t s, bool* supported);
 hipError_t launch_panel(const SolveArgs<float>& a, hipStream_t s, bool* supported);
 size_t panel_frag_bytes(int n, int m, int batch);
 size_t panel_work_bytes(int m, int batch);

@@ -187,3 +187,42 @@ def test_condensed_guards(gpu):
         with pytest.raises(gpad_mpc.GpadError):
             s.run(np.zeros(40, np.float32), np.zeros(60, np.float32), M, g, 20, 0.0, scaled=True, theta=th,
                   beta=be)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nm", [(200, 200), (40, 180), (37, 53), (64, 208), (130, 100), (1, 5), (224, 200)])
+@pytest.mark.parametrize("N,tol", [(60, 0.0), (4000, 1e-4)])
+def test_condensed_panel_batch_bitexact(gpu, oracle, nm, N, tol):
+    """Shared-matrix batches beyond 2 per CU run the condensed operator on the MFMA panels
+    (gpad_cpanel.hip: one H GEMM per iteration; the tests' direct -ML / G_L GEMMs); a ragged
+    last group, warm-started y, a separate e_V; every checked instance bit-exact with its own
+    condensed oracle solve, iteration count included.  The same batch with the panels switched
+    off (one workgroup per instance) must give the same bits."""
+    import gpad_mpc
+    from gpad_mpc import _lib, problems
+    n, m = nm
+    B = 2 * 256 + 37
+    qp = problems.synthetic_qp(n, m, batch=B, seed=23)
+    ML, G = _f32(qp.ML), _f32(qp.G)
+    M, g, L = _f32(qp.M).reshape(B, n), _f32(qp.g).reshape(B, m), np.float32(qp.L)
+    y0 = (0.02 * np.random.default_rng(8).random((B, m))).astype(np.float32)
+    res = {}
+    for cp in (1, 0):
+        z = np.zeros((B, n), np.float32)
+        y = y0.copy()
+        it = np.zeros(B, np.int32)
+        with gpad_mpc.GpadSolver(0) as s:
+            s.setup(ML, G, float(L), n=n, m=m, batch=B, kernel=_lib.KERNEL_CONDENSED, tol_gap=2e-4)
+            s.set_option("condensed_panel", cp)
+            st = s.run(z, y, M, g, N, tol, iters=it)
+        assert st["kernel"] == "condensed"
+        res[cp] = (z, y, it)
+    z, y, it = res[1]
+    np.testing.assert_array_equal(it, res[0][2])
+    np.testing.assert_array_equal(z, res[0][0])
+    np.testing.assert_array_equal(y, res[0][1])
+    for b in list(range(0, B, 13)) + [B - 1]:
+        zo, yo, ito, _ = oracle.solve_condensed_f32(np.zeros(n), y0[b], ML, M[b], G, g[b], N, L, tol, tol_gap=2e-4)
+        assert it[b] == ito, b
+        assert_bitexact(z[b], zo, f"{b} z")
+        assert_bitexact(y[b], yo, f"{b} y")
