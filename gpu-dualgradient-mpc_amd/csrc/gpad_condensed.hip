@@ -72,7 +72,12 @@ __global__ __launch_bounds__(kCondMaxThreads) void gpad_condensed_kernel(SolveAr
     __shared__ float x_l[kCondMaxThreads];                     // its z / zhat (len n)
     __shared__ CheckSlot slots[2][kCondMaxThreads / 64];       // test, decision
 
-    const int tid = threadIdx.x, b = blockIdx.x;
+    // finisher mode (after a condensed panel phase): this block takes survivor blockIdx.x of the
+    // list, resumes at iteration v_begin from the carried y, w, wbar, u
+    const bool fin = a.count_in != nullptr;
+    if (fin && (int)blockIdx.x >= __builtin_amdgcn_readfirstlane(*a.count_in)) return;
+    const int tid = threadIdx.x, b = fin ? a.idx_in[blockIdx.x] : blockIdx.x;
+    const int v0 = fin ? a.v_begin : 0;
     const int n = a.n, m = a.m, nwaves = blockDim.x >> 6;
     const bool live = tid < m;  // constraint row / row of H
     const bool prow = tid < n;  // primal row
@@ -95,8 +100,15 @@ __global__ __launch_bounds__(kCondMaxThreads) void gpad_condensed_kernel(SolveAr
         ci = -chain_gmem(GLt, a.ldm, tid, v_l, n);  // c = -G_L gP
         yi = yg[tid];
         pdi = (float)(a.gscale * (double)a.g[(size_t)b * a.ld_g + tid]);
-        wi = __builtin_fmaf(a.beta[0], yi - yi, yi);  // 8a at v = 0 (y_{-1} = y_0)
-        w_l[0][tid] = wi;
+        if (fin) {
+            const size_t o = (size_t)b * m + tid;
+            wi = a.wc[o];
+            wbar = a.wbc[o];
+            ui = a.uc[o];
+        } else {
+            wi = __builtin_fmaf(a.beta[0], yi - yi, yi);  // 8a at v = 0 (y_{-1} = y_0)
+        }
+        w_l[v0 & 1][tid] = wi;
     }
     __syncthreads();
 
@@ -116,8 +128,8 @@ __global__ __launch_bounds__(kCondMaxThreads) void gpad_condensed_kernel(SolveAr
     const bool use_tol = a.tol > 0.0;
     int it = 0, done = 0;
     float zout = 0.0f;
-    float th = a.theta[0], bn = a.beta[1];
-    for (int v = 0; v < a.N; ++v) {
+    float th = a.theta[v0], bn = a.beta[v0 + 1];
+    for (int v = v0; v < a.N; ++v) {
         const float th_next = a.theta[v + 1], bn_next = a.beta[v + 2];
         const bool chk = use_tol && ((v + 1) % a.check_every) == 0;
         const float acc = chain_regs<KH, KH>(r, w_l[v & 1]);  // (uniform: DPP reads every lane)
@@ -215,7 +227,7 @@ hipError_t launch_condensed(const SolveArgs<float>& a, hipStream_t s, bool* supp
     *supported = condensed_supported(a.n, a.m) && a.Hc != nullptr;
     if (!*supported) return hipSuccess;
     const int rows = a.n > a.m ? a.n : a.m;
-    const dim3 grid(a.batch), block(64 * ((rows + 63) / 64));
+    const dim3 grid(a.batch), block(64 * ((rows + 63) / 64));  // finisher: blocks past the count exit
     switch (res_bucket(a.m)) {
         case 32: hipLaunchKernelGGL((gpad_condensed_kernel<32>), grid, block, 0, s, a); break;
         case 64: hipLaunchKernelGGL((gpad_condensed_kernel<64>), grid, block, 0, s, a); break;

@@ -29,7 +29,6 @@ typedef float cf32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned cu32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kCpWaves = 8;   // 2 per SIMD: 256 VGPRs each (no spills)
-constexpr int kCpPanels = 2;  // panels per group (32 instances)
 
 __device__ __forceinline__ int cp_pi16(int rho) { return 4 * (rho & 3) + (rho >> 2); }
 
@@ -112,21 +111,22 @@ struct CpSlot {  // per unit: per column partials of the Algorithm-1 test
     double gap[16];
 };
 
-template <int T>
+template <int T, int P>
 struct CpLds {
-    float4 W[kCpPanels][2][T * 64];  // w, double buffered (B of the H GEMM)
-    float4 WB[kCpPanels][T * 64];    // wbar (B of test A's direct GEMM and of the final z)
-    float4 Z[kCpPanels][T * 64];     // X = -ML V - g_P (B of the direct G_L GEMM); g_P at group start
-    float4 PD[kCpPanels][T * 64];    // p_D of the unit rows (parked in LDS, not VGPRs)
-    CpSlot slots[kCpPanels * T];
+    float4 W[P][2][T * 64];  // w, double buffered (B of the H GEMM)
+    float4 WB[P][T * 64];    // wbar (B of test A's direct GEMM and of the final z)
+    float4 Z[P][T * 64];     // X = -ML V - g_P (B of the direct G_L GEMM); g_P at group start
+    float4 PD[P][T * 64];    // p_D of the unit rows (parked in LDS, not VGPRs)
+    CpSlot slots[P * T];
 };
 constexpr int kCpMaxTiles = 14;  // LDS: 6 T KiB per panel + slots <= 160 KiB
 
-template <int T>
+template <int T, int P>
 __global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<float> a) {
+    constexpr int kCpPanels = P;  // panels per group: 2 (32 instances) or 1 (16)
     constexpr int NU = (T + kCpWaves - 1) / kCpWaves;  // tiles per wave (each for both panels)
     extern __shared__ __attribute__((aligned(16))) float4 cp_lds[];
-    CpLds<T>* Lp = reinterpret_cast<CpLds<T>*>(cp_lds);
+    CpLds<T, P>* Lp = reinterpret_cast<CpLds<T, P>*>(cp_lds);
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int j = lane >> 4, c = lane & 15;
@@ -142,7 +142,8 @@ __global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<fl
     auto tile = [&](int q) { return w + kCpWaves * q; };  // tile of unit q (valid when < T)
     // acc[pp] = A (tile of unit q) x B_pp, both panels sharing each A fragment
     auto gemm = [&](int q, __amdgpu_buffer_rsrc_t PA, const float4* B0, const float4* B1, cf32x4 (&acc)[2]) {
-        cp_gemm_dual<T>(PA, B0, B1, tile(q) * 1024 + lane * 16, lane, acc[0], acc[1]);
+        if constexpr (P == 2) cp_gemm_dual<T>(PA, B0, B1, tile(q) * 1024 + lane * 16, lane, acc[0], acc[1]);
+        else acc[0] = cp_gemm<T>(PA, B0, tile(q) * 1024 + lane * 16, lane);
     };
 
     for (int grp = blockIdx.x; grp < groups; grp += gridDim.x) {
@@ -184,7 +185,7 @@ __global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<fl
 #pragma unroll
         for (int q = 0; q < NU; ++q) {  // c = -G_L g_P (one chain per row, as orc_chain)
             cf32x4 acc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
-            if (tile(q) < T) gemm(q, PA2, Lp->Z[0], Lp->Z[1], acc);
+            if (tile(q) < T) gemm(q, PA2, Lp->Z[0], Lp->Z[P - 1], acc);
 #pragma unroll
             for (int pp = 0; pp < kCpPanels; ++pp)
 #pragma unroll
@@ -295,7 +296,7 @@ __global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<fl
                     const int t = tile(q), fo = t * 64 + lane;
                     if (t < T) {
                         cf32x4 acc[2];
-                        gemm(q, PH, Lp->W[0][rb], Lp->W[1][rb], acc);
+                        gemm(q, PH, Lp->W[0][rb], Lp->W[P - 1][rb], acc);
 #pragma unroll
                         for (int pp = 0; pp < kCpPanels; ++pp) {
                             const bool act = (live >> (16 * pp + c)) & 1u;
@@ -341,7 +342,7 @@ __global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<fl
             th = th_next;
             bn = bn_next;
             __syncthreads();
-            if (!chk && v < N) continue;
+            if (!chk && v < a.v_end) continue;
 
             if (chk) {
                 double vz, vh, mh, wm, gq;
@@ -354,13 +355,13 @@ __global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<fl
                 const unsigned mB = (unsigned)__ballot(nomB);
                 __syncthreads();  // every wave's slot reads precede the rewrites below
                 if (mA) {  // (A): decide on G_L z of z = -ML wbar - g_P, u reset to it
-                    direct_x(Lp->WB[0], Lp->WB[1]);
+                    direct_x(Lp->WB[0], Lp->WB[P - 1]);
 #pragma unroll
                     for (int q = 0; q < NU; ++q) {
                         const int t = tile(q);
                         if (t < T) {
                             cf32x4 gz[2];
-                            gemm(q, PA2, Lp->Z[0], Lp->Z[1], gz);
+                            gemm(q, PA2, Lp->Z[0], Lp->Z[P - 1], gz);
 #pragma unroll
                             for (int pp = 0; pp < kCpPanels; ++pp) {
                                 const bool nom = (mA >> (16 * pp + c)) & 1u;
@@ -390,13 +391,13 @@ __global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<fl
                 }
                 const unsigned mBv = mB & live;
                 if (mBv) {  // (B): decide on G_L zhat of zhat = -ML w - g_P (w: W[rb], intact)
-                    direct_x(Lp->W[0][rb], Lp->W[1][rb]);
+                    direct_x(Lp->W[0][rb], Lp->W[P - 1][rb]);
 #pragma unroll
                     for (int q = 0; q < NU; ++q) {
                         const int t = tile(q);
                         if (t < T) {
                             cf32x4 gh[2];
-                            gemm(q, PA2, Lp->Z[0], Lp->Z[1], gh);
+                            gemm(q, PA2, Lp->Z[0], Lp->Z[P - 1], gh);
 #pragma unroll
                             for (int pp = 0; pp < kCpPanels; ++pp) {
                                 const bool nom = (mBv >> (16 * pp + c)) & 1u;
@@ -431,12 +432,49 @@ __global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<fl
             }
             if (v >= N && live) {  // the rest ran out of iterations: z = -ML wbar - g_P
                 __syncthreads();
-                direct_x(Lp->WB[0], Lp->WB[1]);
+                direct_x(Lp->WB[0], Lp->WB[P - 1]);
                 put_out(live, v, 0);
                 live = 0u;
             }
-            if (live == 0u) break;
+            if (live == 0u || v >= a.v_end) break;
             if (chk) __syncthreads();  // the tests' LDS traffic precedes the next iteration
+        }
+        // ---- phase end (a.v_end < N): park the survivors for the latency finisher ----------------
+        // y in place; the next w, wbar and u in the carry buffers; ids appended to idx_out
+        if (a.v_end < N && live) {
+#pragma unroll
+            for (int q = 0; q < NU; ++q) {
+                const int t = tile(q), fo = t * 64 + lane;
+                if (t < T) {
+#pragma unroll
+                    for (int pp = 0; pp < kCpPanels; ++pp) {
+                        const int bit = 16 * pp + c;
+                        if ((live >> bit) & 1u) {
+                            const size_t col = (size_t)(k0 + bit);
+                            const float4 w4 = Lp->W[pp][v & 1][fo], b4 = Lp->WB[pp][fo];
+                            const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+                            const float bv[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                const int i = 16 * t + 4 * r + j;
+                                if (i < m) {
+                                    a.y[col * m + i] = y[q][pp][r];
+                                    a.wc[col * m + i] = wv[r];
+                                    a.wbc[col * m + i] = bv[r];
+                                    a.uc[col * m + i] = u[q][pp][r];
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+            if (w == 0) {
+                const bool mine = lane < 32 && ((live >> (lane & 31)) & 1u);
+                int base = 0;
+                if (lane == 0) base = atomicAdd(a.count_out, (int)__popc(live));
+                base = __shfl(base, 0, 64);
+                if (mine) a.idx_out[base + (int)__popc(live & ((1u << lane) - 1u))] = k0 + lane;
+            }
         }
         __syncthreads();  // the next group reuses the LDS arrays
     }
@@ -460,16 +498,58 @@ hipError_t launch_pack_cpanel(const float* Ht, int n, int m, int ldm, void* hfra
     return hipGetLastError();
 }
 
+template <int T, int P>
+static hipError_t launch_cp_tp(const SolveArgs<float>& a, hipStream_t s) {
+    const size_t lds = sizeof(CpLds<T, P>);
+    hipError_t e = hipFuncSetAttribute((const void*)gpad_cpanel_kernel<T, P>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    const int groups = (a.batch + 16 * P - 1) / (16 * P);
+    const int grid = groups < a.num_cus ? groups : a.num_cus;
+    hipLaunchKernelGGL((gpad_cpanel_kernel<T, P>), dim3(grid), dim3(64 * kCpWaves), lds, s, a);
+    return hipGetLastError();
+}
+// two panels per group once single panels outnumber the CUs (a group's iteration is latency-bound:
+// one panel per CU halves it while the batch fits one round)
+static int cp_panels(int batch, int num_cus) { return batch > 16 * num_cus ? 2 : 1; }
 template <int T>
 static hipError_t launch_cp_t(const SolveArgs<float>& a, hipStream_t s) {
-    const size_t lds = sizeof(CpLds<T>);
-    hipError_t e = hipFuncSetAttribute((const void*)gpad_cpanel_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds);
-    if (e != hipSuccess) return e;
-    const int groups = (a.batch + 16 * kCpPanels - 1) / (16 * kCpPanels);
-    const int grid = groups < a.num_cus ? groups : a.num_cus;
-    hipLaunchKernelGGL((gpad_cpanel_kernel<T>), dim3(grid), dim3(64 * kCpWaves), lds, s, a);
-    return hipGetLastError();
+    return cp_panels(a.batch, a.num_cus) == 2 ? launch_cp_tp<T, 2>(a, s) : launch_cp_tp<T, 1>(a, s);
+}
+
+// Takeover iteration of an eps-mode condensed batch from the previous solve's counts: the panels
+// cost ~t_p per iteration while any group is alive (each CU runs its group at the group's latency),
+// the latency kernel ~t_l per iteration per survivor with one survivor per CU at a time; pick the
+// test iteration v minimising  v t_p + max(max_i (it_i - v) t_l, sum_i (it_i - v)+ t_l / CUs).
+// t_p: the busiest SIMD's MFMA chains (2 panels, ceil(T/8) tiles per wave, 2 waves per SIMD) at
+// 32 cycles per MFMA + ~1.5 us; t_l: m dependent DPP steps at ~6 cycles + ~0.2 us (2.2-2.4 GHz).
+int cpanel_takeover(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus) {
+    const int T = ((n > m ? n : m) + 15) / 16;
+    const int tiles_simd = (T + 3) / 4;
+    const double tp = cp_panels(batch, num_cus) * tiles_simd * T * 4 * 32 / 2.2e3 + 1.5;  // us
+    const double tl = m * 6.0 / 2.4e3 + 0.2;
+    const int K = check_every > 0 ? check_every : 10;
+    int mx = 0;
+    for (int b = 0; b < batch; ++b) mx = iters[b] > mx ? iters[b] : mx;
+    int best_v = N;
+    double best = 1e300;
+    for (int v = K; v <= mx && v < N; v += K) {
+        long long rem = 0;
+        int rmax = 0;
+        for (int b = 0; b < batch; ++b)
+            if (iters[b] > v) {
+                rem += iters[b] - v;
+                rmax = iters[b] - v > rmax ? iters[b] - v : rmax;
+            }
+        const double fin = rmax * tl > rem * tl / num_cus ? rmax * tl : rem * tl / num_cus;
+        const double cost = v * tp + fin;
+        if (cost < best) {
+            best = cost;
+            best_v = v;
+        }
+    }
+    const double none = mx * tp;  // panels to the end
+    return none <= best ? 0 : best_v;
 }
 
 hipError_t launch_cpanel(const SolveArgs<float>& a, hipStream_t s, bool* supported) {

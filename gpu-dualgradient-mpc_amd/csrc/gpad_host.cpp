@@ -122,6 +122,7 @@ struct gpad_handle_s {
     gpad::PanelPlan plan;
     unsigned long long plan_key = 0;    // fingerprint of the counts the plan was built from
     int flat_vpred = 0;                 // flat panels: last iteration of the previous phased solve
+    int cond_vtake = 0;                 // condensed batches: finisher takeover iteration (0: none)
     // asynchronous runs (no stats): the counts of each phased solve are copied to pinned host
     // memory behind it; the next run re-plans from them once that copy has landed, so a pipeline
     // of back-to-back solves plans from its most recent completed solve without a host sync
@@ -296,6 +297,7 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
     h->shadow_ok = false;
     h->plan.nph = 0;
     h->flat_vpred = 0;
+    h->cond_vtake = 0;
     h->plan_pending = false;
     h->last_phased = false;
     h->dims = *d;
@@ -398,6 +400,7 @@ int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* d, int n_u, const float*
     h->shadow_ok = false;
     h->plan.nph = 0;
     h->flat_vpred = 0;
+    h->cond_vtake = 0;
     h->plan_pending = false;
     h->last_phased = false;
     h->dims = *d;
@@ -488,6 +491,11 @@ static int ensure_schedule(gpad_handle_t h, int N, const void* theta_in, const v
 // The phase plan is a pure function of the per-instance counts (and the shape): rebuild it only
 // when they changed (repeated solves of one batch skip the DP).
 static void update_plan(gpad_handle_t h, const int* counts, int batch, int N) {
+    if (h->dims.kernel == GPAD_KERNEL_CONDENSED) {
+        h->cond_vtake = gpad::cpanel_takeover(counts, batch, h->dims.n, h->dims.m, N, h->dims.check_every,
+                                              h->num_cus);
+        return;
+    }
     if (h->flat) {  // the flat panels' phases run to the previous solve's last iteration
         int mx = 0;
         for (int b = 0; b < batch; ++b) mx = std::max(mx, counts[b]);
@@ -666,9 +674,42 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
             // shared-matrix batches beyond ~2 per CU on the MFMA pipe (gpad_cpanel.hip), else one
             // workgroup per instance
             if (d.shared && batch > 2 * h->num_cus && h->tune.cpanel) {
+                // eps mode: the panels run to the takeover iteration planned from the previous
+                // solve's counts (GPAD_OPT_PHASE_LEN forces one), the survivors finish one per
+                // workgroup on the latency kernel from the carried state
+                int vtake = N;
+                if (tol > 0.0 && h->tune.phased)
+                    vtake = h->tune.phase_len > 0 ? h->tune.phase_len : (h->cond_vtake > 0 ? h->cond_vtake : N);
+                a.v_begin = 0;
+                a.v_end = vtake < N ? vtake : N;
+                if (a.v_end < N) {
+                    const size_t pw = gpad::panel_work_bytes(m, batch) + sizeof(float) * (size_t)batch * m;
+                    int rc = h->pwork.ensure(pw);
+                    if (rc) return rc;
+                    int* idx0 = (int*)h->pwork.p;
+                    int* counts = idx0 + 2 * (size_t)batch;
+                    a.wc = reinterpret_cast<float*>(counts + 2 * gpad::kPanelMaxPhases);
+                    a.uc = a.wc + (size_t)batch * m;
+                    a.wbc = a.uc + (size_t)batch * m;
+                    a.idx_out = idx0;
+                    a.count_out = counts;
+                    HIP_TRY(hipMemsetAsync(counts, 0, sizeof(int), h->stream));
+                }
                 e = gpad::launch_cpanel(a, h->stream, &ok);
                 if (e != hipSuccess) return fail(GPAD_ERR_HIP, std::string("condensed panel: ") + hipGetErrorString(e));
                 if (ok) {
+                    if (a.v_end < N) {  // the survivors on the latency kernel
+                        gpad::SolveArgs<T> f = a;
+                        f.v_begin = a.v_end;
+                        f.v_end = N;
+                        f.idx_in = a.idx_out;
+                        f.count_in = a.count_out;
+                        bool ok2 = false;
+                        e = gpad::launch_condensed(f, h->stream, &ok2);
+                        if (e != hipSuccess || !ok2)
+                            return fail(GPAD_ERR_HIP, std::string("condensed finisher: ") + hipGetErrorString(e));
+                    }
+                    h->last_phased = tol > 0.0 && h->tune.phased;  // its counts plan the next takeover
                     *kernel_out = kernel;
                     return GPAD_OK;
                 }

@@ -80,6 +80,7 @@ struct SolveArgs {
     int* count_out;        // ... and counted here (device)
     float* wc;             // carried w  [batch][m]
     float* uc;             // carried u = G_L z [batch][m]
+    float* wbc;            // condensed phases: carried wbar [batch][m]
     int fin_thresh;        // survivors <= this: the resident finisher takes them (0: none)
     int* qctr;             // duo kernel: zeroed device counter of its work-list claims
     int fin_solo;          // duo kernel: workgroups that run the list's first (longest) entries
@@ -119,6 +120,7 @@ bool cpanel_supported(int n, int m);
 size_t cpanel_frag_bytes(int n, int m);
 hipError_t launch_pack_cpanel(const float* Ht, int n, int m, int ldm, void* hfrag, hipStream_t s);
 hipError_t launch_cpanel(const SolveArgs<float>& a, hipStream_t s, bool* supported);
+int cpanel_takeover(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus);
 hipError_t launch_panel(const SolveArgs<float>& a, hipStream_t s, bool* supported);
 size_t panel_frag_bytes(int n, int m, int batch);
 size_t panel_work_bytes(int m, int batch);

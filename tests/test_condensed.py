@@ -196,8 +196,9 @@ def test_condensed_panel_batch_bitexact(gpu, oracle, nm, N, tol):
     """Shared-matrix batches beyond 2 per CU run the condensed operator on the MFMA panels
     (gpad_cpanel.hip: one H GEMM per iteration; the tests' direct -ML / G_L GEMMs); a ragged
     last group, warm-started y, a separate e_V; every checked instance bit-exact with its own
-    condensed oracle solve, iteration count included.  The same batch with the panels switched
-    off (one workgroup per instance) must give the same bits."""
+    condensed oracle solve, iteration count included.  The same bits with the panels switched off
+    (one workgroup per instance), with forced finisher takeovers (the survivors' y, w, wbar, u
+    carried to the latency kernel) and with the takeover planned from a previous solve."""
     import gpad_mpc
     from gpad_mpc import _lib, problems
     n, m = nm
@@ -207,20 +208,27 @@ def test_condensed_panel_batch_bitexact(gpu, oracle, nm, N, tol):
     M, g, L = _f32(qp.M).reshape(B, n), _f32(qp.g).reshape(B, m), np.float32(qp.L)
     y0 = (0.02 * np.random.default_rng(8).random((B, m))).astype(np.float32)
     res = {}
-    for cp in (1, 0):
+    # panels to the end / panels to a forced takeover then the latency finisher (eps mode) /
+    # no panels (one workgroup per instance); then a second solve planned from the first's counts
+    for key, opts in (("panel", dict(phased=0)), ("take30", dict(phase_len=30)), ("take150", dict(phase_len=150)),
+                      ("latency", dict(condensed_panel=0)), ("planned", {})):
         z = np.zeros((B, n), np.float32)
         y = y0.copy()
         it = np.zeros(B, np.int32)
         with gpad_mpc.GpadSolver(0) as s:
             s.setup(ML, G, float(L), n=n, m=m, batch=B, kernel=_lib.KERNEL_CONDENSED, tol_gap=2e-4)
-            s.set_option("condensed_panel", cp)
-            st = s.run(z, y, M, g, N, tol, iters=it)
+            s.set_options(**opts)
+            for _ in range(2 if key == "planned" else 1):
+                z[:] = 0.0
+                y[:] = y0
+                st = s.run(z, y, M, g, N, tol, iters=it)
         assert st["kernel"] == "condensed"
-        res[cp] = (z, y, it)
-    z, y, it = res[1]
-    np.testing.assert_array_equal(it, res[0][2])
-    np.testing.assert_array_equal(z, res[0][0])
-    np.testing.assert_array_equal(y, res[0][1])
+        res[key] = (z, y, it)
+    z, y, it = res["panel"]
+    for key in res:
+        np.testing.assert_array_equal(res[key][2], it, err_msg=key)
+        np.testing.assert_array_equal(res[key][0], z, err_msg=key)
+        np.testing.assert_array_equal(res[key][1], y, err_msg=key)
     for b in list(range(0, B, 13)) + [B - 1]:
         zo, yo, ito, _ = oracle.solve_condensed_f32(np.zeros(n), y0[b], ML, M[b], G, g[b], N, L, tol, tol_gap=2e-4)
         assert it[b] == ito, b
