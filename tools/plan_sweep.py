@@ -15,7 +15,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def one(reps):
+def one(reps, fresh=False):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "gpu-dualgradient-mpc_amd"))
     import numpy as np
@@ -30,6 +30,8 @@ def one(reps):
     ML, G, L, M, g = bench.make_shard(n, m, B, 0)
     f32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)  # noqa: E731
     dML, dG, dM, dg = f32(ML), f32(G), f32(M), f32(g)
+    # --fresh: a new batch every solve (bench.make_stream, the bench's honest mode)
+    stream = [(f32(a), f32(b)) for a, b in bench.make_stream(n, m, B, reps + 2, 0)] if fresh else None
     z = torch.zeros(B, n, device=dev)
     y = torch.zeros(B, m, device=dev)
     s = gpad_mpc.GpadSolver(0)
@@ -38,13 +40,14 @@ def one(reps):
     for i in range(reps + 2):
         z.zero_()
         y.zero_()
-        s.run(z, y, dM, dg, 5000, 1e-4, stats=False)
+        Mv, gv = stream[i] if fresh else (dM, dg)
+        s.run(z, y, Mv, gv, 5000, 1e-4, stats=False)
         st = s.last_stats()
         if i >= 2:
             t.append(st["kernel_ms"])
     t.sort()
     plan = s.phase_plan()
-    print(json.dumps({"env": {k: v for k, v in os.environ.items() if k.startswith("GPAD_")},
+    print(json.dumps({"fresh": fresh, "env": {k: v for k, v in os.environ.items() if k.startswith("GPAD_")},
                       "best_ms": round(t[0], 4), "median_ms": round(t[len(t) // 2], 4),
                       "plan": plan}), flush=True)
 
@@ -53,18 +56,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--one", action="store_true")
+    ap.add_argument("--fresh", action="store_true")
     args = ap.parse_args()
     if args.one:
-        one(args.reps)
+        one(args.reps, args.fresh)
         return
-    settings = [{}]
+    settings = [{}, {"GPAD_FINISHER": "resident"}, {"GPAD_NO_LPT": "1"}, {"GPAD_FINISH_SOLO": "256"}]
     for ph in (20, 40, 80, 260):
         for fin in (512, 1024, 2048, 4096):
             settings.append({"GPAD_PANEL_NOPLAN": "1", "GPAD_PANEL_PHASE": str(ph), "GPAD_FINISH_THRESH": str(fin)})
     for st in settings:
         env = {k: v for k, v in os.environ.items() if not k.startswith("GPAD_")}
         env.update(st)
-        subprocess.run([sys.executable, __file__, "--one", "--reps", str(args.reps)], env=env, check=True)
+        cmd = [sys.executable, __file__, "--one", "--reps", str(args.reps)] + (["--fresh"] if args.fresh else [])
+        subprocess.run(cmd, env=env, check=True)
 
 
 if __name__ == "__main__":
