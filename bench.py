@@ -326,7 +326,7 @@ def c3_leg(dev, n=200, m=200, batch=4096, reps=3, max_iters=5000, tol=1e-4, ref=
     return out
 
 
-def condensed_leg(dev, n=200, m=200, batch=8192, reps=3, max_iters=5000, tol=1e-4):
+def condensed_leg(dev, n=200, m=200, batch=8192, reps=3, max_iters=5000, tol=1e-4, cpanel=1):
     """The headline C4 shard on the opt-in condensed operator (GPAD_KERNEL_CONDENSED: one H GEMM
     per iteration on the MFMA panels, gpad_cpanel.hip; NOT the reference's arithmetic) beside the
     bit-exact panels on the same inputs: rate, the norm-wise distance of z* from the bit-exact z*,
@@ -345,6 +345,8 @@ def condensed_leg(dev, n=200, m=200, batch=8192, reps=3, max_iters=5000, tol=1e-
         y = torch.zeros(batch, m, device=dev)
         with gpad_mpc.GpadSolver(dev.index or 0, stream=torch.cuda.current_stream(dev).cuda_stream) as s:
             s.setup(dML, dG, float(np.float32(L)), n=n, m=m, batch=batch, shared=True, check_every=10, kernel=kern)
+            if kern == _lib.KERNEL_CONDENSED:
+                s.set_option("condensed_panel", cpanel)
             best, st = 1e30, None
             for _ in range(reps + 2):
                 r = s.run(z.zero_(), y.zero_(), dM, dg, max_iters, tol)

@@ -7,12 +7,14 @@
 // side (wbar = theta-average of w, so z = -ML wbar - g_P is formed only when Algorithm 1 decides
 // and at the end): half the MFMA work at n = m, one barrier per iteration.
 //
-// Layout: an 8-wave workgroup owns a group of two panels (32 instances) at a time, grid-stride
-// over groups.  Row tile t of BOTH panels belongs to wave t mod 8 (one A stream feeds two
-// interleaved MFMA chains; T = 13: 4, 3, 3, 3 tiles per SIMD), its row state (y, u, c of 16 rows x
-// 32 columns) in the wave's registers (256 VGPRs at 2 waves per SIMD), p_D and wbar in LDS.  W is double buffered in LDS in
-// MFMA B-fragment order (the accumulator layout of the fragment-permuted A images equals the
-// next B fragment, see gpad_panel.hip), so an iteration reads W[v & 1] and writes W[(v+1) & 1].
+// Layout: a workgroup owns a group of P panels (P = 2: 32 instances beyond 16 per CU, else 1) at a
+// time, grid-stride over groups.  Default: 16 waves (4 per SIMD), wave w owns the single
+// (panel, row tile) chains w and w + 16 (T = 13, P = 2: 7,7,6,6 chains per SIMD); option: 8 waves
+// owning tiles w, w + 8 of all P panels, both panels' chains on one A stream.  A unit's row state
+// (y, u, c) stays in the owning wave's registers, p_D and wbar in LDS.  W is double buffered in
+// LDS in MFMA B-fragment order (the accumulator layout of the fragment-permuted A images equals
+// the next B fragment, see gpad_panel.hip), so an iteration reads W[v & 1] and writes
+// W[(v+1) & 1]: one barrier per iteration.
 // The direct GEMMs of a decided test -- X = (-ML) V (V = wbar for test A, w for test B) and
 // G_L X -- reuse the panel kernels' packed -ML / G_L images; the H image is packed the same way.
 // Bit-exact against oracle/gpad_oracle.c orc_solve_condensed_f32 (each output row one
@@ -28,7 +30,6 @@ namespace gpad {
 typedef float cf32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned cu32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kCpWaves = 8;   // 2 per SIMD: 256 VGPRs each (no spills)
 
 __device__ __forceinline__ int cp_pi16(int rho) { return 4 * (rho & 3) + (rho >> 2); }
 
@@ -121,10 +122,16 @@ struct CpLds {
 };
 constexpr int kCpMaxTiles = 14;  // LDS: 6 T KiB per panel + slots <= 160 KiB
 
-template <int T, int P>
-__global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<float> a) {
+// S = false: WV = 8 waves, wave w owns tiles w, w+8 of ALL P panels (one A stream per tile);
+// S = true:  WV = 16 waves, wave w owns the single (panel, tile) units w, w+16 (unit u = panel
+// u / T, tile u % T), 4 waves per SIMD, every chain its own A stream -- at P = 2, T = 13 the SIMDs
+// carry 7,7,6,6 chains instead of 8,6,6,6.
+template <int T, int P, bool S>
+__global__ __launch_bounds__(S ? 1024 : 512) void gpad_cpanel_kernel(SolveArgs<float> a) {
     constexpr int kCpPanels = P;  // panels per group: 2 (32 instances) or 1 (16)
-    constexpr int NU = (T + kCpWaves - 1) / kCpWaves;  // tiles per wave (each for both panels)
+    constexpr int WV = S ? 16 : 8;
+    constexpr int NU = S ? (P * T + WV - 1) / WV : (T + WV - 1) / WV;  // units per wave
+    constexpr int PU = S ? 1 : P;  // panels per unit
     extern __shared__ __attribute__((aligned(16))) float4 cp_lds[];
     CpLds<T, P>* Lp = reinterpret_cast<CpLds<T, P>*>(cp_lds);
     const int lane = threadIdx.x & 63;
@@ -139,10 +146,14 @@ __global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<fl
     const bool use_tol = a.tol > 0.0;
     const int count = a.batch;
     const int groups = (count + 16 * kCpPanels - 1) / (16 * kCpPanels);
-    auto tile = [&](int q) { return w + kCpWaves * q; };  // tile of unit q (valid when < T)
-    // acc[pp] = A (tile of unit q) x B_pp, both panels sharing each A fragment
+    auto uid = [&](int q) { return w + WV * q; };
+    auto tile = [&](int q) { return S ? uid(q) % T : uid(q); };
+    auto uvalid = [&](int q) { return S ? uid(q) < P * T : uid(q) < T; };
+    auto upan = [&](int q, int k) { return S ? uid(q) / T : k; };  // panel of slot k of unit q
+    // acc[k] = A (tile of unit q) x B of the unit's k-th panel (both panels share each A fragment)
     auto gemm = [&](int q, __amdgpu_buffer_rsrc_t PA, const float4* B0, const float4* B1, cf32x4 (&acc)[2]) {
-        if constexpr (P == 2) cp_gemm_dual<T>(PA, B0, B1, tile(q) * 1024 + lane * 16, lane, acc[0], acc[1]);
+        if constexpr (S) acc[0] = cp_gemm<T>(PA, upan(q, 0) ? B1 : B0, tile(q) * 1024 + lane * 16, lane);
+        else if constexpr (P == 2) cp_gemm_dual<T>(PA, B0, B1, tile(q) * 1024 + lane * 16, lane, acc[0], acc[1]);
         else acc[0] = cp_gemm<T>(PA, B0, tile(q) * 1024 + lane * 16, lane);
     };
 
@@ -154,26 +165,27 @@ __global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<fl
             live |= (left >= 16 ? 0xFFFFu : (left > 0 ? (1u << left) - 1u : 0u)) << (16 * pp);
         }
         // ---- unit state (y, u, c in registers; p_D, wbar, w in LDS); g_P into Z -----------------
-        float y[NU][2][4], u[NU][2][4], cv[NU][2][4];
+        float y[NU][PU][4], u[NU][PU][4], cv[NU][PU][4];
 #pragma unroll
         for (int q = 0; q < NU; ++q) {
             const int t = tile(q), fo = t * 64 + lane;
 #pragma unroll
-            for (int pp = 0; pp < kCpPanels; ++pp) {
+            for (int k = 0; k < PU; ++k) {
+                const int pp = upan(q, k);
                 const int col = k0 + 16 * pp + c;
-                const bool act = t < T && col < count;
+                const bool act = uvalid(q) && col < count;
                 float gp[4], wv[4], pdv[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int i = 16 * t + 4 * r + j;
                     const bool okm = act && i < m, okn = act && i < n;
-                    y[q][pp][r] = okm ? a.y[(size_t)col * m + i] : 0.0f;
+                    y[q][k][r] = okm ? a.y[(size_t)col * m + i] : 0.0f;
                     pdv[r] = okm ? (float)(a.gscale * (double)a.g[(size_t)col * a.ld_g + i]) : 0.0f;
                     gp[r] = okn ? a.gP[(size_t)col * a.ld_gP + i] : 0.0f;
-                    wv[r] = __builtin_fmaf(a.beta[0], y[q][pp][r] - y[q][pp][r], y[q][pp][r]);
-                    u[q][pp][r] = 0.0f;  // theta_0 = 1: u_0 = s whatever the seed
+                    wv[r] = __builtin_fmaf(a.beta[0], y[q][k][r] - y[q][k][r], y[q][k][r]);
+                    u[q][k][r] = 0.0f;  // theta_0 = 1: u_0 = s whatever the seed
                 }
-                if (t < T) {
+                if (uvalid(q)) {
                     Lp->Z[pp][fo] = make_float4(gp[0], gp[1], gp[2], gp[3]);
                     Lp->W[pp][0][fo] = make_float4(wv[0], wv[1], wv[2], wv[3]);
                     Lp->WB[pp][fo] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -185,11 +197,11 @@ __global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<fl
 #pragma unroll
         for (int q = 0; q < NU; ++q) {  // c = -G_L g_P (one chain per row, as orc_chain)
             cf32x4 acc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
-            if (tile(q) < T) gemm(q, PA2, Lp->Z[0], Lp->Z[P - 1], acc);
+            if (uvalid(q)) gemm(q, PA2, Lp->Z[0], Lp->Z[P - 1], acc);
 #pragma unroll
-            for (int pp = 0; pp < kCpPanels; ++pp)
+            for (int k = 0; k < PU; ++k)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) cv[q][pp][r] = -acc[pp][r];
+                for (int r = 0; r < 4; ++r) cv[q][k][r] = -acc[k][r];
         }
         __syncthreads();  // Z is rewritten by the tests
 
@@ -199,18 +211,19 @@ __global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<fl
 #pragma unroll
             for (int q = 0; q < NU; ++q) {
                 const int t = tile(q);
-                if (t < T) {
+                if (uvalid(q)) {
                     cf32x4 acc[2];
                     gemm(q, PA1, B0, B1, acc);
 #pragma unroll
-                    for (int pp = 0; pp < kCpPanels; ++pp) {
+                    for (int k = 0; k < PU; ++k) {
+                const int pp = upan(q, k);
                         const int col = k0 + 16 * pp + c;
                         float xo[4];
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             const int i = 16 * t + 4 * r + j;
                             const float gpi = (i < n && col < count) ? a.gP[(size_t)col * a.ld_gP + i] : 0.0f;
-                            xo[r] = i < n ? acc[pp][r] - gpi : 0.0f;  // seq_functions.cpp:61-62 order
+                            xo[r] = i < n ? acc[k][r] - gpi : 0.0f;  // seq_functions.cpp:61-62 order
                         }
                         Lp->Z[pp][t * 64 + lane] = make_float4(xo[0], xo[1], xo[2], xo[3]);
                     }
@@ -258,9 +271,10 @@ __global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<fl
 #pragma unroll
             for (int q = 0; q < NU; ++q) {
                 const int t = tile(q);
-                if (t < T) {
+                if (uvalid(q)) {
 #pragma unroll
-                    for (int pp = 0; pp < kCpPanels; ++pp) {
+                    for (int k = 0; k < PU; ++k) {
+                const int pp = upan(q, k);
                         const int bit = 16 * pp + c;
                         if ((done >> bit) & 1u) {
                             const size_t col = (size_t)(k0 + bit);
@@ -270,7 +284,7 @@ __global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<fl
                             for (int r = 0; r < 4; ++r) {
                                 const int i = 16 * t + 4 * r + j;
                                 if (i < n) a.z[col * n + i] = xo[r];
-                                if (i < m) a.y[col * m + i] = y[q][pp][r];
+                                if (i < m) a.y[col * m + i] = y[q][k][r];
                             }
                         }
                     }
@@ -294,11 +308,12 @@ __global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<fl
 #pragma unroll
                 for (int q = 0; q < NU; ++q) {
                     const int t = tile(q), fo = t * 64 + lane;
-                    if (t < T) {
+                    if (uvalid(q)) {
                         cf32x4 acc[2];
                         gemm(q, PH, Lp->W[0][rb], Lp->W[P - 1][rb], acc);
 #pragma unroll
-                        for (int pp = 0; pp < kCpPanels; ++pp) {
+                        for (int k = 0; k < PU; ++k) {
+                const int pp = upan(q, k);
                             const bool act = (live >> (16 * pp + c)) & 1u;
                             const float4 w4 = Lp->W[pp][rb][fo], b4 = Lp->WB[pp][fo], p4 = Lp->PD[pp][fo];
                             const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
@@ -309,19 +324,19 @@ __global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<fl
                             double gp = 0.0;
 #pragma unroll
                             for (int r = 0; r < 4; ++r) {
-                                const float sc = acc[pp][r] + cv[q][pp][r];  // G_L zhat, condensed
+                                const float sc = acc[k][r] + cv[q][k][r];  // G_L zhat, condensed
                                 wbn[r] = __builtin_fmaf(omt, wbv[r], th * wv[r]);
                                 const float sv = (wv[r] + pdv[r]) + sc;
                                 const float yp = (__builtin_fabsf(sv) + sv) * 0.5f;
-                                const float un2 = __builtin_fmaf(omt, u[q][pp][r], th * sc);
-                                wn[r] = __builtin_fmaf(bn, yp - y[q][pp][r], yp);
+                                const float un2 = __builtin_fmaf(omt, u[q][k][r], th * sc);
+                                wn[r] = __builtin_fmaf(bn, yp - y[q][k][r], yp);
                                 if (act) {
-                                    if (use_tol) u[q][pp][r] = un2;
-                                    y[q][pp][r] = yp;
+                                    if (use_tol) u[q][k][r] = un2;
+                                    y[q][k][r] = yp;
                                 }
                                 if (chk && act && 16 * t + 4 * r + j < m) {
                                     const float tt = sc + pdv[r];
-                                    vz = fmaxf(vz, u[q][pp][r] + pdv[r]);
+                                    vz = fmaxf(vz, u[q][k][r] + pdv[r]);
                                     vh = fmaxf(vh, tt);
                                     mh = fmaxf(mh, __builtin_fabsf(sc) + __builtin_fabsf(pdv[r]));
                                     wm = fminf(wm, wv[r]);
@@ -359,21 +374,22 @@ __global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<fl
 #pragma unroll
                     for (int q = 0; q < NU; ++q) {
                         const int t = tile(q);
-                        if (t < T) {
+                        if (uvalid(q)) {
                             cf32x4 gz[2];
                             gemm(q, PA2, Lp->Z[0], Lp->Z[P - 1], gz);
 #pragma unroll
-                            for (int pp = 0; pp < kCpPanels; ++pp) {
+                            for (int k = 0; k < PU; ++k) {
+                const int pp = upan(q, k);
                                 const bool nom = (mA >> (16 * pp + c)) & 1u;
                                 const float4 p4 = Lp->PD[pp][t * 64 + lane];
                                 const float pdv[4] = {p4.x, p4.y, p4.z, p4.w};
                                 float vc = -INFINITY, mc = 0.0f;
 #pragma unroll
                                 for (int r = 0; r < 4; ++r) {
-                                    if (nom) u[q][pp][r] = gz[pp][r];
+                                    if (nom) u[q][k][r] = gz[k][r];
                                     if (nom && 16 * t + 4 * r + j < m) {
-                                        vc = fmaxf(vc, gz[pp][r] + pdv[r]);
-                                        mc = fmaxf(mc, __builtin_fabsf(gz[pp][r]) + __builtin_fabsf(pdv[r]));
+                                        vc = fmaxf(vc, gz[k][r] + pdv[r]);
+                                        mc = fmaxf(mc, __builtin_fabsf(gz[k][r]) + __builtin_fabsf(pdv[r]));
                                     }
                                 }
                                 publish(pp, t, vc, -INFINITY, mc, INFINITY, 0.0);
@@ -395,11 +411,12 @@ __global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<fl
 #pragma unroll
                     for (int q = 0; q < NU; ++q) {
                         const int t = tile(q);
-                        if (t < T) {
+                        if (uvalid(q)) {
                             cf32x4 gh[2];
                             gemm(q, PA2, Lp->Z[0], Lp->Z[P - 1], gh);
 #pragma unroll
-                            for (int pp = 0; pp < kCpPanels; ++pp) {
+                            for (int k = 0; k < PU; ++k) {
+                const int pp = upan(q, k);
                                 const bool nom = (mBv >> (16 * pp + c)) & 1u;
                                 const float4 w4 = Lp->W[pp][rb][t * 64 + lane], p4 = Lp->PD[pp][t * 64 + lane];
                                 const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
@@ -409,9 +426,9 @@ __global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<fl
 #pragma unroll
                                 for (int r = 0; r < 4; ++r) {
                                     if (nom && 16 * t + 4 * r + j < m) {
-                                        const float tt = gh[pp][r] + pdv[r];
+                                        const float tt = gh[k][r] + pdv[r];
                                         vh2 = fmaxf(vh2, tt);
-                                        mh2 = fmaxf(mh2, __builtin_fabsf(gh[pp][r]) + __builtin_fabsf(pdv[r]));
+                                        mh2 = fmaxf(mh2, __builtin_fabsf(gh[k][r]) + __builtin_fabsf(pdv[r]));
                                         wm2 = fminf(wm2, wv[r]);
                                         gp2 -= (double)wv[r] * (double)tt;
                                     }
@@ -445,9 +462,10 @@ __global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<fl
 #pragma unroll
             for (int q = 0; q < NU; ++q) {
                 const int t = tile(q), fo = t * 64 + lane;
-                if (t < T) {
+                if (uvalid(q)) {
 #pragma unroll
-                    for (int pp = 0; pp < kCpPanels; ++pp) {
+                    for (int k = 0; k < PU; ++k) {
+                const int pp = upan(q, k);
                         const int bit = 16 * pp + c;
                         if ((live >> bit) & 1u) {
                             const size_t col = (size_t)(k0 + bit);
@@ -458,10 +476,10 @@ __global__ __launch_bounds__(64 * kCpWaves) void gpad_cpanel_kernel(SolveArgs<fl
                             for (int r = 0; r < 4; ++r) {
                                 const int i = 16 * t + 4 * r + j;
                                 if (i < m) {
-                                    a.y[col * m + i] = y[q][pp][r];
+                                    a.y[col * m + i] = y[q][k][r];
                                     a.wc[col * m + i] = wv[r];
                                     a.wbc[col * m + i] = bv[r];
-                                    a.uc[col * m + i] = u[q][pp][r];
+                                    a.uc[col * m + i] = u[q][k][r];
                                 }
                             }
                         }
@@ -498,16 +516,23 @@ hipError_t launch_pack_cpanel(const float* Ht, int n, int m, int ldm, void* hfra
     return hipGetLastError();
 }
 
-template <int T, int P>
-static hipError_t launch_cp_tp(const SolveArgs<float>& a, hipStream_t s) {
+template <int T, int P, bool S>
+static hipError_t launch_cp_tps(const SolveArgs<float>& a, hipStream_t s) {
     const size_t lds = sizeof(CpLds<T, P>);
-    hipError_t e = hipFuncSetAttribute((const void*)gpad_cpanel_kernel<T, P>,
+    hipError_t e = hipFuncSetAttribute((const void*)gpad_cpanel_kernel<T, P, S>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     const int groups = (a.batch + 16 * P - 1) / (16 * P);
     const int grid = groups < a.num_cus ? groups : a.num_cus;
-    hipLaunchKernelGGL((gpad_cpanel_kernel<T, P>), dim3(grid), dim3(64 * kCpWaves), lds, s, a);
+    hipLaunchKernelGGL((gpad_cpanel_kernel<T, P, S>), dim3(grid), dim3(S ? 1024 : 512), lds, s, a);
     return hipGetLastError();
+}
+template <int T, int P>
+static hipError_t launch_cp_tp(const SolveArgs<float>& a, hipStream_t s) {
+    // 16 waves dealing single (panel, tile) chains (default: 2.43 vs 2.68 ms at the C4 shard, 1.47 vs
+    // 1.50 ms at 4096, profiles/r02_condensed_panel_waves.txt); GPAD_OPT_CONDENSED_PANEL 2: 8 waves
+    // with both panels' chains on one A stream
+    return (a.tune && a.tune->cpanel == 2) ? launch_cp_tps<T, P, false>(a, s) : launch_cp_tps<T, P, true>(a, s);
 }
 // two panels per group once single panels outnumber the CUs (a group's iteration is latency-bound:
 // one panel per CU halves it while the batch fits one round)
@@ -521,12 +546,12 @@ static hipError_t launch_cp_t(const SolveArgs<float>& a, hipStream_t s) {
 // cost ~t_p per iteration while any group is alive (each CU runs its group at the group's latency),
 // the latency kernel ~t_l per iteration per survivor with one survivor per CU at a time; pick the
 // test iteration v minimising  v t_p + max(max_i (it_i - v) t_l, sum_i (it_i - v)+ t_l / CUs).
-// t_p: the busiest SIMD's MFMA chains (2 panels, ceil(T/8) tiles per wave, 2 waves per SIMD) at
-// 32 cycles per MFMA + ~1.5 us; t_l: m dependent DPP steps at ~6 cycles + ~0.2 us (2.2-2.4 GHz).
+// t_p: the busiest SIMD's MFMA chains (ceil(P T / 4)) at 32 cycles per MFMA + ~1.5 us; t_l: m
+// dependent DPP steps at ~6 cycles + ~0.2 us (2.2-2.4 GHz).
 int cpanel_takeover(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus) {
     const int T = ((n > m ? n : m) + 15) / 16;
-    const int tiles_simd = (T + 3) / 4;
-    const double tp = cp_panels(batch, num_cus) * tiles_simd * T * 4 * 32 / 2.2e3 + 1.5;  // us
+    const int chains_simd = (cp_panels(batch, num_cus) * T + 3) / 4;  // 16-wave single-chain deal
+    const double tp = chains_simd * T * 4 * 32 / 2.2e3 + 1.5;  // us
     const double tl = m * 6.0 / 2.4e3 + 0.2;
     const int K = check_every > 0 ? check_every : 10;
     int mx = 0;

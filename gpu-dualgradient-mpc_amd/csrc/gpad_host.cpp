@@ -249,7 +249,7 @@ int gpad_set_option(gpad_handle_t h, int option, int value) {
             return set(t.flat_waves, 0, 16, def.flat_waves);
         case GPAD_OPT_FLAT_A_LDS: return set(t.flat_a_lds, 0, 1, def.flat_a_lds);
         case GPAD_OPT_FINISH_SOLO: return set(t.finish_solo, 0, big, def.finish_solo);
-        case GPAD_OPT_CONDENSED_PANEL: return set(t.cpanel, 0, 1, def.cpanel);
+        case GPAD_OPT_CONDENSED_PANEL: return set(t.cpanel, 0, 2, def.cpanel);
         default: return fail(GPAD_ERR_INVALID, "gpad_set_option: unknown option");
     }
 }

@@ -316,7 +316,8 @@ int gpad_schedule(int N, int kind, double* theta, double* beta);
 #define GPAD_OPT_FLAT_A_LDS 12     /* 1: flat fragment image staged in LDS when it fits (default)  */
 #define GPAD_OPT_FINISH_SOLO 13    /* finisher CUs that run one (the longest) survivor each         */
 #define GPAD_OPT_CONDENSED_PANEL 14 /* 1: GPAD_KERNEL_CONDENSED batches (shared, > 2/CU) on the MFMA
-                                     * panels (default); 0: one workgroup per instance             */
+                                     * panels, 16 waves (default); 2: 8 waves sharing A streams;
+                                     * 0: one workgroup per instance                               */
 int gpad_set_option(gpad_handle_t h, int option, int value);
 
 /* Synchronise the handle's stream (for callers using device memory + async runs). */
