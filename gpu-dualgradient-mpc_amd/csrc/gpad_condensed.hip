@@ -72,22 +72,28 @@ __global__ __launch_bounds__(kCondMaxThreads) void gpad_condensed_kernel(SolveAr
     __shared__ float x_l[kCondMaxThreads];                     // its z / zhat (len n)
     __shared__ CheckSlot slots[2][kCondMaxThreads / 64];       // test, decision
 
-    // finisher mode (after a condensed panel phase): this block takes survivor blockIdx.x of the
-    // list, resumes at iteration v_begin from the carried y, w, wbar, u
+    // finisher mode (after a condensed panel phase): a persistent grid walks the survivor list,
+    // each instance resumed at iteration v_begin from the carried y, w, wbar, u, c; shared H rows
+    // are loaded once per workgroup
     const bool fin = a.count_in != nullptr;
-    if (fin && (int)blockIdx.x >= __builtin_amdgcn_readfirstlane(*a.count_in)) return;
-    const int tid = threadIdx.x, b = fin ? a.idx_in[blockIdx.x] : blockIdx.x;
+    const int count = fin ? __builtin_amdgcn_readfirstlane(*a.count_in) : a.batch;
+    const int tid = threadIdx.x;
     const int v0 = fin ? a.v_begin : 0;
     const int n = a.n, m = a.m, nwaves = blockDim.x >> 6;
     const bool live = tid < m;  // constraint row / row of H
     const bool prow = tid < n;  // primal row
+    float r[KH];  // row tid of H, zero-padded (padded steps are fma(0, 0, acc) = acc)
+    bool have_r = false;
+    for (int kk = blockIdx.x; kk < count; kk += gridDim.x) {
+    const int b = fin ? a.idx_in[kk] : kk;
     const float* __restrict__ MGt = a.MGt + b * a.strideA;
     const float* __restrict__ GLt = a.GLt + b * a.strideB;
-    const float* __restrict__ Ht = a.Hc + b * a.strideH;
-
-    float r[KH];  // row tid of H, zero-padded (padded steps are fma(0, 0, acc) = acc)
+    if (!have_r || a.strideH != 0) {
+        const float* __restrict__ Ht = a.Hc + b * a.strideH;
 #pragma unroll
-    for (int k = 0; k < KH; ++k) r[k] = (live && k < m) ? Ht[(size_t)k * a.ldm + tid] : 0.0f;
+        for (int k = 0; k < KH; ++k) r[k] = (live && k < m) ? Ht[(size_t)k * a.ldm + tid] : 0.0f;
+        have_r = true;
+    }
 
     float* zg = a.z + (size_t)b * n;
     float* yg = a.y + (size_t)b * m;
@@ -97,7 +103,7 @@ __global__ __launch_bounds__(kCondMaxThreads) void gpad_condensed_kernel(SolveAr
     if (prow) v_l[tid] = gpi;
     __syncthreads();
     if (live) {
-        ci = -chain_gmem(GLt, a.ldm, tid, v_l, n);  // c = -G_L gP
+        ci = fin ? a.cc[(size_t)b * m + tid] : -chain_gmem(GLt, a.ldm, tid, v_l, n);  // c = -G_L gP
         yi = yg[tid];
         pdi = (float)(a.gscale * (double)a.g[(size_t)b * a.ld_g + tid]);
         if (fin) {
@@ -211,6 +217,8 @@ __global__ __launch_bounds__(kCondMaxThreads) void gpad_condensed_kernel(SolveAr
         a.iters[b] = it;
         a.conv[b] = done;
     }
+    __syncthreads();  // the next instance reuses the LDS vectors
+    }
 }
 
 bool condensed_supported(int n, int m) { return m <= kResidentMaxRow && n <= kCondMaxThreads && n > 0 && m > 0; }
@@ -227,7 +235,10 @@ hipError_t launch_condensed(const SolveArgs<float>& a, hipStream_t s, bool* supp
     *supported = condensed_supported(a.n, a.m) && a.Hc != nullptr;
     if (!*supported) return hipSuccess;
     const int rows = a.n > a.m ? a.n : a.m;
-    const dim3 grid(a.batch), block(64 * ((rows + 63) / 64));  // finisher: blocks past the count exit
+    // one instance per workgroup; as the finisher a persistent grid over the survivor list (a grid
+    // of `batch` mostly empty workgroups cost ~0.1 ms of dispatch alone)
+    const int g = a.count_in ? (a.batch < 2 * a.num_cus ? a.batch : 2 * a.num_cus) : a.batch;
+    const dim3 grid(g), block(64 * ((rows + 63) / 64));
     switch (res_bucket(a.m)) {
         case 32: hipLaunchKernelGGL((gpad_condensed_kernel<32>), grid, block, 0, s, a); break;
         case 64: hipLaunchKernelGGL((gpad_condensed_kernel<64>), grid, block, 0, s, a); break;

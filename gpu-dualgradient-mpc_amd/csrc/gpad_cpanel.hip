@@ -480,6 +480,7 @@ __global__ __launch_bounds__(S ? 1024 : 512) void gpad_cpanel_kernel(SolveArgs<f
                                     a.wc[col * m + i] = wv[r];
                                     a.wbc[col * m + i] = bv[r];
                                     a.uc[col * m + i] = u[q][k][r];
+                                    a.cc[col * m + i] = cv[q][k][r];
                                 }
                             }
                         }
@@ -543,16 +544,18 @@ static hipError_t launch_cp_t(const SolveArgs<float>& a, hipStream_t s) {
 }
 
 // Takeover iteration of an eps-mode condensed batch from the previous solve's counts: the panels
-// cost ~t_p per iteration while any group is alive (each CU runs its group at the group's latency),
-// the latency kernel ~t_l per iteration per survivor with one survivor per CU at a time; pick the
-// test iteration v minimising  v t_p + max(max_i (it_i - v) t_l, sum_i (it_i - v)+ t_l / CUs).
-// t_p: the busiest SIMD's MFMA chains (ceil(P T / 4)) at 32 cycles per MFMA + ~1.5 us; t_l: m
-// dependent DPP steps at ~6 cycles + ~0.2 us (2.2-2.4 GHz).
+// cost ~t_p per iteration while any group is alive (each CU runs its group at the group's
+// latency); the latency kernel finishes the survivors two per CU (DPP issue shared, ~1.6 us per
+// iteration each) after a ~25 us start (H rows and c per workgroup).  Pick the test iteration v
+// minimising  v t_p + 25 + max(max_i (it_i - v) 1.6, sum_i (it_i - v)+ 1.6 / CUs)  [us].
+// t_p: the busiest SIMD's MFMA chains (ceil(P T / 4)) at 32 cycles per MFMA + ~1.5 us.  Calibrated
+// on the C4 shard (tools/cond_take_sweep.py, profiles/r02_cond_takeover.jsonl: t_p = 6.8 us;
+// forced takeovers 260 / 280 / 300 / 330 / none: 2.69 / 2.32 / 2.25 / 2.37 / 2.58 ms).
 int cpanel_takeover(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus) {
     const int T = ((n > m ? n : m) + 15) / 16;
     const int chains_simd = (cp_panels(batch, num_cus) * T + 3) / 4;  // 16-wave single-chain deal
-    const double tp = chains_simd * T * 4 * 32 / 2.2e3 + 1.5;  // us
-    const double tl = m * 6.0 / 2.4e3 + 0.2;
+    const double tp = chains_simd * T * 4 * 32 / 2.2e3 + 1.5;        // us
+    const double tl = 1.6 * (m / 200.0 > 0.25 ? m / 200.0 : 0.25);   // us per iteration, 2 per CU
     const int K = check_every > 0 ? check_every : 10;
     int mx = 0;
     for (int b = 0; b < batch; ++b) mx = iters[b] > mx ? iters[b] : mx;
@@ -566,8 +569,8 @@ int cpanel_takeover(const int* iters, int batch, int n, int m, int N, int check_
                 rem += iters[b] - v;
                 rmax = iters[b] - v > rmax ? iters[b] - v : rmax;
             }
-        const double fin = rmax * tl > rem * tl / num_cus ? rmax * tl : rem * tl / num_cus;
-        const double cost = v * tp + fin;
+        const double lat = rmax * tl, thr = rem * tl / num_cus;
+        const double cost = v * tp + 25.0 + (lat > thr ? lat : thr);
         if (cost < best) {
             best = cost;
             best_v = v;

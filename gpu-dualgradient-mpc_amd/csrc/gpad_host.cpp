@@ -683,7 +683,7 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
                 a.v_begin = 0;
                 a.v_end = vtake < N ? vtake : N;
                 if (a.v_end < N) {
-                    const size_t pw = gpad::panel_work_bytes(m, batch) + sizeof(float) * (size_t)batch * m;
+                    const size_t pw = gpad::panel_work_bytes(m, batch) + 2 * sizeof(float) * (size_t)batch * m;
                     int rc = h->pwork.ensure(pw);
                     if (rc) return rc;
                     int* idx0 = (int*)h->pwork.p;
@@ -691,6 +691,7 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
                     a.wc = reinterpret_cast<float*>(counts + 2 * gpad::kPanelMaxPhases);
                     a.uc = a.wc + (size_t)batch * m;
                     a.wbc = a.uc + (size_t)batch * m;
+                    a.cc = a.wbc + (size_t)batch * m;
                     a.idx_out = idx0;
                     a.count_out = counts;
                     HIP_TRY(hipMemsetAsync(counts, 0, sizeof(int), h->stream));

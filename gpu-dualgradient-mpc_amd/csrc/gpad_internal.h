@@ -81,6 +81,7 @@ struct SolveArgs {
     float* wc;             // carried w  [batch][m]
     float* uc;             // carried u = G_L z [batch][m]
     float* wbc;            // condensed phases: carried wbar [batch][m]
+    float* cc;             // condensed phases: carried c = -G_L g_P [batch][m]
     int fin_thresh;        // survivors <= this: the resident finisher takes them (0: none)
     int* qctr;             // duo kernel: zeroed device counter of its work-list claims
     int fin_solo;          // duo kernel: workgroups that run the list's first (longest) entries
