@@ -326,7 +326,7 @@ def c3_leg(dev, n=200, m=200, batch=4096, reps=3, max_iters=5000, tol=1e-4, ref=
     return out
 
 
-def condensed_leg(dev, n=200, m=200, batch=8192, reps=3, max_iters=5000, tol=1e-4, cpanel=1):
+def condensed_leg(dev, n=200, m=200, batch=8192, reps=6, max_iters=5000, tol=1e-4, cpanel=1):
     """The headline C4 shard on the opt-in condensed operator (GPAD_KERNEL_CONDENSED: one H GEMM
     per iteration on the MFMA panels, gpad_cpanel.hip; NOT the reference's arithmetic) beside the
     bit-exact panels on the same inputs: rate, the norm-wise distance of z* from the bit-exact z*,
