@@ -235,3 +235,28 @@ def test_condensed_panel_batch_bitexact(gpu, oracle, nm, N, tol):
         assert it[b] == ito, b
         assert_bitexact(z[b], zo, f"{b} z")
         assert_bitexact(y[b], yo, f"{b} y")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [1, 600])
+def test_condensed_through_gpad_solve(gpu, oracle, B):
+    """The north-star symbol gpad_solve with dims.kernel = GPAD_KERNEL_CONDENSED (host pointers,
+    one cached handle): the latency kernel at B = 1, the condensed panels at B = 600 (> 2 per CU),
+    each instance bit-exact with its condensed oracle solve; a repeated call (cache hit) too."""
+    from test_boundary import c_solve
+    from gpad_mpc import _lib, problems
+    n, m = 120, 150
+    qp = problems.synthetic_qp(n, m, batch=B, seed=31)
+    ML, G = _f32(qp.ML), _f32(qp.G)
+    M, g, L = _f32(qp.M).reshape(B, n), _f32(qp.g).reshape(B, m), np.float32(qp.L)
+    for rep in range(2):
+        Z = np.zeros((B, n), np.float32)
+        Y = np.zeros((B, m), np.float32)
+        it = np.zeros(B, np.int32)
+        st = c_solve(Z, Y, ML, M, G, g, 3000, L, 1e-4, batch=B, kernel=_lib.KERNEL_CONDENSED, iters=it)
+        assert st.kernel == _lib.KERNEL_CONDENSED
+        for b in list(range(0, B, 97)) + [B - 1]:
+            zo, yo, ito, _ = oracle.solve_condensed_f32(np.zeros(n), np.zeros(m), ML, M[b], G, g[b], 3000, L, 1e-4)
+            assert it[b] == ito, (rep, b)
+            assert_bitexact(Z[b], zo, f"{rep} z[{b}]")
+            assert_bitexact(Y[b], yo, f"{rep} y[{b}]")
