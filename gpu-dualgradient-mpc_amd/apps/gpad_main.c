@@ -15,6 +15,11 @@
  *               library's own theta/beta schedule (the same recursion as the file's tables)
  *   --repeat R: one-shot only: call gpad_solve R more times on the same inputs and print the
  *               mean wall time per call ("solve_us", host clock around each synchronous call)
+ *   --scenarios B [--devices D | --devices a,b,c]: a battery-scenario batch of B instances of the
+ *               file's problem (shared ML, G; instance b's g_P scaled by 1 + 1e-3 ((31 b + i) mod 17))
+ *               solved over D devices (default: every visible one) with gpad_solve_sharded -- the
+ *               main.cu-shaped C caller using all GPUs of a node, no Python; prints the batch's
+ *               iteration total, converged count, wall ms and an FNV-1a hash of the z*, y* bits
  * Output: "n_u N m", "iterations", "kernel_ms", then "z" and "y" lines with %.9g values.
  */
 #define _POSIX_C_SOURCE 199309L
@@ -36,7 +41,8 @@ int main(int argc, char** argv) {
         return 2;
     }
     const char* path = argv[1];
-    int layout = GPAD_FILE_ROWMAJOR, N_v = 100, device = 0, one_shot = 0, repeat = 0;
+    int layout = GPAD_FILE_ROWMAJOR, N_v = 100, device = 0, one_shot = 0, repeat = 0, scenarios = 0;
+    int devs[64], ndev = 0;
     double tol = 0.0;
     for (int a = 2; a < argc; a++) {
         if (!strcmp(argv[a], "--flipped")) layout = GPAD_FILE_FLIPPED;
@@ -45,6 +51,19 @@ int main(int argc, char** argv) {
         else if (!strcmp(argv[a], "--device") && a + 1 < argc) device = atoi(argv[++a]);
         else if (!strcmp(argv[a], "--one-shot")) one_shot = 1;
         else if (!strcmp(argv[a], "--repeat") && a + 1 < argc) repeat = atoi(argv[++a]);
+        else if (!strcmp(argv[a], "--scenarios") && a + 1 < argc) scenarios = atoi(argv[++a]);
+        else if (!strcmp(argv[a], "--devices") && a + 1 < argc) {
+            const char* s = argv[++a];
+            if (!strchr(s, ',')) {  /* a count: devices 0 .. D-1 */
+                ndev = atoi(s);
+                for (int k = 0; k < ndev && k < 64; k++) devs[k] = k;
+            } else {                 /* an explicit list (may repeat a device) */
+                for (char* p = (char*)s; *p && ndev < 64;) {
+                    devs[ndev++] = (int)strtol(p, &p, 10);
+                    if (*p == ',') p++;
+                }
+            }
+        }
         else {
             fprintf(stderr, "gpad_main: unknown argument %s\n", argv[a]);
             return 2;
@@ -78,6 +97,58 @@ int main(int argc, char** argv) {
     memset(&st, 0, sizeof(st));
     int ret = 0;
     double solve_us = -1.0;
+    if (scenarios > 0) {  /* the scenario batch over several devices (gpad_solve_sharded) */
+        if (ndev <= 0) {
+            ndev = gpad_device_count();
+            if (ndev <= 0) return die(ndev < 0 ? ndev : GPAD_ERR_NO_DEVICE, "device count");
+            if (ndev > 64) ndev = 64;
+            for (int k = 0; k < ndev; k++) devs[k] = k;
+        }
+        const int B = scenarios;
+        const size_t nm = (size_t)n * m;
+        float* ML = (float*)malloc(sizeof(float) * nm);
+        float* G = (float*)malloc(sizeof(float) * nm);
+        float* M = (float*)malloc(sizeof(float) * (size_t)B * n);
+        float* g = (float*)malloc(sizeof(float) * (size_t)B * m);
+        float* Z = (float*)calloc((size_t)B * n, sizeof(float));
+        float* Y = (float*)calloc((size_t)B * m, sizeof(float));
+        for (size_t k = 0; k < nm; k++) {
+            ML[k] = -f.M_G[k];
+            G[k] = (float)((double)f.L * (double)f.G_L[k]);
+        }
+        for (int b = 0; b < B; b++) {
+            for (int i = 0; i < n; i++)
+                M[(size_t)b * n + i] = (float)((double)f.g_P[i] * (1.0 + 1e-3 * (double)((31 * b + i) % 17)));
+            for (int i = 0; i < m; i++) g[(size_t)b * m + i] = (float)(-(double)f.L * (double)f.p_D[i]);
+        }
+        d.batch = B;
+        struct timespec t0, t1;
+        clock_gettime(CLOCK_MONOTONIC, &t0);
+        rc = gpad_solve_sharded(ndev, devs, Z, Y, ML, M, G, g, N_v, (double)f.L, tol, &d, &st);
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        if (rc) ret = die(rc, "gpad_solve_sharded");
+        else {
+            unsigned long long hsh = 1469598103934665603ull;
+            const unsigned char* pz = (const unsigned char*)Z;
+            const unsigned char* py = (const unsigned char*)Y;
+            for (size_t k = 0; k < sizeof(float) * (size_t)B * n; k++) hsh = (hsh ^ pz[k]) * 1099511628211ull;
+            for (size_t k = 0; k < sizeof(float) * (size_t)B * m; k++) hsh = (hsh ^ py[k]) * 1099511628211ull;
+            printf("scenarios %d devices %d\n", B, ndev);
+            printf("total_iterations %lld converged %d\n", st.total_iterations, st.converged);
+            printf("wall_ms %.3f\n", (double)(t1.tv_sec - t0.tv_sec) * 1e3 + (double)(t1.tv_nsec - t0.tv_nsec) * 1e-6);
+            printf("hash %016llx\n", hsh);
+        }
+        free(ML);
+        free(G);
+        free(M);
+        free(g);
+        free(Z);
+        free(Y);
+        gpad_datafile_free(&f);
+        free(z);
+        free(y);
+        return ret;
+    }
     if (one_shot) {
         /* the unscaled problem: ML = -M_G, G = L G_L, g = -L p_D (acceldualgrad.m:20-23 undone) */
         const size_t nm = (size_t)n * m;

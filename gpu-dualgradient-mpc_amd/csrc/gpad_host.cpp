@@ -145,7 +145,13 @@ struct gpad_handle_s {
 
 extern "C" {
 
-const char* gpad_version(void) { return "gpad-mi355x 0.1 (gfx950)"; }
+const char* gpad_version(void) { return "gpad-mi355x 0.2 (gfx950)"; }
+
+int gpad_device_count(void) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) return fail(GPAD_ERR_NO_DEVICE, "gpad_device_count: no HIP runtime");
+    return count;
+}
 
 const char* gpad_strerror(int status) {
     switch (status) {

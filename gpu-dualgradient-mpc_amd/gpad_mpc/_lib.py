@@ -34,7 +34,7 @@ EXPORTS = [
     "gpad_setup_flat", "gpad_step2_primal_flat", "gpad_step4_project_flat", "gpad_precompute",
     "gpad_accumulate_iterations", "gpad_set_option",
     "gpad_group_create", "gpad_group_destroy", "gpad_group_transport", "gpad_group_setup", "gpad_group_run",
-    "gpad_solve_sharded",
+    "gpad_solve_sharded", "gpad_device_count",
 ]
 GROUP_RCCL, GROUP_PEER = 1, 2
 

@@ -89,6 +89,9 @@ typedef struct gpad_stats {
 typedef struct gpad_handle_s* gpad_handle_t;
 
 const char* gpad_version(void);
+/* HIP devices visible to this process (>= 0), or a negative GPAD_ERR_* status; the device list
+ * of gpad_group_create / gpad_solve_sharded (main.cu picks device 0, :116) */
+int gpad_device_count(void);
 const char* gpad_strerror(int status);
 const char* gpad_last_error(void); /* thread-local detail of the last failure */
 

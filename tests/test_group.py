@@ -98,3 +98,49 @@ def test_solve_sharded_one_shot(gpu, oracle, devices):
             assert it[b] == ito
             np.testing.assert_array_equal(Z[b], zo)
             np.testing.assert_array_equal(Y[b], yo)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tol", [0.0, 1e-4])
+def test_c_app_scenarios_over_devices(gpu, tol):
+    """apps/gpad_main.c --scenarios: the main.cu-shaped C caller solving a battery-scenario batch
+    over several devices with gpad_solve_sharded (no Python in the loop).  On this one-GPU box
+    the device lists 1, "0,0" and "0,0,0" shard the batch differently (peer copies when a device
+    repeats); every layout must give the bits of one handle solving the whole batch."""
+    import os
+    import subprocess
+
+    import gpad_mpc
+    from conftest import GOLDEN, PKG
+    from gpad_mpc import _lib, datafile
+    app = os.path.join(PKG, "gpad_mpc", "gpad_main")
+    path = os.path.join(GOLDEN, "datafile_battery_3x4.txt")
+    B, N = 600, 100
+    out = {}
+    for devs in ("1", "0,0", "0,0,0"):
+        r = subprocess.run([app, path, "--scenarios", str(B), "--devices", devs, "--iters", str(N), "--tol", str(tol)],
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        out[devs] = {ln.split()[0]: ln.split()[1:] for ln in r.stdout.splitlines()}
+    assert out["1"]["hash"] == out["0,0"]["hash"] == out["0,0,0"]["hash"]
+    assert out["1"]["total_iterations"] == out["0,0,0"]["total_iterations"]
+    # the same batch through one handle (gpad_mpc.solve), hashed the app's way (FNV-1a of z*, y*)
+    d = datafile.read(path, 0)
+    n, m = d.n, d.m
+    L = np.float32(d.L)
+    ML = (-d.M_G).astype(np.float32)
+    G = (np.float64(L) * d.G_L.astype(np.float64)).astype(np.float32)
+    g1 = (-np.float64(L) * d.p_D.astype(np.float64)).astype(np.float32)
+    bi, ii = np.meshgrid(np.arange(B), np.arange(n), indexing="ij")
+    M = (d.g_P.astype(np.float64)[None, :] * (1.0 + 1e-3 * ((31 * bi + ii) % 17))).astype(np.float32)
+    g = np.repeat(g1[None, :], B, axis=0)
+    Z = np.zeros((B, n), np.float32)
+    Y = np.zeros((B, m), np.float32)
+    with gpad_mpc.GpadSolver(0) as s:
+        s.setup(ML, G, float(L), n=n, m=m, batch=B, kernel=_lib.KERNEL_AUTO)
+        st = s.run(Z, Y, M, g, N, tol)
+    h = 1469598103934665603
+    for byte in Z.tobytes() + Y.tobytes():
+        h = ((h ^ byte) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    assert out["1"]["hash"][0] == f"{h:016x}"
+    assert int(out["1"]["total_iterations"][0]) == st["total_iterations"]
