@@ -304,7 +304,9 @@ int gpad_schedule(int N, int kind, double* theta, double* beta);
  * value GPAD_OPT_DEFAULT restores the default.  Returns GPAD_ERR_INVALID for an unknown option
  * or an out-of-range value. */
 #define GPAD_OPT_DEFAULT (-1)
-#define GPAD_OPT_PHASE_LEN 1       /* panel phase length in iterations (default 4 * check_every)   */
+#define GPAD_OPT_PHASE_LEN 1       /* panel phase length in iterations (default 4 * check_every);
+                                    * flat panels: the first phase; condensed batches: the finisher
+                                    * takeover iteration (default planned from the previous solve) */
 #define GPAD_OPT_FINISH_THRESH 2   /* survivors at which the finisher takes over (default 2/CU)    */
 #define GPAD_OPT_PLAN 3            /* 1: plan phases from the previous solve's counts (default)    */
 #define GPAD_OPT_PHASED 4          /* 1: phased compaction of tol > 0 panel solves (default; flat
