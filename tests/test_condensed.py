@@ -260,3 +260,38 @@ def test_condensed_through_gpad_solve(gpu, oracle, B):
             assert it[b] == ito, (rep, b)
             assert_bitexact(Z[b], zo, f"{rep} z[{b}]")
             assert_bitexact(Y[b], yo, f"{rep} y[{b}]")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [1, 3])
+@pytest.mark.parametrize("B,take", [(4097, 0), (4097, 25), (1100, 7)])
+def test_condensed_panel_check_every_and_takeover_edges(gpu, oracle, K, B, take):
+    """Edge cases of the condensed panels: a test every iteration (K = 1: slot rewrites in back-to-
+    back iterations) or every 3rd, two panels per group just past 16 per CU (B = 4097: a one-column
+    last group), takeovers that are not multiples of K, a takeover planned from a first solve;
+    checked instances bit-exact with the condensed oracle, iteration counts included."""
+    import gpad_mpc
+    from gpad_mpc import _lib, problems
+    n, m = 48, 64
+    qp = problems.synthetic_qp(n, m, batch=1, seed=41)
+    rng = np.random.default_rng(K * 1000 + B)
+    ML, G, L = _f32(qp.ML), _f32(qp.G), np.float32(qp.L)
+    M = (qp.M[None, :] * (1.0 + 0.3 * rng.normal(size=(B, 1)))).astype(np.float32)
+    g = (qp.g[None, :] + 0.2 * rng.random((B, m))).astype(np.float32)
+    z = np.zeros((B, n), np.float32)
+    y = np.zeros((B, m), np.float32)
+    it = np.zeros(B, np.int32)
+    with gpad_mpc.GpadSolver(0) as s:
+        s.setup(ML, G, float(L), n=n, m=m, batch=B, kernel=_lib.KERNEL_CONDENSED, check_every=K)
+        s.set_options(phase_len=take)
+        for _ in range(2):  # the second solve plans its takeover from the first (take = 0)
+            z[:] = 0.0
+            y[:] = 0.0
+            st = s.run(z, y, M, g, 3000, 1e-4, iters=it)
+    assert st["kernel"] == "condensed" and st["converged"] == B
+    for b in list(range(0, B, 211)) + [B - 1]:
+        zo, yo, ito, _ = oracle.solve_condensed_f32(np.zeros(n), np.zeros(m), ML, M[b], G, g[b], 3000, L, 1e-4,
+                                                    check_every=K)
+        assert it[b] == ito, b
+        assert_bitexact(z[b], zo, f"z[{b}]")
+        assert_bitexact(y[b], yo, f"y[{b}]")
