@@ -362,3 +362,33 @@ def test_flat_panel_grid_stride_large_batch(gpu, oracle):
         z, y, _, _ = oracle.solve_flat_f32(np.zeros(qp.n), np.zeros(qp.m), MGf32, GP[b], GLf32, PD[b], n_u, N, L32)
         np.testing.assert_array_equal(Zc[b], z, err_msg=f"z[{b}]")
         np.testing.assert_array_equal(Yc[b], y, err_msg=f"y[{b}]")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K,phase_len", [(1, 10), (3, 10), (7, 20)])
+def test_flat_panel_phased_check_every(gpu, oracle, K, phase_len):
+    """Flat-panel phases whose boundaries do not fall on the test grid (phase lengths that are not
+    multiples of K, K = 1 testing every iteration): every instance bit-exact with the oracle."""
+    from gpad_mpc import problems
+    import gpad_mpc
+    n_u, Nh, B = 4, 10, 16 * 5 + 3
+    qp = problems.battery_scenarios(n_u, Nh, B, seed=17)
+    MGf, GLf, L = problems.flatten_battery(qp, n_u, Nh)
+    f32 = lambda a: np.ascontiguousarray(np.asarray(a, np.float64).astype(np.float32))  # noqa: E731
+    L32 = np.float32(L)
+    MGf32, GLf32, GP = f32(MGf), f32(GLf), f32(qp.M)
+    PD = np.ascontiguousarray(oracle.scale_vec(f32(qp.g), L32))
+    s = gpad_mpc.GpadSolver(0)
+    s.setup_flat(MGf32, GLf32, float(L32), n_u=n_u, batch=B, kernel=gpad_mpc.KERNEL_PANEL, check_every=K)
+    s.set_options(phase_len=phase_len, phased=2)
+    Z = np.zeros((B, qp.n), np.float32)
+    Y = np.zeros((B, qp.m), np.float32)
+    it = np.zeros(B, np.int32)
+    st = s.run(Z, Y, GP, PD, 4000, 1e-4, scaled=True, iters=it)
+    assert st["kernel"] == "flat" and st["converged"] == B
+    for b in range(0, B, 3):
+        z, y, its, _ = oracle.solve_flat_f32(np.zeros(qp.n), np.zeros(qp.m), MGf32, GP[b], GLf32, PD[b], n_u, 4000,
+                                             L32, 1e-4, check_every=K)
+        assert it[b] == its, b
+        np.testing.assert_array_equal(Z[b], z, err_msg=f"z[{b}]")
+        np.testing.assert_array_equal(Y[b], y, err_msg=f"y[{b}]")
