@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <vector>
 
 #include "gpad_internal.h"
 
@@ -559,17 +560,18 @@ int cpanel_takeover(const int* iters, int batch, int n, int m, int N, int check_
     const int K = check_every > 0 ? check_every : 10;
     int mx = 0;
     for (int b = 0; b < batch; ++b) mx = iters[b] > mx ? iters[b] : mx;
+    // survivors and remaining work past every v from one histogram of the counts: O(batch + mx)
+    std::vector<long long> cnt((size_t)mx + 2, 0);
+    for (int b = 0; b < batch; ++b) cnt[iters[b] > 0 ? iters[b] : 0]++;
+    std::vector<long long> above((size_t)mx + 2, 0), rem((size_t)mx + 2, 0);  // #(it > v), sum (it - v)+
+    for (int v = mx - 1; v >= 0; --v) {
+        above[v] = above[v + 1] + cnt[v + 1];
+        rem[v] = rem[v + 1] + above[v];
+    }
     int best_v = N;
     double best = 1e300;
-    for (int v = K; v <= mx && v < N; v += K) {
-        long long rem = 0;
-        int rmax = 0;
-        for (int b = 0; b < batch; ++b)
-            if (iters[b] > v) {
-                rem += iters[b] - v;
-                rmax = iters[b] - v > rmax ? iters[b] - v : rmax;
-            }
-        const double lat = rmax * tl, thr = rem * tl / num_cus;
+    for (int v = K; v < mx && v < N; v += K) {
+        const double lat = (mx - v) * tl, thr = rem[v] * tl / num_cus;
         const double cost = v * tp + 25.0 + (lat > thr ? lat : thr);
         if (cost < best) {
             best = cost;
