@@ -111,6 +111,11 @@ struct PanelSlot {  // per wave (row tile), per instance partials of the Algorit
 // A is read with buffer loads: one 32-bit lane offset (t*1 KiB + lane*16 B) in a VGPR and the
 // k-block offset as a compile-time scalar, so the unrolled blocks cost no address registers.
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+// two rows per VALU instruction (v_pk_add / v_pk_mul / v_pk_fma_f32: IEEE f32 per element, the
+// same rounding as the scalar forms, so the epilogues stay bit-identical)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 f2(float a, float b) { return f32x2{a, b}; }
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 __device__ __forceinline__ float4 as_float4(u32x4 v) {
     return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
@@ -689,18 +694,22 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 else
                     acc[0] = acc[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
                 panel_a_prefetch<T, PD>(PA2, voff, ap);
+                float4 g4[Q];
+#pragma unroll
+                for (int q = 0; q < Q; ++q) g4[q] = L.Gp[p0 + q][slot];
+                const f32x2 th2 = f2(th, th), omt2 = f2(omt, omt);
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
-                    const float4 g4 = L.Gp[p0 + q][slot];
-                    const float gp[4] = {g4.x, g4.y, g4.z, g4.w};
-                    float zh[4];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        zh[r] = acc[q][r] - gp[r];
-                        const float zn = __builtin_fmaf(omt, z[q][r], th * zh[r]);
-                        if (act[q]) z[q][r] = zn;
-                    }
-                    L.Zh[p0 + q][slot] = make_float4(zh[0], zh[1], zh[2], zh[3]);
+                    const f32x2 h0 = f2(acc[q][0], acc[q][1]) - f2(g4[q].x, g4[q].y);
+                    const f32x2 h1 = f2(acc[q][2], acc[q][3]) - f2(g4[q].z, g4[q].w);
+                    L.Zh[p0 + q][slot] = make_float4(h0.x, h0.y, h1.x, h1.y);
+                    // 8c on every column (see the epilogue note below)
+                    const f32x2 z0 = pk_fma(omt2, f2(z[q][0], z[q][1]), th2 * h0);
+                    const f32x2 z1 = pk_fma(omt2, f2(z[q][2], z[q][3]), th2 * h1);
+                    z[q][0] = z0.x;
+                    z[q][1] = z0.y;
+                    z[q][2] = z1.x;
+                    z[q][3] = z1.y;
                 }
             }
             __syncthreads();
@@ -725,34 +734,58 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 else
                     acc[0] = acc[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
                 panel_a_prefetch<T, PD>(PA1, voff, ap);
+                // (reading these LDS operands before the GEMM measured no faster: tools/r2_epi2.sh)
+                float4 w4[Q], p4[Q];
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
-                    const float4 w4 = L.Wl[p0 + q][slot];
-                    const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
-                    const float4 p4 = L.Pd[p0 + q][slot];
-                    const float pd[4] = {p4.x, p4.y, p4.z, p4.w};
-                    float wn[4];
+                    w4[q] = L.Wl[p0 + q][slot];
+                    p4[q] = L.Pd[p0 + q][slot];
+                }
+                // The state updates run on every column, packed two rows per instruction: a
+                // finished (or padding) column's z, y, u and w are never read again -- its results
+                // left at the test that finished it, and MFMA output column c depends on B column c
+                // only -- so the per-element masks of the active columns are not needed.  This
+                // epilogue sits between the GEMM and the barrier on every SIMD at once; packing
+                // halves its VALU issue: C4 to eps +1.3-1.5 % (profiles/r02_epilogue_ab.txt).
+                const f32x2 th2 = f2(th, th), omt2 = f2(omt, omt), bn2 = f2(bn, bn), half2 = f2(0.5f, 0.5f);
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const float cv = acc[q][r];
-                        const float sv = (wv[r] + pd[r]) + cv;
-                        const float yp = (__builtin_fabsf(sv) + sv) * 0.5f;
-                        wn[r] = __builtin_fmaf(bn, yp - y[q][r], yp);
-                        if (use_tol) {
-                            const float un = __builtin_fmaf(omt, u[q][r], th * cv);
-                            if (act[q]) u[q][r] = un;
-                            if (chk && act[q] && (16 * t + 4 * r + j) < m) {
-                                const float tt = cv + pd[r];
-                                violh[q] = fmaxf(violh[q], tt);
-                                magh[q] = fmaxf(magh[q], __builtin_fabsf(cv) + __builtin_fabsf(pd[r]));
-                                wmin[q] = fminf(wmin[q], wv[r]);
-                                gap[q] -= (double)wv[r] * (double)tt;
-                                violz[q] = fmaxf(violz[q], u[q][r] + pd[r]);
+                for (int q = 0; q < Q; ++q) {
+                    const f32x2 c0 = f2(acc[q][0], acc[q][1]), c1 = f2(acc[q][2], acc[q][3]);
+                    const f32x2 s0 = (f2(w4[q].x, w4[q].y) + f2(p4[q].x, p4[q].y)) + c0;
+                    const f32x2 s1 = (f2(w4[q].z, w4[q].w) + f2(p4[q].z, p4[q].w)) + c1;
+                    const f32x2 y0 = f2(__builtin_fabsf(s0.x) + s0.x, __builtin_fabsf(s0.y) + s0.y) * half2;
+                    const f32x2 y1 = f2(__builtin_fabsf(s1.x) + s1.x, __builtin_fabsf(s1.y) + s1.y) * half2;
+                    const f32x2 n0 = pk_fma(bn2, y0 - f2(y[q][0], y[q][1]), y0);
+                    const f32x2 n1 = pk_fma(bn2, y1 - f2(y[q][2], y[q][3]), y1);
+                    L.Wl[p0 + q][slot] = make_float4(n0.x, n0.y, n1.x, n1.y);
+                    y[q][0] = y0.x;
+                    y[q][1] = y0.y;
+                    y[q][2] = y1.x;
+                    y[q][3] = y1.y;
+                    if (use_tol) {
+                        const f32x2 u0 = pk_fma(omt2, f2(u[q][0], u[q][1]), th2 * c0);
+                        const f32x2 u1 = pk_fma(omt2, f2(u[q][2], u[q][3]), th2 * c1);
+                        u[q][0] = u0.x;
+                        u[q][1] = u0.y;
+                        u[q][2] = u1.x;
+                        u[q][3] = u1.y;
+                        if (chk && act[q]) {
+                            const float wv[4] = {w4[q].x, w4[q].y, w4[q].z, w4[q].w};
+                            const float pd[4] = {p4[q].x, p4[q].y, p4[q].z, p4[q].w};
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) {
+                                if ((16 * t + 4 * r + j) < m) {
+                                    const float cv = acc[q][r];
+                                    const float tt = cv + pd[r];
+                                    violh[q] = fmaxf(violh[q], tt);
+                                    magh[q] = fmaxf(magh[q], __builtin_fabsf(cv) + __builtin_fabsf(pd[r]));
+                                    wmin[q] = fminf(wmin[q], wv[r]);
+                                    gap[q] -= (double)wv[r] * (double)tt;
+                                    violz[q] = fmaxf(violz[q], u[q][r] + pd[r]);
+                                }
                             }
                         }
-                        if (act[q]) y[q][r] = yp;
                     }
-                    if (act[q]) L.Wl[p0 + q][slot] = make_float4(wn[0], wn[1], wn[2], wn[3]);
                     if (chk) {  // this tile's per-column partials of the test -> LDS
 #pragma unroll
                         for (int o = 16; o < 64; o <<= 1) {
