@@ -572,6 +572,54 @@ __device__ __forceinline__ void panel_gemm_rt(__amdgpu_buffer_rsrc_t PA, const f
     else asm volatile("" : "+v"(acc0)::"memory");
 }
 
+// k-blocks [KB0, KB1) of one chain, continuing acc (not reset): the A ring PD blocks deep is
+// seeded with blocks KB0.. by panel_a_prefetch_from; the last matrix block issues kq steps.
+template <int T, int PD, int KB0, int KB1>
+__device__ __forceinline__ void panel_chain(__amdgpu_buffer_rsrc_t PA, const float4* B0, int voff, int lane,
+                                            f32x4& acc, const float4 (&ap)[PD], int kq) {
+    constexpr int R = PD + 1;
+    float4 a[R], b[2];
+#pragma unroll
+    for (int p = 0; p < PD; ++p) a[p] = ap[p];
+    b[0] = B0[KB0 * 64 + lane];
+#pragma unroll
+    for (int kb = KB0; kb < KB1; ++kb) {
+        const int i = kb - KB0, cur = i & 1, nxt = cur ^ 1;
+        const float4 ak = a[i % R];
+        if (kb + PD < KB1)
+            a[(i + PD) % R] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb + PD) * T * 1024, 0));
+        if (kb + 1 < KB1) b[nxt] = B0[(kb + 1) * 64 + lane];
+        __builtin_amdgcn_sched_barrier(0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, b[cur].x, acc, 0, 0, 0);
+        if (kb + 1 < T || kq > 1) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, b[cur].y, acc, 0, 0, 0);
+        if (kb + 1 < T || kq > 2) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, b[cur].z, acc, 0, 0, 0);
+        if (kb + 1 < T || kq > 3) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, b[cur].w, acc, 0, 0, 0);
+        asm volatile("" : "+v"(acc)::"memory");
+    }
+}
+
+template <int T, int PD>
+__device__ __forceinline__ void panel_a_prefetch_from(__amdgpu_buffer_rsrc_t PA, int voff, float4 (&ap)[PD],
+                                                      int kb0) {
+#pragma unroll
+    for (int p = 0; p < PD; ++p)
+        if (kb0 + p < T) ap[p] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb0 + p) * T * 1024, 0));
+}
+
+// Chain hand-off (odd T, both GEMMs full-length): with 2T chains per GEMM on 4 SIMDs the pair
+// layout leaves SIMDs 0,1 one chain above SIMDs 2,3 (T = 13: 7,7,6,6 -- the phase lasts 7 chains
+// of a mean 6.5).  The single wave on SIMD 2 (3) that owns tile T-1 of panel 0 (1) first runs
+// k-blocks [0, S) of tile T-2 of the same panel -- the chain of the single wave 12 (13) on SIMD 0
+// (1) -- parks its accumulator in LDS and raises a flag; wave 12 (13) waits for the flag and
+// continues its chain from block S with that accumulator as the MFMA's C operand.  The chain is
+// the same ascending-k sequence of f32 MFMAs, only split across two SIMDs, so results stay
+// bit-identical; every SIMD then carries 6.5 chains per GEMM.
+template <int T>
+struct Handoff {
+    static constexpr bool on = T == 13;  // the C4 shape (n = m = 200); other odd T are untested
+    static constexpr int S = T / 2;      // helper blocks: 4S MFMAs vs 4(T-S)-4+kq on the receiver
+};
+
 template <int T>
 struct Panel2Lds {
     float4 Wl[2][T * 64];  // fragment order, per panel: w    (B of GEMM 1)
@@ -579,7 +627,36 @@ struct Panel2Lds {
     float4 Gp[2][T * 64];  //                            g_P rows
     float4 Pd[2][T * 64];  //                            p_D rows
     PanelSlot slots[2][T];
+    float4 hand[2][64];    // hand-off accumulators, per panel
+    int hflag[2];          // hand-off generation, per panel
 };
+
+// helper side: blocks [0, S) of the receiver's tile (voff_r), accumulator to LDS, flag raised
+template <int T, int PD>
+__device__ __forceinline__ void handoff_give(__amdgpu_buffer_rsrc_t PA, const float4* B0, int voff_r, int lane,
+                                             const float4 (&aph)[PD], float4* hand, int* flag, int gen) {
+    f32x4 h = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    panel_chain<T, PD, 0, Handoff<T>::S>(PA, B0, voff_r, lane, h, aph, 4);
+    hand[lane] = make_float4(h[0], h[1], h[2], h[3]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the accumulator lands before the flag
+    __hip_atomic_store(flag, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// receiver side: wait for the flag (bounded: a missing hand-off yields wrong results, caught by
+// the parity tests, rather than a hang), then blocks [S, T) from the parked accumulator
+template <int T, int PD>
+__device__ __forceinline__ void handoff_take(__amdgpu_buffer_rsrc_t PA, const float4* B0, int voff, int lane,
+                                             const float4 (&ap)[PD], const float4* hand, int* flag, int gen,
+                                             int kq, f32x4& acc) {
+    for (int s = 0; s < (1 << 20); ++s) {
+        if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == gen) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    asm volatile("" ::: "memory");
+    const float4 hv = hand[lane];
+    acc = f32x4{hv.x, hv.y, hv.z, hv.w};
+    panel_chain<T, PD, Handoff<T>::S, T>(PA, B0, voff, lane, acc, ap, kq);
+}
 
 // The work of one wave role, NU = units per wave (2: double, 1: single, 0: idle).  Each role
 // is its own instantiation, so a single wave does not carry a double's registers; every role
@@ -587,9 +664,11 @@ struct Panel2Lds {
 // A-ring depth: 2 for single waves; 1 for double waves (2 spills at 128 VGPRs, measured no
 // better; deeper rings for singles within +-1 %, tools/ab_mb.sh)
 
-template <int T, int NU>
+// ROLE (single waves of a hand-off pair only): 0 none, 1 helper (gives), 2 receiver (takes).
+template <int T, int NU, int ROLE = 0>
 __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<T>& L, int t, int p0,
                                            bool pair, int items, int count) {
+    static_assert(ROLE == 0 || (NU == 1 && Handoff<T>::on), "hand-off roles are single waves");
     const int lane = threadIdx.x & 63;
     const int j = lane >> 4, c = lane & 15;
     const int n = a.n, m = a.m, N = a.N, K = a.check_every;
@@ -610,6 +689,8 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
     const int nkb1 = (m + 15) / 16, nkb2 = (n + 15) / 16;  // k-blocks of each GEMM (<= T)
     const int kq1 = (m - 16 * (nkb1 - 1) + 3) / 4, kq2 = (n - 16 * (nkb2 - 1) + 3) / 4;
     const bool on1 = 16 * t < n, on2 = 16 * t < m;
+    const int voff_r = voff - 1024;  // helper: the receiver's tile t - 1 (Handoff)
+    int hgen = 0;                    // hand-off generation, counted alike by helper and receiver
 
     for (int it = blockIdx.x; it < items; it += gridDim.x) {
         // columns still running, bit 16 pp + c for panel pp of this item: the same word in every
@@ -674,7 +755,13 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
 
         constexpr int PD = NU == 2 ? 1 : 2;
         float4 ap[PD];  // A blocks of the next GEMM, in flight across the barrier before it
-        if constexpr (NU > 0) panel_a_prefetch<T, PD>(PA1, voff, ap);
+        float4 aph[PD];  // helper: the receiver's first blocks
+        auto prefetch = [&](__amdgpu_buffer_rsrc_t PA) {
+            if constexpr (ROLE == 2) panel_a_prefetch_from<T, PD>(PA, voff, ap, Handoff<T>::S);
+            else if constexpr (NU > 0) panel_a_prefetch<T, PD>(PA, voff, ap);
+            if constexpr (ROLE == 1) panel_a_prefetch<T, PD>(PA, voff_r, aph);
+        };
+        prefetch(PA1);
         int v = a.v_begin;
         float th = a.theta[v], bn = a.beta[v + 1];
         while (true) {
@@ -685,7 +772,11 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             // ---- GEMM 1 + epilogue: zhat = -ML w - g_P (8b), z = (1-th) z + th zhat (8c) ----
             if constexpr (NU > 0) {
                 f32x4 acc[2];
-                if (on1 && nkb1 == T)
+                if constexpr (ROLE == 1)
+                    handoff_give<T, PD>(PA1, L.Wl[p0], voff_r, lane, aph, L.hand[p0], &L.hflag[p0], ++hgen);
+                if constexpr (ROLE == 2)
+                    handoff_take<T, PD>(PA1, L.Wl[p0], voff, lane, ap, L.hand[p0], &L.hflag[p0], ++hgen, kq1, acc[0]);
+                else if (on1 && nkb1 == T)
                     panel_gemm3<T, NU == 2, PD>(PA1, L.Wl[p0], L.Wl[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1],
                                                 ap, kq1);
                 else if (on1)
@@ -693,7 +784,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                                                   acc[1], ap, nkb1, kq1);
                 else
                     acc[0] = acc[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-                panel_a_prefetch<T, PD>(PA2, voff, ap);
+                prefetch(PA2);
                 float4 g4[Q];
 #pragma unroll
                 for (int q = 0; q < Q; ++q) g4[q] = L.Gp[p0 + q][slot];
@@ -725,7 +816,11 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             }
             if constexpr (NU > 0) {
                 f32x4 acc[2];
-                if (on2 && nkb2 == T)
+                if constexpr (ROLE == 1)
+                    handoff_give<T, PD>(PA2, L.Zh[p0], voff_r, lane, aph, L.hand[p0], &L.hflag[p0], ++hgen);
+                if constexpr (ROLE == 2)
+                    handoff_take<T, PD>(PA2, L.Zh[p0], voff, lane, ap, L.hand[p0], &L.hflag[p0], ++hgen, kq2, acc[0]);
+                else if (on2 && nkb2 == T)
                     panel_gemm3<T, NU == 2, PD>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1],
                                                 ap, kq2);
                 else if (on2)
@@ -733,7 +828,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                                                   acc[1], ap, nkb2, kq2);
                 else
                     acc[0] = acc[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-                panel_a_prefetch<T, PD>(PA1, voff, ap);
+                prefetch(PA1);
                 // (reading these LDS operands before the GEMM measured no faster: tools/r2_epi2.sh)
                 float4 w4[Q], p4[Q];
 #pragma unroll
@@ -973,8 +1068,20 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
     const bool pair = panels > (int)gridDim.x;
     const int items = pair ? (panels + 1) / 2 : panels;
     if (pair) {
+        // hand-off pairs: waves 12, 13 (SIMDs 0, 1; tile T-2) receive from 14, 15 (SIMDs 2, 3;
+        // tile T-1) when both GEMMs run full-length chains on those tiles
+        const bool ho = Handoff<T>::on && 16 * (T - 1) < a.n && 16 * (T - 1) < a.m &&
+                        (a.m + 15) / 16 == T && (a.n + 15) / 16 == T;
+        if (threadIdx.x < 2) L.hflag[threadIdx.x] = 0;
+        __syncthreads();
         if (w < D) panel2_run<T, 2>(a, L, w, 0, true, items, count);
-        else panel2_run<T, 1>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
+        else if constexpr (Handoff<T>::on) {
+            if (ho && w >= 14) panel2_run<T, 1, 1>(a, L, T - 1, w & 1, true, items, count);
+            else if (ho && w >= 12) panel2_run<T, 1, 2>(a, L, T - 2, w & 1, true, items, count);
+            else panel2_run<T, 1>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
+        } else {
+            panel2_run<T, 1>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
+        }
     } else {
         if (w < T) panel2_run<T, 1>(a, L, w, 0, false, items, count);
         else panel2_run<T, 0>(a, L, 0, 0, false, items, count);
