@@ -606,18 +606,30 @@ __device__ __forceinline__ void panel_a_prefetch_from(__amdgpu_buffer_rsrc_t PA,
         if (kb0 + p < T) ap[p] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb0 + p) * T * 1024, 0));
 }
 
-// Chain hand-off (odd T, both GEMMs full-length): with 2T chains per GEMM on 4 SIMDs the pair
-// layout leaves SIMDs 0,1 one chain above SIMDs 2,3 (T = 13: 7,7,6,6 -- the phase lasts 7 chains
-// of a mean 6.5).  The single wave on SIMD 2 (3) that owns tile T-1 of panel 0 (1) first runs
-// k-blocks [0, S) of tile T-2 of the same panel -- the chain of the single wave 12 (13) on SIMD 0
-// (1) -- parks its accumulator in LDS and raises a flag; wave 12 (13) waits for the flag and
-// continues its chain from block S with that accumulator as the MFMA's C operand.  The chain is
-// the same ascending-k sequence of f32 MFMAs, only split across two SIMDs, so results stay
-// bit-identical; every SIMD then carries 6.5 chains per GEMM.
+// Chain hand-off (T = 13, both GEMMs full-length).  A chain is an ascending-k sequence of f32
+// MFMAs whose C operand is the previous step's result; it may be cut at any k-block and continued
+// on another wave -- even on another SIMD -- from an accumulator parked in LDS, and the result
+// is bit-identical.  The layouts use this to even out the SIMDs' chain loads:
+// * pairs: with 2T chains per GEMM the 16-wave deal leaves SIMDs 0,1 one chain above SIMDs 2,3
+//   (7,7,6,6; the phase lasts 7 chains of a mean 6.5).  The single wave on SIMD 2 (3) that owns
+//   tile T-1 of panel 0 (1) first runs k-blocks [0, S) of tile T-2 of the same panel -- the chain
+//   of wave 12 (13) on SIMD 0 (1) -- then its own chain; wave 12 (13) continues from block S.
+//   Every SIMD then carries 6.5 chains.
+// * one panel per workgroup: T waves put 4,3,3,3 chains on the SIMDs while waves 13..15 idle.
+//   Tile T-1's chain (wave 12, SIMD 0) instead runs as a relay: blocks [0,4) on wave 13 (SIMD 1),
+//   [4,8) on 14 (SIMD 2), [8,T) and the epilogue on wave 12 -- the busiest SIMD carries 3.36
+//   chains.  The relay is a sequential path through three SIMDs (each piece issues at most
+//   every other MFMA slot of its SIMD, plus ~300 cycles per hand-off), so it must stay shorter
+//   than the SIMDs' own chains: raised issue priorities, whole pieces prefetched before the
+//   barrier, and a fourth hop (a 4-way relay) measured slower than none.
+// A slot's flag carries the hand-off generation (one per GEMM, counted alike by every wave), so
+// flags are never reset; a receiver waits with a bound (a missing hand-off yields wrong results,
+// caught by the parity tests, rather than a hang).
 template <int T>
 struct Handoff {
-    static constexpr bool on = T == 13;  // the C4 shape (n = m = 200); other odd T are untested
-    static constexpr int S = T / 2;      // helper blocks: 4S MFMAs vs 4(T-S)-4+kq on the receiver
+    static constexpr bool on = T == 13;  // the C4 shape (n = m = 200); other T are untested
+    static constexpr int S = T / 2;      // pairs: helper blocks 4S MFMAs vs 4(T-S)-4+kq on the receiver
+    static constexpr int R1 = 4, R2 = 8;  // one panel: relay cuts (pieces of 4 k-blocks prefetched whole)
 };
 
 template <int T>
@@ -627,48 +639,64 @@ struct Panel2Lds {
     float4 Gp[2][T * 64];  //                            g_P rows
     float4 Pd[2][T * 64];  //                            p_D rows
     PanelSlot slots[2][T];
-    float4 hand[2][64];    // hand-off accumulators, per panel
-    int hflag[2];          // hand-off generation, per panel
+    float4 hand[3][64];    // hand-off accumulators
+    int hflag[3];          // hand-off generation per slot
 };
 
-// helper side: blocks [0, S) of the receiver's tile (voff_r), accumulator to LDS, flag raised
-template <int T, int PD>
-__device__ __forceinline__ void handoff_give(__amdgpu_buffer_rsrc_t PA, const float4* B0, int voff_r, int lane,
-                                             const float4 (&aph)[PD], float4* hand, int* flag, int gen) {
-    f32x4 h = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    panel_chain<T, PD, 0, Handoff<T>::S>(PA, B0, voff_r, lane, h, aph, 4);
-    hand[lane] = make_float4(h[0], h[1], h[2], h[3]);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the accumulator lands before the flag
-    __hip_atomic_store(flag, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
+struct HoSlots {
+    int in, out;  // LDS hand-off slots taken / given (-1: none)
+};
 
-// receiver side: wait for the flag (bounded: a missing hand-off yields wrong results, caught by
-// the parity tests, rather than a hang), then blocks [S, T) from the parked accumulator
-template <int T, int PD>
-__device__ __forceinline__ void handoff_take(__amdgpu_buffer_rsrc_t PA, const float4* B0, int voff, int lane,
-                                             const float4 (&ap)[PD], const float4* hand, int* flag, int gen,
-                                             int kq, f32x4& acc) {
+template <int T>
+__device__ __forceinline__ f32x4 handoff_wait(Panel2Lds<T>& L, int slot, int gen, int lane) {
     for (int s = 0; s < (1 << 20); ++s) {
-        if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == gen) break;
+        if (__hip_atomic_load(&L.hflag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == gen) break;
         __builtin_amdgcn_s_sleep(1);
     }
     asm volatile("" ::: "memory");
-    const float4 hv = hand[lane];
-    acc = f32x4{hv.x, hv.y, hv.z, hv.w};
-    panel_chain<T, PD, Handoff<T>::S, T>(PA, B0, voff, lane, acc, ap, kq);
+    const float4 hv = L.hand[slot][lane];
+    return f32x4{hv.x, hv.y, hv.z, hv.w};
 }
 
-// The work of one wave role, NU = units per wave (2: double, 1: single, 0: idle).  Each role
-// is its own instantiation, so a single wave does not carry a double's registers; every role
-// executes the same sequence of barriers.
-// A-ring depth: 2 for single waves; 1 for double waves (2 spills at 128 VGPRs, measured no
-// better; deeper rings for singles within +-1 %, tools/ab_mb.sh)
+template <int T>
+__device__ __forceinline__ void handoff_post(Panel2Lds<T>& L, int slot, int gen, int lane, const f32x4& h) {
+    L.hand[slot][lane] = make_float4(h[0], h[1], h[2], h[3]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the accumulator lands before the flag
+    __hip_atomic_store(&L.hflag[slot], gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
-// ROLE (single waves of a hand-off pair only): 0 none, 1 helper (gives), 2 receiver (takes).
-template <int T, int NU, int ROLE = 0>
+// a piece of another wave's chain: k-blocks [KB0, KB1) (KB1 < T) of the tile at voff, continued
+// from slot hs.in (or from zero), parked in slot hs.out; PRIO raises the wave's issue priority
+template <int T, int PD, int KB0, int KB1, bool PRIO>
+__device__ __forceinline__ void handoff_piece(Panel2Lds<T>& L, __amdgpu_buffer_rsrc_t PA, const float4* B0, int voff,
+                                              int lane, const float4 (&aph)[PD], HoSlots hs, int gen) {
+    f32x4 h = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (hs.in >= 0) h = handoff_wait(L, hs.in, gen, lane);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
+    panel_chain<T, PD, KB0, KB1>(PA, B0, voff, lane, h, aph, 4);
+    handoff_post(L, hs.out, gen, lane, h);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+}
+
+// the chain's last piece on its owner: blocks [KB0, T) from slot hs.in
+template <int T, int PD, int KB0, bool PRIO>
+__device__ __forceinline__ void handoff_take(Panel2Lds<T>& L, __amdgpu_buffer_rsrc_t PA, const float4* B0, int voff,
+                                             int lane, const float4 (&ap)[PD], HoSlots hs, int gen, int kq,
+                                             f32x4& acc) {
+    acc = handoff_wait(L, hs.in, gen, lane);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(2);
+    panel_chain<T, PD, KB0, T>(PA, B0, voff, lane, acc, ap, kq);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+}
+
+// Hand-off roles (Handoff): 0 none; 1 pair helper (NU = 1: blocks [KB0, KB1) of tile t-1 into
+// slot hs.out, then its own chain); 2 receiver (NU = 1: its own chain from block KB0, slot hs.in);
+// 3 relay (NU = 0: blocks [KB0, KB1) of tile t from slot hs.in, or zero, into slot hs.out).
+// PRIO: the one-panel relay raises issue priority for its pieces.
+template <int T, int NU, int ROLE = 0, int KB0 = 0, int KB1 = 0, bool PRIO = false>
 __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<T>& L, int t, int p0,
-                                           bool pair, int items, int count) {
-    static_assert(ROLE == 0 || (NU == 1 && Handoff<T>::on), "hand-off roles are single waves");
+                                           bool pair, int items, int count, HoSlots hs = HoSlots{-1, -1}) {
+    static_assert(ROLE == 0 || (Handoff<T>::on && (ROLE == 3 ? NU == 0 : NU == 1)), "hand-off roles");
     const int lane = threadIdx.x & 63;
     const int j = lane >> 4, c = lane & 15;
     const int n = a.n, m = a.m, N = a.N, K = a.check_every;
@@ -753,13 +781,14 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
         }
         __syncthreads();
 
-        constexpr int PD = NU == 2 ? 1 : 2;
+        constexpr int PD = NU == 2 ? 1 : (ROLE == 3 ? Handoff<T>::R1 : 2);
         float4 ap[PD];  // A blocks of the next GEMM, in flight across the barrier before it
-        float4 aph[PD];  // helper: the receiver's first blocks
+        float4 aph[PD];  // helper / relay: the piece's first blocks
         auto prefetch = [&](__amdgpu_buffer_rsrc_t PA) {
-            if constexpr (ROLE == 2) panel_a_prefetch_from<T, PD>(PA, voff, ap, Handoff<T>::S);
+            if constexpr (ROLE == 2) panel_a_prefetch_from<T, PD>(PA, voff, ap, KB0);
             else if constexpr (NU > 0) panel_a_prefetch<T, PD>(PA, voff, ap);
             if constexpr (ROLE == 1) panel_a_prefetch<T, PD>(PA, voff_r, aph);
+            if constexpr (ROLE == 3) panel_a_prefetch_from<T, PD>(PA, voff, aph, KB0);
         };
         prefetch(PA1);
         int v = a.v_begin;
@@ -772,10 +801,11 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             // ---- GEMM 1 + epilogue: zhat = -ML w - g_P (8b), z = (1-th) z + th zhat (8c) ----
             if constexpr (NU > 0) {
                 f32x4 acc[2];
+                ++hgen;
                 if constexpr (ROLE == 1)
-                    handoff_give<T, PD>(PA1, L.Wl[p0], voff_r, lane, aph, L.hand[p0], &L.hflag[p0], ++hgen);
+                    handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA1, L.Wl[p0], voff_r, lane, aph, hs, hgen);
                 if constexpr (ROLE == 2)
-                    handoff_take<T, PD>(PA1, L.Wl[p0], voff, lane, ap, L.hand[p0], &L.hflag[p0], ++hgen, kq1, acc[0]);
+                    handoff_take<T, PD, KB0, PRIO>(L, PA1, L.Wl[p0], voff, lane, ap, hs, hgen, kq1, acc[0]);
                 else if (on1 && nkb1 == T)
                     panel_gemm3<T, NU == 2, PD>(PA1, L.Wl[p0], L.Wl[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1],
                                                 ap, kq1);
@@ -802,6 +832,10 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                     z[q][2] = z1.x;
                     z[q][3] = z1.y;
                 }
+            } else if constexpr (ROLE == 3) {
+                ++hgen;
+                handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA1, L.Wl[p0], voff, lane, aph, hs, hgen);
+                prefetch(PA2);
             }
             __syncthreads();
             // ---- GEMM 2 + epilogue: y+ = [w + G_L zhat + p_D]+ (8d), next w (8a) ----------
@@ -816,10 +850,11 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             }
             if constexpr (NU > 0) {
                 f32x4 acc[2];
+                ++hgen;
                 if constexpr (ROLE == 1)
-                    handoff_give<T, PD>(PA2, L.Zh[p0], voff_r, lane, aph, L.hand[p0], &L.hflag[p0], ++hgen);
+                    handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA2, L.Zh[p0], voff_r, lane, aph, hs, hgen);
                 if constexpr (ROLE == 2)
-                    handoff_take<T, PD>(PA2, L.Zh[p0], voff, lane, ap, L.hand[p0], &L.hflag[p0], ++hgen, kq2, acc[0]);
+                    handoff_take<T, PD, KB0, PRIO>(L, PA2, L.Zh[p0], voff, lane, ap, hs, hgen, kq2, acc[0]);
                 else if (on2 && nkb2 == T)
                     panel_gemm3<T, NU == 2, PD>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1],
                                                 ap, kq2);
@@ -900,6 +935,10 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                         }
                     }
                 }
+            } else if constexpr (ROLE == 3) {
+                ++hgen;
+                handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA2, L.Zh[p0], voff, lane, aph, hs, hgen);
+                prefetch(PA1);
             }
             th = th_next;
             bn = bn_next;
@@ -1067,21 +1106,32 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
     const int panels = (count + 15) / 16;
     const bool pair = panels > (int)gridDim.x;
     const int items = pair ? (panels + 1) / 2 : panels;
-    if (pair) {
-        // hand-off pairs: waves 12, 13 (SIMDs 0, 1; tile T-2) receive from 14, 15 (SIMDs 2, 3;
-        // tile T-1) when both GEMMs run full-length chains on those tiles
-        const bool ho = Handoff<T>::on && 16 * (T - 1) < a.n && 16 * (T - 1) < a.m &&
-                        (a.m + 15) / 16 == T && (a.n + 15) / 16 == T;
-        if (threadIdx.x < 2) L.hflag[threadIdx.x] = 0;
-        __syncthreads();
-        if (w < D) panel2_run<T, 2>(a, L, w, 0, true, items, count);
-        else if constexpr (Handoff<T>::on) {
-            if (ho && w >= 14) panel2_run<T, 1, 1>(a, L, T - 1, w & 1, true, items, count);
-            else if (ho && w >= 12) panel2_run<T, 1, 2>(a, L, T - 2, w & 1, true, items, count);
+    // hand-off (Handoff): both GEMMs run full-length chains on tiles T-2 and T-1
+    const bool ho = Handoff<T>::on && 16 * (T - 1) < a.n && 16 * (T - 1) < a.m && (a.m + 15) / 16 == T &&
+                    (a.n + 15) / 16 == T;
+    if (threadIdx.x < 3) L.hflag[threadIdx.x] = 0;
+    __syncthreads();
+    if constexpr (Handoff<T>::on) {
+        using H = Handoff<T>;
+        if (pair) {  // waves 12, 13 (SIMDs 0, 1; tile T-2) receive from 14, 15 (SIMDs 2, 3; tile T-1)
+            if (w < D) panel2_run<T, 2>(a, L, w, 0, true, items, count);
+            else if (ho && w >= 14)
+                panel2_run<T, 1, 1, 0, H::S>(a, L, T - 1, w & 1, true, items, count, HoSlots{-1, w & 1});
+            else if (ho && w >= 12)
+                panel2_run<T, 1, 2, H::S>(a, L, T - 2, w & 1, true, items, count, HoSlots{w & 1, -1});
             else panel2_run<T, 1>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
-        } else {
-            panel2_run<T, 1>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
+        } else {  // tile T-1 as a relay: waves 13 -> 14 -> 12
+            if (ho && w == T - 1) panel2_run<T, 1, 2, H::R2, 0, true>(a, L, w, 0, false, items, count, HoSlots{1, -1});
+            else if (ho && w == T)
+                panel2_run<T, 0, 3, 0, H::R1, true>(a, L, T - 1, 0, false, items, count, HoSlots{-1, 0});
+            else if (ho && w == T + 1)
+                panel2_run<T, 0, 3, H::R1, H::R2, true>(a, L, T - 1, 0, false, items, count, HoSlots{0, 1});
+            else if (w < T) panel2_run<T, 1>(a, L, w, 0, false, items, count);
+            else panel2_run<T, 0>(a, L, 0, 0, false, items, count);
         }
+    } else if (pair) {
+        if (w < D) panel2_run<T, 2>(a, L, w, 0, true, items, count);
+        else panel2_run<T, 1>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
     } else {
         if (w < T) panel2_run<T, 1>(a, L, w, 0, false, items, count);
         else panel2_run<T, 0>(a, L, 0, 0, false, items, count);
@@ -1122,7 +1172,8 @@ int panel_fin_thresh(int n, int m, int num_cus, const Tuning* t) {
 //
 // Cost model (us; constants from profiles/r01_timeline.txt and profiles/r01_microbench.jsonl):
 //   panel iteration  = (busiest SIMD's MFMA chains) x t_chain,  t_chain = 0.055 (kb1 + kb2) + 0.2
-//                      single panels: ceil(T/4) chains, pairs: ceil(2T/4), T <= 8: co-resident
+//                      single panels: ceil(T/4) chains, pairs: ceil(2T/4) (2T/4 on the hand-off
+//                      shapes, r02_handoff_ab.txt: 8192 at 10.5-10.9 us), T <= 8: co-resident
 //                      panels share the CU's four SIMDs
 //   phase overhead   = 2 launches (finisher + panel, 5 us each) + one seed iteration
 //                      + carried z, y, w, u (16 (n + m) bytes per survivor at 5 TB/s)
@@ -1132,16 +1183,19 @@ int panel_fin_thresh(int n, int m, int num_cus, const Tuning* t) {
 namespace {
 struct PlanModel {
     int T, n, m, num_cus, grid;
+    bool handoff;  // gpad_panel2_kernel's hand-off shapes (Handoff)
     double t_chain, t_res, t_launch = 5.0;
     double iter_time(long long panels) const {
         if (panels <= 0) return 0.0;
-        int chains;
+        double chains;
         if (T > 8) {
             if (panels <= grid) {
                 chains = (T + 3) / 4;
             } else {
                 const long long pairs = (panels + 1) / 2;
-                chains = (int)((pairs + grid - 1) / grid) * ((2 * T + 3) / 4);
+                // the chain hand-off evens the pair layout's SIMD loads (7,7,6,6 -> 6.5 at T = 13)
+                const double per = handoff ? 2 * T / 4.0 : (double)((2 * T + 3) / 4);
+                chains = (double)((pairs + grid - 1) / grid) * per;
             }
         } else {
             const int per_cu_max = 32 / T;
@@ -1149,7 +1203,7 @@ struct PlanModel {
             const long long last = panels - (rounds - 1) * (long long)grid;
             long long q = (last + num_cus - 1) / num_cus;
             if (rounds > 1 || q > per_cu_max) q = per_cu_max;
-            chains = (int)(rounds - 1) * ((per_cu_max * T + 3) / 4) + (int)((q * T + 3) / 4);
+            chains = (double)((rounds - 1) * ((per_cu_max * T + 3) / 4) + (q * T + 3) / 4);
         }
         return chains * t_chain;
     }
@@ -1202,6 +1256,8 @@ int panel_plan(const int* iters, int batch, int n, int m, int N, int check_every
     md.m = m;
     md.num_cus = num_cus;
     md.grid = T > 8 ? num_cus : num_cus * (32 / T);
+    md.handoff = T == 13 && Handoff<13>::on && n > 16 * (T - 1) && m > 16 * (T - 1) && (n + 15) / 16 == T &&
+                 (m + 15) / 16 == T;
     md.t_chain = 0.055 * ((m + 15) / 16 + (n + 15) / 16) + 0.2;
     md.t_res = 0.0021 * (n + m) + 0.38;
     const bool fin_ok = resident_supported(n, m);
