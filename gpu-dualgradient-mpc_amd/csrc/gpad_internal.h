@@ -31,6 +31,7 @@ struct Tuning {
     int finish_solo = -1;     // GPAD_OPT_FINISH_SOLO: duo workgroups running one instance each
                               // (the longest-predicted survivors; -1: default)
     int cpanel = 1;           // GPAD_OPT_CONDENSED_PANEL: condensed batches on the MFMA panels
+    int plan_fin_cost = 100;  // GPAD_OPT_PLAN_FIN_COST: the plan model's finisher cost, percent
 };
 
 // Rounding margin of the Algorithm 1 decisions, in units of max_i(|chain_i| + |pD_i|): a test

@@ -1184,7 +1184,7 @@ namespace {
 struct PlanModel {
     int T, n, m, num_cus, grid;
     bool handoff;  // gpad_panel2_kernel's hand-off shapes (Handoff)
-    double t_chain, t_res, t_launch = 5.0;
+    double t_chain, t_res, t_launch = 5.0, fin_scale = 1.0;
     double iter_time(long long panels) const {
         if (panels <= 0) return 0.0;
         double chains;
@@ -1214,7 +1214,7 @@ struct PlanModel {
     double finisher(int longest, long long work) const {
         const double lat = longest * 1.4 * t_res;
         const double thr = (double)work * 1.1 * t_res / num_cus;
-        return 2 * t_launch + (lat > thr ? lat : thr);
+        return fin_scale * (2 * t_launch + (lat > thr ? lat : thr));
     }
 };
 }  // namespace
@@ -1260,6 +1260,7 @@ int panel_plan(const int* iters, int batch, int n, int m, int N, int check_every
                  (m + 15) / 16 == T;
     md.t_chain = 0.055 * ((m + 15) / 16 + (n + 15) / 16) + 0.2;
     md.t_res = 0.0021 * (n + m) + 0.38;
+    if (t) md.fin_scale = t->plan_fin_cost / 100.0;
     const bool fin_ok = resident_supported(n, m);
     // best[j]: cheapest finish from boundary j (survivors surv[j] in panels); nxt[j] = next
     // boundary (or -1: finisher takes over at j)

@@ -44,12 +44,13 @@ OPT_PHASE_LEN, OPT_FINISH_THRESH, OPT_PLAN, OPT_PHASED, OPT_FINISHER, OPT_LPT = 
 OPT_PANEL_MAX_GRID, OPT_DUO_MAX_GRID, OPT_FLAT_PANEL_MIN, OPT_FLAT_PANELS = 7, 8, 9, 10
 OPT_FLAT_WAVES, OPT_FLAT_A_LDS, OPT_FINISH_SOLO = 11, 12, 13
 OPT_CONDENSED_PANEL = 14
+OPT_PLAN_FIN_COST = 15
 OPTIONS = {"phase_len": OPT_PHASE_LEN, "finish_thresh": OPT_FINISH_THRESH, "plan": OPT_PLAN,
            "phased": OPT_PHASED, "finisher": OPT_FINISHER, "lpt": OPT_LPT,
            "panel_max_grid": OPT_PANEL_MAX_GRID, "duo_max_grid": OPT_DUO_MAX_GRID,
            "flat_panel_min": OPT_FLAT_PANEL_MIN, "flat_panels": OPT_FLAT_PANELS,
            "flat_waves": OPT_FLAT_WAVES, "flat_a_lds": OPT_FLAT_A_LDS, "finish_solo": OPT_FINISH_SOLO,
-           "condensed_panel": OPT_CONDENSED_PANEL}
+           "condensed_panel": OPT_CONDENSED_PANEL, "plan_fin_cost": OPT_PLAN_FIN_COST}
 
 FILE_ROWMAJOR, FILE_FLIPPED, FILE_FLAT = 0, 1, 2
 

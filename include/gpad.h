@@ -323,6 +323,8 @@ int gpad_schedule(int N, int kind, double* theta, double* beta);
 #define GPAD_OPT_CONDENSED_PANEL 14 /* 1: GPAD_KERNEL_CONDENSED batches (shared, > 2/CU) on the MFMA
                                      * panels, 16 waves (default); 2: 8 waves sharing A streams;
                                      * 0: one workgroup per instance                               */
+#define GPAD_OPT_PLAN_FIN_COST 15  /* phase plan: the finisher's modelled cost in percent (default
+                                    * 100; > 100 moves the takeover later)                         */
 int gpad_set_option(gpad_handle_t h, int option, int value);
 
 /* Synchronise the handle's stream (for callers using device memory + async runs). */

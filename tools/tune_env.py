@@ -25,6 +25,7 @@ _MAP = {  # env name -> (option, value transform)
     "GPAD_FLAT_WAVES": ("flat_waves", int),
     "GPAD_FLAT_NO_ALDS": ("flat_a_lds", lambda v: 0),
     "GPAD_FINISH_SOLO": ("finish_solo", int),
+    "GPAD_PLAN_FIN_COST": ("plan_fin_cost", int),
 }
 
 
