@@ -12,5 +12,5 @@ python3 -c "
 import json; d=json.loads(open('gpurun_out/${T}_bench.json').read().strip().splitlines()[-1])
 print('value', d['value'], 'rep', d['value_repeated_inputs'], 'ms', d['ms_per_step'], 'frac', d['roofline']['frac'])
 c=d['legs']['c4_condensed']; print('condensed', c['condensed']['solve_ms'], c['bit_exact']['solve_ms'], c['speedup'])"
-timeout -k 10 900 bash tools/profile.sh r02 > gpurun_out/${T}_prof.log 2>&1 || { tail -20 gpurun_out/${T}_prof.log; exit 1; }
+timeout -k 10 900 bash tools/profile.sh ${PTAG:-r02} > gpurun_out/${T}_prof.log 2>&1 || { tail -20 gpurun_out/${T}_prof.log; exit 1; }
 echo profiled
