@@ -295,3 +295,38 @@ def test_condensed_panel_check_every_and_takeover_edges(gpu, oracle, K, B, take)
         assert it[b] == ito, b
         assert_bitexact(z[b], zo, f"z[{b}]")
         assert_bitexact(y[b], yo, f"y[{b}]")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nm", [(200, 200), (150, 207)])
+@pytest.mark.parametrize("N,tol,take", [(60, 0.0, 0), (3000, 1e-4, 0), (3000, 1e-4, 40)])
+def test_condensed_panel_pairs_handoff_bitexact(gpu, oracle, nm, N, tol, take):
+    """Two panels per group at T = 13 (the C4 shape; 16 waves, 7,7,6,6 chains per SIMD), fixed N,
+    planned and forced takeovers: instances across the grid bit-exact with the condensed oracle.
+    (A chain hand-off as in the bit-exact pairs measured no gain here, profiles/r02_cpanel_handoff_ab.txt:
+    a condensed group's iteration is latency-bound, not SIMD-issue-bound.)"""
+    import gpad_mpc
+    from gpad_mpc import _lib, problems
+    n, m = nm
+    B = 16 * 256 + 301
+    qp = problems.synthetic_qp(n, m, batch=1, seed=43)
+    rng = np.random.default_rng(N + n)
+    ML, G, L = _f32(qp.ML), _f32(qp.G), np.float32(qp.L)
+    M = (qp.M[None, :] * (1.0 + 0.3 * rng.normal(size=(B, 1)))).astype(np.float32)
+    g = (qp.g[None, :] + 0.2 * rng.random((B, m))).astype(np.float32)
+    z = np.zeros((B, n), np.float32)
+    y = np.zeros((B, m), np.float32)
+    it = np.zeros(B, np.int32)
+    with gpad_mpc.GpadSolver(0) as s:
+        s.setup(ML, G, float(L), n=n, m=m, batch=B, kernel=_lib.KERNEL_CONDENSED)
+        s.set_options(phase_len=take)
+        for _ in range(2):
+            z[:] = 0.0
+            y[:] = 0.0
+            st = s.run(z, y, M, g, N, tol, iters=it)
+    assert st["kernel"] == "condensed"
+    for b in list(range(0, B, 397)) + [B - 1]:
+        zo, yo, ito, _ = oracle.solve_condensed_f32(np.zeros(n), np.zeros(m), ML, M[b], G, g[b], N, L, tol)
+        assert it[b] == ito, b
+        assert_bitexact(z[b], zo, f"z[{b}]")
+        assert_bitexact(y[b], yo, f"y[{b}]")
