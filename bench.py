@@ -795,6 +795,10 @@ def main():
             "repeated_inputs_note": "the same q/b every step: the phase plan and the finisher's "
                                     "longest-first queue are built from the previous solve's exact "
                                     "per-instance counts, i.e. perfect foresight",
+            "eps_parity": "iteration counts to eps are parity unpinned against the reference (its "
+                          "termination test is commented out, acceldualgrad.m:66-79, absent from "
+                          "main.cu); bit-exact with the oracle restatement, fp64 max(G z* - g) <= eps "
+                          "certified (DESIGN.md section 3)",
             "batching": util,
             "converged": int(head["converged_all"]),
             "kernel": st["kernel"],
