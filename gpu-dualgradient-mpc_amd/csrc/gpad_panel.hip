@@ -606,7 +606,7 @@ __device__ __forceinline__ void panel_a_prefetch_from(__amdgpu_buffer_rsrc_t PA,
         if (kb0 + p < T) ap[p] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb0 + p) * T * 1024, 0));
 }
 
-// Chain hand-off (T = 13, both GEMMs full-length).  A chain is an ascending-k sequence of f32
+// Chain hand-off (T = 9, 11, 13, both GEMMs full-length).  A chain is an ascending-k sequence of f32
 // MFMAs whose C operand is the previous step's result; it may be cut at any k-block and continued
 // on another wave -- even on another SIMD -- from an accumulator parked in LDS, and the result
 // is bit-identical.  The layouts use this to even out the SIMDs' chain loads:
@@ -618,7 +618,7 @@ __device__ __forceinline__ void panel_a_prefetch_from(__amdgpu_buffer_rsrc_t PA,
 // * one panel per workgroup: T waves put 4,3,3,3 chains on the SIMDs while waves 13..15 idle.
 //   Tile T-1's chain (wave 12, SIMD 0) instead runs as a relay: blocks [0,4) on wave 13 (SIMD 1),
 //   [4,8) on 14 (SIMD 2), [8,T) and the epilogue on wave 12 -- the busiest SIMD carries 3.36
-//   chains.  The relay is a sequential path through three SIMDs (each piece issues at most
+//   chains (T = 9 likewise: 3,2,2,2 chains, tile 8 over waves 9 -> 10 -> 8).  The relay is a sequential path through three SIMDs (each piece issues at most
 //   every other MFMA slot of its SIMD, plus ~300 cycles per hand-off), so it must stay shorter
 //   than the SIMDs' own chains: raised issue priorities, whole pieces prefetched before the
 //   barrier, and a fourth hop (a 4-way relay) measured slower than none.
@@ -627,9 +627,12 @@ __device__ __forceinline__ void panel_a_prefetch_from(__amdgpu_buffer_rsrc_t PA,
 // caught by the parity tests, rather than a hang).
 template <int T>
 struct Handoff {
-    static constexpr bool on = T == 13;  // the C4 shape (n = m = 200); other T are untested
+    // pairs: odd T with singles on waves 12..15 (T = 9, 11, 13: SIMD loads 5,5,4,4 / 6,6,5,5 /
+    // 7,7,6,6); one panel: T = 9, 13 (T % 4 == 1: SIMD 0 carries the extra tile, waves T, T+1 idle)
+    static constexpr bool on = T == 9 || T == 11 || T == 13;
+    static constexpr bool relay = T == 9 || T == 13;
     static constexpr int S = T / 2;      // pairs: helper blocks 4S MFMAs vs 4(T-S)-4+kq on the receiver
-    static constexpr int R1 = 4, R2 = 8;  // one panel: relay cuts (pieces of 4 k-blocks prefetched whole)
+    static constexpr int R1 = T / 3, R2 = 2 * (T / 3);  // one panel: relay cuts (equal pieces, prefetched whole)
 };
 
 template <int T>
@@ -1120,8 +1123,11 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
             else if (ho && w >= 12)
                 panel2_run<T, 1, 2, H::S>(a, L, T - 2, w & 1, true, items, count, HoSlots{w & 1, -1});
             else panel2_run<T, 1>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
-        } else {  // tile T-1 as a relay: waves 13 -> 14 -> 12
-            if (ho && w == T - 1) panel2_run<T, 1, 2, H::R2, 0, true>(a, L, w, 0, false, items, count, HoSlots{1, -1});
+        } else {  // tile T-1 as a relay: waves T -> T+1 -> T-1
+            if constexpr (!H::relay) {
+                if (w < T) panel2_run<T, 1>(a, L, w, 0, false, items, count);
+                else panel2_run<T, 0>(a, L, 0, 0, false, items, count);
+            } else if (ho && w == T - 1) panel2_run<T, 1, 2, H::R2, 0, true>(a, L, w, 0, false, items, count, HoSlots{1, -1});
             else if (ho && w == T)
                 panel2_run<T, 0, 3, 0, H::R1, true>(a, L, T - 1, 0, false, items, count, HoSlots{-1, 0});
             else if (ho && w == T + 1)
@@ -1256,8 +1262,8 @@ int panel_plan(const int* iters, int batch, int n, int m, int N, int check_every
     md.m = m;
     md.num_cus = num_cus;
     md.grid = T > 8 ? num_cus : num_cus * (32 / T);
-    md.handoff = T == 13 && Handoff<13>::on && n > 16 * (T - 1) && m > 16 * (T - 1) && (n + 15) / 16 == T &&
-                 (m + 15) / 16 == T;
+    md.handoff = (T == 9 || T == 11 || T == 13) && n > 16 * (T - 1) && m > 16 * (T - 1) &&
+                 (n + 15) / 16 == T && (m + 15) / 16 == T;
     md.t_chain = 0.055 * ((m + 15) / 16 + (n + 15) / 16) + 0.2;
     md.t_res = 0.0021 * (n + m) + 0.38;
     if (t) md.fin_scale = t->plan_fin_cost / 100.0;

@@ -176,12 +176,13 @@ def test_panel_two_wave_panels_large_batch(gpu, oracle, nm):
                                             (0, 0, None), (0, 10, 24)])
 @pytest.mark.parametrize("tol,N", [(1e-4, 3000), (0.0, 57)])
 @pytest.mark.parametrize("nm,B", [((40, 72), 150), ((150, 130), 40), ((131, 256), 37), ((200, 200), 120),
-                                  ((193, 207), 101), ((207, 194), 70)])
+                                  ((193, 207), 101), ((207, 194), 70), ((140, 135), 90), ((170, 176), 80)])
 def test_panel_phased_compaction_bitexact(gpu, oracle, grid, phase, fin, tol, N, nm, B):
     """Phased compaction + grid-stride panels (+ panel pairs for T > 8 when panels outnumber
     workgroups) + the resident finisher for the tail (fin = its threshold; 0 disables it);
-    n, m in (192, 208] run the panel pairs' chain hand-off (T = 13, gpad_panel.hip Handoff) with
-    the receiver's last k-block at every kq:
+    n, m in (192, 208], (160, 176] and (128, 144] run the panel pairs' chain hand-off (T = 13, 11,
+    9, gpad_panel.hip Handoff; one-panel relays at T = 13, 9) with the receiver's last k-block at
+    every kq:
     survivors of each phase are re-packed into new panels (different columns, workgroups,
     pairs and phases) or finished one per workgroup; every instance must still match its own
     oracle solve exactly, including its iteration count."""
