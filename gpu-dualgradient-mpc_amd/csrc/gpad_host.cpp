@@ -256,7 +256,10 @@ int gpad_set_option(gpad_handle_t h, int option, int value) {
         case GPAD_OPT_FLAT_A_LDS: return set(t.flat_a_lds, 0, 1, def.flat_a_lds);
         case GPAD_OPT_FINISH_SOLO: return set(t.finish_solo, 0, big, def.finish_solo);
         case GPAD_OPT_CONDENSED_PANEL: return set(t.cpanel, 0, 2, def.cpanel);
-        case GPAD_OPT_PLAN_FIN_COST: return set(t.plan_fin_cost, 1, 10000, def.plan_fin_cost);
+        case GPAD_OPT_PLAN_FIN_COST:  // re-plan from the next counts
+            h->plan.nph = 0;
+            h->plan_key = 0;
+            return set(t.plan_fin_cost, 1, 10000, def.plan_fin_cost);
         default: return fail(GPAD_ERR_INVALID, "gpad_set_option: unknown option");
     }
 }

@@ -259,8 +259,8 @@ def test_finisher_queue_bitexact(gpu, oracle, finisher, grid, solo, nm, B, z0s):
         assert_bitexact(y[b], yo, f"instance {b} y")
 
 
-@pytest.mark.parametrize("fin", [None, 0])
-def test_panel_phase_plan_reuse_bitexact(gpu, oracle, fin):
+@pytest.mark.parametrize("fin,fin_cost", [(None, None), (0, None), (None, 300), (None, 1)])
+def test_panel_phase_plan_reuse_bitexact(gpu, oracle, fin, fin_cost):
     """A handle plans its phases from the previous solve's iteration counts (csrc/gpad_panel.hip
     panel_plan); a later solve that needs more (or fewer) iterations than the plan expects must
     still be exact -- the plan moves launch boundaries and the finisher takeover only."""
@@ -274,6 +274,8 @@ def test_panel_phase_plan_reuse_bitexact(gpu, oracle, fin):
     with gpad_mpc.GpadSolver(0) as s:
         s.setup(ML, G, float(L), n=n, m=m, batch=B, kernel=kcode("panel"))
         s.set_options(phase_len=10, finish_thresh=-1 if fin is None else fin)
+        if fin_cost is not None:  # the plan model's finisher cost (moves the takeover only)
+            s.set_options(plan_fin_cost=fin_cost)
         for scale, tol in ((1.0, 1e-3), (3.0, 1e-5), (1.0, 1e-4)):  # easy, harder, middle
             M = (qp.M * scale).astype(np.float32)
             g = (qp.g + 0.1 * rng.random((B, m))).astype(np.float32)
@@ -477,6 +479,11 @@ def test_error_paths(gpu):
         s.run(np.zeros(300, np.float32), np.zeros(300, np.float32), np.zeros(300, np.float32),
               np.zeros(300, np.float32), 10, 0.0)
     assert e.value.code == _lib.ERR_UNSUPPORTED
+    for name, bad in (("plan_fin_cost", 0), ("condensed_panel", 3), (99, 1)):  # out of range / unknown
+        with pytest.raises(gpad_mpc.GpadError) as e:
+            s.set_option(name, bad)
+        assert e.value.code == _lib.ERR_INVALID
+    s.set_option("plan_fin_cost", _lib.OPT_DEFAULT)
     s.close()
 
 
