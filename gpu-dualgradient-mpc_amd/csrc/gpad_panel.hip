@@ -1190,13 +1190,16 @@ namespace {
 struct PlanModel {
     int T, n, m, num_cus, grid;
     bool handoff;  // gpad_panel2_kernel's hand-off shapes (Handoff)
+    bool relay;    // ... and its one-panel relay (T = 9, 13)
     double t_chain, t_res, t_launch = 5.0, fin_scale = 1.0;
     double iter_time(long long panels) const {
         if (panels <= 0) return 0.0;
         double chains;
         if (T > 8) {
             if (panels <= grid) {
-                chains = (T + 3) / 4;
+                // the one-panel relay (Handoff): 4 -> 3.36 chains on the busiest SIMD, measured
+                // 6.02 -> 5.65-5.75 us per iteration at one CU (r02_relay_ab.txt): priced as 3.5
+                chains = relay ? 3.5 : (double)((T + 3) / 4);
             } else {
                 const long long pairs = (panels + 1) / 2;
                 // the chain hand-off evens the pair layout's SIMD loads (7,7,6,6 -> 6.5 at T = 13)
@@ -1264,6 +1267,7 @@ int panel_plan(const int* iters, int batch, int n, int m, int N, int check_every
     md.grid = T > 8 ? num_cus : num_cus * (32 / T);
     md.handoff = (T == 9 || T == 11 || T == 13) && n > 16 * (T - 1) && m > 16 * (T - 1) &&
                  (n + 15) / 16 == T && (m + 15) / 16 == T;
+    md.relay = md.handoff && (T == 9 || T == 13);
     md.t_chain = 0.055 * ((m + 15) / 16 + (n + 15) / 16) + 0.2;
     md.t_res = 0.0021 * (n + m) + 0.38;
     if (t) md.fin_scale = t->plan_fin_cost / 100.0;
