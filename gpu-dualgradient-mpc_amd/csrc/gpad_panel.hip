@@ -606,10 +606,10 @@ __device__ __forceinline__ void panel_a_prefetch_from(__amdgpu_buffer_rsrc_t PA,
         if (kb0 + p < T) ap[p] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb0 + p) * T * 1024, 0));
 }
 
-// Chain hand-off (T = 9, 11, 13, both GEMMs full-length).  A chain is an ascending-k sequence of f32
-// MFMAs whose C operand is the previous step's result; it may be cut at any k-block and continued
-// on another wave -- even on another SIMD -- from an accumulator parked in LDS, and the result
-// is bit-identical.  The layouts use this to even out the SIMDs' chain loads:
+// Chain hand-off (T = 9, 11, 13, both GEMMs full-length).  A chain is an ascending-k sequence of
+// f32 MFMAs whose C operand is the previous step's result; it may be cut at any k-block and
+// continued on another wave -- even on another SIMD -- from an accumulator parked in LDS, and the
+// result is bit-identical.  The layouts use this to even out the SIMDs' chain loads:
 // * pairs: with 2T chains per GEMM the 16-wave deal leaves SIMDs 0,1 one chain above SIMDs 2,3
 //   (7,7,6,6; the phase lasts 7 chains of a mean 6.5).  The single wave on SIMD 2 (3) that owns
 //   tile T-1 of panel 0 (1) first runs k-blocks [0, S) of tile T-2 of the same panel -- the chain
@@ -618,10 +618,11 @@ __device__ __forceinline__ void panel_a_prefetch_from(__amdgpu_buffer_rsrc_t PA,
 // * one panel per workgroup: T waves put 4,3,3,3 chains on the SIMDs while waves 13..15 idle.
 //   Tile T-1's chain (wave 12, SIMD 0) instead runs as a relay: blocks [0,4) on wave 13 (SIMD 1),
 //   [4,8) on 14 (SIMD 2), [8,T) and the epilogue on wave 12 -- the busiest SIMD carries 3.36
-//   chains (T = 9 likewise: 3,2,2,2 chains, tile 8 over waves 9 -> 10 -> 8).  The relay is a sequential path through three SIMDs (each piece issues at most
-//   every other MFMA slot of its SIMD, plus ~300 cycles per hand-off), so it must stay shorter
-//   than the SIMDs' own chains: raised issue priorities, whole pieces prefetched before the
-//   barrier, and a fourth hop (a 4-way relay) measured slower than none.
+//   chains (T = 9 likewise: 3,2,2,2 chains, tile 8 over waves 9 -> 10 -> 8).  The relay is a
+//   sequential path through three SIMDs (each piece issues at most every other MFMA slot of its
+//   SIMD, plus ~300 cycles per hand-off), so it must stay shorter than the SIMDs' own chains:
+//   raised issue priorities, whole pieces prefetched before the barrier, and a fourth hop (a
+//   4-way relay) measured slower than none.
 // A slot's flag carries the hand-off generation (one per GEMM, counted alike by every wave), so
 // flags are never reset; a receiver waits with a bound (a missing hand-off yields wrong results,
 // caught by the parity tests, rather than a hang).
