@@ -657,9 +657,11 @@ def main():
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         ev0.record(stream)
+        ev_solved = torch.cuda.Event(enable_timing=True)
         for k in range(args.steps):
             step(*inputs(args.warmup + k))
             solver.accumulate_iterations(acc)
+        ev_solved.record(stream)  # every solve enqueued; the last gathers may still be in flight
         drain()
         ev1.record(stream)
         torch.cuda.synchronize(dev)
@@ -667,6 +669,8 @@ def main():
             dist.barrier()
         dt = time.perf_counter() - t0
         kern_ms = ev0.elapsed_time(ev1)
+        # the drain: from the last solve's end to the last gather's completion, on the solve stream
+        drain_ms = ev_solved.elapsed_time(ev1)
         total_iters = int(acc.item())
         iters_host = np.zeros(B, np.int32)
         st = solver.last_stats(iters=iters_host)  # the last step's counters, outside the timed region
@@ -681,13 +685,52 @@ def main():
             dt_all, iters_all, conv_all = float(tmax.item()), float(work[0].item()), float(work[2].item())
         else:
             dt_all, iters_all, conv_all = dt, float(total_iters), float(st["converged"])
+        per_rank = None
+        if world > 1:  # per-rank step time, device time and drain, for attributing a scaling loss
+            mine = torch.tensor([dt / args.steps * 1e3, kern_ms / args.steps, drain_ms], dtype=torch.float64,
+                                device=comm_dev)
+            allr = [torch.empty_like(mine) for _ in range(world)]
+            dist.all_gather(allr, mine)
+            per_rank = [[float(v) for v in t.cpu()] for t in allr]
         return dict(dt=dt_all, iters_all=iters_all, converged_all=conv_all, total_iters=total_iters,
-                    kern_ms=kern_ms, st=st, iters_host=iters_host, plan=solver.phase_plan())
+                    kern_ms=kern_ms, st=st, iters_host=iters_host, plan=solver.phase_plan(),
+                    drain_ms=drain_ms, per_rank=per_rank)
+
+    def gather_ms(reps=3):
+        """One step's gather of (z*, y*) to rank 0 on its own: barrier, blocking gather, device
+        sync; the best of ``reps`` (after the timed regions; max over ranks)."""
+        sl = slots[0]
+        best = 1e30
+        for _ in range(reps):
+            dist.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            dist.gather(sl["packed"], sl["gl"], dst=0)
+            torch.cuda.synchronize(dev)
+            best = min(best, (time.perf_counter() - t0) * 1e3)
+        t = torch.tensor([best], dtype=torch.float64, device=comm_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
 
     fresh_run = timed(lambda k: fresh[k])
     repeat_run = timed(lambda k: (dM, dg))
     head = repeat_run if args.repeat_inputs else fresh_run
     side = fresh_run if args.repeat_inputs else repeat_run
+    multi = None
+    if world > 1:
+        pr = head["per_rank"]
+        multi = {
+            "per_rank_step_ms": [r[0] for r in pr],
+            "per_rank_kernel_ms": [r[1] for r in pr],
+            "solve_ms_min": min(r[1] for r in pr), "solve_ms_max": max(r[1] for r in pr),
+            "drain_ms_max": max(r[2] for r in pr),
+            "gather_ms": gather_ms(),
+            "gather_bytes_per_rank": B * (n + m) * 4,
+            "backend": args.dist_backend,
+            "note": "per_rank_kernel_ms: device time per step on each rank's solve stream (solve + "
+                    "resets + gather copies); drain_ms: last solve's end to the last gather's completion; "
+                    "gather_ms: one blocking gather of a step's (z*, y*) measured alone after the timed "
+                    "regions (max over ranks)"}
 
     # CPU reference on rank 0 (all ranks' timed regions are over: the barrier above)
     ref = None
@@ -788,7 +831,9 @@ def main():
                                    f"shared ML/G, Algorithm 1 eps={args.tol}, K=10",
                        "batch_per_gpu": B, "global_batch": B * world, "n": n, "m": m,
                        "inputs": "repeated" if args.repeat_inputs else "fresh per step",
-                       "parallelism": f"instance-sharded x{world}, RCCL gather"},
+                       "parallelism": (f"instance-sharded x{world}, "
+                                       + ("RCCL gather" if args.dist_backend == "nccl" else "gloo gather")
+                                       if world > 1 else "single GPU (no gather)")},
             "qp_solves_per_s": solves,
             "mean_iters_to_eps": mean_iters,
             ("value_fresh_inputs" if args.repeat_inputs else "value_repeated_inputs"): side_value,
@@ -801,6 +846,7 @@ def main():
                           "certified (DESIGN.md section 3)",
             "batching": util,
             "converged": int(head["converged_all"]),
+            "multi_gpu": multi,
             "kernel": st["kernel"],
             "single_instance": singles["c2"],
             "single_instance_c1": singles["c1"],

@@ -64,6 +64,9 @@ struct gpad_group_s {
     std::vector<size_t> vec_bytes;
     std::vector<void*> mat;          // per device: raw ML | G before packing
     std::vector<size_t> mat_bytes;
+    hipStream_t caller = nullptr;    // the caller's stream on devices[0] (gpad_group_set_stream;
+                                     // NULL = the device's null stream)
+    hipEvent_t caller_ev = nullptr;  // recorded on it before the group touches device buffers
 };
 
 namespace {
@@ -77,6 +80,10 @@ int release(gpad_group_s* g) {
         if (d < (int)g->mat.size() && g->mat[d]) (void)hipFree(g->mat[d]);
         if (d < (int)g->ev.size() && g->ev[d]) (void)hipEventDestroy(g->ev[d]);
         if (d < (int)g->st.size() && g->st[d]) (void)hipStreamDestroy(g->st[d]);
+    }
+    if (g->caller_ev) {
+        (void)hipSetDevice(g->dev[0]);
+        (void)hipEventDestroy(g->caller_ev);
     }
     for (ncclComm_t c : g->comm) (void)ncclCommDestroy(c);
     delete g;
@@ -150,6 +157,19 @@ int gather(gpad_group_s* g, const std::vector<Move>& mv) {
     return GPAD_OK;
 }
 
+// Device-memory callers produce their buffers on their own stream of devices[0]; the group's
+// streams are non-blocking, so every one of them first waits for the work queued there so far
+// (else a producer kernel still in flight could race with the scatter or the root's solve).
+int order_after_caller(gpad_group_s* g) {
+    G_HIP(hipSetDevice(g->dev[0]));
+    G_HIP(hipEventRecord(g->caller_ev, g->caller));
+    for (int d = 0; d < g->ndev; ++d) {
+        G_HIP(hipSetDevice(g->dev[d]));
+        G_HIP(hipStreamWaitEvent(g->st[d], g->caller_ev, 0));
+    }
+    return GPAD_OK;
+}
+
 int sync_all(gpad_group_s* g) {
     for (int d = 0; d < g->ndev; ++d) {
         G_HIP(hipSetDevice(g->dev[d]));
@@ -193,6 +213,11 @@ int gpad_group_create(gpad_group_t* out, int ndev, const int* devices) {
             return rc;
         }
     }
+    if (hipSetDevice(g->dev[0]) != hipSuccess ||
+        hipEventCreateWithFlags(&g->caller_ev, hipEventDisableTiming) != hipSuccess) {
+        release(g);
+        return gfail(GPAD_ERR_HIP, "gpad_group_create: event creation failed");
+    }
     std::vector<int> sorted(g->dev);
     std::sort(sorted.begin(), sorted.end());
     const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
@@ -219,6 +244,12 @@ int gpad_group_transport(gpad_group_t g) {
     return g->comm.empty() ? GPAD_GROUP_PEER : GPAD_GROUP_RCCL;
 }
 
+int gpad_group_set_stream(gpad_group_t g, void* hip_stream) {
+    if (!g) return gfail(GPAD_ERR_INVALID, "gpad_group_set_stream: null group");
+    g->caller = static_cast<hipStream_t>(hip_stream);
+    return GPAD_OK;
+}
+
 int gpad_group_setup(gpad_group_t g, const gpad_dims_t* dims, const void* ML, const void* G, double L) {
     if (!g || !dims || !ML || !G) return gfail(GPAD_ERR_INVALID, "gpad_group_setup: bad arguments");
     if (dims->batch < 1 || dims->n <= 0 || dims->m <= 0)
@@ -237,6 +268,7 @@ int gpad_group_setup(gpad_group_t g, const gpad_dims_t* dims, const void* ML, co
     std::vector<Move> mv;
     std::vector<const void*> mlp(nd), gp(nd);
     int rc;
+    if (!host && (rc = order_after_caller(g))) return rc;
     for (int d = 0; d < nd; ++d) {
         const int c = std::max(g->count[d], 1);
         const size_t per = dims->shared ? nm : nm * (size_t)c;  // each of ML and G
@@ -302,6 +334,7 @@ int gpad_group_run(gpad_group_t g, void* z0, void* y0, const void* M, const void
     std::vector<char*> Mp(nd), gp(nd), zp(nd), yp(nd);
     std::vector<Move> in, out;
     int rc;
+    if (!host && (rc = order_after_caller(g))) return rc;
     for (int d = 0; d < nd; ++d) {
         const size_t c = (size_t)g->count[d], s0 = (size_t)g->start[d];
         if (!host && d == 0) {  // root shard in place
@@ -348,6 +381,8 @@ int gpad_group_run(gpad_group_t g, void* z0, void* y0, const void* M, const void
         }
     }
     if ((rc = sync_all(g))) return rc;
+    for (int d = 0; d < nd; ++d)  // device-side failures of any shard fail the run (GPAD_ERR_DEVICE)
+        if (g->count[d] > 0 && (rc = gpad_sync(g->h[d]))) return rc;
     if (st) {  // per-shard counters (host copies), aggregated; st->iters [batch] in global order
         gpad_stats_t tot{};
         tot.iters = nullptr;
@@ -361,6 +396,8 @@ int gpad_group_run(gpad_group_t g, void* z0, void* y0, const void* M, const void
             tot.total_iterations += sd.total_iterations;
             tot.kernel = sd.kernel;
             tot.kernel_ms = std::max(tot.kernel_ms, sd.kernel_ms);
+            tot.tol_floor = std::max(tot.tol_floor, sd.tol_floor);
+            tot.flags |= sd.flags;
         }
         int* keep = st->iters;
         *st = tot;

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstddef>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -114,6 +115,12 @@ struct gpad_handle_s {
     int sched_len = 0, sched_kind = -1, sched_dtype = -1;
     DevBuf work, counters, pwork;
     std::vector<int> h_counts;
+    // run status block on the device, zeroed per run: {int error bits (gpad::kDevErr*), pad,
+    // double max |g|} -- the error word the kernels report into and the certification floor's
+    // data term (include/gpad.h gpad_run)
+    DevBuf status;
+    double last_tol = 0.0;          // tol of the last run
+    double last_floor_scale = 0.0;  // tol_floor = this * max |g| (margin * L * |gscale|)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int last_kernel = 0, last_batch = 0, last_steps = 1;
     // phased panel solves: the plan made from the previous solve (gpad::panel_plan)
@@ -143,6 +150,38 @@ struct gpad_handle_s {
     gpad::Tuning tune;                  // gpad_set_option
 };
 
+// Run status block (gpad_handle_s::status): zeroed before a run's first launch.
+struct RunStatus {
+    int err;
+    int pad;
+    double gmax;
+};
+
+static int reset_status(gpad_handle_t h, double tol, double floor_scale) {
+    int rc = h->status.ensure(sizeof(RunStatus));
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(h->status.p, 0, sizeof(RunStatus), h->stream));
+    h->last_tol = tol;
+    h->last_floor_scale = floor_scale;
+    return GPAD_OK;
+}
+
+// Enqueue the copy of the status block to *rs (the caller synchronises the stream).
+static int fetch_status(gpad_handle_t h, RunStatus* rs) {
+    *rs = RunStatus{};
+    if (!h->status.p) return GPAD_OK;
+    HIP_TRY(hipMemcpyAsync(rs, h->status.p, sizeof(RunStatus), hipMemcpyDeviceToHost, h->stream));
+    return GPAD_OK;
+}
+
+static int status_error(const RunStatus& rs) {
+    if (rs.err == 0) return GPAD_OK;
+    return fail(GPAD_ERR_DEVICE, std::string("device error bits 0x") + std::to_string(rs.err) +
+                                     ((rs.err & gpad::kDevErrHandoff) ? ": a chain hand-off wait expired "
+                                                                        "(the run's results are invalid)"
+                                                                      : ""));
+}
+
 extern "C" {
 
 const char* gpad_version(void) { return "gpad-mi355x 0.2 (gfx950)"; }
@@ -162,6 +201,7 @@ const char* gpad_strerror(int status) {
         case GPAD_ERR_UNSUPPORTED: return "unsupported shape/kernel combination";
         case GPAD_ERR_NOT_SETUP: return "gpad_run before gpad_setup";
         case GPAD_ERR_NO_DEVICE: return "no HIP device";
+        case GPAD_ERR_DEVICE: return "device-side failure (results invalid)";
         default: return "unknown status";
     }
 }
@@ -206,6 +246,7 @@ int gpad_destroy(gpad_handle_t h) {
     h->work.release();
     h->counters.release();
     h->pwork.release();
+    h->status.release();
     h->plant.release();
     h->state.release();
     if (h->ev0) (void)hipEventDestroy(h->ev0);
@@ -260,14 +301,19 @@ int gpad_set_option(gpad_handle_t h, int option, int value) {
             h->plan.nph = 0;
             h->plan_key = 0;
             return set(t.plan_fin_cost, 1, 10000, def.plan_fin_cost);
+        case GPAD_OPT_DEBUG_DROP_HANDOFF: return set(t.debug_drop_handoff, 0, 1, def.debug_drop_handoff);
         default: return fail(GPAD_ERR_INVALID, "gpad_set_option: unknown option");
     }
 }
 
 int gpad_sync(gpad_handle_t h) {
     if (!h) return fail(GPAD_ERR_INVALID, "gpad_sync: null handle");
+    HIP_TRY(hipSetDevice(h->device));
+    RunStatus rs;
+    int rc = fetch_status(h, &rs);
+    if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(h->stream));
-    return GPAD_OK;
+    return status_error(rs);
 }
 
 int gpad_schedule(int N, int kind, double* theta, double* beta) {
@@ -291,6 +337,7 @@ static int validate_dims(const gpad_dims_t* d) {
     if (d->kernel == GPAD_KERNEL_CONDENSED && (d->dtype != GPAD_DTYPE_F32 || !gpad::condensed_supported(d->n, d->m)))
         return fail(GPAD_ERR_UNSUPPORTED, "dims: the condensed kernel needs f32, m <= 208, n <= 256");
     if (!std::isfinite(d->tol_gap)) return fail(GPAD_ERR_INVALID, "dims: tol_gap must be finite");
+    if (d->reserved != 0) return fail(GPAD_ERR_INVALID, "dims: reserved must be 0");
     return GPAD_OK;
 }
 
@@ -528,6 +575,9 @@ static int collect_stats(gpad_handle_t h, gpad_stats_t* st) {
     h->h_counts.resize(2 * entries);
     HIP_TRY(hipMemcpyAsync(h->h_counts.data(), h->counters.p, sizeof(int) * 2 * entries,
                            hipMemcpyDeviceToHost, h->stream));
+    RunStatus rs;
+    int rc = fetch_status(h, &rs);
+    if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(h->stream));
     st->iterations = 0;
     st->converged = 0;
@@ -550,7 +600,9 @@ static int collect_stats(gpad_handle_t h, gpad_stats_t* st) {
     float ms = 0.0f;
     st->kernel_ms = 0.0;
     if (h->timed && hipEventElapsedTime(&ms, h->ev0, h->ev1) == hipSuccess) st->kernel_ms = ms;
-    return GPAD_OK;
+    st->tol_floor = h->last_tol > 0.0 ? h->last_floor_scale * rs.gmax : 0.0;
+    st->flags = (h->last_tol > 0.0 && h->last_tol < st->tol_floor) ? GPAD_FLAG_TOL_FLOOR : 0;
+    return status_error(rs);
 }
 
 int gpad_accumulate_iterations(gpad_handle_t h, long long* acc) {
@@ -638,6 +690,12 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
     a.Hc = h->Hc_ok ? (const float*)h->Hc.p : nullptr;
     a.hfrag = h->Hfrag_ok ? h->Hfrag.p : nullptr;
     a.strideH = d.shared ? 0 : (long long)m * h->ldm;
+    a.err = (int*)h->status.p;
+    a.debug = h->tune.debug_drop_handoff ? gpad::kDebugDropHandoff : 0;
+    if (tol > 0.0)  // the certification floor's data term (stats: tol_floor, GPAD_FLAG_TOL_FLOOR)
+        HIP_TRY(gpad::launch_absmax<T>(dg, (long long)batch * m,
+                                       reinterpret_cast<double*>((char*)h->status.p + offsetof(RunStatus, gmax)),
+                                       h->stream));
     int kernel = d.kernel;
     const bool prev_phased = h->last_phased;  // the previous launch's counts are still in `iters`
     h->last_phased = false;  // set again below when this launch is a phased panel solve
@@ -802,6 +860,8 @@ static int run_typed(gpad_handle_t h, T* z, T* y, const T* M, const T* g, int N,
     }
     int* iters = (int*)h->counters.p;
     int kernel = 0;
+    const double margin = sizeof(T) == sizeof(float) ? gpad::ViolMargin<float>::value : gpad::ViolMargin<double>::value;
+    if ((rc = reset_status(h, tol, margin * h->L * (scaled_vec ? 1.0 : 1.0 / h->L)))) return rc;
     if (h->plan_pending && hipEventQuery(h->plan_ev) == hipSuccess) {  // a previous solve's counts landed
         if (h->plan_pending_batch == batch) update_plan(h, h->plan_pin, batch, h->plan_pending_N);
         h->plan_pending = false;
@@ -817,6 +877,10 @@ static int run_typed(gpad_handle_t h, T* z, T* y, const T* M, const T* g, int N,
     if (!st && h->last_phased && h->tune.plan) {  // asynchronous run: counts to the host behind it
         const size_t want = sizeof(int) * (size_t)batch;
         if (h->plan_pin_cap < want) {
+            if (h->plan_pending) {  // the previous run's copy into the old buffer must land first
+                HIP_TRY(hipEventSynchronize(h->plan_ev));
+                h->plan_pending = false;
+            }
             if (h->plan_pin) (void)hipHostFree(h->plan_pin);
             h->plan_pin = nullptr;
             h->plan_pin_cap = 0;
@@ -830,12 +894,18 @@ static int run_typed(gpad_handle_t h, T* z, T* y, const T* M, const T* g, int N,
         h->plan_pending_N = N;
         h->plan_pending_batch = batch;
     }
+    if (st) {
+        if (d.memory == GPAD_MEM_HOST) {
+            HIP_TRY(hipMemcpyAsync(z, dz, zb, hipMemcpyDeviceToHost, h->stream));
+            HIP_TRY(hipMemcpyAsync(y, dy, yb, hipMemcpyDeviceToHost, h->stream));
+        }
+        return collect_stats(h, st);  // synchronises; a device error fails the run
+    }
     if (d.memory == GPAD_MEM_HOST) {
         HIP_TRY(hipMemcpyAsync(z, dz, zb, hipMemcpyDeviceToHost, h->stream));
         HIP_TRY(hipMemcpyAsync(y, dy, yb, hipMemcpyDeviceToHost, h->stream));
-        HIP_TRY(hipStreamSynchronize(h->stream));
+        return gpad_sync(h);
     }
-    if (st) return collect_stats(h, st);
     return GPAD_OK;
 }
 
@@ -867,6 +937,13 @@ int gpad_run(gpad_handle_t h, void* z0, void* y0, const void* M, const void* g, 
 int gpad_run_scaled(gpad_handle_t h, void* z0, void* y0, const void* gP, const void* pD, int N,
                     double tol, const void* theta, const void* beta, gpad_stats_t* st) {
     return run_impl(h, z0, y0, gP, pD, N, tol, theta, beta, true, st);
+}
+
+// field by field: a stack-built dims may carry different padding bytes on every call
+static bool same_dims(const gpad_dims_t& a, const gpad_dims_t& b) {
+    return a.n == b.n && a.m == b.m && a.batch == b.batch && a.shared == b.shared && a.dtype == b.dtype &&
+           a.memory == b.memory && a.schedule == b.schedule && a.check_every == b.check_every &&
+           a.kernel == b.kernel && a.reserved == b.reserved && a.tol_gap == b.tol_gap;
 }
 
 int gpad_solve(void* z0, void* y0, const void* ML, const void* M, const void* G, const void* g, int N,
@@ -901,8 +978,8 @@ int gpad_solve(void* z0, void* y0, const void* ML, const void* M, const void* G,
     const bool host = dims->memory == GPAD_MEM_HOST;
     const size_t bytes = (size_t)dims->n * dims->m * esize(dims->dtype) * (dims->shared ? 1 : dims->batch);
     bool same = false;
-    if (host && h->ready && h->shadow_ok && L == h->shadow_L &&
-        std::memcmp(&h->shadow_dims, dims, sizeof(gpad_dims_t)) == 0 && h->shadow.size() == 2 * bytes)
+    if (host && h->ready && h->shadow_ok && L == h->shadow_L && same_dims(h->shadow_dims, *dims) &&
+        h->shadow.size() == 2 * bytes)
         same = std::memcmp(h->shadow.data(), ML, bytes) == 0 && std::memcmp(h->shadow.data() + bytes, G, bytes) == 0;
     if (!same) {
         if ((rc = gpad_setup(h, dims, ML, G, L))) return rc;
@@ -1082,6 +1159,8 @@ static int state_typed(gpad_handle_t h, T* x, T* z, T* y, int steps, int N, doub
     const T* P = (const T*)h->plant.p;
     int* counters = (int*)h->counters.p;
     int kernel = 0;
+    const double margin = sizeof(T) == sizeof(float) ? gpad::ViolMargin<float>::value : gpad::ViolMargin<double>::value;
+    if ((rc = reset_status(h, tol, margin))) return rc;  // g(x) unscaled: margin * L * (1/L)
     HIP_TRY(hipEventRecord(h->ev0, h->stream));
     T* xc = xa;
     T* xnext = xb;
@@ -1113,7 +1192,7 @@ static int state_typed(gpad_handle_t h, T* x, T* z, T* y, int steps, int N, doub
         HIP_TRY(hipMemcpyAsync(y, dy, sizeof(T) * yn, hipMemcpyDeviceToHost, h->stream));
         if (xsn) HIP_TRY(hipMemcpyAsync(xs, dxs, sizeof(T) * xsn, hipMemcpyDeviceToHost, h->stream));
         if (usn) HIP_TRY(hipMemcpyAsync(us, dus, sizeof(T) * usn, hipMemcpyDeviceToHost, h->stream));
-        HIP_TRY(hipStreamSynchronize(h->stream));
+        if (!st) return gpad_sync(h);
     }
     if (st) return collect_stats(h, st);
     return GPAD_OK;

@@ -32,7 +32,14 @@ struct Tuning {
                               // (the longest-predicted survivors; -1: default)
     int cpanel = 1;           // GPAD_OPT_CONDENSED_PANEL: condensed batches on the MFMA panels
     int plan_fin_cost = 100;  // GPAD_OPT_PLAN_FIN_COST: the plan model's finisher cost, percent
+    int debug_drop_handoff = 0;  // GPAD_OPT_DEBUG_DROP_HANDOFF: test-only fault injection
 };
+
+// Device error word of a run (SolveArgs::err): kernels OR these bits in with a vector atomic;
+// the host turns a non-zero word into GPAD_ERR_DEVICE when it collects or syncs the run.
+constexpr int kDevErrHandoff = 1;  // a chain hand-off wait expired (gpad_panel.hip handoff_wait)
+// SolveArgs::debug bits (fault injection for tests; 0 in production)
+constexpr int kDebugDropHandoff = 1;  // the first hand-off helper skips its first post
 
 // Rounding margin of the Algorithm 1 decisions, in units of max_i(|chain_i| + |pD_i|): a test
 // passes when L max(chain + pD) + kViolMargin L max(|chain| + |pD|) <= tol (16 units of 2^-24 /
@@ -96,6 +103,8 @@ struct SolveArgs {
     const float* Hc;       // condensed operator H = G_L (-ML), k-major [m][ldm] (gpad_condensed.hip)
     const void* hfrag;     // H in the panel fragment layout (gpad_cpanel.hip), or null
     long long strideH;     // elements between consecutive instances' H images (0 = shared)
+    int* err;              // device error word (kDevErr* bits), never null on a solve launch
+    int debug;             // kDebug* fault-injection bits (tests only)
 };
 
 // launchers (return hipError_t of the launch)
@@ -177,6 +186,9 @@ hipError_t launch_precompute(int n, int m, int nf, const double* H, long long sH
                              int count, hipStream_t s);
 hipError_t launch_apply_inv(int n, int batch, const double* Hinv, const double* f, double* gP, hipStream_t s);
 hipError_t launch_accumulate_iters(const int* iters, long long count, long long* acc, hipStream_t s);
+// *out = max(*out, max |g_i|) over count elements (device double; zero it before the first call)
+template <typename T>
+hipError_t launch_absmax(const T* g, long long count, double* out, hipStream_t s);
 // flat battery data on the MFMA pipe (gpad_flatpanel.hip): per-cell skinny GEMMs over panels
 bool flatpanel_supported(int n, int m, int n_u);
 size_t flatpanel_frag_bytes(int n, int m, int n_u);

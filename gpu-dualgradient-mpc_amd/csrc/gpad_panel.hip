@@ -624,8 +624,8 @@ __device__ __forceinline__ void panel_a_prefetch_from(__amdgpu_buffer_rsrc_t PA,
 //   raised issue priorities, whole pieces prefetched before the barrier, and a fourth hop (a
 //   4-way relay) measured slower than none.
 // A slot's flag carries the hand-off generation (one per GEMM, counted alike by every wave), so
-// flags are never reset; a receiver waits with a bound (a missing hand-off yields wrong results,
-// caught by the parity tests, rather than a hang).
+// flags are never reset; a receiver waits with a bound, and a wait that expires fails the run
+// (handoff_wait: GPAD_ERR_DEVICE) rather than hanging the GPU or returning stale results.
 template <int T>
 struct Handoff {
     // pairs: odd T with singles on waves 12..15 (T = 9, 11, 13: SIMD loads 5,5,4,4 / 6,6,5,5 /
@@ -651,12 +651,18 @@ struct HoSlots {
     int in, out;  // LDS hand-off slots taken / given (-1: none)
 };
 
+// The waves of a workgroup are co-resident, so a post always arrives unless the layout logic is
+// broken; the wait is still bounded (2^20 sleeps, ~30 ms) so that such a bug cannot hang the GPU,
+// and an expired wait sets kDevErrHandoff in the run's error word: the host then fails the run
+// with GPAD_ERR_DEVICE instead of returning the stale accumulator's results as GPAD_OK.
 template <int T>
-__device__ __forceinline__ f32x4 handoff_wait(Panel2Lds<T>& L, int slot, int gen, int lane) {
-    for (int s = 0; s < (1 << 20); ++s) {
+__device__ __forceinline__ f32x4 handoff_wait(Panel2Lds<T>& L, int slot, int gen, int lane, int* err) {
+    int s = 0;
+    for (; s < (1 << 20); ++s) {
         if (__hip_atomic_load(&L.hflag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == gen) break;
         __builtin_amdgcn_s_sleep(1);
     }
+    if (s == (1 << 20) && lane == 0) atomicOr(err, kDevErrHandoff);  // uniform: s is
     asm volatile("" ::: "memory");
     const float4 hv = L.hand[slot][lane];
     return f32x4{hv.x, hv.y, hv.z, hv.w};
@@ -671,14 +677,17 @@ __device__ __forceinline__ void handoff_post(Panel2Lds<T>& L, int slot, int gen,
 
 // a piece of another wave's chain: k-blocks [KB0, KB1) (KB1 < T) of the tile at voff, continued
 // from slot hs.in (or from zero), parked in slot hs.out; PRIO raises the wave's issue priority
+// drop: fault injection (kDebugDropHandoff) -- the first piece of the first hand-off withholds
+// its post, so its receiver's wait expires
 template <int T, int PD, int KB0, int KB1, bool PRIO>
 __device__ __forceinline__ void handoff_piece(Panel2Lds<T>& L, __amdgpu_buffer_rsrc_t PA, const float4* B0, int voff,
-                                              int lane, const float4 (&aph)[PD], HoSlots hs, int gen) {
+                                              int lane, const float4 (&aph)[PD], HoSlots hs, int gen, int* err,
+                                              bool drop) {
     f32x4 h = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    if (hs.in >= 0) h = handoff_wait(L, hs.in, gen, lane);
+    if (hs.in >= 0) h = handoff_wait(L, hs.in, gen, lane, err);
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
     panel_chain<T, PD, KB0, KB1>(PA, B0, voff, lane, h, aph, 4);
-    handoff_post(L, hs.out, gen, lane, h);
+    if (!(drop && gen == 1 && hs.in < 0)) handoff_post(L, hs.out, gen, lane, h);
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
@@ -686,8 +695,8 @@ __device__ __forceinline__ void handoff_piece(Panel2Lds<T>& L, __amdgpu_buffer_r
 template <int T, int PD, int KB0, bool PRIO>
 __device__ __forceinline__ void handoff_take(Panel2Lds<T>& L, __amdgpu_buffer_rsrc_t PA, const float4* B0, int voff,
                                              int lane, const float4 (&ap)[PD], HoSlots hs, int gen, int kq,
-                                             f32x4& acc) {
-    acc = handoff_wait(L, hs.in, gen, lane);
+                                             f32x4& acc, int* err) {
+    acc = handoff_wait(L, hs.in, gen, lane, err);
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(2);
     panel_chain<T, PD, KB0, T>(PA, B0, voff, lane, acc, ap, kq);
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
@@ -723,6 +732,8 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
     const bool on1 = 16 * t < n, on2 = 16 * t < m;
     const int voff_r = voff - 1024;  // helper: the receiver's tile t - 1 (Handoff)
     int hgen = 0;                    // hand-off generation, counted alike by helper and receiver
+    // fault injection (tests): the first workgroup's first piece withholds its first post
+    const bool drop = (a.debug & kDebugDropHandoff) && blockIdx.x == 0;
 
     for (int it = blockIdx.x; it < items; it += gridDim.x) {
         // columns still running, bit 16 pp + c for panel pp of this item: the same word in every
@@ -807,9 +818,9 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 f32x4 acc[2];
                 ++hgen;
                 if constexpr (ROLE == 1)
-                    handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA1, L.Wl[p0], voff_r, lane, aph, hs, hgen);
+                    handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA1, L.Wl[p0], voff_r, lane, aph, hs, hgen, a.err, drop);
                 if constexpr (ROLE == 2)
-                    handoff_take<T, PD, KB0, PRIO>(L, PA1, L.Wl[p0], voff, lane, ap, hs, hgen, kq1, acc[0]);
+                    handoff_take<T, PD, KB0, PRIO>(L, PA1, L.Wl[p0], voff, lane, ap, hs, hgen, kq1, acc[0], a.err);
                 else if (on1 && nkb1 == T)
                     panel_gemm3<T, NU == 2, PD>(PA1, L.Wl[p0], L.Wl[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1],
                                                 ap, kq1);
@@ -838,7 +849,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 }
             } else if constexpr (ROLE == 3) {
                 ++hgen;
-                handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA1, L.Wl[p0], voff, lane, aph, hs, hgen);
+                handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA1, L.Wl[p0], voff, lane, aph, hs, hgen, a.err, drop);
                 prefetch(PA2);
             }
             __syncthreads();
@@ -856,9 +867,9 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 f32x4 acc[2];
                 ++hgen;
                 if constexpr (ROLE == 1)
-                    handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA2, L.Zh[p0], voff_r, lane, aph, hs, hgen);
+                    handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA2, L.Zh[p0], voff_r, lane, aph, hs, hgen, a.err, drop);
                 if constexpr (ROLE == 2)
-                    handoff_take<T, PD, KB0, PRIO>(L, PA2, L.Zh[p0], voff, lane, ap, hs, hgen, kq2, acc[0]);
+                    handoff_take<T, PD, KB0, PRIO>(L, PA2, L.Zh[p0], voff, lane, ap, hs, hgen, kq2, acc[0], a.err);
                 else if (on2 && nkb2 == T)
                     panel_gemm3<T, NU == 2, PD>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1],
                                                 ap, kq2);
@@ -868,7 +879,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 else
                     acc[0] = acc[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
                 prefetch(PA1);
-                // (reading these LDS operands before the GEMM measured no faster: tools/r2_epi2.sh)
+                // (reading these LDS operands before the GEMM measured no faster: profiles/r02_epilogue_ab.txt)
                 float4 w4[Q], p4[Q];
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
@@ -941,7 +952,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 }
             } else if constexpr (ROLE == 3) {
                 ++hgen;
-                handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA2, L.Zh[p0], voff, lane, aph, hs, hgen);
+                handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA2, L.Zh[p0], voff, lane, aph, hs, hgen, a.err, drop);
                 prefetch(PA1);
             }
             th = th_next;

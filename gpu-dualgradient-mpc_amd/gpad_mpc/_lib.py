@@ -14,6 +14,8 @@ LIB_PATH = os.path.join(HERE, "libgpad.so")
 
 GPAD_OK = 0
 ERR_INVALID, ERR_HIP, ERR_NOMEM, ERR_UNSUPPORTED, ERR_NOT_SETUP, ERR_NO_DEVICE = -1, -2, -3, -4, -5, -6
+ERR_DEVICE = -7  # a kernel reported a device-side failure (include/gpad.h)
+FLAG_TOL_FLOOR = 1  # gpad_stats_t.flags: tol below the certification floor
 SCHEDULE_MATLAB, SCHEDULE_PAPER = 0, 1
 MEM_HOST, MEM_DEVICE = 0, 1
 DTYPE_F32, DTYPE_F64 = 0, 1
@@ -34,7 +36,7 @@ EXPORTS = [
     "gpad_setup_flat", "gpad_step2_primal_flat", "gpad_step4_project_flat", "gpad_precompute",
     "gpad_accumulate_iterations", "gpad_set_option",
     "gpad_group_create", "gpad_group_destroy", "gpad_group_transport", "gpad_group_setup", "gpad_group_run",
-    "gpad_solve_sharded", "gpad_device_count",
+    "gpad_solve_sharded", "gpad_device_count", "gpad_group_set_stream",
 ]
 GROUP_RCCL, GROUP_PEER = 1, 2
 
@@ -45,12 +47,14 @@ OPT_PANEL_MAX_GRID, OPT_DUO_MAX_GRID, OPT_FLAT_PANEL_MIN, OPT_FLAT_PANELS = 7, 8
 OPT_FLAT_WAVES, OPT_FLAT_A_LDS, OPT_FINISH_SOLO = 11, 12, 13
 OPT_CONDENSED_PANEL = 14
 OPT_PLAN_FIN_COST = 15
+OPT_DEBUG_DROP_HANDOFF = 16  # test-only fault injection
 OPTIONS = {"phase_len": OPT_PHASE_LEN, "finish_thresh": OPT_FINISH_THRESH, "plan": OPT_PLAN,
            "phased": OPT_PHASED, "finisher": OPT_FINISHER, "lpt": OPT_LPT,
            "panel_max_grid": OPT_PANEL_MAX_GRID, "duo_max_grid": OPT_DUO_MAX_GRID,
            "flat_panel_min": OPT_FLAT_PANEL_MIN, "flat_panels": OPT_FLAT_PANELS,
            "flat_waves": OPT_FLAT_WAVES, "flat_a_lds": OPT_FLAT_A_LDS, "finish_solo": OPT_FINISH_SOLO,
-           "condensed_panel": OPT_CONDENSED_PANEL, "plan_fin_cost": OPT_PLAN_FIN_COST}
+           "condensed_panel": OPT_CONDENSED_PANEL, "plan_fin_cost": OPT_PLAN_FIN_COST,
+           "debug_drop_handoff": OPT_DEBUG_DROP_HANDOFF}
 
 FILE_ROWMAJOR, FILE_FLIPPED, FILE_FLAT = 0, 1, 2
 
@@ -58,13 +62,15 @@ FILE_ROWMAJOR, FILE_FLIPPED, FILE_FLAT = 0, 1, 2
 class Dims(C.Structure):
     _fields_ = [("n", C.c_int), ("m", C.c_int), ("batch", C.c_int), ("shared", C.c_int),
                 ("dtype", C.c_int), ("memory", C.c_int), ("schedule", C.c_int),
-                ("check_every", C.c_int), ("kernel", C.c_int), ("tol_gap", C.c_double)]
+                ("check_every", C.c_int), ("kernel", C.c_int), ("reserved", C.c_int),
+                ("tol_gap", C.c_double)]
 
 
 class Stats(C.Structure):
     _fields_ = [("iterations", C.c_int), ("converged", C.c_int),
                 ("total_iterations", C.c_longlong), ("kernel", C.c_int),
-                ("kernel_ms", C.c_double), ("iters", C.POINTER(C.c_int))]
+                ("kernel_ms", C.c_double), ("iters", C.POINTER(C.c_int)),
+                ("tol_floor", C.c_double), ("flags", C.c_int)]
 
 
 class DataFile(C.Structure):
@@ -134,6 +140,7 @@ def load(path: str | None = None) -> C.CDLL:
     L.gpad_group_create.argtypes = [C.POINTER(vp), i, ip]
     L.gpad_group_destroy.argtypes = [vp]
     L.gpad_group_transport.argtypes = [vp]
+    L.gpad_group_set_stream.argtypes = [vp, vp]
     L.gpad_group_setup.argtypes = [vp, C.POINTER(Dims), cvp, cvp, d]
     L.gpad_group_run.argtypes = [vp, vp, vp, cvp, cvp, i, d, C.POINTER(Stats)]
     L.gpad_solve_sharded.argtypes = [i, ip, vp, vp, cvp, cvp, cvp, cvp, i, d, d, C.POINTER(Dims), C.POINTER(Stats)]
@@ -147,7 +154,7 @@ def load(path: str | None = None) -> C.CDLL:
                  "gpad_datafile_write", "gpad_setup_flat", "gpad_step2_primal_flat",
                  "gpad_step4_project_flat", "gpad_precompute", "gpad_accumulate_iterations",
                  "gpad_set_option", "gpad_group_create", "gpad_group_destroy", "gpad_group_transport",
-                 "gpad_group_setup", "gpad_group_run", "gpad_solve_sharded"]:
+                 "gpad_group_set_stream", "gpad_group_setup", "gpad_group_run", "gpad_solve_sharded"]:
         getattr(L, name).restype = i
     _LIB = L
     return L

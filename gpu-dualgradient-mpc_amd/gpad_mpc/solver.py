@@ -189,7 +189,8 @@ class GpadSolver:
     def _stats_dict(st: Stats) -> dict:
         return dict(iterations=st.iterations, converged=st.converged,
                     total_iterations=st.total_iterations, kernel=_lib.KERNEL_NAMES.get(st.kernel),
-                    kernel_ms=st.kernel_ms)
+                    kernel_ms=st.kernel_ms, tol_floor=st.tol_floor,
+                    below_tol_floor=bool(st.flags & _lib.FLAG_TOL_FLOOR))
 
     def sync(self) -> None:
         check(self.lib.gpad_sync(self.h), "gpad_sync")

@@ -26,7 +26,8 @@ extern "C" {
 #endif
 
 #define GPAD_VERSION_MAJOR 0
-#define GPAD_VERSION_MINOR 1
+#define GPAD_VERSION_MINOR 3 /* 0.3: gpad_stats_t gained tol_floor / flags, gpad_dims_t an explicit reserved
+                              * word (layouts changed: rebuild callers against this header) */
 
 /* status codes */
 #define GPAD_OK 0
@@ -36,6 +37,11 @@ extern "C" {
 #define GPAD_ERR_UNSUPPORTED (-4)  /* shape/kernel combination not supported            */
 #define GPAD_ERR_NOT_SETUP (-5)    /* gpad_run before gpad_setup                        */
 #define GPAD_ERR_NO_DEVICE (-6)    /* no HIP device visible                             */
+#define GPAD_ERR_DEVICE (-7)       /* a kernel reported a failure on the device (e.g. a chain
+                                    * hand-off that never arrived): the run's z, y are invalid.
+                                    * Returned by the call that collects the run's stats or
+                                    * synchronises it (gpad_run with st, gpad_last_stats,
+                                    * gpad_sync, host-memory runs) -- never GPAD_OK            */
 
 /* theta/beta schedule (acceldualgrad.m:18,27,55-56 vs paper eq. 8e) */
 #define GPAD_SCHEDULE_MATLAB 0 /* beta lagged one iteration, as the reference's MATLAB  */
@@ -73,6 +79,7 @@ typedef struct gpad_dims {
     int schedule;    /* GPAD_SCHEDULE_*                                                 */
     int check_every; /* termination test period K when tol > 0 (<= 0 -> 10)            */
     int kernel;      /* GPAD_KERNEL_*                                                   */
+    int reserved;    /* must be 0 (explicit padding before tol_gap; reserved for extensions) */
     double tol_gap;  /* e_V of acceldualgrad.m:13: tolerance of test (B)'s duality-gap term
                       * -w'(G zhat - g); <= 0 (e.g. a zeroed struct): the run's tol (= e_g) */
 } gpad_dims_t;
@@ -84,7 +91,14 @@ typedef struct gpad_stats {
     int kernel;                  /* GPAD_KERNEL_* that ran                               */
     double kernel_ms;            /* device time of the solve launch (HIP events)        */
     int* iters;                  /* optional caller array [batch] (host) or NULL        */
+    double tol_floor;            /* tol > 0: the certification floor of this run's data, see
+                                  * gpad_run (0 when tol <= 0)                             */
+    int flags;                   /* GPAD_FLAG_* of the run                                  */
 } gpad_stats_t;
+
+/* gpad_stats_t.flags */
+#define GPAD_FLAG_TOL_FLOOR 1 /* 0 < tol < tol_floor: no instance with an active constraint can be
+                               * certified; expect converged == 0 (use f64 or a larger tol)   */
 
 typedef struct gpad_handle_s* gpad_handle_t;
 
@@ -137,6 +151,12 @@ int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* dims, int n_u, const flo
  *     exactly on the returned z*.  The value-function branches of acceldualgrad.m:73,76
  *     (valuefcn(zhat) e_V/(1+e_V), valuefcn - dualfcn <= e_V max(dualfcn, 1)) need H and q,
  *     which this surface does not carry: they are not evaluated.
+ *   Certification floor: the margin above is at least 2^-20 max_i |g_i| (f32; f64: 2^-49), so
+ *     a tol below tol_floor = 2^-20 max_{b,i} |g_{b,i}| can never certify an instance whose
+ *     solution has an active constraint (G z* - g = 0 in some row) -- e.g. the reference's own
+ *     e_g = 1e-6 (acceldualgrad.m:12) on data with |g| of order 10.  Such a run is not rejected
+ *     (an instance with no active constraint can still pass) but flagged: st->tol_floor holds
+ *     the floor of the run's data and st->flags GPAD_FLAG_TOL_FLOOR is set when tol < it.
  * Host memory: synchronous.  Device memory: enqueued on the handle's stream; synchronous only
  * when st != NULL (stats need the per-instance counters). */
 int gpad_run(gpad_handle_t h, void* z0, void* y0, const void* M, const void* g, int N, double tol,
@@ -261,6 +281,11 @@ typedef struct gpad_group_s* gpad_group_t;
 int gpad_group_create(gpad_group_t* g, int ndev, const int* devices);
 int gpad_group_destroy(gpad_group_t g);
 int gpad_group_transport(gpad_group_t g); /* GPAD_GROUP_RCCL or GPAD_GROUP_PEER */
+/* Device memory: the stream of devices[0] on which the caller produces / consumes the buffers it
+ * passes (NULL, the default: the null stream).  Setup and run first make every device stream of
+ * the group wait for the work queued on it so far; runs are synchronous, so the results are
+ * complete when gpad_group_run returns. */
+int gpad_group_set_stream(gpad_group_t g, void* hip_stream);
 /* dims.batch is the WHOLE batch (as for gpad_setup); ML, G as gpad_setup's. */
 int gpad_group_setup(gpad_group_t g, const gpad_dims_t* dims, const void* ML, const void* G, double L);
 /* The whole batch's vectors (gpad_run's meaning).  Synchronous.  st aggregates every shard
@@ -325,6 +350,10 @@ int gpad_schedule(int N, int kind, double* theta, double* beta);
                                      * 0: one workgroup per instance                               */
 #define GPAD_OPT_PLAN_FIN_COST 15  /* phase plan: the finisher's modelled cost in percent (default
                                     * 100; > 100 moves the takeover later)                         */
+#define GPAD_OPT_DEBUG_DROP_HANDOFF 16 /* test only (fault injection): 1 = every panel solve that
+                                    * uses the chain hand-off withholds its first post, so the
+                                    * receiver's bounded wait expires and the run ends in
+                                    * GPAD_ERR_DEVICE; 0 (default) = off                          */
 int gpad_set_option(gpad_handle_t h, int option, int value);
 
 /* Synchronise the handle's stream (for callers using device memory + async runs). */

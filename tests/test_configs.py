@@ -70,3 +70,43 @@ def test_c4_shard_certified_on_the_constraint(gpu, oracle):
         zo, yo, ito, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), ML32, M32[b], G32, g32[b], N, L32, tol)
         assert it[b] == ito, b
         np.testing.assert_array_equal(Z[b].astype(np.float32), zo)
+
+
+def test_c3_batch4096_bitexact(gpu, oracle):
+    """C3 at its full size (BASELINE.json configs[2]): 4096 instances sharing ML/G, N = 50
+    (n = 200), m = 200, eps = 1e-4 -- one panel per workgroup (256 panels = 256 CUs, tile 12 as
+    the 3-hop relay), phased with the finisher.  Run twice so the second solve follows the plan
+    made from the first one's counts (the default path of a repeated caller); every 257th instance
+    bit-exact against the oracle, iteration count included, and every instance certified in fp64
+    on the returned z*."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    import torch
+
+    import gpad_mpc
+    n = m = 200
+    B, tol, N = 4096, 1e-4, 5000
+    ML, G, L, M, g = bench.make_shard(n, m, B, 0)
+    f32 = np.float32
+    ML32, G32, M32, g32, L32 = ML.astype(f32), G.astype(f32), M.astype(f32), g.astype(f32), f32(L)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)  # noqa: E731
+    it = np.zeros(B, np.int32)
+    with gpad_mpc.GpadSolver(0) as s:
+        s.setup(t(ML32), t(G32), float(L32), n=n, m=m, batch=B, check_every=10)
+        for rep in range(2):
+            z = torch.zeros(B, n, device=gpu)
+            y = torch.zeros(B, m, device=gpu)
+            st = s.run(z, y, t(M32), t(g32), N, tol, iters=it)
+            assert st["kernel"] == "panel" and st["converged"] == B
+        plan = s.phase_plan()
+    assert plan["ends"], "the second solve follows a plan"
+    Z, Y = z.cpu().numpy(), y.cpu().numpy()
+    viol = (Z.astype(np.float64) @ G32.astype(np.float64).T - g32.astype(np.float64)).max(axis=1)
+    assert viol.max() <= tol, (viol.max(), int(viol.argmax()))
+    for b in list(range(0, B, 257)) + [B - 1]:
+        zo, yo, ito, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), ML32, M32[b], G32, g32[b], N, L32, tol)
+        assert it[b] == ito, b
+        np.testing.assert_array_equal(Z[b], zo, err_msg=f"z[{b}]")
+        np.testing.assert_array_equal(Y[b], yo, err_msg=f"y[{b}]")

@@ -99,3 +99,9 @@ def test_bench_two_ranks_rehearsal(gpu):
     assert d["config"]["global_batch"] == 4096 and d["config"]["batch_per_gpu"] == 2048
     assert d["converged"] == 4096
     assert d["value"] > 0 and d["steps"] == 3
+    mg = d["multi_gpu"]  # attribution of a scaling loss: per-rank solve, drain and gather times
+    assert len(mg["per_rank_step_ms"]) == 2 and len(mg["per_rank_kernel_ms"]) == 2
+    assert 0 < mg["solve_ms_min"] <= mg["solve_ms_max"]
+    assert mg["gather_ms"] > 0 and mg["drain_ms_max"] >= 0
+    assert mg["gather_bytes_per_rank"] == 2048 * 400 * 4
+    assert d["config"]["parallelism"] == "instance-sharded x2, gloo gather"

@@ -63,6 +63,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--only", default="")
+    ap.add_argument("--batch", type=int, default=0, help="only cases of this batch size")
+    ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--check-every", type=int, default=10)
     ap.add_argument("--tol", type=float, default=0.0,
                     help="> 0: run the Algorithm-1 test path (tiny tol: never converges, N its)")
@@ -85,7 +87,9 @@ def main():
     for c in cases:
         if args.only and args.only not in c[0]:
             continue
-        print(json.dumps(case(*c, tol=args.tol, check_every=args.check_every)), flush=True)
+        if args.batch and c[3] != args.batch:
+            continue
+        print(json.dumps(case(*c, reps=args.reps, tol=args.tol, check_every=args.check_every)), flush=True)
 
 
 if __name__ == "__main__":
