@@ -110,6 +110,8 @@ struct gpad_handle_s {
     double shadow_L = 0.0;
     bool shadow_ok = false;
     DevBuf GLx;  // flat path: flat G_L expanded to the full k-major image (flat resident kernel)
+    DevBuf Hq;           // gpad_setup_hessian: H, k-major [n][ldn] per matrix (value-function branches)
+    bool hess_ok = false;
     int frag_tiles = 0;
     DevBuf theta, beta;
     int sched_len = 0, sched_kind = -1, sched_dtype = -1;
@@ -239,6 +241,7 @@ int gpad_destroy(gpad_handle_t h) {
     h->Hc.release();
     h->Hfrag.release();
     h->GLx.release();
+    h->Hq.release();
     h->frag.release();
     h->stage.release();
     h->theta.release();
@@ -352,6 +355,7 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
     h->ready = false;
     h->flat = false;
     h->shadow_ok = false;
+    h->hess_ok = false;
     h->plan.nph = 0;
     h->flat_vpred = 0;
     h->cond_vtake = 0;
@@ -438,6 +442,37 @@ int gpad_setup_scaled(gpad_handle_t h, const gpad_dims_t* d, const void* MGneg, 
     return setup_impl(h, d, MGneg, GL, L, true);
 }
 
+int gpad_setup_hessian(gpad_handle_t h, const void* H) {
+    if (!h) return fail(GPAD_ERR_INVALID, "gpad_setup_hessian: null handle");
+    if (!h->ready) return fail(GPAD_ERR_NOT_SETUP, "gpad_setup_hessian: call gpad_setup first");
+    if (h->flat) return fail(GPAD_ERR_UNSUPPORTED, "gpad_setup_hessian: not on the flat battery path");
+    h->hess_ok = false;
+    if (!H) return GPAD_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    const gpad_dims_t& d = h->dims;
+    const int n = d.n, nmats = d.shared ? 1 : d.batch;
+    const size_t es = esize(d.dtype), raw = (size_t)n * n * nmats * es;
+    int rc;
+    if ((rc = h->Hq.ensure(es * (size_t)n * h->ldn * nmats))) return rc;
+    const void* dH = H;
+    DevBuf stage;
+    if (d.memory == GPAD_MEM_HOST) {
+        if ((rc = stage.ensure(raw))) return rc;
+        HIP_TRY(hipMemcpyAsync(stage.p, H, raw, hipMemcpyHostToDevice, h->stream));
+        dH = stage.p;
+    }
+    const long long in_stride = d.shared ? 0 : (long long)n * n, out_stride = (long long)n * h->ldn;
+    if (d.dtype == GPAD_DTYPE_F32)
+        HIP_TRY(gpad::launch_pack_kmajor<float>((const float*)dH, (float*)h->Hq.p, n, n, h->ldn, 1.0, nmats, in_stride,
+                                                out_stride, h->stream));
+    else
+        HIP_TRY(gpad::launch_pack_kmajor<double>((const double*)dH, (double*)h->Hq.p, n, n, h->ldn, 1.0, nmats,
+                                                 in_stride, out_stride, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    h->hess_ok = true;
+    return GPAD_OK;
+}
+
 int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* d, int n_u, const float* MGf, const float* GLf,
                     double L) {
     if (!h) return fail(GPAD_ERR_INVALID, "gpad_setup_flat: null handle");
@@ -455,6 +490,7 @@ int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* d, int n_u, const float*
     h->ready = false;
     h->flat = false;
     h->shadow_ok = false;
+    h->hess_ok = false;
     h->plan.nph = 0;
     h->flat_vpred = 0;
     h->cond_vtake = 0;
@@ -590,6 +626,7 @@ static int collect_stats(gpad_handle_t h, gpad_stats_t* st) {
             st->converged += cv[b] != 0;
             st->total_iterations += it[b];
             if (st->iters) st->iters[(size_t)t * batch + b] = it[b];
+            if (st->codes) st->codes[(size_t)t * batch + b] = cv[b];
         }
     }
     if (h->last_phased && h->last_steps == 1) {
@@ -633,6 +670,17 @@ int gpad_phase_plan(gpad_handle_t h, int* ends, int* fins, int cap, double* cost
     if (cost_us) *cost_us = h->plan.cost_us;
     return n;
 }
+
+#ifdef GPAD_STAMP
+namespace gpad {
+hipError_t read_stamps(unsigned long long* out, size_t bytes);  // gpad_panel.hip (diagnostic builds)
+}
+// diagnostic builds only (not declared in gpad.h): the phase-anatomy stamps of the last panel-pair run
+int gpad_debug_stamps(unsigned long long* out, size_t bytes) {
+    HIP_TRY(gpad::read_stamps(out, bytes));
+    return GPAD_OK;
+}
+#endif
 
 int gpad_plan_phases(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus,
                      int* ends, int* fins, int cap, double* cost_us) {
@@ -690,6 +738,8 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
     a.Hc = h->Hc_ok ? (const float*)h->Hc.p : nullptr;
     a.hfrag = h->Hfrag_ok ? h->Hfrag.p : nullptr;
     a.strideH = d.shared ? 0 : (long long)m * h->ldm;
+    a.Hq = (h->hess_ok && tol > 0.0) ? (const T*)h->Hq.p : nullptr;
+    a.strideHq = d.shared ? 0 : (long long)n * h->ldn;
     a.err = (int*)h->status.p;
     a.debug = h->tune.debug_drop_handoff ? gpad::kDebugDropHandoff : 0;
     if (tol > 0.0)  // the certification floor's data term (stats: tol_floor, GPAD_FLAG_TOL_FLOOR)
@@ -708,8 +758,15 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
         *kernel_out = d.kernel == GPAD_KERNEL_AUTO ? GPAD_KERNEL_STREAM : d.kernel;
         return GPAD_OK;
     }
+    if (a.Hq) {  // value-function branches: evaluated by the stream kernel family only
+        if (kernel != GPAD_KERNEL_AUTO && kernel != GPAD_KERNEL_STREAM)
+            return fail(GPAD_ERR_UNSUPPORTED, "the value-function test (gpad_setup_hessian) runs on the stream kernel");
+        kernel = GPAD_KERNEL_STREAM;
+    }
     if constexpr (sizeof(T) == sizeof(float)) {
-        if (h->flat) {  // structure-exploiting battery path (gpad_setup_flat)
+        if (kernel == GPAD_KERNEL_STREAM && !h->flat) {
+            // forced stream kernel (or the value-function test): none of the f32 families below
+        } else if (h->flat) {  // (flat data with STREAM forced: the LDS flat kernel)  // structure-exploiting battery path (gpad_setup_flat)
             a.n_u = h->n_u;
             // flat panels from 8 instances per CU when the register-resident flat chains exist
             // (their per-CU cost grows with the batch, a panel's does not until every CU holds

@@ -103,6 +103,9 @@ struct SolveArgs {
     const float* Hc;       // condensed operator H = G_L (-ML), k-major [m][ldm] (gpad_condensed.hip)
     const void* hfrag;     // H in the panel fragment layout (gpad_cpanel.hip), or null
     long long strideH;     // elements between consecutive instances' H images (0 = shared)
+    const T* Hq;           // QP Hessian H, k-major [n][ldn] (gpad_setup_hessian), or null: enables the
+                           // value-function branches of the test (stream kernel only)
+    long long strideHq;    // elements between consecutive instances' H images (0 = shared)
     int* err;              // device error word (kDevErr* bits), never null on a solve launch
     int debug;             // kDebug* fault-injection bits (tests only)
 };

@@ -44,6 +44,8 @@ template <typename T>
 struct StreamLds {
     T *w, *zh, *zs, *ys, *gp, *pd, *us;
     CheckSlot* slots;
+    double* red;  // [waves] block-sum partials of the value functions
+    double* zp;   // [ldn] z(y+) of the dual function (value-function branches only)
 };
 
 template <typename T>
@@ -57,7 +59,17 @@ __device__ __forceinline__ StreamLds<T> stream_lds(unsigned char* smem, int ldn,
     s.pd = s.gp + ldn;                  // [ldm] p_D
     s.us = s.pd + ldm;                  // [ldm] u = G_L z (termination test, by recursion)
     s.slots = reinterpret_cast<CheckSlot*>(s.us + ldm);  // [2][waves]: test, verification of (A)
+    s.red = reinterpret_cast<double*>(s.slots + 2 * (kStreamBlock / 64));
+    s.zp = s.red + kStreamBlock / 64;
     return s;
+}
+
+// LDS bytes of the stream kernel: the vectors, the test slots and (value branches) the block-sum
+// partials and z(y+)
+template <typename T>
+size_t stream_lds_bytes(int ldn, int ldm, bool value) {
+    return sizeof(T) * (size_t)(3 * ldn + 4 * ldm) + sizeof(CheckSlot) * 2 * (kStreamBlock / 64) +
+           (value ? sizeof(double) * (size_t)(kStreamBlock / 64 + ldn) : 0);
 }
 
 // acc[r] = sum_k Mt[k*ld + r0 + r] * v[k], sequential in k, 4 rows per lane.
@@ -88,6 +100,81 @@ __device__ __forceinline__ void chain4(const T* __restrict__ Mt, int ld, int r0,
         acc[2] = fmad(a.z, vk, acc[2]);
         acc[3] = fmad(a.w, vk, acc[3]);
     }
+}
+
+// acc[r] = sum_k Mt[k*ld + r0 + r] * v[k] as fp64 fma chains (ascending k) over the run's own
+// matrix and vector values: the products of the value-function branches
+template <typename T, typename V>
+__device__ __forceinline__ void chain4d(const T* __restrict__ Mt, int ld, int r0, const V* v, int K,
+                                        double (&acc)[4]) {
+    using W = typename V4<T>::type;
+    const T* col = Mt + r0;
+    for (int k = 0; k < K; ++k) {
+        const W x = *reinterpret_cast<const W*>(col + (size_t)k * ld);
+        const double vk = (double)v[k];
+        acc[0] = __builtin_fma((double)x.x, vk, acc[0]);
+        acc[1] = __builtin_fma((double)x.y, vk, acc[1]);
+        acc[2] = __builtin_fma((double)x.z, vk, acc[2]);
+        acc[3] = __builtin_fma((double)x.w, vk, acc[3]);
+    }
+}
+
+// sum over the workgroup (every thread gets it): wave sums, then the waves' partials in order
+__device__ __forceinline__ double block_sum(double v, double* red) {
+    v = wave_sum(v);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double t = 0.0;
+    for (int i = 0; i < kStreamBlock / 64; ++i) t += red[i];
+    __syncthreads();  // red is reused by the next sum
+    return t;
+}
+
+// valuefcn V(x) = sum_i (x_i / 2 + M_i) (H x)_i (acceldualgrad.m:30 with f = H M)
+template <typename T, typename V>
+__device__ __forceinline__ double stream_valuefcn(const T* __restrict__ Hq, int ldn, int n, const V* x, const T* gp,
+                                                  double* red) {
+    double part = 0.0;
+    for (int r0 = 4 * threadIdx.x; r0 < n; r0 += 4 * kStreamBlock) {
+        double hx[4] = {0.0, 0.0, 0.0, 0.0};
+        chain4d<T, V>(Hq, ldn, r0, x, n, hx);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (r0 + r < n) part += (0.5 * (double)x[r0 + r] + (double)gp[r0 + r]) * hx[r];
+    }
+    return block_sum(part, red);
+}
+
+// The value-function branches of Algorithm 1 (acceldualgrad.m:73,76), reached after test (B)'s
+// violation part passed (w_ok: w >= 0 with the gap term above e_V, else w not >= 0); the same
+// fp64 quantities as orc_value_branch_f32 / _f64 (oracle/gpad_oracle.c).  Returns 3, 4 or 0.
+template <typename T>
+__device__ int stream_value_branch(const SolveArgs<T>& a, const StreamLds<T>& s, const T* __restrict__ MGt,
+                                   const T* __restrict__ GLt, const T* __restrict__ Hq, bool w_ok, double gapL) {
+    const int n = a.n, m = a.m, ldn = a.ldn, ldm = a.ldm;
+    const double eV = a.tol_gap;
+    const double V = stream_valuefcn<T, T>(Hq, ldn, n, s.zh, s.gp, s.red);
+    if (w_ok) return gapL <= V * eV / (1.0 + eV) ? 3 : 0;  // :73
+    // dualfcn(y+) = V(z(y+)) + y+'(G z(y+) - g), z(y+) = -ML y+ - M       (:31-33, :76)
+    for (int r0 = 4 * threadIdx.x; r0 < n; r0 += 4 * kStreamBlock) {
+        double acc[4] = {0.0, 0.0, 0.0, 0.0};
+        chain4d<T, T>(MGt, ldn, r0, s.ys, m, acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (r0 + r < n) s.zp[r0 + r] = acc[r] - (double)s.gp[r0 + r];
+    }
+    __syncthreads();
+    const double Vp = stream_valuefcn<T, double>(Hq, ldn, n, s.zp, s.gp, s.red);
+    double lin = 0.0;
+    for (int r0 = 4 * threadIdx.x; r0 < m; r0 += 4 * kStreamBlock) {
+        double c[4] = {0.0, 0.0, 0.0, 0.0};
+        chain4d<T, double>(GLt, ldm, r0, s.zp, n, c);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (r0 + r < m) lin += (double)s.ys[r0 + r] * (c[r] + (double)s.pd[r0 + r]);
+    }
+    const double D = Vp + a.L * block_sum(lin, s.red);
+    return V - D <= eV * (D > 1.0 ? D : 1.0) ? 4 : 0;  // :76
 }
 
 template <typename T>
@@ -207,10 +294,22 @@ __global__ __launch_bounds__(kStreamBlock) void gpad_stream_kernel(SolveArgs<T> 
                 verified = check_verify<T>(s.slots + nwaves, nwaves, a.L, a.tol);
             }
             done = check_code(st1, verified);
+            if (!done && a.Hq) {  // value-function branches where the MATLAB test reaches them
+                double vh = -INFINITY, mh = 0.0, wm = INFINITY, gq = 0.0;
+                for (int i = 0; i < nwaves; ++i) {
+                    vh = fmax(vh, s.slots[i].violh);
+                    mh = fmax(mh, s.slots[i].magh);
+                    wm = fmin(wm, s.slots[i].wmin);
+                    gq += s.slots[i].gap;
+                }
+                if (viol_ok(vh, mh, a.L, a.tol, ViolMargin<T>::value))  // uniform
+                    done = stream_value_branch<T>(a, s, MGt, GLt, a.Hq + (size_t)b * a.strideHq, wm >= 0.0,
+                                                  gq * a.L);
+            }
         }
         if (done) break;
     }
-    const T* zout = done == 2 ? s.zh : s.zs;  // test (B) certifies zhat
+    const T* zout = done >= 2 ? s.zh : s.zs;  // tests (B), (B'), (B'') certify zhat
     for (int i = tid; i < n; i += kStreamBlock) zg[i] = zout[i];
     for (int i = tid; i < m; i += kStreamBlock) yg[i] = s.ys[i];
     if (tid == 0) {
@@ -221,8 +320,7 @@ __global__ __launch_bounds__(kStreamBlock) void gpad_stream_kernel(SolveArgs<T> 
 
 template <typename T>
 hipError_t launch_stream(const SolveArgs<T>& a, hipStream_t st) {
-    const size_t lds = sizeof(T) * (size_t)(3 * a.ldn + 4 * a.ldm) +
-                       sizeof(CheckSlot) * 2 * (kStreamBlock / 64);
+    const size_t lds = stream_lds_bytes<T>(a.ldn, a.ldm, a.Hq != nullptr);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute((const void*)gpad_stream_kernel<T>,

@@ -636,16 +636,74 @@ struct Handoff {
     static constexpr int R1 = T / 3, R2 = 2 * (T / 3);  // one panel: relay cuts (equal pieces, prefetched whole)
 };
 
+// Per (panel, row tile) partials of the test, one entry per column: the four float terms packed
+// (violz, violh, magh, wmin: one ds_read_b128 per tile on the reduction side) and the fp64 gap.
+// The verification of a nominated (A) reuses .x / .z for max(G_L z + pD) / max(|G_L z| + |pD|).
+struct PanelSlot2 {
+    float4 f[16];
+    double gap[16];
+};
+
+// The tile reduction of the test, every wave at once (uniform result, no vote barrier): lane
+// 16 pp + cc reduces tiles [0, H) of column cc of panel pp, lane 32 + 16 pp + cc tiles [H, T);
+// the halves meet through one xor-32 exchange.  The f32 maxima / minima are exact in any order
+// (one conversion to fp64 after them instead of one per tile); the fp64 gap is summed per half,
+// then the halves added.
+template <int T>
+__device__ __forceinline__ void panel2_reduce(const PanelSlot2 (&S)[2][T], int lane, float4& f, double& gap) {
+    constexpr int H = (T + 1) / 2;
+    const int pp = (lane >> 4) & 1, cc = lane & 15, lo = lane < 32 ? 0 : H, hi = lane < 32 ? H : T;
+    f = make_float4(-INFINITY, -INFINITY, 0.0f, INFINITY);
+    gap = 0.0;
+#pragma unroll
+    for (int s2 = 0; s2 < H; ++s2) {
+        if (lo + s2 < hi) {
+            const float4 e = S[pp][lo + s2].f[cc];
+            f.x = fmaxf(f.x, e.x);
+            f.y = fmaxf(f.y, e.y);
+            f.z = fmaxf(f.z, e.z);
+            f.w = fminf(f.w, e.w);
+            gap += S[pp][lo + s2].gap[cc];
+        }
+    }
+    f.x = fmaxf(f.x, __shfl_xor(f.x, 32, 64));
+    f.y = fmaxf(f.y, __shfl_xor(f.y, 32, 64));
+    f.z = fmaxf(f.z, __shfl_xor(f.z, 32, 64));
+    f.w = fminf(f.w, __shfl_xor(f.w, 32, 64));
+    const double other = __shfl_xor(gap, 32, 64);
+    gap = lane < 32 ? gap + other : other + gap;
+}
+
 template <int T>
 struct Panel2Lds {
     float4 Wl[2][T * 64];  // fragment order, per panel: w    (B of GEMM 1)
     float4 Zh[2][T * 64];  //                            zhat (B of GEMM 2)
     float4 Gp[2][T * 64];  //                            g_P rows
     float4 Pd[2][T * 64];  //                            p_D rows
-    PanelSlot slots[2][T];
+    PanelSlot2 slots[2][T];
     float4 hand[3][64];    // hand-off accumulators
     int hflag[3];          // hand-off generation per slot
+    int herr;              // a wait expired (handoff_wait): reported to the run's error word at exit
+    int hdrop;             // fault injection (kDebugDropHandoff) for this workgroup
 };
+
+// Phase anatomy stamps (diagnostic builds only, -DGPAD_STAMP; never in the product library): the
+// shader clock (s_memtime) of workgroup 0, every wave, iterations [kStampV0, kStampV0 + kStampIts),
+// at six points per iteration -- loop top, GEMM-1 issued, before its barrier, after it, GEMM-2
+// issued, before the closing barrier -- read back with gpad_debug_stamps (tools/stamp_panel.py).
+#ifdef GPAD_STAMP
+constexpr int kStampV0 = 101, kStampIts = 4, kStampPts = 6;
+__device__ unsigned long long g_stamps[16][kStampIts][kStampPts];
+#define GPAD_STAMP_AT(P)                                                                          \
+    do {                                                                                          \
+        if (blockIdx.x == 0 && v >= kStampV0 && v < kStampV0 + kStampIts && lane == 0)            \
+            g_stamps[threadIdx.x >> 6][v - kStampV0][P] = __builtin_amdgcn_s_memtime();           \
+    } while (0)
+#else
+#define GPAD_STAMP_AT(P) \
+    do {                 \
+    } while (0)
+#endif
 
 struct HoSlots {
     int in, out;  // LDS hand-off slots taken / given (-1: none)
@@ -653,16 +711,20 @@ struct HoSlots {
 
 // The waves of a workgroup are co-resident, so a post always arrives unless the layout logic is
 // broken; the wait is still bounded (2^20 sleeps, ~30 ms) so that such a bug cannot hang the GPU,
-// and an expired wait sets kDevErrHandoff in the run's error word: the host then fails the run
-// with GPAD_ERR_DEVICE instead of returning the stale accumulator's results as GPAD_OK.
+// and an expired wait is recorded (L.herr) and ORed into the run's error word when the workgroup
+// exits (gpad_panel2_kernel): the host then fails the run with GPAD_ERR_DEVICE instead of
+// returning the stale accumulator's results as GPAD_OK.  Nothing of this sits on the hand-off's
+// own path: the record is made only after the bound expired.
 template <int T>
-__device__ __forceinline__ f32x4 handoff_wait(Panel2Lds<T>& L, int slot, int gen, int lane, int* err) {
-    int s = 0;
-    for (; s < (1 << 20); ++s) {
+__device__ __forceinline__ f32x4 handoff_wait(Panel2Lds<T>& L, int slot, int gen, int lane) {
+    for (int s = 0;; ++s) {
         if (__hip_atomic_load(&L.hflag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == gen) break;
+        if (s == (1 << 20)) {
+            L.herr = 1;
+            break;
+        }
         __builtin_amdgcn_s_sleep(1);
     }
-    if (s == (1 << 20) && lane == 0) atomicOr(err, kDevErrHandoff);  // uniform: s is
     asm volatile("" ::: "memory");
     const float4 hv = L.hand[slot][lane];
     return f32x4{hv.x, hv.y, hv.z, hv.w};
@@ -677,17 +739,16 @@ __device__ __forceinline__ void handoff_post(Panel2Lds<T>& L, int slot, int gen,
 
 // a piece of another wave's chain: k-blocks [KB0, KB1) (KB1 < T) of the tile at voff, continued
 // from slot hs.in (or from zero), parked in slot hs.out; PRIO raises the wave's issue priority
-// drop: fault injection (kDebugDropHandoff) -- the first piece of the first hand-off withholds
+// fault injection (kDebugDropHandoff, L.hdrop): the first piece of the first hand-off withholds
 // its post, so its receiver's wait expires
 template <int T, int PD, int KB0, int KB1, bool PRIO>
 __device__ __forceinline__ void handoff_piece(Panel2Lds<T>& L, __amdgpu_buffer_rsrc_t PA, const float4* B0, int voff,
-                                              int lane, const float4 (&aph)[PD], HoSlots hs, int gen, int* err,
-                                              bool drop) {
+                                              int lane, const float4 (&aph)[PD], HoSlots hs, int gen) {
     f32x4 h = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    if (hs.in >= 0) h = handoff_wait(L, hs.in, gen, lane, err);
+    if (hs.in >= 0) h = handoff_wait(L, hs.in, gen, lane);
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
     panel_chain<T, PD, KB0, KB1>(PA, B0, voff, lane, h, aph, 4);
-    if (!(drop && gen == 1 && hs.in < 0)) handoff_post(L, hs.out, gen, lane, h);
+    if (!(gen == 1 && hs.in < 0 && L.hdrop)) handoff_post(L, hs.out, gen, lane, h);
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
@@ -695,8 +756,8 @@ __device__ __forceinline__ void handoff_piece(Panel2Lds<T>& L, __amdgpu_buffer_r
 template <int T, int PD, int KB0, bool PRIO>
 __device__ __forceinline__ void handoff_take(Panel2Lds<T>& L, __amdgpu_buffer_rsrc_t PA, const float4* B0, int voff,
                                              int lane, const float4 (&ap)[PD], HoSlots hs, int gen, int kq,
-                                             f32x4& acc, int* err) {
-    acc = handoff_wait(L, hs.in, gen, lane, err);
+                                             f32x4& acc) {
+    acc = handoff_wait(L, hs.in, gen, lane);
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(2);
     panel_chain<T, PD, KB0, T>(PA, B0, voff, lane, acc, ap, kq);
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
@@ -706,7 +767,10 @@ __device__ __forceinline__ void handoff_take(Panel2Lds<T>& L, __amdgpu_buffer_rs
 // slot hs.out, then its own chain); 2 receiver (NU = 1: its own chain from block KB0, slot hs.in);
 // 3 relay (NU = 0: blocks [KB0, KB1) of tile t from slot hs.in, or zero, into slot hs.out).
 // PRIO: the one-panel relay raises issue priority for its pieces.
-template <int T, int NU, int ROLE = 0, int KB0 = 0, int KB1 = 0, bool PRIO = false>
+// KQ > 0: the shape is known at compile time to have full-length chains on every tile of both
+// GEMMs (16 (T-1) < n, m <= 16 T) whose last k-block issues KQ steps in both: no runtime kq tests
+// (scalar branches whose conditions the compiler spilled to VGPR lanes) and no short-chain paths.
+template <int T, int NU, int ROLE = 0, int KB0 = 0, int KB1 = 0, bool PRIO = false, int KQ = 0, int SPD = 0>
 __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<T>& L, int t, int p0,
                                            bool pair, int items, int count, HoSlots hs = HoSlots{-1, -1}) {
     static_assert(ROLE == 0 || (Handoff<T>::on && (ROLE == 3 ? NU == 0 : NU == 1)), "hand-off roles");
@@ -727,13 +791,12 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
     // GEMM 1: K = m, output rows n; GEMM 2: K = n, output rows m.  The last k-block issues only
     // the steps inside K when K is the padded dimension (kq), and a wave whose tile lies past
     // the output rows skips its GEMM (zeros).
-    const int nkb1 = (m + 15) / 16, nkb2 = (n + 15) / 16;  // k-blocks of each GEMM (<= T)
-    const int kq1 = (m - 16 * (nkb1 - 1) + 3) / 4, kq2 = (n - 16 * (nkb2 - 1) + 3) / 4;
-    const bool on1 = 16 * t < n, on2 = 16 * t < m;
+    constexpr bool FULL = KQ > 0;
+    const int nkb1 = FULL ? T : (m + 15) / 16, nkb2 = FULL ? T : (n + 15) / 16;  // k-blocks of each GEMM (<= T)
+    const int kq1 = FULL ? KQ : (m - 16 * (nkb1 - 1) + 3) / 4, kq2 = FULL ? KQ : (n - 16 * (nkb2 - 1) + 3) / 4;
+    const bool on1 = FULL || 16 * t < n, on2 = FULL || 16 * t < m;
     const int voff_r = voff - 1024;  // helper: the receiver's tile t - 1 (Handoff)
     int hgen = 0;                    // hand-off generation, counted alike by helper and receiver
-    // fault injection (tests): the first workgroup's first piece withholds its first post
-    const bool drop = (a.debug & kDebugDropHandoff) && blockIdx.x == 0;
 
     for (int it = blockIdx.x; it < items; it += gridDim.x) {
         // columns still running, bit 16 pp + c for panel pp of this item: the same word in every
@@ -796,8 +859,10 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
         }
         __syncthreads();
 
-        constexpr int PD = NU == 2 ? 1 : (ROLE == 3 ? Handoff<T>::R1 : 2);
+        constexpr int PD = SPD ? SPD : (NU == 2 ? 1 : (ROLE == 3 ? Handoff<T>::R1 : 2));
         float4 ap[PD];  // A blocks of the next GEMM, in flight across the barrier before it
+        constexpr int PDR = PD > 2 ? 2 : PD;  // the runtime-length GEMM keeps a ring of 1 or 2
+        const float4 (&apr)[PDR] = *reinterpret_cast<const float4 (*)[PDR]>(&ap);
         float4 aph[PD];  // helper / relay: the piece's first blocks
         auto prefetch = [&](__amdgpu_buffer_rsrc_t PA) {
             if constexpr (ROLE == 2) panel_a_prefetch_from<T, PD>(PA, voff, ap, KB0);
@@ -813,22 +878,24 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             ++v;
             const bool chk = use_tol && (v % K) == 0;
             const float omt = 1.0f - th;
+            GPAD_STAMP_AT(0);
             // ---- GEMM 1 + epilogue: zhat = -ML w - g_P (8b), z = (1-th) z + th zhat (8c) ----
             if constexpr (NU > 0) {
                 f32x4 acc[2];
                 ++hgen;
                 if constexpr (ROLE == 1)
-                    handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA1, L.Wl[p0], voff_r, lane, aph, hs, hgen, a.err, drop);
+                    handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA1, L.Wl[p0], voff_r, lane, aph, hs, hgen);
                 if constexpr (ROLE == 2)
-                    handoff_take<T, PD, KB0, PRIO>(L, PA1, L.Wl[p0], voff, lane, ap, hs, hgen, kq1, acc[0], a.err);
+                    handoff_take<T, PD, KB0, PRIO>(L, PA1, L.Wl[p0], voff, lane, ap, hs, hgen, kq1, acc[0]);
                 else if (on1 && nkb1 == T)
                     panel_gemm3<T, NU == 2, PD>(PA1, L.Wl[p0], L.Wl[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1],
                                                 ap, kq1);
                 else if (on1)
-                    panel_gemm_rt<T, NU == 2, PD>(PA1, L.Wl[p0], L.Wl[NU == 2 ? 1 : p0], voff, lane, acc[0],
-                                                  acc[1], ap, nkb1, kq1);
+                    panel_gemm_rt<T, NU == 2, PDR>(PA1, L.Wl[p0], L.Wl[NU == 2 ? 1 : p0], voff, lane, acc[0],
+                                                   acc[1], apr, nkb1, kq1);
                 else
                     acc[0] = acc[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+                GPAD_STAMP_AT(1);
                 prefetch(PA2);
                 float4 g4[Q];
 #pragma unroll
@@ -849,10 +916,12 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 }
             } else if constexpr (ROLE == 3) {
                 ++hgen;
-                handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA1, L.Wl[p0], voff, lane, aph, hs, hgen, a.err, drop);
+                handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA1, L.Wl[p0], voff, lane, aph, hs, hgen);
                 prefetch(PA2);
             }
+            GPAD_STAMP_AT(2);
             __syncthreads();
+            GPAD_STAMP_AT(3);
             // ---- GEMM 2 + epilogue: y+ = [w + G_L zhat + p_D]+ (8d), next w (8a) ----------
             float violz[Q], violh[Q], wmin[Q], magh[Q];
             double gap[Q];
@@ -867,17 +936,18 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 f32x4 acc[2];
                 ++hgen;
                 if constexpr (ROLE == 1)
-                    handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA2, L.Zh[p0], voff_r, lane, aph, hs, hgen, a.err, drop);
+                    handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA2, L.Zh[p0], voff_r, lane, aph, hs, hgen);
                 if constexpr (ROLE == 2)
-                    handoff_take<T, PD, KB0, PRIO>(L, PA2, L.Zh[p0], voff, lane, ap, hs, hgen, kq2, acc[0], a.err);
+                    handoff_take<T, PD, KB0, PRIO>(L, PA2, L.Zh[p0], voff, lane, ap, hs, hgen, kq2, acc[0]);
                 else if (on2 && nkb2 == T)
                     panel_gemm3<T, NU == 2, PD>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1],
                                                 ap, kq2);
                 else if (on2)
-                    panel_gemm_rt<T, NU == 2, PD>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, acc[0],
-                                                  acc[1], ap, nkb2, kq2);
+                    panel_gemm_rt<T, NU == 2, PDR>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, acc[0],
+                                                   acc[1], apr, nkb2, kq2);
                 else
                     acc[0] = acc[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+                GPAD_STAMP_AT(4);
                 prefetch(PA1);
                 // (reading these LDS operands before the GEMM measured no faster: profiles/r02_epilogue_ab.txt)
                 float4 w4[Q], p4[Q];
@@ -941,22 +1011,20 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                             gap[q] += __shfl_xor(gap[q], o, 64);
                         }
                         if (j == 0) {
-                            PanelSlot& S = L.slots[p0 + q][t];
-                            S.violz[c] = violz[q];
-                            S.violh[c] = violh[q];
-                            S.magh[c] = magh[q];
-                            S.wmin[c] = wmin[q];
+                            PanelSlot2& S = L.slots[p0 + q][t];
+                            S.f[c] = make_float4(violz[q], violh[q], magh[q], wmin[q]);
                             S.gap[c] = gap[q];
                         }
                     }
                 }
             } else if constexpr (ROLE == 3) {
                 ++hgen;
-                handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA2, L.Zh[p0], voff, lane, aph, hs, hgen, a.err, drop);
+                handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA2, L.Zh[p0], voff, lane, aph, hs, hgen);
                 prefetch(PA1);
             }
             th = th_next;
             bn = bn_next;
+            GPAD_STAMP_AT(5);
             __syncthreads();
             if (!chk && v < a.v_end) continue;
 
@@ -967,22 +1035,13 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             bool zh_out = true;  // this iteration's zhat still in L.Zh (no verification GEMM ran)
             if (chk) {
                 int st1 = 0;
-                const int pp = (lane >> 4) & 1, cc = lane & 15;
-                if (lane < 32 && ((live >> lane) & 1u)) {
-                    double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gq = 0.0, mh = 0.0;
-#pragma unroll
-                    for (int s2 = 0; s2 < T; ++s2) {
-                        const PanelSlot& S = L.slots[pp][s2];
-                        vz = fmax(vz, (double)S.violz[cc]);
-                        vh = fmax(vh, (double)S.violh[cc]);
-                        mh = fmax(mh, (double)S.magh[cc]);
-                        wm = fmin(wm, (double)S.wmin[cc]);
-                        gq += S.gap[cc];
-                    }
-                    st1 = (vz * a.L <= a.tol ? 1 : 0) |
-                          ((viol_ok(vh, mh, a.L, a.tol, ViolMargin<float>::value) && (wm >= 0.0) &&
-                            (gq * a.L <= a.tol_gap)) ? 2 : 0);
-                }
+                float4 red;
+                double gq;
+                panel2_reduce<T>(L.slots, lane, red, gq);
+                if (lane < 32 && ((live >> lane) & 1u))
+                    st1 = ((double)red.x * a.L <= a.tol ? 1 : 0) |
+                          ((viol_ok((double)red.y, (double)red.z, a.L, a.tol, ViolMargin<float>::value) &&
+                            (red.w >= 0.0f) && (gq * a.L <= a.tol_gap)) ? 2 : 0);
                 const unsigned mA = (unsigned)__ballot(st1 & 1);
                 m2 = (unsigned)__ballot(st1 & 2);
                 if (mA) {  // (A) nominated for some column of the item: G_L z of both panels
@@ -1026,23 +1085,17 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                                 vc = fmaxf(vc, __shfl_xor(vc, o, 64));
                                 mc = fmaxf(mc, __shfl_xor(mc, o, 64));
                             }
-                            if (j == 0) {  // the stage-1 reads of every wave precede the barrier above
-                                L.slots[p0 + q][t].violz[c] = vc;
-                                L.slots[p0 + q][t].magh[c] = mc;
-                            }
+                            if (j == 0)  // the stage-1 reads of every wave precede the barrier above
+                                L.slots[p0 + q][t].f[c] = make_float4(vc, vc, mc, INFINITY);
                         }
                     }
                     __syncthreads();
                     bool ver = false;
-                    if (lane < 32 && ((mA >> lane) & 1u)) {
-                        double vcc = -INFINITY, mcc = 0.0;
-#pragma unroll
-                        for (int s2 = 0; s2 < T; ++s2) {
-                            vcc = fmax(vcc, (double)L.slots[pp][s2].violz[cc]);
-                            mcc = fmax(mcc, (double)L.slots[pp][s2].magh[cc]);
-                        }
-                        ver = viol_ok(vcc, mcc, a.L, a.tol, ViolMargin<float>::value);
-                    }
+                    float4 vred;
+                    double vgap;
+                    panel2_reduce<T>(L.slots, lane, vred, vgap);
+                    if (lane < 32 && ((mA >> lane) & 1u))
+                        ver = viol_ok((double)vred.x, (double)vred.z, a.L, a.tol, ViolMargin<float>::value);
                     m1 = (unsigned)__ballot(ver);
                     m2 &= ~m1;
                 }
@@ -1110,7 +1163,12 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
     }
 }
 
-template <int T>
+#ifndef GPAD_SPD
+#define GPAD_SPD 0
+#endif
+constexpr int kSinglePD = GPAD_SPD;  // A ring depth of the one-panel layout's single chains (0: 2)
+
+template <int T, int KQ>
 __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
     static_assert(T > 8 && T <= 16, "panel pairs need 8 < T <= 16");
     constexpr int D = 2 * T - 16;  // double waves
@@ -1122,37 +1180,45 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
     const bool pair = panels > (int)gridDim.x;
     const int items = pair ? (panels + 1) / 2 : panels;
     // hand-off (Handoff): both GEMMs run full-length chains on tiles T-2 and T-1
-    const bool ho = Handoff<T>::on && 16 * (T - 1) < a.n && 16 * (T - 1) < a.m && (a.m + 15) / 16 == T &&
-                    (a.n + 15) / 16 == T;
+    const bool ho = Handoff<T>::on && (KQ > 0 || (16 * (T - 1) < a.n && 16 * (T - 1) < a.m &&
+                                                  (a.m + 15) / 16 == T && (a.n + 15) / 16 == T));
     if (threadIdx.x < 3) L.hflag[threadIdx.x] = 0;
+    if (threadIdx.x == 0) {
+        L.herr = 0;
+        L.hdrop = (a.debug & kDebugDropHandoff) && blockIdx.x == 0;  // tests: workgroup 0 drops one post
+    }
     __syncthreads();
     if constexpr (Handoff<T>::on) {
         using H = Handoff<T>;
         if (pair) {  // waves 12, 13 (SIMDs 0, 1; tile T-2) receive from 14, 15 (SIMDs 2, 3; tile T-1)
-            if (w < D) panel2_run<T, 2>(a, L, w, 0, true, items, count);
+            if (w < D) panel2_run<T, 2, 0, 0, 0, false, KQ>(a, L, w, 0, true, items, count);
             else if (ho && w >= 14)
-                panel2_run<T, 1, 1, 0, H::S>(a, L, T - 1, w & 1, true, items, count, HoSlots{-1, w & 1});
+                panel2_run<T, 1, 1, 0, H::S, false, KQ>(a, L, T - 1, w & 1, true, items, count, HoSlots{-1, w & 1});
             else if (ho && w >= 12)
-                panel2_run<T, 1, 2, H::S>(a, L, T - 2, w & 1, true, items, count, HoSlots{w & 1, -1});
-            else panel2_run<T, 1>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
+                panel2_run<T, 1, 2, H::S, 0, false, KQ>(a, L, T - 2, w & 1, true, items, count, HoSlots{w & 1, -1});
+            else panel2_run<T, 1, 0, 0, 0, false, KQ>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
         } else {  // tile T-1 as a relay: waves T -> T+1 -> T-1
             if constexpr (!H::relay) {
-                if (w < T) panel2_run<T, 1>(a, L, w, 0, false, items, count);
-                else panel2_run<T, 0>(a, L, 0, 0, false, items, count);
-            } else if (ho && w == T - 1) panel2_run<T, 1, 2, H::R2, 0, true>(a, L, w, 0, false, items, count, HoSlots{1, -1});
+                if (w < T) panel2_run<T, 1, 0, 0, 0, false, KQ, kSinglePD>(a, L, w, 0, false, items, count);
+                else panel2_run<T, 0, 0, 0, 0, false, KQ>(a, L, 0, 0, false, items, count);
+            } else if (ho && w == T - 1) panel2_run<T, 1, 2, H::R2, 0, true, KQ>(a, L, w, 0, false, items, count, HoSlots{1, -1});
             else if (ho && w == T)
-                panel2_run<T, 0, 3, 0, H::R1, true>(a, L, T - 1, 0, false, items, count, HoSlots{-1, 0});
+                panel2_run<T, 0, 3, 0, H::R1, true, KQ>(a, L, T - 1, 0, false, items, count, HoSlots{-1, 0});
             else if (ho && w == T + 1)
-                panel2_run<T, 0, 3, H::R1, H::R2, true>(a, L, T - 1, 0, false, items, count, HoSlots{0, 1});
-            else if (w < T) panel2_run<T, 1>(a, L, w, 0, false, items, count);
-            else panel2_run<T, 0>(a, L, 0, 0, false, items, count);
+                panel2_run<T, 0, 3, H::R1, H::R2, true, KQ>(a, L, T - 1, 0, false, items, count, HoSlots{0, 1});
+            else if (w < T) panel2_run<T, 1, 0, 0, 0, false, KQ, kSinglePD>(a, L, w, 0, false, items, count);
+            else panel2_run<T, 0, 0, 0, 0, false, KQ>(a, L, 0, 0, false, items, count);
         }
     } else if (pair) {
-        if (w < D) panel2_run<T, 2>(a, L, w, 0, true, items, count);
-        else panel2_run<T, 1>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
+        if (w < D) panel2_run<T, 2, 0, 0, 0, false, KQ>(a, L, w, 0, true, items, count);
+        else panel2_run<T, 1, 0, 0, 0, false, KQ>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
     } else {
-        if (w < T) panel2_run<T, 1>(a, L, w, 0, false, items, count);
-        else panel2_run<T, 0>(a, L, 0, 0, false, items, count);
+        if (w < T) panel2_run<T, 1, 0, 0, 0, false, KQ, kSinglePD>(a, L, w, 0, false, items, count);
+        else panel2_run<T, 0, 0, 0, 0, false, KQ>(a, L, 0, 0, false, items, count);
+    }
+    if constexpr (Handoff<T>::on) {  // an expired hand-off wait fails the run (GPAD_ERR_DEVICE)
+        __syncthreads();
+        if (threadIdx.x == 0 && L.herr) atomicOr(a.err, kDevErrHandoff);
     }
 }
 
@@ -1405,11 +1471,23 @@ __global__ __launch_bounds__(1024) void survivor_sort_kernel(int* idx, const int
 
 template <int T>
 static void launch_panel_kernel(const SolveArgs<float>& a, int grid, hipStream_t s) {
-    if constexpr (T == 0)
+    if constexpr (T == 0) {
         (void)launch_bigpanel(a, grid, s);
-    else if constexpr (T > 8)
-        hipLaunchKernelGGL((gpad_panel2_kernel<T>), dim3(grid), dim3(1024), 0, s, a);
-    else
+    } else if constexpr (T > 8) {
+        // the C3/C4 shapes (T = 13) with full-length chains and one last-block length in both
+        // GEMMs: the compile-time variant (panel2_run KQ)
+        const int nkb1 = (a.m + 15) / 16, nkb2 = (a.n + 15) / 16;
+        const int kq1 = (a.m - 16 * (nkb1 - 1) + 3) / 4, kq2 = (a.n - 16 * (nkb2 - 1) + 3) / 4;
+        const bool full = nkb1 == T && nkb2 == T && kq1 == kq2;
+        if constexpr (T == 13) {
+            if (full && kq1 == 1) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 1>), dim3(grid), dim3(1024), 0, s, a); return; }
+            if (full && kq1 == 2) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 2>), dim3(grid), dim3(1024), 0, s, a); return; }
+            if (full && kq1 == 3) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 3>), dim3(grid), dim3(1024), 0, s, a); return; }
+            if (full && kq1 == 4) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 4>), dim3(grid), dim3(1024), 0, s, a); return; }
+        }
+        (void)full;
+        hipLaunchKernelGGL((gpad_panel2_kernel<T, 0>), dim3(grid), dim3(1024), 0, s, a);
+    } else
         hipLaunchKernelGGL((gpad_panel_kernel<T>), dim3(grid), dim3(64 * T), 0, s, a);
 }
 
@@ -1451,7 +1529,7 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     int v0 = 0;
     for (int ph = 0; v0 < a.N; ++ph) {
         int plen = len;
-        if (ph >= 10) plen = len << (ph - 9 < 20 ? ph - 9 : 20);
+        if (ph >= 10 && tn.phase_len <= 0) plen = len << (ph - 9 < 20 ? ph - 9 : 20);  // explicit: uniform
         a.fin_thresh = fin_default;
         if (plan && ph < plan->nph) {  // the previous solve's plan (panel_plan)
             plen = plan->ends[ph] - v0;
@@ -1486,6 +1564,13 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     }
     return hipSuccess;
 }
+
+#ifdef GPAD_STAMP
+hipError_t read_stamps(unsigned long long* out, size_t bytes) {
+    if (bytes > sizeof(g_stamps)) bytes = sizeof(g_stamps);
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 hipError_t launch_panel(const SolveArgs<float>& a, hipStream_t s, bool* supported) {
     const int T = panel_tiles_for(a.n, a.m);

@@ -128,20 +128,30 @@ hipError_t launch_accumulate_iters(const int* iters, long long count, long long*
     return hipGetLastError();
 }
 
-// *out = max(*out, max_i |g_i|) (for the certification floor, include/gpad.h gpad_run): at most 64
-// workgroups, each reducing its grid-stride share through LDS to ONE 64-bit atomic (non-negative
-// doubles order like their bit patterns); thousands of same-address atomics cost ~30 us
+// *out = max(*out, max_i |g_i|) (for the certification floor, include/gpad.h gpad_run): at most 128
+// workgroups of 256 threads, 16 elements per thread and pass with the loads of a pass issued
+// together, each workgroup reducing through LDS to ONE 64-bit atomic (non-negative doubles order
+// like their bit patterns; thousands of same-address atomics cost ~30 us)
 template <typename T>
-__global__ __launch_bounds__(1024) void absmax_kernel(const T* __restrict__ g, long long count, double* out) {
-    __shared__ double part[16];
+__global__ __launch_bounds__(256) void absmax_kernel(const T* __restrict__ g, long long count, double* out) {
+    __shared__ double part[4];
     double mx = 0.0;
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (long long)gridDim.x * blockDim.x)
-        mx = fmax(mx, fabs((double)g[i]));
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long base = (long long)blockIdx.x * blockDim.x + threadIdx.x; base < count; base += 16 * stride) {
+        T v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const long long i = base + u * stride;
+            v[u] = i < count ? g[i] : T(0);
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) mx = fmax(mx, fabs((double)v[u]));
+    }
     for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = mx;
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) mx = fmax(mx, part[w]);
+        mx = fmax(fmax(part[0], part[1]), fmax(part[2], part[3]));
         atomicMax(reinterpret_cast<unsigned long long*>(out), (unsigned long long)__double_as_longlong(mx));
     }
 }
@@ -149,9 +159,9 @@ __global__ __launch_bounds__(1024) void absmax_kernel(const T* __restrict__ g, l
 template <typename T>
 hipError_t launch_absmax(const T* g, long long count, double* out, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    long long blocks = (count + 32767) / 32768;
-    if (blocks > 64) blocks = 64;
-    hipLaunchKernelGGL(absmax_kernel<T>, dim3((unsigned)blocks), dim3(1024), 0, s, g, count, out);
+    long long blocks = (count + 4095) / 4096;
+    if (blocks > 128) blocks = 128;
+    hipLaunchKernelGGL(absmax_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, s, g, count, out);
     return hipGetLastError();
 }
 template hipError_t launch_absmax<float>(const float*, long long, double*, hipStream_t);

@@ -37,6 +37,7 @@ EXPORTS = [
     "gpad_accumulate_iterations", "gpad_set_option",
     "gpad_group_create", "gpad_group_destroy", "gpad_group_transport", "gpad_group_setup", "gpad_group_run",
     "gpad_solve_sharded", "gpad_device_count", "gpad_group_set_stream",
+    "gpad_setup_hessian",
 ]
 GROUP_RCCL, GROUP_PEER = 1, 2
 
@@ -70,7 +71,7 @@ class Stats(C.Structure):
     _fields_ = [("iterations", C.c_int), ("converged", C.c_int),
                 ("total_iterations", C.c_longlong), ("kernel", C.c_int),
                 ("kernel_ms", C.c_double), ("iters", C.POINTER(C.c_int)),
-                ("tol_floor", C.c_double), ("flags", C.c_int)]
+                ("tol_floor", C.c_double), ("flags", C.c_int), ("codes", C.POINTER(C.c_int))]
 
 
 class DataFile(C.Structure):
@@ -101,6 +102,20 @@ def load(path: str | None = None) -> C.CDLL:
         raise ImportError(f"libgpad.so not built at {path}: run `make -C gpu-dualgradient-mpc_amd` "
                           "(or __graft_entry__.build()); there is no CPU fallback")
     L = C.CDLL(path)
+    if os.environ.get("GPAD_LIB"):  # A/B runs may load an older build: bind what it exports
+        class _Tolerant:
+            def __init__(self, lib):
+                self.__dict__["_lib"] = lib
+
+            def __getattr__(self, name):
+                try:
+                    return getattr(self._lib, name)
+                except AttributeError:
+                    return C.CFUNCTYPE(C.c_int)(lambda *a: ERR_UNSUPPORTED)
+
+            def __setattr__(self, name, value):
+                setattr(self._lib, name, value)
+        L = _Tolerant(L)
     vp, cvp, i, d = C.c_void_p, C.c_void_p, C.c_int, C.c_double
     L.gpad_version.restype = C.c_char_p
     L.gpad_strerror.restype = C.c_char_p
@@ -112,6 +127,7 @@ def load(path: str | None = None) -> C.CDLL:
     L.gpad_sync.argtypes = [vp]
     L.gpad_setup.argtypes = [vp, C.POINTER(Dims), cvp, cvp, d]
     L.gpad_setup_scaled.argtypes = [vp, C.POINTER(Dims), cvp, cvp, d]
+    L.gpad_setup_hessian.argtypes = [vp, cvp]
     L.gpad_run.argtypes = [vp, vp, vp, cvp, cvp, i, d, C.POINTER(Stats)]
     L.gpad_run_scaled.argtypes = [vp, vp, vp, cvp, cvp, i, d, cvp, cvp, C.POINTER(Stats)]
     L.gpad_last_stats.argtypes = [vp, C.POINTER(Stats)]
@@ -146,7 +162,7 @@ def load(path: str | None = None) -> C.CDLL:
     L.gpad_solve_sharded.argtypes = [i, ip, vp, vp, cvp, cvp, cvp, cvp, i, d, d, C.POINTER(Dims), C.POINTER(Stats)]
     L.gpad_step2_primal_flat.argtypes = [vp, vp, vp, vp, vp, i, i, i]
     L.gpad_step4_project_flat.argtypes = [vp, vp, vp, vp, vp, vp, i, i, i]
-    for name in ["gpad_create", "gpad_destroy", "gpad_set_stream", "gpad_sync", "gpad_setup",
+    for name in ["gpad_create", "gpad_destroy", "gpad_set_stream", "gpad_sync", "gpad_setup", "gpad_setup_hessian",
                  "gpad_setup_scaled", "gpad_run", "gpad_run_scaled", "gpad_last_stats",
                  "gpad_phase_plan", "gpad_plan_phases", "gpad_solve", "gpad_step1_extrapolate", "gpad_step2_primal",
                  "gpad_step3_average", "gpad_step4_project", "gpad_schedule", "gpad_setup_plant",

@@ -126,8 +126,14 @@ class GpadSolver:
         check(self.lib.gpad_setup_flat(self.h, C.byref(self.dims), int(n_u), _ptr(MGf), _ptr(GLf),
                                        float(L)), "gpad_setup_flat")
 
+    def setup_hessian(self, H) -> None:
+        """gpad_setup_hessian: bind the QP Hessian (same dtype / memory kind as ``setup``) so
+        tol > 0 runs also evaluate the value-function branches (acceldualgrad.m:73,76); None
+        unbinds."""
+        check(self.lib.gpad_setup_hessian(self.h, _ptr(H) if H is not None else None), "gpad_setup_hessian")
+
     def run(self, z, y, M, g, N: int, tol: float = 0.0, *, stats: bool = True, iters=None,
-            scaled: bool = False, theta=None, beta=None):
+            scaled: bool = False, theta=None, beta=None, codes=None):
         """Run GPAD in place on z [batch][n] / y [batch][m].  Returns a dict of stats, or None
         when ``stats`` is False and the inputs are device tensors (asynchronous launch)."""
         st = Stats()
@@ -135,6 +141,8 @@ class GpadSolver:
         if iters is not None:
             it_arr = iters
             st.iters = it_arr.ctypes.data_as(C.POINTER(C.c_int))
+        if codes is not None:  # per-instance termination codes 0..4 (host int32 [batch])
+            st.codes = codes.ctypes.data_as(C.POINTER(C.c_int))
         want = stats or not _is_torch(z)
         for tab in (theta, beta):  # host tables whatever the memory kind (include/gpad.h)
             if tab is not None and (_is_torch(tab) or not isinstance(tab, np.ndarray)):

@@ -94,6 +94,9 @@ typedef struct gpad_stats {
     double tol_floor;            /* tol > 0: the certification floor of this run's data, see
                                   * gpad_run (0 when tol <= 0)                             */
     int flags;                   /* GPAD_FLAG_* of the run                                  */
+    int* codes;                  /* optional caller array [batch] (host) or NULL: per-instance
+                                  * termination code, 0 = ran to N, 1..4 = the test that
+                                  * stopped it (gpad_run)                                   */
 } gpad_stats_t;
 
 /* gpad_stats_t.flags */
@@ -135,6 +138,16 @@ int gpad_setup_scaled(gpad_handle_t h, const gpad_dims_t* dims, const void* MGne
 int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* dims, int n_u, const float* MGf,
                     const float* GLf, double L);
 
+/* Bind the QP Hessian H (n x n row-major; dims.shared: one for the batch, else [batch][n][n];
+ * dims.dtype / dims.memory of the bound problem; symmetric positive definite) and so enable the
+ * value-function branches of Algorithm 1 (acceldualgrad.m:30-33,73,76) in later gpad_run /
+ * gpad_run_state calls with tol > 0.  The QP is then min 1/2 z'Hz + f'z, G z <= g with f = H M
+ * (M = H^-1 f is the vector gpad_run takes).  Those solves run on the stream kernel family (f32 or
+ * f64; the latency and panel kernels do not evaluate the value functions: forcing them returns
+ * GPAD_ERR_UNSUPPORTED).  H = NULL unbinds.  gpad_setup / gpad_setup_scaled unbind as well.
+ * Replaces acceldualgrad.m's own H (the MATLAB function receives H, :1). */
+int gpad_setup_hessian(gpad_handle_t h, const void* H);
+
 /* Run GPAD on the bound problem for every instance of the batch.
  *   z0: in z_{-1}, out z*      [batch][n]   (acceldualgrad.m:17, :83)
  *   y0: in y_0 = y_{-1}, out y* [batch][m]  (acceldualgrad.m:16)
@@ -148,9 +161,13 @@ int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* dims, int n_u, const flo
  *     e_V = dims.tol_gap (default tol).  Both violation tests are decided on directly evaluated
  *     chains (G/L z, G/L zhat) with a rounding margin of 16 units of 2^-24 (f32) / 2^-53 (f64)
  *     of max_i |(G x)_i| + |g_i| / L, so a reported convergence holds for G z* - g evaluated
- *     exactly on the returned z*.  The value-function branches of acceldualgrad.m:73,76
- *     (valuefcn(zhat) e_V/(1+e_V), valuefcn - dualfcn <= e_V max(dualfcn, 1)) need H and q,
- *     which this surface does not carry: they are not evaluated.
+ *     exactly on the returned z*.  With H bound (gpad_setup_hessian) the value-function branches
+ *     of acceldualgrad.m:73,76 follow where the MATLAB test reaches them -- after (B)'s
+ *     violation part passed -- with valuefcn V(x) = (1/2 x'H + f) x and dualfcn D(y) = V(z(y)) +
+ *     y'(G z(y) - g), z(y) = -ML y - M, evaluated in fp64 on the run's data:
+ *     (B') w >= 0, -w'(G zhat - g) > e_V, -w'(G zhat - g) <= V(zhat) e_V/(1+e_V) -> z* = zhat, 3
+ *     (B'') w not >= 0, V(zhat) - D(y+) <= e_V max(D(y+), 1)                  -> z* = zhat, 4
+ *     Without H (the solve(...) surface carries no H, q) they are not evaluated.
  *   Certification floor: the margin above is at least 2^-20 max_i |g_i| (f32; f64: 2^-49), so
  *     a tol below tol_floor = 2^-20 max_{b,i} |g_{b,i}| can never certify an instance whose
  *     solution has an active constraint (G z* - g = 0 in some row) -- e.g. the reference's own
@@ -329,7 +346,8 @@ int gpad_schedule(int N, int kind, double* theta, double* beta);
  * value GPAD_OPT_DEFAULT restores the default.  Returns GPAD_ERR_INVALID for an unknown option
  * or an out-of-range value. */
 #define GPAD_OPT_DEFAULT (-1)
-#define GPAD_OPT_PHASE_LEN 1       /* panel phase length in iterations (default 4 * check_every);
+#define GPAD_OPT_PHASE_LEN 1       /* panel phase length in iterations (default 4 * check_every,
+                                    * doubling after the 10th phase; set: uniform, with PLAN 0);
                                     * flat panels: the first phase; condensed batches: the finisher
                                     * takeover iteration (default planned from the previous solve) */
 #define GPAD_OPT_FINISH_THRESH 2   /* survivors at which the finisher takes over (default 2/CU)    */

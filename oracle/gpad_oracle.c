@@ -102,8 +102,73 @@ static float orc_chain(const float* row, const float* x, int n) {
 /* chain of row i of G_L on x: full rows (row-major m x n) or the flat battery rows */
 typedef float (*orc_row_fn)(const void* ctx, int i, const float* x);
 
+/* ---- value-function branches (acceldualgrad.m:30-33, 73, 76) ---------------------------
+ * With the QP Hessian H bound (gpad_setup_hessian), the QP is min 1/2 z'Hz + f'z, G z <= g with
+ * f = H M (M = g_P = H^-1 f is what the caller passes), and
+ *   valuefcn(x)  V(x) = (1/2 x'H + f) x = sum_i (x_i / 2 + M_i) (H x)_i
+ *   dualfcn(y)   D(y) = lagrangian(z(y), y) = V(z(y)) + y'(G z(y) - g),  z(y) = -ML y - M
+ * evaluated in fp64 on the solve's own (f32 or f64) data: every product (H x)_i, (MGneg y)_i,
+ * (G_L x)_i is one fp64 fma chain over ascending k, G x - g = L (G_L x + p_D); the sums over rows
+ * are fp64 (the kernels sum them in a wave/workgroup tree: the same value to ~1e-16 relative).
+ * Evaluated only where the MATLAB test reaches them: after test (B)'s violation part passed,
+ *   w >= 0 and -w'g(zhat) > e_V:  -w'g(zhat) <= V(zhat) e_V / (1 + e_V)   -> code 3  (:73)
+ *   w not >= 0:                    V(zhat) - D(y+) <= e_V max(D(y+), 1)     -> code 4  (:76)
+ * both returning zhat (as test (B)). */
+struct orc_value_ctx {
+    const double* H;      /* n x n row-major (fp64 copy of the bound H) */
+    const float* MGneg;   /* f32 path: -ML, n x m */
+    const float* GL;      /* f32 path: G_L, m x n */
+    const float* gP;      /* M */
+    const float* pD;
+    const float* zhat;
+    const float* yp;      /* y_{v+1} */
+    int n, m;
+    double L;
+};
+
+static double orc_valuefcn(const double* H, const float* gP, const double* x, int n) {
+    double v = 0.0;
+    for (int i = 0; i < n; i++) {
+        double hx = 0.0;
+        for (int j = 0; j < n; j++) hx = fma(H[(size_t)i * n + j], x[j], hx);
+        v += (0.5 * x[i] + (double)gP[i]) * hx;
+    }
+    return v;
+}
+
+static double orc_dualfcn_f32(const struct orc_value_ctx* c) {
+    const int n = c->n, m = c->m;
+    double* zp = (double*)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    for (int i = 0; i < n; i++) {  /* z(y+) = -ML y+ - M */
+        double a = 0.0;
+        for (int j = 0; j < m; j++) a = fma((double)c->MGneg[(size_t)i * m + j], (double)c->yp[j], a);
+        zp[i] = a - (double)c->gP[i];
+    }
+    double lin = 0.0;  /* y+'(G z - g) / L */
+    for (int k = 0; k < m; k++) {
+        double a = 0.0;
+        for (int j = 0; j < n; j++) a = fma((double)c->GL[(size_t)k * n + j], zp[j], a);
+        lin += (double)c->yp[k] * (a + (double)c->pD[k]);
+    }
+    const double d = orc_valuefcn(c->H, c->gP, zp, n) + c->L * lin;
+    free(zp);
+    return d;
+}
+
+/* value branches after the violation part of (B) passed: 3, 4 or 0 */
+static int orc_value_branch_f32(const struct orc_value_ctx* c, int w_ok, double gapL, double e_V) {
+    double* x = (double*)malloc(sizeof(double) * (size_t)(c->n > 0 ? c->n : 1));
+    for (int i = 0; i < c->n; i++) x[i] = (double)c->zhat[i];
+    const double V = orc_valuefcn(c->H, c->gP, x, c->n);
+    free(x);
+    if (w_ok) return gapL <= V * e_V / (1.0 + e_V) ? 3 : 0;                    /* :73 */
+    const double D = orc_dualfcn_f32(c);
+    return V - D <= e_V * (D > 1.0 ? D : 1.0) ? 4 : 0;                          /* :76 */
+}
+
 static int orc_check_f32(float* u, const float* ch, const float* pD, const float* w, const float* z,
-                         int m, orc_row_fn rowf, const void* ctx, double L, double tol, double tol_gap) {
+                         int m, orc_row_fn rowf, const void* ctx, double L, double tol, double tol_gap,
+                         const struct orc_value_ctx* vc_ctx) {
     float viol = -INFINITY;
     for (int i = 0; i < m; i++) viol = fmaxf(viol, u[i] + pD[i]);
     if ((double)viol * L <= tol) {  /* (A) nominated by the recursion: decide on G_L z itself */
@@ -125,8 +190,10 @@ static int orc_check_f32(float* u, const float* ch, const float* pD, const float
         wmin = fminf(wmin, w[i]);
         gap -= (double)w[i] * (double)t;
     }
-    return (((double)violh * L + ORC_MARGIN_F32 * (double)magh * L <= tol) && (wmin >= 0.0f) &&
-            (gap * L <= tol_gap)) ? 2 : 0;
+    const int vh_ok = (double)violh * L + ORC_MARGIN_F32 * (double)magh * L <= tol;
+    if (vh_ok && wmin >= 0.0f && gap * L <= tol_gap) return 2;
+    if (vh_ok && vc_ctx) return orc_value_branch_f32(vc_ctx, wmin >= 0.0f, gap * L, tol_gap);
+    return 0;
 }
 
 struct orc_full_rows { const float* GL; int n; };
@@ -137,9 +204,29 @@ static float orc_full_row(const void* ctx, int i, const float* x) {
 
 static double orc_tol_gap(double tol, double tol_gap) { return tol_gap > 0.0 ? tol_gap : tol; }
 
+static int orc_solve_f32_h(float* z, float* y, const float* MGneg, const float* gP, const float* GL,
+                           const float* pD, const float* H, int n, int m, int N, float L, double tol,
+                           double tol_gap, int check_every, const float* theta, const float* beta,
+                           int* converged);
+
 int orc_solve_f32(float* z, float* y, const float* MGneg, const float* gP, const float* GL,
                   const float* pD, int n, int m, int N, float L, double tol, double tol_gap,
                   int check_every, const float* theta, const float* beta, int* converged) {
+    return orc_solve_f32_h(z, y, MGneg, gP, GL, pD, NULL, n, m, N, L, tol, tol_gap, check_every, theta, beta,
+                           converged);
+}
+
+int orc_solve_value_f32(float* z, float* y, const float* MGneg, const float* gP, const float* GL,
+                        const float* pD, const float* H, int n, int m, int N, float L, double tol,
+                        double tol_gap, int check_every, const float* theta, const float* beta, int* converged) {
+    return orc_solve_f32_h(z, y, MGneg, gP, GL, pD, H, n, m, N, L, tol, tol_gap, check_every, theta, beta,
+                           converged);
+}
+
+static int orc_solve_f32_h(float* z, float* y, const float* MGneg, const float* gP, const float* GL,
+                           const float* pD, const float* H, int n, int m, int N, float L, double tol,
+                           double tol_gap, int check_every, const float* theta, const float* beta,
+                           int* converged) {
     const int mm = m > 0 ? m : 1;
     float* base = (float*)malloc(sizeof(float) * (size_t)mm * 6);
     float* ycur = base;
@@ -155,6 +242,11 @@ int orc_solve_f32(float* z, float* y, const float* MGneg, const float* gP, const
     const int use_tol = tol > 0.0;
     const double tgap = orc_tol_gap(tol, tol_gap);
     const struct orc_full_rows rows = {GL, n};
+    double* Hd = NULL;
+    if (H) {
+        Hd = (double*)malloc(sizeof(double) * (size_t)n * n + 1);
+        for (size_t k = 0; k < (size_t)n * n; k++) Hd[k] = (double)H[k];
+    }
     if (use_tol)
         for (int i = 0; i < m; i++) u[i] = orc_chain(GL + (size_t)i * n, z, n);
     int it = 0, conv = 0;
@@ -172,9 +264,11 @@ int orc_solve_f32(float* z, float* y, const float* MGneg, const float* gP, const
                 u[i] = fmaf(omt, u[i], th * ch[i]);
             }
             if ((it % check_every) == 0) {
-                const int c = orc_check_f32(u, ch, pD, w, z, m, orc_full_row, &rows, (double)L, tol, tgap);
+                const struct orc_value_ctx vctx = {Hd, MGneg, GL, gP, pD, zhat, ycur, n, m, (double)L};
+                const int c = orc_check_f32(u, ch, pD, w, z, m, orc_full_row, &rows, (double)L, tol, tgap,
+                                            Hd ? &vctx : NULL);
                 if (c) {
-                    if (c == 2) memcpy(z, zhat, sizeof(float) * n);
+                    if (c >= 2) memcpy(z, zhat, sizeof(float) * n);
                     conv = c;
                     break;
                 }
@@ -184,6 +278,7 @@ int orc_solve_f32(float* z, float* y, const float* MGneg, const float* gP, const
     memcpy(y, ycur, sizeof(float) * m);
     free(base);
     free(zhat);
+    free(Hd);
     if (converged) *converged = conv;
     return it;
 }
@@ -297,8 +392,47 @@ int orc_solve_condensed_f32(float* z, float* y, const float* MGneg, const float*
 
 /* ---- fp64, acceldualgrad.m operation order ------------------------------------- */
 /* the fp64 twin of orc_check_f32 (margin ORC_MARGIN_F64 = 16 units of 2^-53) */
+/* fp64 twins of the value functions (orc_valuefcn's sums; ML is +H^-1 G' here) */
+static double orc_valuefcn_d(const double* H, const double* gP, const double* x, int n) {
+    double v = 0.0;
+    for (int i = 0; i < n; i++) {
+        double hx = 0.0;
+        for (int j = 0; j < n; j++) hx = fma(H[(size_t)i * n + j], x[j], hx);
+        v += (0.5 * x[i] + gP[i]) * hx;
+    }
+    return v;
+}
+
+struct orc_value_ctx_d {
+    const double *H, *ML, *GL, *gP, *pD, *zhat, *yp;
+    int n, m;
+    double L;
+};
+
+static int orc_value_branch_f64(const struct orc_value_ctx_d* c, int w_ok, double gapL, double e_V) {
+    const int n = c->n, m = c->m;
+    const double V = orc_valuefcn_d(c->H, c->gP, c->zhat, n);
+    if (w_ok) return gapL <= V * e_V / (1.0 + e_V) ? 3 : 0;
+    double* zp = (double*)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    for (int i = 0; i < n; i++) {
+        double a = 0.0;
+        for (int j = 0; j < m; j++) a = fma(-c->ML[(size_t)i * m + j], c->yp[j], a);
+        zp[i] = a - c->gP[i];
+    }
+    double lin = 0.0;
+    for (int k = 0; k < m; k++) {
+        double a = 0.0;
+        for (int j = 0; j < n; j++) a = fma(c->GL[(size_t)k * n + j], zp[j], a);
+        lin += c->yp[k] * (a + c->pD[k]);
+    }
+    const double D = orc_valuefcn_d(c->H, c->gP, zp, n) + c->L * lin;
+    free(zp);
+    return V - D <= e_V * (D > 1.0 ? D : 1.0) ? 4 : 0;
+}
+
 static int orc_check_f64(double* u, const double* ch, const double* pD, const double* w, const double* z,
-                         const double* GL, int n, int m, double L, double tol, double tol_gap) {
+                         const double* GL, int n, int m, double L, double tol, double tol_gap,
+                         const struct orc_value_ctx_d* vc_ctx) {
     double viol = -INFINITY;
     for (int i = 0; i < m; i++) viol = fmax(viol, u[i] + pD[i]);
     if (viol * L <= tol) {
@@ -320,12 +454,31 @@ static int orc_check_f64(double* u, const double* ch, const double* pD, const do
         wmin = fmin(wmin, w[i]);
         gap -= w[i] * t;
     }
-    return ((violh * L + ORC_MARGIN_F64 * magh * L <= tol) && (wmin >= 0.0) && (gap * L <= tol_gap)) ? 2 : 0;
+    const int vh_ok = violh * L + ORC_MARGIN_F64 * magh * L <= tol;
+    if (vh_ok && wmin >= 0.0 && gap * L <= tol_gap) return 2;
+    if (vh_ok && vc_ctx) return orc_value_branch_f64(vc_ctx, wmin >= 0.0, gap * L, tol_gap);
+    return 0;
 }
+
+static int orc_solve_f64_h(double* z, double* y, const double* ML, const double* gP, const double* G,
+                           const double* g, const double* H, int n, int m, int N, double L, double tol,
+                           double tol_gap, int check_every, int schedule, int* converged);
 
 int orc_solve_f64(double* z, double* y, const double* ML, const double* gP, const double* G,
                   const double* g, int n, int m, int N, double L, double tol, double tol_gap,
                   int check_every, int schedule, int* converged) {
+    return orc_solve_f64_h(z, y, ML, gP, G, g, NULL, n, m, N, L, tol, tol_gap, check_every, schedule, converged);
+}
+
+int orc_solve_value_f64(double* z, double* y, const double* ML, const double* gP, const double* G,
+                        const double* g, const double* H, int n, int m, int N, double L, double tol,
+                        double tol_gap, int check_every, int schedule, int* converged) {
+    return orc_solve_f64_h(z, y, ML, gP, G, g, H, n, m, N, L, tol, tol_gap, check_every, schedule, converged);
+}
+
+static int orc_solve_f64_h(double* z, double* y, const double* ML, const double* gP, const double* G,
+                           const double* g, const double* H, int n, int m, int N, double L, double tol,
+                           double tol_gap, int check_every, int schedule, int* converged) {
     const size_t nm = (size_t)n * m;
     double* GL = (double*)malloc(sizeof(double) * (nm + 1));
     double* pD = (double*)malloc(sizeof(double) * (m + 1));
@@ -372,9 +525,11 @@ int orc_solve_f64(double* z, double* y, const double* ML, const double* gP, cons
         double* t = yvm1; yvm1 = yv; yv = yp1; yp1 = t;                               /* :60-64 */
         it = v + 1;
         if (use_tol && (it % check_every) == 0) {
-            const int c = orc_check_f64(u, ch, pD, w, z, GL, n, m, L, tol, orc_tol_gap(tol, tol_gap));
+            const struct orc_value_ctx_d vctx = {H, ML, GL, gP, pD, zhat, yv, n, m, L};
+            const int c = orc_check_f64(u, ch, pD, w, z, GL, n, m, L, tol, orc_tol_gap(tol, tol_gap),
+                                        H ? &vctx : NULL);
             if (c) {
-                if (c == 2) memcpy(z, zhat, sizeof(double) * n);
+                if (c >= 2) memcpy(z, zhat, sizeof(double) * n);
                 conv = c;
                 break;
             }
@@ -543,7 +698,7 @@ int orc_solve_flat_f32(float* z, float* y, const float* MGf, const float* gP, co
                 u[r] = fmaf(omt, u[r], th * ch[r]);
             }
             if ((it % check_every) == 0) {
-                const int c = orc_check_f32(u, ch, pD, w, z, m, orc_flat_row, &rows, (double)L, tol, tgap);
+                const int c = orc_check_f32(u, ch, pD, w, z, m, orc_flat_row, &rows, (double)L, tol, tgap, NULL);
                 if (c) {
                     if (c == 2) memcpy(z, zhat, sizeof(float) * n);
                     conv = c;

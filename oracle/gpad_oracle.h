@@ -67,6 +67,17 @@ int orc_solve_f32(float* z, float* y, const float* MGneg, const float* gP, const
                   const float* pD, int n, int m, int N, float L, double tol, double tol_gap,
                   int check_every, const float* theta, const float* beta, int* converged);
 
+/* orc_solve_f32 with the value-function branches of Algorithm 1 (acceldualgrad.m:73,76; see
+ * orc_value_branch_f32 in gpad_oracle.c): H is the QP Hessian (n x n row-major, f32), the linear
+ * term is f = H gP.  *converged additionally 3 (:73, relative gap) or 4 (:76, value - dual gap),
+ * both returning zhat. */
+int orc_solve_value_f32(float* z, float* y, const float* MGneg, const float* gP, const float* GL,
+                        const float* pD, const float* H, int n, int m, int N, float L, double tol,
+                        double tol_gap, int check_every, const float* theta, const float* beta, int* converged);
+int orc_solve_value_f64(double* z, double* y, const double* ML, const double* gP, const double* G,
+                        const double* g, const double* H, int n, int m, int N, double L, double tol,
+                        double tol_gap, int check_every, int schedule, int* converged);
+
 /* fp64 solve in acceldualgrad.m:43-64 order: inputs are ML (+H^-1 G^T), gP, G, g, L. */
 /* condensed operator (opt-in GPAD_KERNEL_CONDENSED; not the reference's arithmetic):
  * H = fl32(G_L MGneg) by an fp64 fma chain over k; the solve as orc_solve_f32's semantics with

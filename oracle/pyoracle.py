@@ -60,6 +60,12 @@ class Oracle:
         L.orc_solve_f64.argtypes = [_d, _d, _d, _d, _d, _d, C.c_int, C.c_int, C.c_int, C.c_double,
                                     C.c_double, C.c_double, C.c_int, C.c_int, _i]
         L.orc_solve_f64.restype = C.c_int
+        L.orc_solve_value_f32.argtypes = [_f, _f, _f, _f, _f, _f, _f, C.c_int, C.c_int, C.c_int, C.c_float,
+                                          C.c_double, C.c_double, C.c_int, _f, _f, C.POINTER(C.c_int)]
+        L.orc_solve_value_f32.restype = C.c_int
+        L.orc_solve_value_f64.argtypes = [_d, _d, _d, _d, _d, _d, _d, C.c_int, C.c_int, C.c_int, C.c_double,
+                                          C.c_double, C.c_double, C.c_int, C.c_int, C.POINTER(C.c_int)]
+        L.orc_solve_value_f64.restype = C.c_int
         L.orc_solve_batch_f32.argtypes = [_f, _f, _f, _f, _f, _f, C.c_int, C.c_int, C.c_int, C.c_int,
                                           C.c_int, C.c_float, C.c_double, C.c_double, C.c_int, _f, _f, _i,
                                           C.c_int]
@@ -196,6 +202,35 @@ class Oracle:
                                     _dp(np.ascontiguousarray(g, np.float64)), n, m, N, float(L),
                                     float(tol), float(tol_gap), check_every, schedule, C.byref(conv))
         return z, y, it, bool(conv.value)
+
+    # -- Algorithm 1 with the value-function branches (acceldualgrad.m:73,76; f = H M) -------
+    def solve_value_f32(self, z0, y0, ML, M, G, g, H, N, L, tol=0.0, check_every=10,
+                        schedule=SCHEDULE_MATLAB, tol_gap=0.0):
+        """solve_f32 with the QP Hessian H bound: returns (z, y, iterations, code), code 0..4."""
+        MGneg, GL, pD = self.scale(ML, G, g, L)
+        n, m = MGneg.shape
+        z = np.array(z0, np.float32, copy=True).reshape(n)
+        y = np.array(y0, np.float32, copy=True).reshape(m)
+        theta, beta = self.schedule_f32(max(N, 1), schedule)
+        conv = C.c_int(0)
+        it = self.lib.orc_solve_value_f32(_fp(z), _fp(y), _fp(MGneg), _fp(np.ascontiguousarray(M, np.float32).reshape(n)),
+                                          _fp(GL), _fp(pD), _fp(np.ascontiguousarray(H, np.float32)), n, m, N,
+                                          np.float32(L), float(tol), float(tol_gap), check_every, _fp(theta),
+                                          _fp(beta), C.byref(conv))
+        return z, y, it, conv.value
+
+    def solve_value_f64(self, z0, y0, ML, M, G, g, H, N, L, tol=0.0, check_every=10,
+                        schedule=SCHEDULE_MATLAB, tol_gap=0.0):
+        ML = np.ascontiguousarray(ML, np.float64); n, m = ML.shape
+        z = np.array(z0, np.float64, copy=True).reshape(n)
+        y = np.array(y0, np.float64, copy=True).reshape(m)
+        conv = C.c_int(0)
+        it = self.lib.orc_solve_value_f64(_dp(z), _dp(y), _dp(ML), _dp(np.ascontiguousarray(M, np.float64)),
+                                          _dp(np.ascontiguousarray(G, np.float64)),
+                                          _dp(np.ascontiguousarray(g, np.float64)),
+                                          _dp(np.ascontiguousarray(H, np.float64)), n, m, N, float(L),
+                                          float(tol), float(tol_gap), check_every, schedule, C.byref(conv))
+        return z, y, it, conv.value
 
     def solve_batch_f32(self, Z0, Y0, MGneg, GP, GL, PD, N, L, tol=0.0, check_every=10,
                         shared=True, threads=1, schedule=SCHEDULE_MATLAB, tol_gap=0.0):

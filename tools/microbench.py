@@ -65,6 +65,8 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--batch", type=int, default=0, help="only cases of this batch size")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--case", action="append", default=[],
+                    help="kernel,n,m,batch,N (repeatable): run these instead of the default list")
     ap.add_argument("--check-every", type=int, default=10)
     ap.add_argument("--tol", type=float, default=0.0,
                     help="> 0: run the Algorithm-1 test path (tiny tol: never converges, N its)")
@@ -84,6 +86,8 @@ def main():
     ]
     if args.quick:
         cases = cases[:6]
+    if args.case:
+        cases = [(k, int(n), int(m), int(b), int(N), True) for k, n, m, b, N in (c.split(",") for c in args.case)]
     for c in cases:
         if args.only and args.only not in c[0]:
             continue
