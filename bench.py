@@ -566,6 +566,8 @@ def main():
     ap.add_argument("--kernel", default="auto", choices=["auto", "stream", "resident", "panel"])
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C2/C5 side legs")
+    ap.add_argument("--condensed", action="store_true",
+                    help="also time the frozen, not parity-compliant condensed operator (off by default)")
     ap.add_argument("--repeat-inputs", action="store_true",
                     help="headline on the SAME inputs every step (the planner then sees its own future); "
                          "default: fresh inputs per step, the repeated-input rate reported beside it")
@@ -765,7 +767,7 @@ def main():
                        float(np.float32(qp1.L)), 1000)}.items():
             nn, mm = mML.shape
             res = {}
-            for kk in (_lib.KERNEL_AUTO, _lib.KERNEL_CONDENSED):
+            for kk in ((_lib.KERNEL_AUTO, _lib.KERNEL_CONDENSED) if args.condensed else (_lib.KERNEL_AUTO,)):
                 with gpad_mpc.GpadSolver(dev.index, stream=stream.cuda_stream) as s1:
                     s1.setup(mML, mG, mL, n=nn, m=mm, batch=1, kernel=kk)
                     z1 = torch.zeros(1, nn, device=dev)
@@ -776,18 +778,19 @@ def main():
                         st1 = s1.run(z1.zero_(), y1.zero_(), mM, mg_, iters, 0.0)
                         t.append(st1["kernel_ms"])
                 res[kk] = (st1["kernel"], iters / (min(t) / 1e3), z1.double().cpu(), y1.double().cpu())
-            kb, kc = res[_lib.KERNEL_AUTO], res[_lib.KERNEL_CONDENSED]
+            kb = res[_lib.KERNEL_AUTO]
             rel = lambda a, b: float((a - b).norm() / b.norm())  # noqa: E731
             singles[name] = {"config": ("C2 single instance n=200 m=200" if name == "c2" else
                                         f"C1 single instance: battery n_u=4, N=10 (n={nn}, m={mm})"),
-                             "kernel": kb[0], "iters_per_s": kb[1],
-                             "condensed": {
-                                 "kernel": kc[0], "iters_per_s": kc[1],
-                                 "rel_dev_z": rel(kc[2], kb[2]), "rel_dev_y": rel(kc[3], kb[3]),
-                                 "note": "opt-in GPAD_KERNEL_CONDENSED (one m-long chain per iteration, "
-                                         "not bit-exact); rel_dev_* = norm-wise distance from the bit-exact "
-                                         "kernel's z/y after the same iterations (tests/test_condensed.py "
-                                         "bounds it by the reference's own fp32-vs-fp64 spread at N<=100)"}}
+                             "kernel": kb[0], "iters_per_s": kb[1]}
+            if args.condensed:
+                kc = res[_lib.KERNEL_CONDENSED]
+                singles[name]["condensed"] = {
+                    "kernel": kc[0], "iters_per_s": kc[1],
+                    "rel_dev_z": rel(kc[2], kb[2]), "rel_dev_y": rel(kc[3], kb[3]),
+                    "note": "opt-in GPAD_KERNEL_CONDENSED (one m-long chain per iteration, not bit-exact, "
+                            "frozen); rel_dev_* = norm-wise distance from the bit-exact kernel's z/y after "
+                            "the same iterations"}
             if ref is not None:  # the reference's CPU steps on the same instance, one thread
                 O = ref.O
                 hm = [a.cpu().numpy() for a in (mML, mG, mM, mg_)]
@@ -804,7 +807,8 @@ def main():
             extra["hbm_bound_c5"] = hbm_leg(dev, ref=ref)
             extra["distinct_c2_batch"] = distinct_leg(dev, n, m, ref=ref)
             extra["c3_batch4096"] = c3_leg(dev, n, m, ref=ref)
-            extra["c4_condensed"] = condensed_leg(dev, n, m, batch=B)
+            if args.condensed:
+                extra["c4_condensed"] = condensed_leg(dev, n, m, batch=B)
             extra["closed_loop_battery"] = closed_loop_leg(dev, cpu=not args.no_cpu)
             extra["closed_loop_battery_flat"] = closed_loop_leg(dev, cpu=False, flat=True)
             extra["flat_battery_c1"] = flat_leg(dev, ref=ref)

@@ -77,37 +77,6 @@ __device__ __forceinline__ cf32x4 cp_gemm(__amdgpu_buffer_rsrc_t PA, const float
     return acc;
 }
 
-// two accumulators sharing every A fragment (the same tile of both panels), MFMAs interleaved
-template <int T>
-__device__ __forceinline__ void cp_gemm_dual(__amdgpu_buffer_rsrc_t PA, const float4* B0, const float4* B1, int voff,
-                                             int lane, cf32x4& acc0, cf32x4& acc1) {
-    acc0 = cf32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    acc1 = cf32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    float4 a[2], b0[2], b1[2];
-    a[0] = cp_f4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, 0, 0));
-    b0[0] = B0[lane];
-    b1[0] = B1[lane];
-#pragma unroll
-    for (int kb = 0; kb < T; ++kb) {
-        const int cur = kb & 1, nxt = cur ^ 1;
-        if (kb + 1 < T) {
-            a[nxt] = cp_f4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb + 1) * T * 1024, 0));
-            b0[nxt] = B0[(kb + 1) * 64 + lane];
-            b1[nxt] = B1[(kb + 1) * 64 + lane];
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].x, b0[cur].x, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].x, b1[cur].x, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].y, b0[cur].y, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].y, b1[cur].y, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].z, b0[cur].z, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].z, b1[cur].z, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].w, b0[cur].w, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[cur].w, b1[cur].w, acc1, 0, 0, 0);
-        asm volatile("" ::: "memory");
-    }
-}
-
 struct CpSlot {  // per unit: per column partials of the Algorithm-1 test
     float violz[16], violh[16], wmin[16], magh[16];
     double gap[16];
@@ -123,16 +92,16 @@ struct CpLds {
 };
 constexpr int kCpMaxTiles = 14;  // LDS: 6 T KiB per panel + slots <= 160 KiB
 
-// S = false: WV = 8 waves, wave w owns tiles w, w+8 of ALL P panels (one A stream per tile);
-// S = true:  WV = 16 waves, wave w owns the single (panel, tile) units w, w+16 (unit u = panel
-// u / T, tile u % T), 4 waves per SIMD, every chain its own A stream -- at P = 2, T = 13 the SIMDs
-// carry 7,7,6,6 chains instead of 8,6,6,6.
-template <int T, int P, bool S>
-__global__ __launch_bounds__(S ? 1024 : 512) void gpad_cpanel_kernel(SolveArgs<float> a) {
+// 16 waves: wave w owns the single (panel, tile) units w, w+16 (unit u = panel u / T, tile u % T),
+// 4 waves per SIMD, every chain its own A stream -- at P = 2, T = 13 the SIMDs carry 7,7,6,6
+// chains.  (An 8-wave deal with both panels' chains on one A stream measured slower, 2.68 vs
+// 2.43 ms at the C4 shard, profiles/r02_condensed_panel_waves.txt, and was removed in round 3.)
+template <int T, int P>
+__global__ __launch_bounds__(1024) void gpad_cpanel_kernel(SolveArgs<float> a) {
     constexpr int kCpPanels = P;  // panels per group: 2 (32 instances) or 1 (16)
-    constexpr int WV = S ? 16 : 8;
-    constexpr int NU = S ? (P * T + WV - 1) / WV : (T + WV - 1) / WV;  // units per wave
-    constexpr int PU = S ? 1 : P;  // panels per unit
+    constexpr int WV = 16;
+    constexpr int NU = (P * T + WV - 1) / WV;  // units per wave
+    constexpr int PU = 1;  // panels per unit
     extern __shared__ __attribute__((aligned(16))) float4 cp_lds[];
     CpLds<T, P>* Lp = reinterpret_cast<CpLds<T, P>*>(cp_lds);
     const int lane = threadIdx.x & 63;
@@ -148,14 +117,12 @@ __global__ __launch_bounds__(S ? 1024 : 512) void gpad_cpanel_kernel(SolveArgs<f
     const int count = a.batch;
     const int groups = (count + 16 * kCpPanels - 1) / (16 * kCpPanels);
     auto uid = [&](int q) { return w + WV * q; };
-    auto tile = [&](int q) { return S ? uid(q) % T : uid(q); };
-    auto uvalid = [&](int q) { return S ? uid(q) < P * T : uid(q) < T; };
-    auto upan = [&](int q, int k) { return S ? uid(q) / T : k; };  // panel of slot k of unit q
-    // acc[k] = A (tile of unit q) x B of the unit's k-th panel (both panels share each A fragment)
+    auto tile = [&](int q) { return uid(q) % T; };
+    auto uvalid = [&](int q) { return uid(q) < P * T; };
+    auto upan = [&](int q, int) { return uid(q) / T; };  // panel of unit q
+    // acc[0] = A (tile of unit q) x B of the unit's panel
     auto gemm = [&](int q, __amdgpu_buffer_rsrc_t PA, const float4* B0, const float4* B1, cf32x4 (&acc)[2]) {
-        if constexpr (S) acc[0] = cp_gemm<T>(PA, upan(q, 0) ? B1 : B0, tile(q) * 1024 + lane * 16, lane);
-        else if constexpr (P == 2) cp_gemm_dual<T>(PA, B0, B1, tile(q) * 1024 + lane * 16, lane, acc[0], acc[1]);
-        else acc[0] = cp_gemm<T>(PA, B0, tile(q) * 1024 + lane * 16, lane);
+        acc[0] = cp_gemm<T>(PA, upan(q, 0) ? B1 : B0, tile(q) * 1024 + lane * 16, lane);
     };
 
     for (int grp = blockIdx.x; grp < groups; grp += gridDim.x) {
@@ -518,23 +485,16 @@ hipError_t launch_pack_cpanel(const float* Ht, int n, int m, int ldm, void* hfra
     return hipGetLastError();
 }
 
-template <int T, int P, bool S>
-static hipError_t launch_cp_tps(const SolveArgs<float>& a, hipStream_t s) {
+template <int T, int P>
+static hipError_t launch_cp_tp(const SolveArgs<float>& a, hipStream_t s) {
     const size_t lds = sizeof(CpLds<T, P>);
-    hipError_t e = hipFuncSetAttribute((const void*)gpad_cpanel_kernel<T, P, S>,
+    hipError_t e = hipFuncSetAttribute((const void*)gpad_cpanel_kernel<T, P>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     const int groups = (a.batch + 16 * P - 1) / (16 * P);
     const int grid = groups < a.num_cus ? groups : a.num_cus;
-    hipLaunchKernelGGL((gpad_cpanel_kernel<T, P, S>), dim3(grid), dim3(S ? 1024 : 512), lds, s, a);
+    hipLaunchKernelGGL((gpad_cpanel_kernel<T, P>), dim3(grid), dim3(1024), lds, s, a);
     return hipGetLastError();
-}
-template <int T, int P>
-static hipError_t launch_cp_tp(const SolveArgs<float>& a, hipStream_t s) {
-    // 16 waves dealing single (panel, tile) chains (default: 2.43 vs 2.68 ms at the C4 shard, 1.47 vs
-    // 1.50 ms at 4096, profiles/r02_condensed_panel_waves.txt); GPAD_OPT_CONDENSED_PANEL 2: 8 waves
-    // with both panels' chains on one A stream
-    return (a.tune && a.tune->cpanel == 2) ? launch_cp_tps<T, P, false>(a, s) : launch_cp_tps<T, P, true>(a, s);
 }
 // two panels per group once single panels outnumber the CUs (a group's iteration is latency-bound:
 // one panel per CU halves it while the batch fits one round)

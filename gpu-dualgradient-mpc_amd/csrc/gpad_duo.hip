@@ -224,23 +224,19 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs
     for (int i = c.tid; i < 2 * PA; i += blockDim.x) (&w_l[0][0])[i] = 0.0f;
     for (int i = c.tid; i < 2 * PB; i += blockDim.x) (&zh_l[0][0])[i] = 0.0f;
     for (int i = c.tid; i < PB; i += blockDim.x) z_l[i] = 0.0f;
-    // Static start: slot 0 of workgroup b takes list position b, slot 1 position G + (b - S) --
-    // except the S "solo" workgroups (b < S), whose slot 1 stays empty: the list is sorted
-    // longest-first, so the S longest survivors run one per CU at the single-slot pace instead of
-    // sharing their CU (the tail's critical path); later positions are claimed from the counter.
-    const int S = a.fin_solo < c.G ? (a.fin_solo > 0 ? a.fin_solo : 0) : c.G - 1;
-    const bool solo = (int)blockIdx.x < S;
-    c.claim_base = 2 * c.G - S;
-    if (c.tid == 0) {  // first claims of the queue (positions 2G - S, ...)
+    // Static start: slot 0 of workgroup b takes list position b, slot 1 position G + b (the list is
+    // sorted longest-predicted-first); later positions are claimed from the counter.
+    c.claim_base = 2 * c.G;
+    if (c.tid == 0) {  // first claims of the queue (positions 2G, ...)
         claim_l[0] = c.claim_base + atomicAdd(a.qctr, 1);
-        claim_l[1] = solo ? c.count : c.claim_base + atomicAdd(a.qctr, 1);
+        claim_l[1] = c.claim_base + atomicAdd(a.qctr, 1);
     }
     __syncthreads();
     DuoSlot s0, s1;
     s0.nextp = claim_l[0];
     s1.nextp = claim_l[1];
     duo_refill<KB, K>(a, c, s0, blockIdx.x, w_l[0], gp_l[0], pd_l[0], z_l, r);
-    duo_refill<KB, K>(a, c, s1, solo ? c.count : blockIdx.x + c.G - S, w_l[1], gp_l[1], pd_l[1], z_l, r);
+    duo_refill<KB, K>(a, c, s1, blockIdx.x + c.G, w_l[1], gp_l[1], pd_l[1], z_l, r);
     while (s0.pos < c.count || s1.pos < c.count) {
         duo_step<KA, KB, K>(a, c, s0, s1, w_l[0], zh_l[0], gp_l[0], w_l[1], zh_l[1], gp_l[1], pd_l[1], slots[1],
                             vslots, &claim_l[1], z_l, r);

@@ -287,7 +287,6 @@ int gpad_set_option(gpad_handle_t h, int option, int value) {
         case GPAD_OPT_FINISH_THRESH: return set(t.finish_thresh, 0, big, def.finish_thresh);
         case GPAD_OPT_PLAN: h->plan.nph = 0; h->plan_key = 0; return set(t.plan, 0, 1, def.plan);
         case GPAD_OPT_PHASED: return set(t.phased, 0, 2, def.phased);
-        case GPAD_OPT_FINISHER: return set(t.finisher, 0, 1, def.finisher);
         case GPAD_OPT_LPT: return set(t.lpt, 0, 1, def.lpt);
         case GPAD_OPT_PANEL_MAX_GRID: return set(t.panel_max_grid, 0, big, def.panel_max_grid);
         case GPAD_OPT_DUO_MAX_GRID: return set(t.duo_max_grid, 0, big, def.duo_max_grid);
@@ -298,12 +297,7 @@ int gpad_set_option(gpad_handle_t h, int option, int value) {
                 return fail(GPAD_ERR_INVALID, "gpad_set_option: flat waves must be 0, 8 or 16");
             return set(t.flat_waves, 0, 16, def.flat_waves);
         case GPAD_OPT_FLAT_A_LDS: return set(t.flat_a_lds, 0, 1, def.flat_a_lds);
-        case GPAD_OPT_FINISH_SOLO: return set(t.finish_solo, 0, big, def.finish_solo);
-        case GPAD_OPT_CONDENSED_PANEL: return set(t.cpanel, 0, 2, def.cpanel);
-        case GPAD_OPT_PLAN_FIN_COST:  // re-plan from the next counts
-            h->plan.nph = 0;
-            h->plan_key = 0;
-            return set(t.plan_fin_cost, 1, 10000, def.plan_fin_cost);
+        case GPAD_OPT_CONDENSED_PANEL: return set(t.cpanel, 0, 1, def.cpanel);
         case GPAD_OPT_DEBUG_DROP_HANDOFF: return set(t.debug_drop_handoff, 0, 1, def.debug_drop_handoff);
         default: return fail(GPAD_ERR_INVALID, "gpad_set_option: unknown option");
     }
@@ -672,8 +666,15 @@ int gpad_phase_plan(gpad_handle_t h, int* ends, int* fins, int cap, double* cost
 }
 
 #ifdef GPAD_STAMP
+}  // extern "C"
 namespace gpad {
-hipError_t read_stamps(unsigned long long* out, size_t bytes);  // gpad_panel.hip (diagnostic builds)
+hipError_t read_stamps(unsigned long long* out, size_t bytes);      // gpad_panel.hip (diagnostic builds)
+hipError_t read_res_stamps(unsigned long long* out, size_t bytes);  // gpad_kernels.hip
+}
+extern "C" {
+int gpad_debug_res_stamps(unsigned long long* out, size_t bytes) {
+    HIP_TRY(gpad::read_res_stamps(out, bytes));
+    return GPAD_OK;
 }
 // diagnostic builds only (not declared in gpad.h): the phase-anatomy stamps of the last panel-pair run
 int gpad_debug_stamps(unsigned long long* out, size_t bytes) {

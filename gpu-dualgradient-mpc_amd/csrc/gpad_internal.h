@@ -20,7 +20,6 @@ struct Tuning {
     int finish_thresh = -1;   // GPAD_OPT_FINISH_THRESH: finisher takeover (-1: 2 per CU)
     int plan = 1;             // GPAD_OPT_PLAN: phase plan from the previous solve
     int phased = 1;           // GPAD_OPT_PHASED: phased compaction of tol > 0 panel solves
-    int finisher = 0;         // GPAD_OPT_FINISHER: 0 = duo work queue, 1 = one instance/workgroup
     int lpt = 1;              // GPAD_OPT_LPT: longest-predicted-first finisher queue
     int panel_max_grid = 0;   // GPAD_OPT_PANEL_MAX_GRID: cap on the panel grid (0: none)
     int duo_max_grid = 0;     // GPAD_OPT_DUO_MAX_GRID: cap on the finisher grid (0: none)
@@ -28,10 +27,7 @@ struct Tuning {
     int flat_panels = 0;      // GPAD_OPT_FLAT_PANELS: panels per flat-panel workgroup (0: auto)
     int flat_waves = 0;       // GPAD_OPT_FLAT_WAVES: 0 auto, 8 or 16 waves per workgroup
     int flat_a_lds = 1;       // GPAD_OPT_FLAT_A_LDS: flat fragment image in LDS when it fits
-    int finish_solo = -1;     // GPAD_OPT_FINISH_SOLO: duo workgroups running one instance each
-                              // (the longest-predicted survivors; -1: default)
     int cpanel = 1;           // GPAD_OPT_CONDENSED_PANEL: condensed batches on the MFMA panels
-    int plan_fin_cost = 100;  // GPAD_OPT_PLAN_FIN_COST: the plan model's finisher cost, percent
     int debug_drop_handoff = 0;  // GPAD_OPT_DEBUG_DROP_HANDOFF: test-only fault injection
 };
 
@@ -92,8 +88,6 @@ struct SolveArgs {
     float* cc;             // condensed phases: carried c = -G_L g_P [batch][m]
     int fin_thresh;        // survivors <= this: the resident finisher takes them (0: none)
     int* qctr;             // duo kernel: zeroed device counter of its work-list claims
-    int fin_solo;          // duo kernel: workgroups that run the list's first (longest) entries
-                           // one per CU (their second slot stays empty)
     const int* pred;       // phased solves: per-instance iteration counts predicted from the
                            // previous solve (or null); orders the finisher's queue longest first
     int n_u;               // flat battery path: cells (n = n_u * horizon), see gpad_flat.hip
@@ -114,9 +108,6 @@ struct SolveArgs {
 template <typename T>
 hipError_t launch_stream(const SolveArgs<T>& a, hipStream_t s);
 hipError_t launch_resident(const SolveArgs<float>& a, hipStream_t s, bool* supported);
-// resident kernel over the survivors of a phased panel solve (idx_in/count_in, carried state,
-// iterations v_begin..N); a no-op unless *count_in <= a.fin_thresh.  grid >= fin_thresh.
-hipError_t launch_resident_finisher(const SolveArgs<float>& a, int grid, hipStream_t s);
 // two-instance ping-pong kernel over a work list (shared matrices; gpad_kernels.hip): the
 // list is idx_in/count_in (a no-op unless *count_in <= a.fin_thresh) or 0..batch-1; needs a
 // zeroed a.qctr.  Persistent grid of `grid` workgroups (one per CU).

@@ -343,6 +343,27 @@ template hipError_t launch_stream<double>(const SolveArgs<double>&, hipStream_t)
 // added terms are exact zeros), with the flat step's epilogue (s + w) + p_D, y < 0 -> 0.
 constexpr int kFlatMaxCells = 16;
 
+// Iteration anatomy stamps of the resident kernel (diagnostic builds only, -DGPAD_STAMP): shader
+// clock of workgroup 0, every wave, iterations [101, 105), at six points -- loop top, 8b chain done,
+// after the first barrier, 8d chain done, its epilogue done, after the second barrier
+// (gpad_debug_res_stamps, tools/stamp_resident.py).
+#ifdef GPAD_STAMP
+__device__ unsigned long long g_res_stamps[8][4][6];
+#define GPAD_RSTAMP(P)                                                                         \
+    do {                                                                                       \
+        if (blockIdx.x == 0 && v >= 101 && v < 105 && (tid & 63) == 0)                        \
+            g_res_stamps[tid >> 6][v - 101][P] = __builtin_amdgcn_s_memtime();                 \
+    } while (0)
+hipError_t read_res_stamps(unsigned long long* out, size_t bytes) {
+    if (bytes > sizeof(g_res_stamps)) bytes = sizeof(g_res_stamps);
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_res_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+#else
+#define GPAD_RSTAMP(P) \
+    do {               \
+    } while (0)
+#endif
+
 template <int KA, int KB, bool FLAT>
 __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(SolveArgs<float> a) {
     constexpr int K = KA > KB ? KA : KB;
@@ -353,14 +374,7 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
     __shared__ CheckSlot slots[2][kResidentMaxThreads / 64];  // test, verification of (A)
 
     const int tid = threadIdx.x;
-    // finisher mode (phased panel solves): this block takes survivor blockIdx.x of the list
-    const bool fin = a.count_in != nullptr;
-    if (fin) {
-        const int count = __builtin_amdgcn_readfirstlane(*a.count_in);
-        if (count > a.fin_thresh || (int)blockIdx.x >= count) return;
-    }
-    const int b = fin ? a.idx_in[blockIdx.x] : blockIdx.x;
-    const int v0 = fin ? a.v_begin : 0;  // resume at the carried iteration
+    const int b = blockIdx.x;
     const int n = a.n, m = a.m;
     const int n_u = FLAT ? a.n_u : 1, Nh = FLAT ? n / n_u : 0, mc = 4 * n_u * Nh;
     const int nq = (Nh + 15) >> 4;  // flat: 16-lane DPP rows per cell
@@ -416,7 +430,7 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
     } else if (live) {
         yi = yg[row];
         pdi = (float)(a.gscale * (double)a.g[(size_t)b * a.ld_g + row]);
-        wi = v0 == 0 ? __builtin_fmaf(a.beta[0], yi - yi, yi) : a.wc[(size_t)b * m + row];
+        wi = __builtin_fmaf(a.beta[0], yi - yi, yi);
     }
     for (int i = tid; i < (FLAT ? kFlatMaxCells * PA : PA); i += blockDim.x) w_l[i] = 0.0f;
     for (int i = tid; i < PB; i += blockDim.x) {
@@ -431,19 +445,21 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
     float ui = 0.0f;  // u = G_L z: seeded once, then the 8c recursion (no extra chain per test)
     if (use_tol && !isA) {
         const float us = chain_regs<KB, K>(r, z_l);  // (uniform control flow around the DPP chain)
-        ui = v0 == 0 ? us : (live ? a.uc[(size_t)b * m + row] : 0.0f);
+        ui = us;
     }
 
     int it = 0;
     int done = 0;
     float zhi = 0.0f;
     // theta/beta are prefetched one iteration ahead (tables hold N + 2 entries)
-    float th = a.theta[v0], bn = a.beta[v0 + 1];
-    for (int v = v0; v < a.N; ++v) {
+    float th = a.theta[0], bn = a.beta[1];
+    for (int v = 0; v < a.N; ++v) {
         const float th_next = a.theta[v + 1], bn_next = a.beta[v + 2];
         const bool chk = a.tol > 0.0 && ((v + 1) % a.check_every) == 0;
+        GPAD_RSTAMP(0);
         if (isA) {  // ---- 8b + 8c --------------------------------------------------------
             const float acc = chain_regs<KA, K>(r, wvec);
+            GPAD_RSTAMP(1);
             if (live) {
                 const float zhv = acc - gpi;
                 zi = __builtin_fmaf(1.0f - th, zi, th * zhv);
@@ -452,10 +468,12 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
             }
         }
         __syncthreads();
+        GPAD_RSTAMP(2);
         float violz = -INFINITY, violh = -INFINITY, wmin = INFINITY, magh = 0.0f;
         double gap = 0.0;
         if (!isA) {  // ---- 8d + next 8a ------------------------------------------------
             const float c = chain_regs<KB, K>(r, zh_l);
+            GPAD_RSTAMP(3);
             if (live) {
                 float sv, yp;
                 if constexpr (FLAT) {
@@ -480,7 +498,9 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
             }
         }
         if (chk) check_publish<float>(slots[0], violz, violh, wmin, gap, magh);
+        GPAD_RSTAMP(4);
         __syncthreads();
+        GPAD_RSTAMP(5);
         it = v + 1;
         th = th_next;
         bn = bn_next;
@@ -560,14 +580,7 @@ static hipError_t launch_resident_grid(const SolveArgs<float>& a, int nblocks, h
 hipError_t launch_resident(const SolveArgs<float>& a, hipStream_t st, bool* supported) {
     *supported = resident_supported(a.n, a.m);
     if (!*supported) return hipSuccess;
-    SolveArgs<float> b = a;
-    b.count_in = nullptr;  // whole batch, from iteration 0
-    b.idx_in = nullptr;
-    return launch_resident_grid(b, a.batch, st);
-}
-
-hipError_t launch_resident_finisher(const SolveArgs<float>& a, int grid, hipStream_t st) {
-    return launch_resident_grid(a, grid, st);
+    return launch_resident_grid(a, a.batch, st);  // whole batch, from iteration 0
 }
 
 // flat battery variant: primal chains of 6N, constraint chains of n (flat G_L expanded to the
@@ -585,9 +598,7 @@ hipError_t launch_flat_resident(const SolveArgs<float>& a, hipStream_t st) {
     const int Nh = a.n / a.n_u;
     const int laneA = a.n_u * ((Nh + 15) / 16) * 16;
     const int threads = 64 * ((laneA + 63) / 64) + 64 * ((a.m + 63) / 64);
-    SolveArgs<float> b = a;
-    b.count_in = nullptr;
-    b.idx_in = nullptr;
+    const SolveArgs<float>& b = a;
     const dim3 grid(a.batch), block(threads);
     const int ka = res_bucket(6 * Nh), kb = res_bucket(a.n);
     switch (ka) {

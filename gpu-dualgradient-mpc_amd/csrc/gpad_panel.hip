@@ -1269,7 +1269,7 @@ struct PlanModel {
     int T, n, m, num_cus, grid;
     bool handoff;  // gpad_panel2_kernel's hand-off shapes (Handoff)
     bool relay;    // ... and its one-panel relay (T = 9, 13)
-    double t_chain, t_res, t_launch = 5.0, fin_scale = 1.0;
+    double t_chain, t_res, t_launch = 5.0;
     double iter_time(long long panels) const {
         if (panels <= 0) return 0.0;
         double chains;
@@ -1301,7 +1301,7 @@ struct PlanModel {
     double finisher(int longest, long long work) const {
         const double lat = longest * 1.4 * t_res;
         const double thr = (double)work * 1.1 * t_res / num_cus;
-        return fin_scale * (2 * t_launch + (lat > thr ? lat : thr));
+        return 2 * t_launch + (lat > thr ? lat : thr);
     }
 };
 }  // namespace
@@ -1348,7 +1348,6 @@ int panel_plan(const int* iters, int batch, int n, int m, int N, int check_every
     md.relay = md.handoff && (T == 9 || T == 13);
     md.t_chain = 0.055 * ((m + 15) / 16 + (n + 15) / 16) + 0.2;
     md.t_res = 0.0021 * (n + m) + 0.38;
-    if (t) md.fin_scale = t->plan_fin_cost / 100.0;
     const bool fin_ok = resident_supported(n, m);
     // best[j]: cheapest finish from boundary j (survivors surv[j] in panels); nxt[j] = next
     // boundary (or -1: finisher takes over at j)
@@ -1419,9 +1418,6 @@ size_t panel_work_bytes(int m, int batch) {
 // The order inside a bin is arbitrary -- results never depend on it, only the schedule.
 // A no-op when the list is not the finisher's (count > thresh) or longer than kSortMax.
 constexpr int kSortMax = 8192;
-// default solo workgroups of the duo finisher (GPAD_OPT_FINISH_SOLO): 0 -- measured on fresh
-// inputs (tools/tl_solo.sh) 16 or 48 solo CUs gave no tail gain beyond run-to-run noise
-constexpr int kFinishSolo = 0;
 constexpr int kSortBins = 4096;
 __global__ __launch_bounds__(1024) void survivor_sort_kernel(int* idx, const int* count_p, const int* pred,
                                                              int thresh) {
@@ -1525,7 +1521,6 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     const int len = panel_phase_len(a.check_every, &tn);
     const PanelPlan* plan = (a.plan && a.plan->nph > 0 && a.plan->N == a.N) ? a.plan : nullptr;
     const int fin_default = a.fin_thresh;
-    const bool duo = tn.finisher == 0;  // else one instance per workgroup
     int v0 = 0;
     for (int ph = 0; v0 < a.N; ++ph) {
         int plen = len;
@@ -1544,19 +1539,15 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
         a.count_in = ph ? counts + ph - 1 : nullptr;
         a.idx_out = (ph & 1) ? idx1 : idx0;
         a.count_out = counts + ph;
-        if (ph && a.fin_thresh) {  // few survivors left: the latency kernels take them, run to N
-            if (duo) {  // two instances per CU in ping-pong, fed from the survivor list
-                a.qctr = qctrs + ph;
-                if (a.pred && tn.lpt)  // longest predicted solves first
-                    hipLaunchKernelGGL(survivor_sort_kernel, dim3(1), dim3(1024), 0, s, const_cast<int*>(a.idx_in),
-                                       a.count_in, a.pred, a.fin_thresh);
-                int g = a.fin_thresh < a.num_cus ? a.fin_thresh : a.num_cus;
-                if (tn.duo_max_grid > 0 && tn.duo_max_grid < g) g = tn.duo_max_grid;  // more claims
-                a.fin_solo = tn.finish_solo >= 0 ? tn.finish_solo : kFinishSolo;
-                if ((e = launch_duo(a, g, s)) != hipSuccess) return e;
-            } else if ((e = launch_resident_finisher(a, a.fin_thresh, s)) != hipSuccess) {
-                return e;  // one instance per workgroup
-            }
+        if (ph && a.fin_thresh) {  // few survivors left: the duo finisher takes them, runs to N --
+            // two instances per CU in ping-pong, fed from the survivor list
+            a.qctr = qctrs + ph;
+            if (a.pred && tn.lpt)  // longest predicted solves first
+                hipLaunchKernelGGL(survivor_sort_kernel, dim3(1), dim3(1024), 0, s, const_cast<int*>(a.idx_in),
+                                   a.count_in, a.pred, a.fin_thresh);
+            int g = a.fin_thresh < a.num_cus ? a.fin_thresh : a.num_cus;
+            if (tn.duo_max_grid > 0 && tn.duo_max_grid < g) g = tn.duo_max_grid;  // more claims
+            if ((e = launch_duo(a, g, s)) != hipSuccess) return e;
         }
         launch_panel_kernel<T>(a, grid, s);
         if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -43,18 +43,18 @@ GROUP_RCCL, GROUP_PEER = 1, 2
 
 # gpad_set_option (include/gpad.h GPAD_OPT_*): schedule / launch tuning, never results
 OPT_DEFAULT = -1
-OPT_PHASE_LEN, OPT_FINISH_THRESH, OPT_PLAN, OPT_PHASED, OPT_FINISHER, OPT_LPT = 1, 2, 3, 4, 5, 6
+OPT_PHASE_LEN, OPT_FINISH_THRESH, OPT_PLAN, OPT_PHASED, OPT_LPT = 1, 2, 3, 4, 6
 OPT_PANEL_MAX_GRID, OPT_DUO_MAX_GRID, OPT_FLAT_PANEL_MIN, OPT_FLAT_PANELS = 7, 8, 9, 10
-OPT_FLAT_WAVES, OPT_FLAT_A_LDS, OPT_FINISH_SOLO = 11, 12, 13
+OPT_FLAT_WAVES, OPT_FLAT_A_LDS = 11, 12
 OPT_CONDENSED_PANEL = 14
-OPT_PLAN_FIN_COST = 15
 OPT_DEBUG_DROP_HANDOFF = 16  # test-only fault injection
+OPT_RETIRED = (5, 13, 15)  # finisher kind, solo finisher workgroups, plan finisher cost (0.3)
 OPTIONS = {"phase_len": OPT_PHASE_LEN, "finish_thresh": OPT_FINISH_THRESH, "plan": OPT_PLAN,
-           "phased": OPT_PHASED, "finisher": OPT_FINISHER, "lpt": OPT_LPT,
+           "phased": OPT_PHASED, "lpt": OPT_LPT,
            "panel_max_grid": OPT_PANEL_MAX_GRID, "duo_max_grid": OPT_DUO_MAX_GRID,
            "flat_panel_min": OPT_FLAT_PANEL_MIN, "flat_panels": OPT_FLAT_PANELS,
-           "flat_waves": OPT_FLAT_WAVES, "flat_a_lds": OPT_FLAT_A_LDS, "finish_solo": OPT_FINISH_SOLO,
-           "condensed_panel": OPT_CONDENSED_PANEL, "plan_fin_cost": OPT_PLAN_FIN_COST,
+           "flat_waves": OPT_FLAT_WAVES, "flat_a_lds": OPT_FLAT_A_LDS,
+           "condensed_panel": OPT_CONDENSED_PANEL,
            "debug_drop_handoff": OPT_DEBUG_DROP_HANDOFF}
 
 FILE_ROWMAJOR, FILE_FLIPPED, FILE_FLAT = 0, 1, 2

@@ -59,7 +59,9 @@ extern "C" {
 #define GPAD_KERNEL_RESIDENT 2 /* matrix rows held in VGPRs; one workgroup/instance; n,m <= 208  */
 #define GPAD_KERNEL_PANEL 3    /* shared ML/G, f32 MFMA 16x16x4 panels; one wave per 16 instances */
 #define GPAD_KERNEL_FLAT 4     /* reported only: the flat battery path bound by gpad_setup_flat      */
-/* Opt-in, NOT bit-exact with the reference: the condensed operator.  G_L zhat = H w + c with
+/* Opt-in, NOT bit-exact with the reference and NOT parity-compliant: the condensed operator
+ * (z*, y* measured up to 7.8e-6 relative from the reference's at the C4 configuration to eps, above
+ * the 1e-6 parity bar; kept for latency studies, no longer developed).  G_L zhat = H w + c with
  * H = G_L (-ML) (m x m, formed once per gpad_setup from an fp64 product) and c = -G_L gP, and
  * z = (-ML) wbar - gP with wbar the theta-averaged dual point -- one m-long chain per iteration
  * instead of the reference's m-long (8b) and n-long (8d) chains (C2 latency ~halved).  A
@@ -354,7 +356,8 @@ int gpad_schedule(int N, int kind, double* theta, double* beta);
 #define GPAD_OPT_PLAN 3            /* 1: plan phases from the previous solve's counts (default)    */
 #define GPAD_OPT_PHASED 4          /* 1: phased compaction of tol > 0 panel solves (default; flat
                                     * panels: from 4 panels per CU), 2: always, 0: one launch       */
-#define GPAD_OPT_FINISHER 5        /* 0: two-slot work-queue finisher (default); 1: one per group  */
+/* 5 (finisher kind), 13 (solo finisher workgroups), 15 (plan finisher cost): retired in 0.3 after
+ * measuring no gain; setting them returns GPAD_ERR_INVALID                         */
 #define GPAD_OPT_LPT 6             /* 1: longest-predicted-first finisher queue (default)          */
 #define GPAD_OPT_PANEL_MAX_GRID 7  /* cap on the panel grid, workgroups (0 = none, default)        */
 #define GPAD_OPT_DUO_MAX_GRID 8    /* cap on the finisher grid (0 = none, default)                 */
@@ -362,12 +365,8 @@ int gpad_schedule(int N, int kind, double* theta, double* beta);
 #define GPAD_OPT_FLAT_PANELS 10    /* panels per flat-panel workgroup, 1..4 (0 = auto, default)    */
 #define GPAD_OPT_FLAT_WAVES 11     /* flat-panel workgroup waves: 0 auto (default), 8 or 16         */
 #define GPAD_OPT_FLAT_A_LDS 12     /* 1: flat fragment image staged in LDS when it fits (default)  */
-#define GPAD_OPT_FINISH_SOLO 13    /* finisher CUs that run one (the longest) survivor each         */
 #define GPAD_OPT_CONDENSED_PANEL 14 /* 1: GPAD_KERNEL_CONDENSED batches (shared, > 2/CU) on the MFMA
-                                     * panels, 16 waves (default); 2: 8 waves sharing A streams;
-                                     * 0: one workgroup per instance                               */
-#define GPAD_OPT_PLAN_FIN_COST 15  /* phase plan: the finisher's modelled cost in percent (default
-                                    * 100; > 100 moves the takeover later)                         */
+                                     * panels (default); 0: one workgroup per instance             */
 #define GPAD_OPT_DEBUG_DROP_HANDOFF 16 /* test only (fault injection): 1 = every panel solve that
                                     * uses the chain hand-off withholds its first post, so the
                                     * receiver's bounded wait expires and the run ends in

@@ -211,8 +211,7 @@ def test_condensed_panel_batch_bitexact(gpu, oracle, nm, N, tol):
     # panels to the end / panels to a forced takeover then the latency finisher (eps mode) /
     # no panels (one workgroup per instance); then a second solve planned from the first's counts
     for key, opts in (("panel", dict(phased=0)), ("take30", dict(phase_len=30)), ("take150", dict(phase_len=150)),
-                      ("latency", dict(condensed_panel=0)), ("planned", {}),
-                      ("panel8", dict(condensed_panel=2, phased=0)), ("take30_8", dict(condensed_panel=2, phase_len=30))):
+                      ("latency", dict(condensed_panel=0)), ("planned", {})):
         z = np.zeros((B, n), np.float32)
         y = y0.copy()
         it = np.zeros(B, np.int32)

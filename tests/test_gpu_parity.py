@@ -229,18 +229,16 @@ def test_bigpanel_bitexact(gpu, oracle, tol, N, nm, B, grid, phase):
         assert_bitexact(y[b], yo, f"instance {b} y")
 
 
-@pytest.mark.parametrize("finisher,grid,solo", [("duo", 1, 0), ("duo", 3, 0), ("duo", 0, 0), ("resident", 0, 0),
-                                                ("duo", 5, 2), ("duo", 0, 40), ("duo", 3, 7)])
+@pytest.mark.parametrize("grid", [1, 3, 5, 0])
 @pytest.mark.parametrize("nm,B,z0s", [((200, 200), 120, 0.0), ((40, 180), 200, 0.1), ((131, 64), 97, 0.1)])
-def test_finisher_queue_bitexact(gpu, oracle, finisher, grid, solo, nm, B, z0s):
-    """The tail of a phased panel solve on the latency kernels: the duo kernel (two instances per
-    workgroup in ping-pong, slots refilled from the survivor list through a device counter;
-    grid capped to 1 or 3 workgroups to force many claims) or the one-per-workgroup resident
-    finisher.  The finisher takes over after the first 10-iteration phase, so nearly the whole
-    solve runs there; every instance must match its own oracle solve, iteration count included."""
+def test_finisher_queue_bitexact(gpu, oracle, grid, nm, B, z0s):
+    """The tail of a phased panel solve on the duo finisher (two instances per workgroup in
+    ping-pong, slots refilled from the survivor list through a device counter; grid capped to 1, 3
+    or 5 workgroups to force many claims).  The finisher takes over after the first 10-iteration
+    phase, so nearly the whole solve runs there; every instance must match its own oracle solve,
+    iteration count included."""
     from gpad_mpc import problems
-    opts = dict(finisher=0 if finisher == "duo" else 1, phase_len=10, finish_thresh=100000,
-                duo_max_grid=grid, finish_solo=solo)  # solo: workgroups with one slot (longest first)
+    opts = dict(phase_len=10, finish_thresh=100000, duo_max_grid=grid)
     n, m = nm
     qp = problems.synthetic_qp(n, m, batch=B, seed=12)
     ML, G = qp.ML.astype(np.float32), qp.G.astype(np.float32)
@@ -259,8 +257,8 @@ def test_finisher_queue_bitexact(gpu, oracle, finisher, grid, solo, nm, B, z0s):
         assert_bitexact(y[b], yo, f"instance {b} y")
 
 
-@pytest.mark.parametrize("fin,fin_cost", [(None, None), (0, None), (None, 300), (None, 1)])
-def test_panel_phase_plan_reuse_bitexact(gpu, oracle, fin, fin_cost):
+@pytest.mark.parametrize("fin", [None, 0])
+def test_panel_phase_plan_reuse_bitexact(gpu, oracle, fin):
     """A handle plans its phases from the previous solve's iteration counts (csrc/gpad_panel.hip
     panel_plan); a later solve that needs more (or fewer) iterations than the plan expects must
     still be exact -- the plan moves launch boundaries and the finisher takeover only."""
@@ -274,8 +272,6 @@ def test_panel_phase_plan_reuse_bitexact(gpu, oracle, fin, fin_cost):
     with gpad_mpc.GpadSolver(0) as s:
         s.setup(ML, G, float(L), n=n, m=m, batch=B, kernel=kcode("panel"))
         s.set_options(phase_len=10, finish_thresh=-1 if fin is None else fin)
-        if fin_cost is not None:  # the plan model's finisher cost (moves the takeover only)
-            s.set_options(plan_fin_cost=fin_cost)
         for scale, tol in ((1.0, 1e-3), (3.0, 1e-5), (1.0, 1e-4)):  # easy, harder, middle
             M = (qp.M * scale).astype(np.float32)
             g = (qp.g + 0.1 * rng.random((B, m))).astype(np.float32)
@@ -479,11 +475,11 @@ def test_error_paths(gpu):
         s.run(np.zeros(300, np.float32), np.zeros(300, np.float32), np.zeros(300, np.float32),
               np.zeros(300, np.float32), 10, 0.0)
     assert e.value.code == _lib.ERR_UNSUPPORTED
-    for name, bad in (("plan_fin_cost", 0), ("condensed_panel", 3), (99, 1)):  # out of range / unknown
-        with pytest.raises(gpad_mpc.GpadError) as e:
+    for name, bad in (("condensed_panel", 2), ("lpt", 2), (99, 1)) + tuple((r, 0) for r in _lib.OPT_RETIRED):
+        with pytest.raises(gpad_mpc.GpadError) as e:  # out of range / unknown / retired
             s.set_option(name, bad)
         assert e.value.code == _lib.ERR_INVALID
-    s.set_option("plan_fin_cost", _lib.OPT_DEFAULT)
+    s.set_option("condensed_panel", _lib.OPT_DEFAULT)
     s.close()
 
 

@@ -16,7 +16,6 @@ _MAP = {  # env name -> (option, value transform)
     "GPAD_FINISH_THRESH": ("finish_thresh", int),
     "GPAD_PANEL_NOPLAN": ("plan", lambda v: 0),
     "GPAD_PANEL_NOPHASE": ("phased", lambda v: 0),
-    "GPAD_FINISHER": ("finisher", lambda v: 1 if v == "resident" else 0),
     "GPAD_NO_LPT": ("lpt", lambda v: 0),
     "GPAD_PANEL_MAX_GRID": ("panel_max_grid", int),
     "GPAD_DUO_MAX_GRID": ("duo_max_grid", int),
@@ -24,8 +23,6 @@ _MAP = {  # env name -> (option, value transform)
     "GPAD_FLAT_PANELS": ("flat_panels", int),
     "GPAD_FLAT_WAVES": ("flat_waves", int),
     "GPAD_FLAT_NO_ALDS": ("flat_a_lds", lambda v: 0),
-    "GPAD_FINISH_SOLO": ("finish_solo", int),
-    "GPAD_PLAN_FIN_COST": ("plan_fin_cost", int),
 }
 
 
