@@ -201,11 +201,17 @@ def phase_util(iters, N, K=10, plan=None, fin=512):
 
 def traffic_from_profile(kernel_name):
     """HBM bytes per solve of the dominant kernel from the committed PMC profile of this same
-    bench command (tools/profile.sh -> profiles/r02_bench_summary.json; FETCH_SIZE x2 +
+    bench command (tools/profile.sh -> the newest profiles/rNN_bench_summary.json; FETCH_SIZE x2 +
     WRITE_SIZE, MI355X_MICROARCH.md §HBM): the kernel's bytes summed over every launch of the
     profiled run / the C4 solves that run made (2 x (--warmup + --steps): the fresh-input and the
-    repeated-input loops; the side legs launch other kernel instantiations).  None when absent."""
-    path = os.path.join(ROOT, "profiles", "r02_bench_summary.json")
+    repeated-input loops; the side legs launch other kernel instantiations).  ``kernel_name`` is
+    a prefix: every instantiation of that kernel family and tile count is summed (the T = 13 pairs
+    are compiled per last-block length, gpad_panel2_kernel<13, KQ>).  None when absent."""
+    import glob
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_bench_summary.json")))
+    if not found:
+        return None, None
+    path = found[-1]
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
@@ -215,10 +221,11 @@ def traffic_from_profile(kernel_name):
         solves = 2 * (int(args[args.index("--steps") + 1]) + int(args[args.index("--warmup") + 1]))
     except (ValueError, IndexError):
         return None, None
-    v = d.get("pmc_per_launch", {}).get(kernel_name)
-    if not v or "hbm_bytes_total" not in v or solves <= 0:
+    tot = [v["hbm_bytes_total"] for k, v in d.get("pmc_per_launch", {}).items()
+           if (k == kernel_name or k.startswith(kernel_name[:-1] + ", ")) and "hbm_bytes_total" in v]
+    if not tot or solves <= 0:
         return None, None
-    return v["hbm_bytes_total"] / solves, os.path.relpath(path, ROOT)
+    return sum(tot) / solves, os.path.relpath(path, ROOT)
 
 
 def hbm_leg(dev, batch=1024, n=800, m=800, N=20, ref=None):

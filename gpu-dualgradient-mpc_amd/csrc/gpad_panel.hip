@@ -739,16 +739,16 @@ __device__ __forceinline__ void handoff_post(Panel2Lds<T>& L, int slot, int gen,
 
 // a piece of another wave's chain: k-blocks [KB0, KB1) (KB1 < T) of the tile at voff, continued
 // from slot hs.in (or from zero), parked in slot hs.out; PRIO raises the wave's issue priority
-// fault injection (kDebugDropHandoff, L.hdrop): the first piece of the first hand-off withholds
-// its post, so its receiver's wait expires
-template <int T, int PD, int KB0, int KB1, bool PRIO>
+// fault injection (DROP, the kernel's test-only instantiation; L.hdrop): the first piece of the
+// first hand-off withholds its post, so its receiver's wait expires
+template <int T, int PD, int KB0, int KB1, bool PRIO, bool DROP>
 __device__ __forceinline__ void handoff_piece(Panel2Lds<T>& L, __amdgpu_buffer_rsrc_t PA, const float4* B0, int voff,
                                               int lane, const float4 (&aph)[PD], HoSlots hs, int gen) {
     f32x4 h = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     if (hs.in >= 0) h = handoff_wait(L, hs.in, gen, lane);
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
     panel_chain<T, PD, KB0, KB1>(PA, B0, voff, lane, h, aph, 4);
-    if (!(gen == 1 && hs.in < 0 && L.hdrop)) handoff_post(L, hs.out, gen, lane, h);
+    if (!(DROP && gen == 1 && hs.in < 0 && L.hdrop)) handoff_post(L, hs.out, gen, lane, h);
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
@@ -770,7 +770,8 @@ __device__ __forceinline__ void handoff_take(Panel2Lds<T>& L, __amdgpu_buffer_rs
 // KQ > 0: the shape is known at compile time to have full-length chains on every tile of both
 // GEMMs (16 (T-1) < n, m <= 16 T) whose last k-block issues KQ steps in both: no runtime kq tests
 // (scalar branches whose conditions the compiler spilled to VGPR lanes) and no short-chain paths.
-template <int T, int NU, int ROLE = 0, int KB0 = 0, int KB1 = 0, bool PRIO = false, int KQ = 0, int SPD = 0>
+// DROP: the fault-injection instantiation (handoff_piece).
+template <int T, int NU, int ROLE = 0, int KB0 = 0, int KB1 = 0, bool PRIO = false, int KQ = 0, bool DROP = false>
 __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<T>& L, int t, int p0,
                                            bool pair, int items, int count, HoSlots hs = HoSlots{-1, -1}) {
     static_assert(ROLE == 0 || (Handoff<T>::on && (ROLE == 3 ? NU == 0 : NU == 1)), "hand-off roles");
@@ -859,10 +860,8 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
         }
         __syncthreads();
 
-        constexpr int PD = SPD ? SPD : (NU == 2 ? 1 : (ROLE == 3 ? Handoff<T>::R1 : 2));
+        constexpr int PD = NU == 2 ? 1 : (ROLE == 3 ? Handoff<T>::R1 : 2);
         float4 ap[PD];  // A blocks of the next GEMM, in flight across the barrier before it
-        constexpr int PDR = PD > 2 ? 2 : PD;  // the runtime-length GEMM keeps a ring of 1 or 2
-        const float4 (&apr)[PDR] = *reinterpret_cast<const float4 (*)[PDR]>(&ap);
         float4 aph[PD];  // helper / relay: the piece's first blocks
         auto prefetch = [&](__amdgpu_buffer_rsrc_t PA) {
             if constexpr (ROLE == 2) panel_a_prefetch_from<T, PD>(PA, voff, ap, KB0);
@@ -884,15 +883,15 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 f32x4 acc[2];
                 ++hgen;
                 if constexpr (ROLE == 1)
-                    handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA1, L.Wl[p0], voff_r, lane, aph, hs, hgen);
+                    handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA1, L.Wl[p0], voff_r, lane, aph, hs, hgen);
                 if constexpr (ROLE == 2)
                     handoff_take<T, PD, KB0, PRIO>(L, PA1, L.Wl[p0], voff, lane, ap, hs, hgen, kq1, acc[0]);
                 else if (on1 && nkb1 == T)
                     panel_gemm3<T, NU == 2, PD>(PA1, L.Wl[p0], L.Wl[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1],
                                                 ap, kq1);
                 else if (on1)
-                    panel_gemm_rt<T, NU == 2, PDR>(PA1, L.Wl[p0], L.Wl[NU == 2 ? 1 : p0], voff, lane, acc[0],
-                                                   acc[1], apr, nkb1, kq1);
+                    panel_gemm_rt<T, NU == 2, PD>(PA1, L.Wl[p0], L.Wl[NU == 2 ? 1 : p0], voff, lane, acc[0],
+                                                   acc[1], ap, nkb1, kq1);
                 else
                     acc[0] = acc[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
                 GPAD_STAMP_AT(1);
@@ -916,7 +915,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 }
             } else if constexpr (ROLE == 3) {
                 ++hgen;
-                handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA1, L.Wl[p0], voff, lane, aph, hs, hgen);
+                handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA1, L.Wl[p0], voff, lane, aph, hs, hgen);
                 prefetch(PA2);
             }
             GPAD_STAMP_AT(2);
@@ -936,15 +935,15 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 f32x4 acc[2];
                 ++hgen;
                 if constexpr (ROLE == 1)
-                    handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA2, L.Zh[p0], voff_r, lane, aph, hs, hgen);
+                    handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA2, L.Zh[p0], voff_r, lane, aph, hs, hgen);
                 if constexpr (ROLE == 2)
                     handoff_take<T, PD, KB0, PRIO>(L, PA2, L.Zh[p0], voff, lane, ap, hs, hgen, kq2, acc[0]);
                 else if (on2 && nkb2 == T)
                     panel_gemm3<T, NU == 2, PD>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1],
                                                 ap, kq2);
                 else if (on2)
-                    panel_gemm_rt<T, NU == 2, PDR>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, acc[0],
-                                                   acc[1], apr, nkb2, kq2);
+                    panel_gemm_rt<T, NU == 2, PD>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, acc[0],
+                                                   acc[1], ap, nkb2, kq2);
                 else
                     acc[0] = acc[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
                 GPAD_STAMP_AT(4);
@@ -1019,7 +1018,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 }
             } else if constexpr (ROLE == 3) {
                 ++hgen;
-                handoff_piece<T, PD, KB0, KB1, PRIO>(L, PA2, L.Zh[p0], voff, lane, aph, hs, hgen);
+                handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA2, L.Zh[p0], voff, lane, aph, hs, hgen);
                 prefetch(PA1);
             }
             th = th_next;
@@ -1163,19 +1162,19 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
     }
 }
 
-#ifndef GPAD_SPD
-#define GPAD_SPD 0
-#endif
-constexpr int kSinglePD = GPAD_SPD;  // A ring depth of the one-panel layout's single chains (0: 2)
-
-template <int T, int KQ>
+// KQ > 0 (panel2_run): the pair layout's compile-time chain shape.  The one-panel layout runs the
+// runtime-shape code (KQ = 0) in every instantiation: specialised, its relay measured slower
+// (6.16 vs 5.98 us per iteration at 4 panels, profiles/r03_single_mode_ab.txt).  DROP: the
+// test-only fault-injection instantiation (GPAD_OPT_DEBUG_DROP_HANDOFF), launched instead of the
+// product kernel only while that option is set, so the product kernel carries no trace of it.
+template <int T, int KQ, bool DROP = false>
 __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
     static_assert(T > 8 && T <= 16, "panel pairs need 8 < T <= 16");
     constexpr int D = 2 * T - 16;  // double waves
     __shared__ Panel2Lds<T> L;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int count = a.count_in ? __builtin_amdgcn_readfirstlane(*a.count_in) : a.batch;
-    if (a.count_in && count <= a.fin_thresh) return;  // the resident finisher has them
+    if (a.count_in && count <= a.fin_thresh) return;  // the finisher has them
     const int panels = (count + 15) / 16;
     const bool pair = panels > (int)gridDim.x;
     const int items = pair ? (panels + 1) / 2 : panels;
@@ -1185,36 +1184,36 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
     if (threadIdx.x < 3) L.hflag[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
         L.herr = 0;
-        L.hdrop = (a.debug & kDebugDropHandoff) && blockIdx.x == 0;  // tests: workgroup 0 drops one post
+        L.hdrop = DROP && blockIdx.x == 0;  // tests: workgroup 0 drops one post
     }
     __syncthreads();
     if constexpr (Handoff<T>::on) {
         using H = Handoff<T>;
         if (pair) {  // waves 12, 13 (SIMDs 0, 1; tile T-2) receive from 14, 15 (SIMDs 2, 3; tile T-1)
-            if (w < D) panel2_run<T, 2, 0, 0, 0, false, KQ>(a, L, w, 0, true, items, count);
+            if (w < D) panel2_run<T, 2, 0, 0, 0, false, KQ, DROP>(a, L, w, 0, true, items, count);
             else if (ho && w >= 14)
-                panel2_run<T, 1, 1, 0, H::S, false, KQ>(a, L, T - 1, w & 1, true, items, count, HoSlots{-1, w & 1});
+                panel2_run<T, 1, 1, 0, H::S, false, KQ, DROP>(a, L, T - 1, w & 1, true, items, count, HoSlots{-1, w & 1});
             else if (ho && w >= 12)
-                panel2_run<T, 1, 2, H::S, 0, false, KQ>(a, L, T - 2, w & 1, true, items, count, HoSlots{w & 1, -1});
-            else panel2_run<T, 1, 0, 0, 0, false, KQ>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
+                panel2_run<T, 1, 2, H::S, 0, false, KQ, DROP>(a, L, T - 2, w & 1, true, items, count, HoSlots{w & 1, -1});
+            else panel2_run<T, 1, 0, 0, 0, false, KQ, DROP>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
         } else {  // tile T-1 as a relay: waves T -> T+1 -> T-1
             if constexpr (!H::relay) {
-                if (w < T) panel2_run<T, 1, 0, 0, 0, false, KQ, kSinglePD>(a, L, w, 0, false, items, count);
-                else panel2_run<T, 0, 0, 0, 0, false, KQ>(a, L, 0, 0, false, items, count);
-            } else if (ho && w == T - 1) panel2_run<T, 1, 2, H::R2, 0, true, KQ>(a, L, w, 0, false, items, count, HoSlots{1, -1});
+                if (w < T) panel2_run<T, 1, 0, 0, 0, false, 0, DROP>(a, L, w, 0, false, items, count);
+                else panel2_run<T, 0, 0, 0, 0, false, 0, DROP>(a, L, 0, 0, false, items, count);
+            } else if (ho && w == T - 1) panel2_run<T, 1, 2, H::R2, 0, true, 0, DROP>(a, L, w, 0, false, items, count, HoSlots{1, -1});
             else if (ho && w == T)
-                panel2_run<T, 0, 3, 0, H::R1, true, KQ>(a, L, T - 1, 0, false, items, count, HoSlots{-1, 0});
+                panel2_run<T, 0, 3, 0, H::R1, true, 0, DROP>(a, L, T - 1, 0, false, items, count, HoSlots{-1, 0});
             else if (ho && w == T + 1)
-                panel2_run<T, 0, 3, H::R1, H::R2, true, KQ>(a, L, T - 1, 0, false, items, count, HoSlots{0, 1});
-            else if (w < T) panel2_run<T, 1, 0, 0, 0, false, KQ, kSinglePD>(a, L, w, 0, false, items, count);
-            else panel2_run<T, 0, 0, 0, 0, false, KQ>(a, L, 0, 0, false, items, count);
+                panel2_run<T, 0, 3, H::R1, H::R2, true, 0, DROP>(a, L, T - 1, 0, false, items, count, HoSlots{0, 1});
+            else if (w < T) panel2_run<T, 1, 0, 0, 0, false, 0, DROP>(a, L, w, 0, false, items, count);
+            else panel2_run<T, 0, 0, 0, 0, false, 0, DROP>(a, L, 0, 0, false, items, count);
         }
     } else if (pair) {
-        if (w < D) panel2_run<T, 2, 0, 0, 0, false, KQ>(a, L, w, 0, true, items, count);
-        else panel2_run<T, 1, 0, 0, 0, false, KQ>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
+        if (w < D) panel2_run<T, 2, 0, 0, 0, false, KQ, DROP>(a, L, w, 0, true, items, count);
+        else panel2_run<T, 1, 0, 0, 0, false, KQ, DROP>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
     } else {
-        if (w < T) panel2_run<T, 1, 0, 0, 0, false, KQ, kSinglePD>(a, L, w, 0, false, items, count);
-        else panel2_run<T, 0, 0, 0, 0, false, KQ>(a, L, 0, 0, false, items, count);
+        if (w < T) panel2_run<T, 1, 0, 0, 0, false, 0, DROP>(a, L, w, 0, false, items, count);
+        else panel2_run<T, 0, 0, 0, 0, false, 0, DROP>(a, L, 0, 0, false, items, count);
     }
     if constexpr (Handoff<T>::on) {  // an expired hand-off wait fails the run (GPAD_ERR_DEVICE)
         __syncthreads();
@@ -1476,6 +1475,11 @@ static void launch_panel_kernel(const SolveArgs<float>& a, int grid, hipStream_t
         const int kq1 = (a.m - 16 * (nkb1 - 1) + 3) / 4, kq2 = (a.n - 16 * (nkb2 - 1) + 3) / 4;
         const bool full = nkb1 == T && nkb2 == T && kq1 == kq2;
         if constexpr (T == 13) {
+            if (a.debug & kDebugDropHandoff) {  // tests only: the fault-injection instantiations
+                if (full && kq1 == 2) hipLaunchKernelGGL((gpad_panel2_kernel<T, 2, true>), dim3(grid), dim3(1024), 0, s, a);
+                else hipLaunchKernelGGL((gpad_panel2_kernel<T, 0, true>), dim3(grid), dim3(1024), 0, s, a);
+                return;
+            }
             if (full && kq1 == 1) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 1>), dim3(grid), dim3(1024), 0, s, a); return; }
             if (full && kq1 == 2) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 2>), dim3(grid), dim3(1024), 0, s, a); return; }
             if (full && kq1 == 3) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 3>), dim3(grid), dim3(1024), 0, s, a); return; }

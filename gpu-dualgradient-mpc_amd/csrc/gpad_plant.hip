@@ -159,8 +159,8 @@ __global__ __launch_bounds__(256) void absmax_kernel(const T* __restrict__ g, lo
 template <typename T>
 hipError_t launch_absmax(const T* g, long long count, double* out, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    long long blocks = (count + 4095) / 4096;
-    if (blocks > 128) blocks = 128;
+    long long blocks = (count + 4095) / 4096;  // one pass of 16 loads per thread up to 1024 blocks
+    if (blocks > 1024) blocks = 1024;
     hipLaunchKernelGGL(absmax_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, s, g, count, out);
     return hipGetLastError();
 }

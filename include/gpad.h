@@ -370,7 +370,9 @@ int gpad_schedule(int N, int kind, double* theta, double* beta);
 #define GPAD_OPT_DEBUG_DROP_HANDOFF 16 /* test only (fault injection): 1 = every panel solve that
                                     * uses the chain hand-off withholds its first post, so the
                                     * receiver's bounded wait expires and the run ends in
-                                    * GPAD_ERR_DEVICE; 0 (default) = off                          */
+                                    * GPAD_ERR_DEVICE; 0 (default) = off.  Honoured by the
+                                    * 193..208-row shapes (the C3/C4 tiling, T = 13), which run
+                                    * a separate test-only kernel instantiation while it is set */
 int gpad_set_option(gpad_handle_t h, int option, int value);
 
 /* Synchronise the handle's stream (for callers using device memory + async runs). */
