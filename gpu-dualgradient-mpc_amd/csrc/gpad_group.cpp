@@ -17,10 +17,12 @@
 // clique (RCCL refuses duplicate devices): the same moves are then peer copies
 // (hipMemcpyPeerAsync), ordered by events exactly where the RCCL calls are.
 #include <hip/hip_runtime.h>
-#include <rccl/rccl.h>
+#include <dlfcn.h>
+#include <rccl/rccl.h>  // types only: librccl is loaded on first use (rccl() below), not linked
 
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -38,11 +40,46 @@ int gfail(int code, const std::string& msg) { return gpad::set_last_error(code, 
             return gfail(_e == hipErrorOutOfMemory ? GPAD_ERR_NOMEM : GPAD_ERR_HIP,                   \
                          std::string(#expr) + ": " + hipGetErrorString(_e));                          \
     } while (0)
+// RCCL entry points, resolved from librccl on the first group over distinct devices, so that
+// single-GPU users of libgpad (gpad_solve, the handle API) never need RCCL installed.  Without it a
+// group falls back to the peer-copy transport (gpad_group_transport reports which).
+struct Rccl {
+    bool ok = false;
+    ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Broadcast)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+const Rccl& rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* lib = nullptr;
+        for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+            if ((lib = dlopen(name, RTLD_NOW | RTLD_LOCAL))) break;
+        if (!lib) return;
+        auto sym = [&](auto& fn, const char* name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(lib, name));
+            return fn != nullptr;
+        };
+        r.ok = sym(r.CommInitAll, "ncclCommInitAll") && sym(r.CommDestroy, "ncclCommDestroy") &&
+               sym(r.GroupStart, "ncclGroupStart") && sym(r.GroupEnd, "ncclGroupEnd") && sym(r.Send, "ncclSend") &&
+               sym(r.Recv, "ncclRecv") && sym(r.Broadcast, "ncclBroadcast") &&
+               sym(r.GetErrorString, "ncclGetErrorString");
+    });
+    return r;
+}
+
 #define G_NCCL(expr)                                                                                  \
     do {                                                                                              \
-        ncclResult_t _r = (expr);                                                                     \
+        ncclResult_t _r = rccl().expr;                                                                \
         if (_r != ncclSuccess)                                                                        \
-            return gfail(GPAD_ERR_HIP, std::string(#expr) + ": " + ncclGetErrorString(_r));            \
+            return gfail(GPAD_ERR_HIP, std::string("nccl" #expr) + ": " + rccl().GetErrorString(_r));  \
     } while (0)
 
 size_t esz(int dtype) { return dtype == GPAD_DTYPE_F64 ? sizeof(double) : sizeof(float); }
@@ -85,7 +122,7 @@ int release(gpad_group_s* g) {
         (void)hipSetDevice(g->dev[0]);
         (void)hipEventDestroy(g->caller_ev);
     }
-    for (ncclComm_t c : g->comm) (void)ncclCommDestroy(c);
+    for (ncclComm_t c : g->comm) (void)rccl().CommDestroy(c);
     delete g;
     return GPAD_OK;
 }
@@ -114,12 +151,12 @@ struct Move {
 int scatter(gpad_group_s* g, const std::vector<Move>& mv) {
     if (mv.empty()) return GPAD_OK;
     if (!g->comm.empty()) {
-        G_NCCL(ncclGroupStart());
+        G_NCCL(GroupStart());
         for (const Move& x : mv) {
-            G_NCCL(ncclSend(x.src, x.bytes, ncclChar, x.d, g->comm[0], g->st[0]));
-            G_NCCL(ncclRecv(x.dst, x.bytes, ncclChar, 0, g->comm[x.d], g->st[x.d]));
+            G_NCCL(Send(x.src, x.bytes, ncclChar, x.d, g->comm[0], g->st[0]));
+            G_NCCL(Recv(x.dst, x.bytes, ncclChar, 0, g->comm[x.d], g->st[x.d]));
         }
-        G_NCCL(ncclGroupEnd());
+        G_NCCL(GroupEnd());
         return GPAD_OK;
     }
     G_HIP(hipSetDevice(g->dev[0]));
@@ -137,12 +174,12 @@ int scatter(gpad_group_s* g, const std::vector<Move>& mv) {
 int gather(gpad_group_s* g, const std::vector<Move>& mv) {
     if (mv.empty()) return GPAD_OK;
     if (!g->comm.empty()) {
-        G_NCCL(ncclGroupStart());
+        G_NCCL(GroupStart());
         for (const Move& x : mv) {
-            G_NCCL(ncclSend(x.src, x.bytes, ncclChar, 0, g->comm[x.d], g->st[x.d]));
-            G_NCCL(ncclRecv(x.dst, x.bytes, ncclChar, x.d, g->comm[0], g->st[0]));
+            G_NCCL(Send(x.src, x.bytes, ncclChar, 0, g->comm[x.d], g->st[x.d]));
+            G_NCCL(Recv(x.dst, x.bytes, ncclChar, x.d, g->comm[0], g->st[0]));
         }
-        G_NCCL(ncclGroupEnd());
+        G_NCCL(GroupEnd());
         return GPAD_OK;
     }
     for (int d = 1; d < g->ndev; ++d) {  // the root copies once every shard's solve is done
@@ -221,13 +258,13 @@ int gpad_group_create(gpad_group_t* out, int ndev, const int* devices) {
     std::vector<int> sorted(g->dev);
     std::sort(sorted.begin(), sorted.end());
     const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
-    if (distinct) {  // one RCCL clique, rank d on devices[d]
+    if (distinct && rccl().ok) {  // one RCCL clique, rank d on devices[d]
         g->comm.assign(ndev, nullptr);
-        const ncclResult_t r = ncclCommInitAll(g->comm.data(), ndev, g->dev.data());
+        const ncclResult_t r = rccl().CommInitAll(g->comm.data(), ndev, g->dev.data());
         if (r != ncclSuccess) {
             g->comm.clear();
             release(g);
-            return gfail(GPAD_ERR_HIP, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+            return gfail(GPAD_ERR_HIP, std::string("ncclCommInitAll: ") + rccl().GetErrorString(r));
         }
     }
     *out = g;
@@ -301,12 +338,12 @@ int gpad_group_setup(gpad_group_t g, const gpad_dims_t* dims, const void* ML, co
         }
     }
     if (!host && dims->shared && !g->comm.empty() && nd > 1) {  // shared matrices: one broadcast each
-        G_NCCL(ncclGroupStart());
+        G_NCCL(GroupStart());
         for (int d = 0; d < nd; ++d) {
-            G_NCCL(ncclBroadcast(d == 0 ? ML : nullptr, const_cast<void*>(mlp[d]), nm, ncclChar, 0, g->comm[d], g->st[d]));
-            G_NCCL(ncclBroadcast(d == 0 ? G : nullptr, const_cast<void*>(gp[d]), nm, ncclChar, 0, g->comm[d], g->st[d]));
+            G_NCCL(Broadcast(d == 0 ? ML : nullptr, const_cast<void*>(mlp[d]), nm, ncclChar, 0, g->comm[d], g->st[d]));
+            G_NCCL(Broadcast(d == 0 ? G : nullptr, const_cast<void*>(gp[d]), nm, ncclChar, 0, g->comm[d], g->st[d]));
         }
-        G_NCCL(ncclGroupEnd());
+        G_NCCL(GroupEnd());
     }
     if ((rc = scatter(g, mv))) return rc;
     for (int d = 0; d < nd; ++d) {  // pack on every device (each handle orders on its stream)
@@ -406,19 +443,31 @@ int gpad_group_run(gpad_group_t g, void* z0, void* y0, const void* M, const void
     return GPAD_OK;
 }
 
+}  // extern "C"
+
+// One group per thread and device list, kept between gpad_solve_sharded calls (communicator set-up
+// is the expensive part).  Freed by gpad_release_cached(), never from a thread-exit destructor: at
+// process exit that can run after the HIP / RCCL runtimes tore down (the OS reclaims it instead).
+namespace {
+struct ShardCache {
+    gpad_group_t grp = nullptr;
+    std::vector<int> devs;
+};
+thread_local ShardCache t_shard_cache;
+}  // namespace
+
+void gpad::release_sharded_cache() {
+    if (t_shard_cache.grp) gpad_group_destroy(t_shard_cache.grp);
+    t_shard_cache.grp = nullptr;
+    t_shard_cache.devs.clear();
+}
+
+extern "C" {
+
 int gpad_solve_sharded(int ndev, const int* devices, void* z0, void* y0, const void* ML, const void* M,
                        const void* G, const void* g, int N, double L, double tol, const gpad_dims_t* dims,
                        gpad_stats_t* st) {
-    // one group per thread and device list, kept between calls (communicator set-up is the
-    // expensive part); the matrices are re-bound every call
-    struct Cache {
-        gpad_group_t grp = nullptr;
-        std::vector<int> devs;
-        ~Cache() {
-            if (grp) gpad_group_destroy(grp);
-        }
-    };
-    thread_local Cache cache;
+    ShardCache& cache = t_shard_cache;
     if (ndev <= 0 || !devices) return gfail(GPAD_ERR_INVALID, "gpad_solve_sharded: bad device list");
     std::vector<int> want(devices, devices + ndev);
     if (!cache.grp || cache.devs != want) {

@@ -86,6 +86,14 @@ void host_schedule(int N, int kind, double* theta, double* beta) {
 
 int gpad::set_last_error(int code, const std::string& msg) { return fail(code, msg); }
 
+// Run status block (gpad_handle_s::status), zeroed before a run's first launch: the device error
+// word, then the per-workgroup maxima of |g| (launch_absmax) from which the host takes gmax.
+struct RunStatus {
+    int err;
+    int pad;
+    double part[gpad::kAbsmaxMaxBlocks];
+};
+
 struct gpad_handle_s {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -120,7 +128,9 @@ struct gpad_handle_s {
     // run status block on the device, zeroed per run: {int error bits (gpad::kDevErr*), pad,
     // double max |g|} -- the error word the kernels report into and the certification floor's
     // data term (include/gpad.h gpad_run)
-    DevBuf status;
+    DevBuf status;             // RunStatus
+    RunStatus h_status;        // ... its host copy for the stats
+    int gmax_blocks = 0;       // RunStatus::part entries the run's absmax launches wrote
     double last_tol = 0.0;          // tol of the last run
     double last_floor_scale = 0.0;  // tol_floor = this * max |g| (margin * L * |gscale|)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -152,12 +162,6 @@ struct gpad_handle_s {
     gpad::Tuning tune;                  // gpad_set_option
 };
 
-// Run status block (gpad_handle_s::status): zeroed before a run's first launch.
-struct RunStatus {
-    int err;
-    int pad;
-    double gmax;
-};
 
 static int reset_status(gpad_handle_t h, double tol, double floor_scale) {
     int rc = h->status.ensure(sizeof(RunStatus));
@@ -165,15 +169,24 @@ static int reset_status(gpad_handle_t h, double tol, double floor_scale) {
     HIP_TRY(hipMemsetAsync(h->status.p, 0, sizeof(RunStatus), h->stream));
     h->last_tol = tol;
     h->last_floor_scale = floor_scale;
+    h->gmax_blocks = 0;
     return GPAD_OK;
 }
 
-// Enqueue the copy of the status block to *rs (the caller synchronises the stream).
-static int fetch_status(gpad_handle_t h, RunStatus* rs) {
-    *rs = RunStatus{};
+// Enqueue the copy of the status block to *rs (the caller synchronises the stream): the error word,
+// and with `maxima` the |g| maxima of the run (RunStatus::part[0 .. gmax_blocks)).
+static int fetch_status(gpad_handle_t h, RunStatus* rs, bool maxima = false) {
+    rs->err = 0;
     if (!h->status.p) return GPAD_OK;
-    HIP_TRY(hipMemcpyAsync(rs, h->status.p, sizeof(RunStatus), hipMemcpyDeviceToHost, h->stream));
+    const size_t bytes = offsetof(RunStatus, part) + (maxima ? sizeof(double) * (size_t)h->gmax_blocks : 0);
+    HIP_TRY(hipMemcpyAsync(rs, h->status.p, bytes, hipMemcpyDeviceToHost, h->stream));
     return GPAD_OK;
+}
+
+static double status_gmax(gpad_handle_t h, const RunStatus& rs) {
+    double g = 0.0;
+    for (int b = 0; b < h->gmax_blocks; ++b) g = std::max(g, rs.part[b]);
+    return g;
 }
 
 static int status_error(const RunStatus& rs) {
@@ -186,7 +199,7 @@ static int status_error(const RunStatus& rs) {
 
 extern "C" {
 
-const char* gpad_version(void) { return "gpad-mi355x 0.2 (gfx950)"; }
+const char* gpad_version(void) { return "gpad-mi355x 0.3 (gfx950)"; }
 
 int gpad_device_count(void) {
     int count = 0;
@@ -306,7 +319,7 @@ int gpad_set_option(gpad_handle_t h, int option, int value) {
 int gpad_sync(gpad_handle_t h) {
     if (!h) return fail(GPAD_ERR_INVALID, "gpad_sync: null handle");
     HIP_TRY(hipSetDevice(h->device));
-    RunStatus rs;
+    RunStatus& rs = h->h_status;
     int rc = fetch_status(h, &rs);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -605,8 +618,8 @@ static int collect_stats(gpad_handle_t h, gpad_stats_t* st) {
     h->h_counts.resize(2 * entries);
     HIP_TRY(hipMemcpyAsync(h->h_counts.data(), h->counters.p, sizeof(int) * 2 * entries,
                            hipMemcpyDeviceToHost, h->stream));
-    RunStatus rs;
-    int rc = fetch_status(h, &rs);
+    RunStatus& rs = h->h_status;
+    int rc = fetch_status(h, &rs, true);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(h->stream));
     st->iterations = 0;
@@ -631,7 +644,7 @@ static int collect_stats(gpad_handle_t h, gpad_stats_t* st) {
     float ms = 0.0f;
     st->kernel_ms = 0.0;
     if (h->timed && hipEventElapsedTime(&ms, h->ev0, h->ev1) == hipSuccess) st->kernel_ms = ms;
-    st->tol_floor = h->last_tol > 0.0 ? h->last_floor_scale * rs.gmax : 0.0;
+    st->tol_floor = h->last_tol > 0.0 ? h->last_floor_scale * status_gmax(h, rs) : 0.0;
     st->flags = (h->last_tol > 0.0 && h->last_tol < st->tol_floor) ? GPAD_FLAG_TOL_FLOOR : 0;
     return status_error(rs);
 }
@@ -744,9 +757,12 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
     a.err = (int*)h->status.p;
     a.debug = h->tune.debug_drop_handoff ? gpad::kDebugDropHandoff : 0;
     if (tol > 0.0)  // the certification floor's data term (stats: tol_floor, GPAD_FLAG_TOL_FLOOR)
+    {
         HIP_TRY(gpad::launch_absmax<T>(dg, (long long)batch * m,
-                                       reinterpret_cast<double*>((char*)h->status.p + offsetof(RunStatus, gmax)),
+                                       reinterpret_cast<double*>((char*)h->status.p + offsetof(RunStatus, part)),
                                        h->stream));
+        h->gmax_blocks = std::max(h->gmax_blocks, gpad::absmax_blocks((long long)batch * m));
+    }
     int kernel = d.kernel;
     const bool prev_phased = h->last_phased;  // the previous launch's counts are still in `iters`
     h->last_phased = false;  // set again below when this launch is a phased panel solve
@@ -1004,19 +1020,33 @@ static bool same_dims(const gpad_dims_t& a, const gpad_dims_t& b) {
            a.kernel == b.kernel && a.reserved == b.reserved && a.tol_gap == b.tol_gap;
 }
 
+}  // extern "C"
+
+// gpad_solve's per-thread handle: freed by gpad_release_cached(), not by a thread-exit destructor
+// (at process exit that may run after the HIP runtime tore down; the OS reclaims it then).
+namespace {
+struct SolveCache {
+    gpad_handle_t h = nullptr;
+    int device = -1;
+};
+thread_local SolveCache t_solve_cache;
+}  // namespace
+
+extern "C" {
+
+void gpad_release_cached(void) {
+    if (t_solve_cache.h) gpad_destroy(t_solve_cache.h);
+    t_solve_cache.h = nullptr;
+    t_solve_cache.device = -1;
+    gpad::release_sharded_cache();
+}
+
 int gpad_solve(void* z0, void* y0, const void* ML, const void* M, const void* G, const void* g, int N,
                double L, double tol, const gpad_dims_t* dims, gpad_stats_t* st) {
     // One handle per thread and device, kept between calls: a per-MPC-step caller (gpad.m:90)
     // pays the handle, the workspaces and -- when the host matrices are unchanged -- the H2D
-    // copy and repack of ML/G once, not per call.
-    struct Cache {
-        gpad_handle_t h = nullptr;
-        int device = -1;
-        ~Cache() {
-            if (h) gpad_destroy(h);
-        }
-    };
-    thread_local Cache cache;
+    // copy and repack of ML/G once, not per call.  gpad_release_cached() frees it.
+    SolveCache& cache = t_solve_cache;
     int rc = validate_dims(dims);
     if (rc) return rc;
     if (!ML || !G) return fail(GPAD_ERR_INVALID, "gpad_solve: null matrix");

@@ -180,9 +180,18 @@ hipError_t launch_precompute(int n, int m, int nf, const double* H, long long sH
                              int count, hipStream_t s);
 hipError_t launch_apply_inv(int n, int batch, const double* Hinv, const double* f, double* gP, hipStream_t s);
 hipError_t launch_accumulate_iters(const int* iters, long long count, long long* acc, hipStream_t s);
-// *out = max(*out, max |g_i|) over count elements (device double; zero it before the first call)
+// part[b] = max(part[b], max |g_i| over workgroup b's share), b < absmax_blocks(count): per-
+// workgroup maxima, no atomics (the host reduces them when it reads the stats; zero part before the
+// first call)
+constexpr int kAbsmaxMaxBlocks = 1024;
+// gpad_release_cached: this thread's gpad_solve_sharded group (gpad_group.cpp)
+void release_sharded_cache();
+inline int absmax_blocks(long long count) {
+    const long long b = (count + 4095) / 4096;
+    return b < 1 ? 1 : (b > kAbsmaxMaxBlocks ? kAbsmaxMaxBlocks : (int)b);
+}
 template <typename T>
-hipError_t launch_absmax(const T* g, long long count, double* out, hipStream_t s);
+hipError_t launch_absmax(const T* g, long long count, double* part, hipStream_t s);
 // flat battery data on the MFMA pipe (gpad_flatpanel.hip): per-cell skinny GEMMs over panels
 bool flatpanel_supported(int n, int m, int n_u);
 size_t flatpanel_frag_bytes(int n, int m, int n_u);

@@ -128,13 +128,14 @@ hipError_t launch_accumulate_iters(const int* iters, long long count, long long*
     return hipGetLastError();
 }
 
-// *out = max(*out, max_i |g_i|) (for the certification floor, include/gpad.h gpad_run): at most 128
-// workgroups of 256 threads, 16 elements per thread and pass with the loads of a pass issued
-// together, each workgroup reducing through LDS to ONE 64-bit atomic (non-negative doubles order
-// like their bit patterns; thousands of same-address atomics cost ~30 us)
+// part[b] = max(part[b], max |g_i| of workgroup b) (the certification floor, include/gpad.h
+// gpad_run): up to 1024 workgroups of 256 threads, 16 elements per thread and pass with the loads of
+// a pass issued together (one pass at the C4 shard), each workgroup reducing through LDS into its
+// own slot.  No atomics: hundreds of same-address atomics serialise at L2 (~30 us per solve
+// measured); the host reduces the slots when it reads the stats.
 template <typename T>
-__global__ __launch_bounds__(256) void absmax_kernel(const T* __restrict__ g, long long count, double* out) {
-    __shared__ double part[4];
+__global__ __launch_bounds__(256) void absmax_kernel(const T* __restrict__ g, long long count, double* part) {
+    __shared__ double red[4];
     double mx = 0.0;
     const long long stride = (long long)gridDim.x * blockDim.x;
     for (long long base = (long long)blockIdx.x * blockDim.x + threadIdx.x; base < count; base += 16 * stride) {
@@ -148,20 +149,18 @@ __global__ __launch_bounds__(256) void absmax_kernel(const T* __restrict__ g, lo
         for (int u = 0; u < 16; ++u) mx = fmax(mx, fabs((double)v[u]));
     }
     for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = mx;
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
     __syncthreads();
     if (threadIdx.x == 0) {
-        mx = fmax(fmax(part[0], part[1]), fmax(part[2], part[3]));
-        atomicMax(reinterpret_cast<unsigned long long*>(out), (unsigned long long)__double_as_longlong(mx));
+        mx = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+        part[blockIdx.x] = fmax(part[blockIdx.x], mx);
     }
 }
 
 template <typename T>
-hipError_t launch_absmax(const T* g, long long count, double* out, hipStream_t s) {
+hipError_t launch_absmax(const T* g, long long count, double* part, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    long long blocks = (count + 4095) / 4096;  // one pass of 16 loads per thread up to 1024 blocks
-    if (blocks > 1024) blocks = 1024;
-    hipLaunchKernelGGL(absmax_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, s, g, count, out);
+    hipLaunchKernelGGL(absmax_kernel<T>, dim3(absmax_blocks(count)), dim3(256), 0, s, g, count, part);
     return hipGetLastError();
 }
 template hipError_t launch_absmax<float>(const float*, long long, double*, hipStream_t);

@@ -281,6 +281,10 @@ int gpad_plan_phases(const int* iters, int batch, int n, int m, int N, int check
  * create + setup + run + destroy (the handle is cached per thread and device). */
 int gpad_solve(void* z0, void* y0, const void* ML, const void* M, const void* G, const void* g,
                int N, double L, double tol, const gpad_dims_t* dims, gpad_stats_t* st);
+/* Free the calling thread's cached gpad_solve handle and gpad_solve_sharded group (device memory,
+ * streams, RCCL communicators).  Call it before a thread that used them exits; the caches are
+ * never freed from a thread-exit destructor (at process exit the OS reclaims them). */
+void gpad_release_cached(void);
 
 /* ---- multi-device: instance shards, RCCL scatter/gather ------------------
  * A group drives several devices from ONE C process (the reference's caller is a single C
@@ -293,7 +297,9 @@ int gpad_solve(void* z0, void* y0, const void* ML, const void* M, const void* G,
  * ncclSend/ncclRecv, and (z*, y*) come back into the root buffers by another.  GPAD_MEM_HOST:
  * every device copies its own shard in and out.  With distinct devices the group holds one RCCL
  * clique (ncclCommInitAll); a device listed twice (one GPU standing in for several) moves the
- * same bytes by peer copies instead (gpad_group_transport tells which). */
+ * same bytes by peer copies instead (gpad_group_transport tells which).  librccl is loaded on the
+ * first group over distinct devices (not linked: single-GPU users need no RCCL); when it cannot
+ * be loaded such a group uses the peer copies too. */
 typedef struct gpad_group_s* gpad_group_t;
 #define GPAD_GROUP_RCCL 1
 #define GPAD_GROUP_PEER 2

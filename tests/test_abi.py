@@ -49,6 +49,25 @@ def test_library_exports_every_declared_symbol():
     assert sorted(_lib.EXPORTS) == syms
 
 
+def test_library_loads_rccl_lazily():
+    """single-GPU users must not need librccl -- it is dlopen'ed by the first group over
+    distinct devices (gpad_group.cpp rccl()), never a NEEDED entry of libgpad.so."""
+    import shutil
+    lib = os.path.join(PKG, "gpad_mpc", "libgpad.so")
+    if not shutil.which("readelf"):
+        pytest.skip("readelf not available")
+    dyn = subprocess.run(["readelf", "-d", lib], capture_output=True, text=True, check=True).stdout
+    needed = re.findall(r"\(NEEDED\).*\[(.*)\]", dyn)
+    assert needed and not any("rccl" in n for n in needed), needed
+
+
+def test_release_cached_without_handles_is_a_noop():
+    from gpad_mpc import _lib
+    L = _lib.load()
+    L.gpad_release_cached()  # nothing cached on this thread: returns, touches no device
+    L.gpad_release_cached()
+
+
 def test_host_only_entry_points():
     from gpad_mpc import _lib, solver
     L = _lib.load()

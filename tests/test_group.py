@@ -76,11 +76,14 @@ def test_group_shards_equal_single_handle(gpu, devices, transport, memory, share
 @pytest.mark.parametrize("devices", [[0], [0, 0, 0, 0]])
 def test_solve_sharded_one_shot(gpu, oracle, devices):
     """gpad_solve_sharded(ndev, devices, z0, y0, ML, M, G, g, N, L, tol, dims, stats) through ctypes,
-    called twice (the cached group re-binds the matrices) -- bit-exact vs the oracle."""
+    called three times (the cached group re-binds the matrices; before the third call
+    gpad_release_cached frees the group, which is then rebuilt) -- bit-exact vs the oracle."""
     from gpad_mpc import _lib
     lib = _lib.load()
     n, m, B, N, tol = 64, 96, 50, 3000, 1e-4
-    for seed in (1, 2):
+    for seed in (1, 2, 3):
+        if seed == 3:
+            lib.gpad_release_cached()
         ML, M, G, g, L = _qp(n, m, B, seed)
         Z = np.zeros((B, n), np.float32)
         Y = np.zeros((B, m), np.float32)
