@@ -484,8 +484,9 @@ __global__ __launch_bounds__(64 * kBigWaves) void gpad_bigpanel_kernel(SolveArgs
             if (v >= a.v_end || live == 0u) break;
         }
         // ---- phase end: park the survivors -----------------------------------------------------
-        if (carry && v >= a.v_end) {
-            if (active) {
+        if (carry) {
+            const bool park = active && v >= a.v_end;
+            if (park) {
 #pragma unroll
                 for (int q = 0; q < NT1; ++q) {
                     const int t = w + kBigWaves * q;
@@ -513,13 +514,7 @@ __global__ __launch_bounds__(64 * kBigWaves) void gpad_bigpanel_kernel(SolveArgs
                     }
                 }
             }
-            if (w == 0) {  // lanes 0..15 (j == 0) speak for the 16 columns
-                const unsigned long long lv = __ballot(active && j == 0);
-                int base = 0;
-                if (lane == 0) base = atomicAdd(a.count_out, (int)__popcll(lv));
-                base = __shfl(base, 0, 64);
-                if (active && j == 0) a.idx_out[base + (int)__popcll(lv & ((1ull << lane) - 1ull))] = inst;
-            }
+            if (w == 0) list_survivors(a, p, park, inst, lane, j);  // lanes 0..15 speak for the columns
         }
         __syncthreads();  // the next panel reuses the LDS tiles
     }

@@ -130,7 +130,6 @@ struct gpad_handle_s {
     // data term (include/gpad.h gpad_run)
     DevBuf status;             // RunStatus
     RunStatus h_status;        // ... its host copy for the stats
-    int gmax_blocks = 0;       // RunStatus::part entries the run's absmax launches wrote
     double last_tol = 0.0;          // tol of the last run
     double last_floor_scale = 0.0;  // tol_floor = this * max |g| (margin * L * |gscale|)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -169,23 +168,22 @@ static int reset_status(gpad_handle_t h, double tol, double floor_scale) {
     HIP_TRY(hipMemsetAsync(h->status.p, 0, sizeof(RunStatus), h->stream));
     h->last_tol = tol;
     h->last_floor_scale = floor_scale;
-    h->gmax_blocks = 0;
     return GPAD_OK;
 }
 
 // Enqueue the copy of the status block to *rs (the caller synchronises the stream): the error word,
-// and with `maxima` the |g| maxima of the run (RunStatus::part[0 .. gmax_blocks)).
+// and with `maxima` the per-workgroup |g| maxima of the run (RunStatus::part).
 static int fetch_status(gpad_handle_t h, RunStatus* rs, bool maxima = false) {
     rs->err = 0;
     if (!h->status.p) return GPAD_OK;
-    const size_t bytes = offsetof(RunStatus, part) + (maxima ? sizeof(double) * (size_t)h->gmax_blocks : 0);
+    const size_t bytes = maxima ? sizeof(RunStatus) : offsetof(RunStatus, part);
     HIP_TRY(hipMemcpyAsync(rs, h->status.p, bytes, hipMemcpyDeviceToHost, h->stream));
     return GPAD_OK;
 }
 
 static double status_gmax(gpad_handle_t h, const RunStatus& rs) {
     double g = 0.0;
-    for (int b = 0; b < h->gmax_blocks; ++b) g = std::max(g, rs.part[b]);
+    for (int b = 0; b < gpad::kAbsmaxMaxBlocks; ++b) g = std::max(g, rs.part[b]);
     return g;
 }
 
@@ -678,6 +676,17 @@ int gpad_phase_plan(gpad_handle_t h, int* ends, int* fins, int cap, double* cost
     return n;
 }
 
+int gpad_phase_counts(gpad_handle_t h, int* counts, int cap) {
+    if (!h || !counts || cap < 0) return fail(GPAD_ERR_INVALID, "gpad_phase_counts: bad argument");
+    if (!h->last_phased || !h->pwork.p) return 0;
+    HIP_TRY(hipSetDevice(h->device));
+    const int k = cap < gpad::kPanelMaxPhases ? cap : gpad::kPanelMaxPhases;
+    const int* dev = reinterpret_cast<const int*>(h->pwork.p) + 2 * (size_t)h->last_batch;  // panel_work_bytes
+    HIP_TRY(hipMemcpyAsync(counts, dev, sizeof(int) * (size_t)k, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return k;
+}
+
 #ifdef GPAD_STAMP
 }  // extern "C"
 namespace gpad {
@@ -756,13 +765,18 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
     a.strideHq = d.shared ? 0 : (long long)n * h->ldn;
     a.err = (int*)h->status.p;
     a.debug = h->tune.debug_drop_handoff ? gpad::kDebugDropHandoff : 0;
-    if (tol > 0.0)  // the certification floor's data term (stats: tol_floor, GPAD_FLAG_TOL_FLOOR)
-    {
-        HIP_TRY(gpad::launch_absmax<T>(dg, (long long)batch * m,
-                                       reinterpret_cast<double*>((char*)h->status.p + offsetof(RunStatus, part)),
-                                       h->stream));
-        h->gmax_blocks = std::max(h->gmax_blocks, gpad::absmax_blocks((long long)batch * m));
-    }
+    // the certification floor's data term max |g| (stats: tol_floor, GPAD_FLAG_TOL_FLOOR): folded
+    // into the panel pairs' own loads, else one launch_absmax after the solve's launches
+    double* gpart = tol > 0.0 ? reinterpret_cast<double*>((char*)h->status.p + offsetof(RunStatus, part)) : nullptr;
+    bool gmax_done = false;
+    if constexpr (sizeof(T) == sizeof(float)) a.gmax_part = gpart;
+    auto finish = [&](int rc) {
+        if (rc == GPAD_OK && gpart && !gmax_done) {
+            const hipError_t ea = gpad::launch_absmax<T>(dg, (long long)batch * m, gpart, h->stream);
+            if (ea != hipSuccess) return fail(GPAD_ERR_HIP, std::string("absmax: ") + hipGetErrorString(ea));
+        }
+        return rc;
+    };
     int kernel = d.kernel;
     const bool prev_phased = h->last_phased;  // the previous launch's counts are still in `iters`
     h->last_phased = false;  // set again below when this launch is a phased panel solve
@@ -773,7 +787,7 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
         HIP_TRY(hipMemsetAsync(a.iters, 0, sizeof(int) * (size_t)batch, h->stream));
         HIP_TRY(hipMemsetAsync(a.conv, 0, sizeof(int) * (size_t)batch, h->stream));
         *kernel_out = d.kernel == GPAD_KERNEL_AUTO ? GPAD_KERNEL_STREAM : d.kernel;
-        return GPAD_OK;
+        return finish(GPAD_OK);
     }
     if (a.Hq) {  // value-function branches: evaluated by the stream kernel family only
         if (kernel != GPAD_KERNEL_AUTO && kernel != GPAD_KERNEL_STREAM)
@@ -810,7 +824,7 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
                 return fail(e == hipErrorInvalidValue ? GPAD_ERR_UNSUPPORTED : GPAD_ERR_HIP,
                             std::string("flat kernel: ") + hipGetErrorString(e));
             *kernel_out = GPAD_KERNEL_FLAT;
-            return GPAD_OK;
+            return finish(GPAD_OK);
         }
         if (kernel == GPAD_KERNEL_CONDENSED) {  // opt-in condensed operator (gpad_condensed.hip)
             // shared-matrix batches beyond ~2 per CU on the MFMA pipe (gpad_cpanel.hip), else one
@@ -854,14 +868,14 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
                     }
                     h->last_phased = tol > 0.0 && h->tune.phased;  // its counts plan the next takeover
                     *kernel_out = kernel;
-                    return GPAD_OK;
+                    return finish(GPAD_OK);
                 }
             }
             e = gpad::launch_condensed(a, h->stream, &ok);
             if (e != hipSuccess) return fail(GPAD_ERR_HIP, std::string("condensed: ") + hipGetErrorString(e));
             if (!ok) return fail(GPAD_ERR_UNSUPPORTED, "condensed kernel: bind with dims.kernel = CONDENSED");
             *kernel_out = kernel;
-            return GPAD_OK;
+            return finish(GPAD_OK);
         }
         // shared matrices: panels once there are more instances than the latency kernel can
         // run at ~one round (4 per CU: 4 x its 1/6-panel iteration time < one panel iteration)
@@ -881,6 +895,7 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
             if (ok) kernel = GPAD_KERNEL_PANEL;
             else if (kernel == GPAD_KERNEL_PANEL)
                 return fail(GPAD_ERR_UNSUPPORTED, "panel kernel: needs shared f32 matrices");
+            gmax_done = ok && gpad::panel_folds_gmax(n, m);
         }
         if (!ok && (kernel == GPAD_KERNEL_RESIDENT || kernel == GPAD_KERNEL_AUTO)) {
             e = gpad::launch_resident(a, h->stream, &ok);
@@ -903,7 +918,7 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
     }
     *kernel_out = kernel;
     h->last_phased = kernel == GPAD_KERNEL_PANEL && a.pwork != nullptr;
-    return GPAD_OK;
+    return finish(GPAD_OK);
 }
 
 template <typename T>

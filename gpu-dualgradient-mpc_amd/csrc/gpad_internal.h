@@ -81,7 +81,12 @@ struct SolveArgs {
     const int* idx_in;     // instances of this phase (null: 0..batch-1)
     const int* count_in;   // their number (device; null: batch)
     int* idx_out;          // survivors appended here ...
-    int* count_out;        // ... and counted here (device)
+    int* count_out;        // ... and counted here (device) -- or, with seg_cnt set, listed per panel:
+    int* seg_cnt;          // [panel] survivors of panel P of this phase (no same-address atomics)
+    int* seg_idx;          // [16 panel + rank] their instances; phase_compact_kernel densifies
+    double* gmax_part;     // [kAbsmaxMaxBlocks] per-workgroup max |g| of the run (the certification
+                           // floor; null: not wanted): the panel pairs fold it into their loads,
+                           // every other path runs launch_absmax
     float* wc;             // carried w  [batch][m]
     float* uc;             // carried u = G_L z [batch][m]
     float* wbc;            // condensed phases: carried wbar [batch][m]
@@ -127,6 +132,38 @@ hipError_t launch_pack_cpanel(const float* Ht, int n, int m, int ldm, void* hfra
 hipError_t launch_cpanel(const SolveArgs<float>& a, hipStream_t s, bool* supported);
 int cpanel_takeover(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus);
 hipError_t launch_panel(const SolveArgs<float>& a, hipStream_t s, bool* supported);
+// launch_panel at (n, m) runs the panel pairs, which fold max |g| into their loads (gmax_part)
+bool panel_folds_gmax(int n, int m);
+
+// Phase end of a panel kernel: list panel P's parked columns.  Called by the wave that speaks for
+// the panel, whose lanes 0..15 (j == 0) hold columns 0..15; `park`: this lane's column carries
+// over.  With a.seg_cnt the panel writes its own slot -- seg_cnt[P], seg_idx[16 P + rank] -- and
+// phase_compact_kernel densifies the list at the boundary: no same-address atomics (hundreds of
+// panels appending to one counter serialise at L2, ~25 us per boundary at 512 panels measured).
+// Without it (flat / condensed panels) the survivors are appended through a.count_out.  Every
+// panel of a phase calls it, parked or not, so no slot keeps a stale count.
+__device__ __forceinline__ void list_survivors(const SolveArgs<float>& a, int P, bool park, int inst, int lane,
+                                               int j) {
+    const unsigned long long lv = __ballot(park && j == 0);
+    const int rank = (int)__popcll(lv & ((1ull << lane) - 1ull));
+    if (a.seg_cnt) {
+        if (lane == 0) a.seg_cnt[P] = (int)__popcll(lv);
+        if (park && j == 0) a.seg_idx[16 * P + rank] = inst;
+    } else {
+        int base = 0;
+        if (lane == 0 && lv) base = atomicAdd(a.count_out, (int)__popcll(lv));
+        base = __shfl(base, 0, 64);
+        if (park && j == 0) a.idx_out[base + rank] = inst;
+    }
+}
+// the boundary before phase ph >= 1: the survivors phase ph - 1 listed per panel (seg_cnt / seg_idx)
+// -> idx_out[0 .. *count_out), optionally ordered longest-predicted-first (pred: the previous
+// solve's counts, when the list is the finisher's: count <= fin_cur).  count_prev / fin_prev:
+// phase ph - 1's own input count and finisher threshold (count_prev <= fin_prev: the finisher
+// took that list and the panel phase listed nothing).
+hipError_t launch_phase_compact(const int* seg_cnt, const int* seg_idx, const int* count_prev, int batch,
+                                int fin_prev, int* idx_out, int* count_out, const int* pred, int fin_cur,
+                                hipStream_t s);
 size_t panel_frag_bytes(int n, int m, int batch);
 size_t panel_work_bytes(int m, int batch);
 int panel_phase_len(int check_every, const Tuning* t);

@@ -390,8 +390,9 @@ __global__ __launch_bounds__(64 * T) void gpad_panel_kernel(SolveArgs<float> a) 
             if (v >= a.v_end || !__syncthreads_or(active ? 1 : 0)) break;
         }
         // ---- phase end: park the survivors for the next phase ------------------------------
-        if (carry && v >= a.v_end) {
-            if (active) {
+        if (carry) {
+            const bool park = active && v >= a.v_end;
+            if (park) {
                 const float4 w4 = Wl4[slot];  // w of iteration v (own slot)
                 const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
@@ -405,13 +406,7 @@ __global__ __launch_bounds__(64 * T) void gpad_panel_kernel(SolveArgs<float> a) 
                     }
                 }
             }
-            if (t == 0) {  // lanes 0..15 (j == 0) speak for the 16 columns
-                const unsigned long long live = __ballot(active && j == 0);
-                int base = 0;
-                if (lane == 0) base = atomicAdd(a.count_out, (int)__popcll(live));
-                base = __shfl(base, 0, 64);
-                if (active && j == 0) a.idx_out[base + (int)__popcll(live & ((1ull << lane) - 1ull))] = inst;
-            }
+            if (t == 0) list_survivors(a, p, park, inst, lane, j);  // lanes 0..15 speak for the columns
         }
         __syncthreads();  // the next panel reuses the LDS tiles
     }
@@ -685,6 +680,7 @@ struct Panel2Lds {
     int hflag[3];          // hand-off generation per slot
     int herr;              // a wait expired (handoff_wait): reported to the run's error word at exit
     int hdrop;             // fault injection (kDebugDropHandoff) for this workgroup
+    float gred[16];        // per wave: max |g| over the rows it loaded (SolveArgs::gmax_part)
 };
 
 // Phase anatomy stamps (diagnostic builds only, -DGPAD_STAMP; never in the product library): the
@@ -798,6 +794,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
     const bool on1 = FULL || 16 * t < n, on2 = FULL || 16 * t < m;
     const int voff_r = voff - 1024;  // helper: the receiver's tile t - 1 (Handoff)
     int hgen = 0;                    // hand-off generation, counted alike by helper and receiver
+    float gmx = 0.0f;                // max |g| over the rows this lane loads (gmax_part)
 
     for (int it = blockIdx.x; it < items; it += gridDim.x) {
         // columns still running, bit 16 pp + c for panel pp of this item: the same word in every
@@ -831,7 +828,9 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 z[q][r] = okn ? a.z[b * n + i] : 0.0f;
                 gp[r] = okn ? a.gP[b * a.ld_gP + i] : 0.0f;
                 y[q][r] = okm ? a.y[b * m + i] : 0.0f;
-                pd[r] = okm ? (float)(a.gscale * (double)a.g[b * a.ld_g + i]) : 0.0f;
+                const float gr = okm ? a.g[b * a.ld_g + i] : 0.0f;
+                pd[r] = (float)(a.gscale * (double)gr);
+                gmx = fmaxf(gmx, __builtin_fabsf(gr));
                 if (fresh) {  // w_0 = y_0 + beta_0 (y_0 - y_{-1}), y_{-1} = y_0
                     wv[r] = __builtin_fmaf(a.beta[0], y[q][r] - y[q][r], y[q][r]);
                     u[q][r] = 0.0f;
@@ -1129,10 +1128,11 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
         }
         // ---- phase end: park the survivors -----------------------------------------------
         if constexpr (NU > 0) {
-            if (carry && v >= a.v_end) {
+            if (carry) {
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
-                    if (act[q]) {
+                    const bool park = act[q] && v >= a.v_end;
+                    if (park) {
                         const float4 w4 = L.Wl[p0 + q][slot];
                         const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
                         const size_t b = (size_t)inst[q];
@@ -1147,18 +1147,16 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                             }
                         }
                     }
-                    if (t == 0) {  // the tile-0 owner of panel p0+q appends its survivors
-                        const unsigned long long live = __ballot(act[q] && j == 0);
-                        int base = 0;
-                        if (lane == 0) base = atomicAdd(a.count_out, (int)__popcll(live));
-                        base = __shfl(base, 0, 64);
-                        if (act[q] && j == 0)
-                            a.idx_out[base + (int)__popcll(live & ((1ull << lane) - 1ull))] = inst[q];
-                    }
+                    if (t == 0)  // the tile-0 owner of panel p0+q lists its survivors
+                        list_survivors(a, pair ? 2 * it + p0 + q : it, park, inst[q], lane, j);
                 }
             }
         }
         __syncthreads();
+    }
+    if (a.gmax_part) {  // this wave's max |g| -> L.gred (reduced by the kernel at exit)
+        for (int o = 32; o > 0; o >>= 1) gmx = fmaxf(gmx, __shfl_xor(gmx, o, 64));
+        if (lane == 0) L.gred[threadIdx.x >> 6] = gmx;
     }
 }
 
@@ -1186,6 +1184,7 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
         L.herr = 0;
         L.hdrop = DROP && blockIdx.x == 0;  // tests: workgroup 0 drops one post
     }
+    if (threadIdx.x < 16) L.gred[threadIdx.x] = 0.0f;
     __syncthreads();
     if constexpr (Handoff<T>::on) {
         using H = Handoff<T>;
@@ -1215,9 +1214,15 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
         if (w < T) panel2_run<T, 1, 0, 0, 0, false, 0, DROP>(a, L, w, 0, false, items, count);
         else panel2_run<T, 0, 0, 0, 0, false, 0, DROP>(a, L, 0, 0, false, items, count);
     }
-    if constexpr (Handoff<T>::on) {  // an expired hand-off wait fails the run (GPAD_ERR_DEVICE)
+    if (Handoff<T>::on || a.gmax_part) {
         __syncthreads();
-        if (threadIdx.x == 0 && L.herr) atomicOr(a.err, kDevErrHandoff);
+        // an expired hand-off wait fails the run (GPAD_ERR_DEVICE)
+        if (Handoff<T>::on && threadIdx.x == 0 && L.herr) atomicOr(a.err, kDevErrHandoff);
+        if (a.gmax_part && threadIdx.x == 0) {  // the run's max |g|: this workgroup's slot
+            float g = 0.0f;
+            for (int i = 0; i < 16; ++i) g = fmaxf(g, L.gred[i]);
+            a.gmax_part[blockIdx.x] = fmax(a.gmax_part[blockIdx.x], (double)g);
+        }
     }
 }
 
@@ -1382,7 +1387,10 @@ int panel_plan(const int* iters, int batch, int n, int m, int N, int check_every
     while (j < J && ph < slots) {
         const int k = nxt[j];
         if (k < 0) break;  // finisher at boundary j
-        out->fins[ph] = fin_default;
+        // a panel phase: the finisher may still take its list early when the survivors fall to
+        // its default threshold -- unless the plan expects several times that many, where its
+        // launch would only test and return (~5 us per boundary)
+        out->fins[ph] = (j > 0 && surv[j] > 4 * (long long)fin_default) ? 0 : fin_default;
         out->ends[ph++] = k * step;
         j = k;
         if (surv[j] == 0) break;
@@ -1406,62 +1414,116 @@ int panel_plan(const int* iters, int batch, int n, int m, int N, int check_every
 
 size_t panel_work_bytes(int m, int batch) {
     // idx ping-pong [2][batch] | phase counts [kPanelMaxPhases] | finisher queue counters
-    // [kPanelMaxPhases] | carried w, u [batch][m] each
-    return sizeof(int) * (2 * (size_t)batch + 2 * kPanelMaxPhases) + 2 * sizeof(float) * (size_t)batch * m;
+    // [kPanelMaxPhases] | carried w, u [batch][m] each | per-panel survivor lists: seg_idx
+    // [batch + 32], seg_cnt [batch / 16 + 2] (list_survivors)
+    return sizeof(int) * (2 * (size_t)batch + 2 * kPanelMaxPhases) + 2 * sizeof(float) * (size_t)batch * m +
+           sizeof(int) * ((size_t)batch + 32 + (size_t)batch / 16 + 2);
 }
 
-// Longest-first order for the finisher's work list: the survivors idx[0..count) reordered by the
-// iteration count the previous solve needed (descending), so the duo kernel's queue starts the
-// longest remaining solves first (list scheduling, LPT).  One workgroup, counting sort on the
-// counts (4096 bins, larger counts share the last): histogram, descending exclusive scan, scatter.
-// The order inside a bin is arbitrary -- results never depend on it, only the schedule.
-// A no-op when the list is not the finisher's (count > thresh) or longer than kSortMax.
+// Phase boundary (launch_phase_compact): the survivors the previous phase listed per panel
+// (list_survivors: seg_cnt[P], seg_idx[16 P + rank]) become the dense list idx[0 .. count) of the
+// next phase.  One workgroup: thread t owns a contiguous run of panels, an LDS scan of the
+// per-thread totals gives each run its base, and the run's entries are copied in panel order.
+//
+// When the list is the finisher's (count <= fin_cur) and the previous solve's counts are known
+// (pred), it is then reordered longest-predicted-first so the duo kernel's queue starts the
+// longest remaining solves first (list scheduling, LPT): a counting sort on the counts (4096
+// bins, larger counts share the last) -- histogram, descending exclusive scan, scatter.  The order
+// inside a bin is arbitrary; results never depend on the order, only the schedule does.
 constexpr int kSortMax = 8192;
 constexpr int kSortBins = 4096;
-__global__ __launch_bounds__(1024) void survivor_sort_kernel(int* idx, const int* count_p, const int* pred,
-                                                             int thresh) {
+__device__ __forceinline__ int block_scan_1024(int* part, int tid, int v) {  // exclusive scan, 1024 threads
+    part[tid] = v;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const int x = tid >= off ? part[tid - off] : 0;
+        __syncthreads();
+        part[tid] += x;
+        __syncthreads();
+    }
+    return part[tid] - v;
+}
+
+constexpr int kCompactMaxPanels = 8192;  // per-panel bases in LDS up to here (131072 instances)
+__global__ __launch_bounds__(1024) void phase_compact_kernel(const int* __restrict__ seg_cnt,
+                                                             const int* __restrict__ seg_idx, const int* count_prev,
+                                                             int batch, int fin_prev, int* idx, int* count_out,
+                                                             const int* pred, int fin_cur) {
     __shared__ int hist[kSortBins];
     __shared__ int ids[kSortMax];
     __shared__ int part[1024];
-    const int count = *count_p;
-    if (count <= 1 || count > thresh || count > kSortMax) return;
+    __shared__ int pbase[kCompactMaxPanels];
+    __shared__ int total_l;
     const int tid = threadIdx.x;
+    const int prev = count_prev ? *count_prev : batch;
+    if (count_prev && prev <= fin_prev) {  // the finisher took the previous list: nothing was listed
+        if (tid == 0) *count_out = 0;
+        return;
+    }
+    const int panels = (prev + 15) / 16;
+    const int per = (panels + 1023) / 1024;
+    const int p0 = tid * per < panels ? tid * per : panels, p1 = p0 + per < panels ? p0 + per : panels;
+    int sum = 0;
+    for (int p = p0; p < p1; ++p) sum += seg_cnt[p];
+    int base = block_scan_1024(part, tid, sum);
+    if (tid == 1023) total_l = base + sum;
+    const bool lds_bases = panels <= kCompactMaxPanels;
+    if (lds_bases) {
+        for (int p = p0; p < p1; ++p) {
+            const int c = seg_cnt[p];
+            pbase[p] = c ? base : -1;
+            base += c;
+        }
+    }
+    __syncthreads();
+    const int count = total_l;
+    const bool sort = pred && count > 1 && count <= fin_cur && count <= kSortMax;
+    int* dst = sort ? ids : idx;
+    if (lds_bases) {  // entry r of panel p by thread (16 p + r) mod 1024: coalesced, independent loads
+        for (int i = tid; i < 16 * panels; i += 1024) {
+            const int p = i >> 4, r = i & 15, b = pbase[p];
+            if (b >= 0 && r < seg_cnt[p]) dst[b + r] = seg_idx[i];
+        }
+    } else {
+        for (int p = p0; p < p1; ++p) {
+            const int c = seg_cnt[p];
+            for (int r = 0; r < c; ++r) dst[base + r] = seg_idx[16 * p + r];
+            base += c;
+        }
+    }
+    if (tid == 0) *count_out = count;
+    if (!sort) return;
     auto bin = [&](int id) {  // descending count -> ascending bin
-        const int p = pred[id];
-        const int k = p < 0 ? 0 : (p >= kSortBins ? kSortBins - 1 : p);
+        const int q = pred[id];
+        const int k = q < 0 ? 0 : (q >= kSortBins ? kSortBins - 1 : q);
         return kSortBins - 1 - k;
     };
     for (int i = tid; i < kSortBins; i += 1024) hist[i] = 0;
     __syncthreads();
-    for (int i = tid; i < count; i += 1024) {
-        const int id = idx[i];
-        ids[i] = id;
-        atomicAdd(&hist[bin(id)], 1);
-    }
+    for (int i = tid; i < count; i += 1024) atomicAdd(&hist[bin(ids[i])], 1);  // (LDS atomics)
     __syncthreads();
-    // exclusive scan of hist: thread tid owns bins 4 tid .. 4 tid + 3
-    int local[4], sum = 0;
+    int local[4], hs = 0;  // thread tid owns bins 4 tid .. 4 tid + 3
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        local[q] = sum;
-        sum += hist[4 * tid + q];
+        local[q] = hs;
+        hs += hist[4 * tid + q];
     }
-    part[tid] = sum;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {  // inclusive scan of the per-thread sums
-        const int v = tid >= off ? part[tid - off] : 0;
-        __syncthreads();
-        part[tid] += v;
-        __syncthreads();
-    }
-    const int base = part[tid] - sum;
+    const int hb = block_scan_1024(part, tid, hs);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) hist[4 * tid + q] = base + local[q];
+    for (int q = 0; q < 4; ++q) hist[4 * tid + q] = hb + local[q];
     __syncthreads();
     for (int i = tid; i < count; i += 1024) {
         const int id = ids[i];
         idx[atomicAdd(&hist[bin(id)], 1)] = id;
     }
+}
+
+hipError_t launch_phase_compact(const int* seg_cnt, const int* seg_idx, const int* count_prev, int batch,
+                                int fin_prev, int* idx_out, int* count_out, const int* pred, int fin_cur,
+                                hipStream_t s) {
+    hipLaunchKernelGGL(phase_compact_kernel, dim3(1), dim3(1024), 0, s, seg_cnt, seg_idx, count_prev, batch,
+                       fin_prev, idx_out, count_out, pred, fin_cur);
+    return hipGetLastError();
 }
 
 template <int T>
@@ -1517,6 +1579,12 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     float* wc = reinterpret_cast<float*>(qctrs + kPanelMaxPhases);
     a.wc = wc;
     a.uc = wc + (size_t)a.batch * a.m;
+    // survivors listed per panel, densified at each boundary by phase_compact_kernel (one idx
+    // list suffices: phase ph reads idx0 while it lists into seg_idx)
+    a.seg_idx = reinterpret_cast<int*>(a.uc + (size_t)a.batch * a.m);
+    a.seg_cnt = a.seg_idx + a.batch + 32;
+    a.idx_out = nullptr;
+    a.count_out = nullptr;
     hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * 2 * kPanelMaxPhases, s);
     if (e != hipSuccess) return e;
     // phase length: a multiple of the test period (phases end right after a test); default
@@ -1525,6 +1593,7 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     const int len = panel_phase_len(a.check_every, &tn);
     const PanelPlan* plan = (a.plan && a.plan->nph > 0 && a.plan->N == a.N) ? a.plan : nullptr;
     const int fin_default = a.fin_thresh;
+    int fin_prev = 0;  // the previous phase's finisher threshold
     int v0 = 0;
     for (int ph = 0; v0 < a.N; ++ph) {
         int plen = len;
@@ -1539,16 +1608,17 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
         const int v1 = (a.N - v0 <= plen) ? a.N : v0 + plen;
         a.v_begin = v0;
         a.v_end = v1;
-        a.idx_in = ph ? ((ph & 1) ? idx0 : idx1) : nullptr;
+        a.idx_in = ph ? idx0 : nullptr;
         a.count_in = ph ? counts + ph - 1 : nullptr;
-        a.idx_out = (ph & 1) ? idx1 : idx0;
-        a.count_out = counts + ph;
+        if (ph) {  // the boundary: phase ph-1's per-panel lists -> idx0 (LPT-ordered for the finisher)
+            e = launch_phase_compact(a.seg_cnt, a.seg_idx, ph >= 2 ? counts + ph - 2 : nullptr, a.batch, fin_prev,
+                                     idx0, counts + ph - 1, (a.pred && tn.lpt) ? a.pred : nullptr, a.fin_thresh, s);
+            if (e != hipSuccess) return e;
+        }
+        fin_prev = a.fin_thresh;
         if (ph && a.fin_thresh) {  // few survivors left: the duo finisher takes them, runs to N --
             // two instances per CU in ping-pong, fed from the survivor list
             a.qctr = qctrs + ph;
-            if (a.pred && tn.lpt)  // longest predicted solves first
-                hipLaunchKernelGGL(survivor_sort_kernel, dim3(1), dim3(1024), 0, s, const_cast<int*>(a.idx_in),
-                                   a.count_in, a.pred, a.fin_thresh);
             int g = a.fin_thresh < a.num_cus ? a.fin_thresh : a.num_cus;
             if (tn.duo_max_grid > 0 && tn.duo_max_grid < g) g = tn.duo_max_grid;  // more claims
             if ((e = launch_duo(a, g, s)) != hipSuccess) return e;
@@ -1566,6 +1636,11 @@ hipError_t read_stamps(unsigned long long* out, size_t bytes) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), bytes, 0, hipMemcpyDeviceToHost);
 }
 #endif
+
+bool panel_folds_gmax(int n, int m) {
+    const int T = panel_tiles_for(n, m);
+    return T > 8 && T <= kPanelMaxTiles;
+}
 
 hipError_t launch_panel(const SolveArgs<float>& a, hipStream_t s, bool* supported) {
     const int T = panel_tiles_for(a.n, a.m);

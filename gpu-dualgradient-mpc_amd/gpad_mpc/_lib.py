@@ -37,7 +37,7 @@ EXPORTS = [
     "gpad_accumulate_iterations", "gpad_set_option",
     "gpad_group_create", "gpad_group_destroy", "gpad_group_transport", "gpad_group_setup", "gpad_group_run",
     "gpad_solve_sharded", "gpad_device_count", "gpad_group_set_stream",
-    "gpad_setup_hessian", "gpad_release_cached",
+    "gpad_setup_hessian", "gpad_release_cached", "gpad_phase_counts",
 ]
 GROUP_RCCL, GROUP_PEER = 1, 2
 
@@ -172,6 +172,8 @@ def load(path: str | None = None) -> C.CDLL:
                  "gpad_set_option", "gpad_group_create", "gpad_group_destroy", "gpad_group_transport",
                  "gpad_group_set_stream", "gpad_group_setup", "gpad_group_run", "gpad_solve_sharded"]:
         getattr(L, name).restype = i
+    L.gpad_phase_counts.argtypes = [vp, ip, i]
+    L.gpad_phase_counts.restype = i
     if hasattr(L, "gpad_release_cached"):
         L.gpad_release_cached.argtypes = []
         L.gpad_release_cached.restype = None

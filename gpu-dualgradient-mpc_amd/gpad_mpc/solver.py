@@ -178,6 +178,18 @@ class GpadSolver:
         check(min(n, 0), "gpad_phase_plan")
         return dict(ends=list(ends[:n]), fins=list(fins[:n]), cost_us=cost.value)
 
+    def phase_counts(self) -> list:
+        """Survivors after each phase of the last phased panel solve (gpad_phase_counts); trailing
+        zeros trimmed."""
+        cap = 64
+        buf = (C.c_int * cap)()
+        n = self.lib.gpad_phase_counts(self.h, buf, cap)
+        check(min(n, 0), "gpad_phase_counts")
+        out = list(buf[:n])
+        while out and out[-1] == 0:
+            out.pop()
+        return out
+
     @staticmethod
     def plan_phases(iters, n: int, m: int, N: int, check_every: int = 10, num_cus: int = 256) -> dict:
         """gpad_plan_phases: the phase plan the panel solver would make from these per-instance

@@ -273,6 +273,11 @@ int gpad_accumulate_iterations(gpad_handle_t h, long long* acc);
  * thresholds, and the modelled solve time in us; returns the number of phases (0: no plan,
  * the default schedule applies). */
 int gpad_phase_plan(gpad_handle_t h, int* ends, int* fins, int cap, double* cost_us);
+/* Diagnostics: the survivors each boundary of the last phased panel solve listed -- counts[ph] =
+ * instances still running after phase ph (the next phase's input) -- for up to cap phases
+ * (synchronises the handle's stream).  Returns the number written, 0 when the last run was not a
+ * phased panel solve. */
+int gpad_phase_counts(gpad_handle_t h, int* counts, int cap);
 /* The planner itself on given iteration counts (host only, no device work; for tests/tools). */
 int gpad_plan_phases(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus,
                      int* ends, int* fins, int cap, double* cost_us);

@@ -46,8 +46,11 @@ def run(args):
         y.zero_()
         Mv, gv = fresh[r] if fresh else (dM, dg)
         prev[:] = it
+        plan = s.phase_plan()
         s.run(z, y, Mv, gv, 5000, 1e-4, stats=False)
         st = s.last_stats(iters=it)
+        print(f"rep {r}: plan ends {plan['ends']} fins {plan['fins']} -> survivors after each phase "
+              f"{s.phase_counts()}; past 260: {int((it > 260).sum())}")
     torch.cuda.synchronize()
     np.save(args.out, it)
     np.save(args.out.replace(".npy", "_prev.npy"), prev)
