@@ -32,13 +32,10 @@ namespace gpad {
 struct DuoSlot {  // one instance slot; bookkeeping is uniform, the floats are this lane's rows
     int pos, vs, nextp;  // list position (>= count: empty), iterations done, pre-claimed next
     bool need8d;         // 8b done, 8d pending
-    float th, bn;        // theta_vs, beta_{vs+1}
-    float thn, bnn;      // ... and the next iteration's, loaded one iteration ahead (a slot running
-                         // alone reaches its next epilogue one chain after its last: too soon
-                         // for an L2 round trip)
-    float x0, x1, x2;    // -ML lanes: z, zhat, -;  G/L lanes: y, w, u = G_L z
-    float x3;            // -ML lanes: g_P;  G/L lanes: p_D (registers: an LDS read after the chain
-                         // would sit on the step's critical path)
+    float th, bn;        // theta_vs, beta_{vs+1}: loaded one step before their use (a deeper
+                         // prefetch, or g_P / p_D in registers instead of LDS, spills: the rows
+                         // take 200 of the 256 VGPRs -- profiles/r03_duo_solo.txt)
+    float x0, x1, x2;    // -ML lanes: z, zhat, -;  G/L lanes: y, w, u = G_L z (g_P, p_D in LDS)
 };
 struct DuoCtx {
     int tid, count, G, v0, n, m, N, Kc, nA, nwaves, row, claim_base;
@@ -46,30 +43,30 @@ struct DuoCtx {
 };
 
 // slot s takes list position p (empty if p >= count); uniform, contains barriers
+// gp_l / pd_l: this slot's per-row constants (g_P of the -ML rows, p_D of the G/L rows)
 template <int KB, int K>
 __device__ __forceinline__ void duo_refill(const SolveArgs<float>& a, const DuoCtx& c, DuoSlot& s, int p,
-                                           float* w_l, float* z_l, const float (&r)[K]) {
+                                           float* w_l, float* gp_l, float* pd_l, float* z_l,
+                                           const float (&r)[K]) {
     s.pos = p;
     s.vs = c.v0;
     s.need8d = false;
     s.th = a.theta[c.v0];
     s.bn = a.beta[c.v0 + 1];
-    s.thn = a.theta[c.v0 + 1];  // (tables hold N + 2 entries; v0 < N)
-    s.bnn = a.beta[c.v0 + 2 <= c.N + 1 ? c.v0 + 2 : c.N + 1];
-    s.x0 = s.x1 = s.x2 = s.x3 = 0.0f;
+    s.x0 = s.x1 = s.x2 = 0.0f;
     const bool has = p < c.count;
     if (has) {
         const size_t b = (size_t)(a.idx_in ? a.idx_in[p] : p);
         if (c.isA) {
             if (c.live) {
                 s.x0 = a.z[b * c.n + c.row];
-                s.x3 = a.gP[b * a.ld_gP + c.row];
+                gp_l[c.row] = a.gP[b * a.ld_gP + c.row];
                 if (c.fresh && c.use_tol) z_l[c.row] = s.x0;
             }
         } else if (c.live) {
             const float yv = a.y[b * c.m + c.row];
             s.x0 = yv;
-            s.x3 = (float)(a.gscale * (double)a.g[b * a.ld_g + c.row]);
+            pd_l[c.row] = (float)(a.gscale * (double)a.g[b * a.ld_g + c.row]);
             s.x1 = c.fresh ? __builtin_fmaf(a.beta[0], yv - yv, yv) : a.wc[b * c.m + c.row];
             if (c.use_tol && !c.fresh) s.x2 = a.uc[b * c.m + c.row];
             w_l[c.row] = s.x1;
@@ -88,18 +85,19 @@ __device__ __forceinline__ void duo_refill(const SolveArgs<float>& a, const DuoC
 // consume the pre-claimed position of slot s, claim its next one (claim_l: this slot's cell)
 template <int KB, int K>
 __device__ __forceinline__ void duo_claim(const SolveArgs<float>& a, const DuoCtx& c, DuoSlot& s, int* claim_l,
-                                          float* w_l, float* z_l, const float (&r)[K]) {
+                                          float* w_l, float* gp_l, float* pd_l, float* z_l,
+                                          const float (&r)[K]) {
     const int p = s.nextp;
     if (c.tid == 0 && p < c.count) *claim_l = c.claim_base + atomicAdd(a.qctr, 1);
-    duo_refill<KB, K>(a, c, s, p, w_l, z_l, r);  // (its barrier publishes *claim_l)
+    duo_refill<KB, K>(a, c, s, p, w_l, gp_l, pd_l, z_l, r);  // (its barrier publishes *claim_l)
     s.nextp = p < c.count ? *claim_l : c.count;
 }
 
 // one step: -ML waves run 8b+8c of slot sa, G/L waves 8d+8a (+ test) of slot sb
 template <int KA, int KB, int K>
 __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx& c, DuoSlot& sa, DuoSlot& sb,
-                                         float* wa_l, float* zha_l, float* wb_l, const float* zhb_l,
-                                         CheckSlot* slots_b,
+                                         float* wa_l, float* zha_l, const float* gpa_l, float* wb_l,
+                                         const float* zhb_l, float* gpb_l, float* pdb_l, CheckSlot* slots_b,
                                          CheckSlot* vslots, int* claim_b, float* z_l, const float (&r)[K]) {
     const bool runA = sa.pos < c.count && !sa.need8d;
     const bool runB = sb.need8d;
@@ -109,7 +107,7 @@ __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx
             const float th = sa.th;
             const float acc = chain_regs<KA, K>(r, wa_l);
             if (c.live) {
-                const float zhv = acc - sa.x3;
+                const float zhv = acc - gpa_l[c.row];
                 sa.x0 = __builtin_fmaf(1.0f - th, sa.x0, th * zhv);
                 zha_l[c.row] = zhv;
                 sa.x1 = zhv;
@@ -122,7 +120,7 @@ __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx
             const float th = sb.th, bn = sb.bn;
             const float cv = chain_regs<KB, K>(r, zhb_l);
             if (c.live) {
-                const float pdi = sb.x3, wi = sb.x1;
+                const float pdi = pdb_l[c.row], wi = sb.x1;
                 const float sv = (wi + pdi) + cv;                     // seq_functions.cpp:84
                 const float yp = (__builtin_fabsf(sv) + sv) * 0.5f;   // seq_functions.cpp:85
                 if (c.use_tol) sb.x2 = __builtin_fmaf(1.0f - th, sb.x2, th * cv);
@@ -146,12 +144,8 @@ __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx
     if (runB) {
         sb.need8d = false;
         const int v = ++sb.vs;
-        sb.th = sb.thn;  // next iteration's schedule, prefetched; the one after it now
-        sb.bn = sb.bnn;
-        if (v < c.N) {  // (tables hold N + 2 entries)
-            sb.thn = a.theta[v + 1];
-            sb.bnn = a.beta[v + 2];
-        }
+        sb.th = a.theta[v];  // next iteration's schedule (tables hold N + 2 entries)
+        sb.bn = a.beta[v + 1];
         int done = 0;
         if (chk) {
             const int st1 = check_stage1<float>(slots_b + c.nA, c.nwaves - c.nA, a.L, a.tol, a.tol_gap);
@@ -164,8 +158,8 @@ __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx
                     const float cz = chain_regs<KB, K>(r, z_l);
                     if (c.live) {
                         sb.x2 = cz;
-                        vc = cz + sb.x3;
-                        mc = __builtin_fabsf(cz) + __builtin_fabsf(sb.x3);
+                        vc = cz + pdb_l[c.row];
+                        mc = __builtin_fabsf(cz) + __builtin_fabsf(pdb_l[c.row]);
                     }
                     check_publish<float>(vslots, vc, vc, vc, 0.0, mc);
                 }
@@ -184,7 +178,7 @@ __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx
                 a.iters[b] = v;
                 a.conv[b] = done;
             }
-            duo_claim<KB, K>(a, c, sb, claim_b, wb_l, z_l, r);
+            duo_claim<KB, K>(a, c, sb, claim_b, wb_l, gpb_l, pdb_l, z_l, r);
         }
     }
 }
@@ -196,6 +190,8 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs
     __shared__ __attribute__((aligned(16))) float w_l[2][PA];   // w per slot (broadcast to -ML rows)
     __shared__ __attribute__((aligned(16))) float zh_l[2][PB];  // zhat per slot (to G/L rows)
     __shared__ __attribute__((aligned(16))) float z_l[PB];      // z_{-1} of a fresh instance (u seed)
+    __shared__ float gp_l[2][PB];                               // per slot: g_P of the -ML rows
+    __shared__ float pd_l[2][PA];                               //           p_D of the G/L rows
     __shared__ CheckSlot slots[2][kResidentMaxThreads / 64];
     __shared__ CheckSlot vslots[kResidentMaxThreads / 64];  // verification of a nominated test (A)
     __shared__ int claim_l[2];
@@ -241,11 +237,13 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs
     DuoSlot s0, s1;
     s0.nextp = claim_l[0];
     s1.nextp = claim_l[1];
-    duo_refill<KB, K>(a, c, s0, blockIdx.x, w_l[0], z_l, r);
-    duo_refill<KB, K>(a, c, s1, blockIdx.x + c.G, w_l[1], z_l, r);
+    duo_refill<KB, K>(a, c, s0, blockIdx.x, w_l[0], gp_l[0], pd_l[0], z_l, r);
+    duo_refill<KB, K>(a, c, s1, blockIdx.x + c.G, w_l[1], gp_l[1], pd_l[1], z_l, r);
     while (s0.pos < c.count || s1.pos < c.count) {
-        duo_step<KA, KB, K>(a, c, s0, s1, w_l[0], zh_l[0], w_l[1], zh_l[1], slots[1], vslots, &claim_l[1], z_l, r);
-        duo_step<KA, KB, K>(a, c, s1, s0, w_l[1], zh_l[1], w_l[0], zh_l[0], slots[0], vslots, &claim_l[0], z_l, r);
+        duo_step<KA, KB, K>(a, c, s0, s1, w_l[0], zh_l[0], gp_l[0], w_l[1], zh_l[1], gp_l[1], pd_l[1], slots[1],
+                            vslots, &claim_l[1], z_l, r);
+        duo_step<KA, KB, K>(a, c, s1, s0, w_l[1], zh_l[1], gp_l[1], w_l[0], zh_l[0], gp_l[0], pd_l[0], slots[0],
+                            vslots, &claim_l[0], z_l, r);
     }
 }
 
