@@ -93,6 +93,27 @@ __device__ __forceinline__ void duo_claim(const SolveArgs<float>& a, const DuoCt
     s.nextp = p < c.count ? *claim_l : c.count;
 }
 
+// Step anatomy stamps (diagnostic builds only, -DGPAD_STAMP): shader clock of workgroup 0, every
+// wave, for the steps whose live slot is at iterations [100, 104): kind 0 = an 8b step (runA),
+// 1 = an 8d step; points: step start, chain done, before the barrier, after it, step end
+// (gpad_debug_duo_stamps, tools/duo_solo.py --stamps; meant for one live slot).
+#ifdef GPAD_STAMP
+__device__ unsigned long long g_duo_stamps[8][4][2][5];
+#define GPAD_DSTAMP(P)                                                                          \
+    do {                                                                                        \
+        if (blockIdx.x == 0 && (runA || runB) && dsv >= 100 && dsv < 104 && (c.tid & 63) == 0)  \
+            g_duo_stamps[c.tid >> 6][dsv - 100][runA ? 0 : 1][P] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+hipError_t read_duo_stamps(unsigned long long* out, size_t bytes) {
+    if (bytes > sizeof(g_duo_stamps)) bytes = sizeof(g_duo_stamps);
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_duo_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+#else
+#define GPAD_DSTAMP(P) \
+    do {               \
+    } while (0)
+#endif
+
 // one step: -ML waves run 8b+8c of slot sa, G/L waves 8d+8a (+ test) of slot sb
 template <int KA, int KB, int K>
 __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx& c, DuoSlot& sa, DuoSlot& sb,
@@ -102,10 +123,13 @@ __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx
     const bool runA = sa.pos < c.count && !sa.need8d;
     const bool runB = sb.need8d;
     const bool chk = runB && c.use_tol && ((sb.vs + 1) % c.Kc) == 0;
+    [[maybe_unused]] const int dsv = runA ? sa.vs : sb.vs;  // (stamp index)
+    GPAD_DSTAMP(0);
     if (c.isA) {
         if (runA) {
             const float th = sa.th;
             const float acc = chain_regs<KA, K>(r, wa_l);
+            GPAD_DSTAMP(1);
             if (c.live) {
                 const float zhv = acc - gpa_l[c.row];
                 sa.x0 = __builtin_fmaf(1.0f - th, sa.x0, th * zhv);
@@ -119,6 +143,7 @@ __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx
         if (runB) {
             const float th = sb.th, bn = sb.bn;
             const float cv = chain_regs<KB, K>(r, zhb_l);
+            GPAD_DSTAMP(1);
             if (c.live) {
                 const float pdi = pdb_l[c.row], wi = sb.x1;
                 const float sv = (wi + pdi) + cv;                     // seq_functions.cpp:84
@@ -139,7 +164,9 @@ __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx
         }
         if (chk) check_publish<float>(slots_b, violz, violh, wmin, gap, magh);
     }
+    GPAD_DSTAMP(2);
     __syncthreads();
+    GPAD_DSTAMP(3);
     if (runA) sa.need8d = true;
     if (runB) {
         sb.need8d = false;
@@ -181,6 +208,7 @@ __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx
             duo_claim<KB, K>(a, c, sb, claim_b, wb_l, gpb_l, pdb_l, z_l, r);
         }
     }
+    GPAD_DSTAMP(4);
 }
 
 template <int KA, int KB>

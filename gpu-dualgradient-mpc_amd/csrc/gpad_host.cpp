@@ -692,10 +692,15 @@ int gpad_phase_counts(gpad_handle_t h, int* counts, int cap) {
 namespace gpad {
 hipError_t read_stamps(unsigned long long* out, size_t bytes);      // gpad_panel.hip (diagnostic builds)
 hipError_t read_res_stamps(unsigned long long* out, size_t bytes);  // gpad_kernels.hip
+hipError_t read_duo_stamps(unsigned long long* out, size_t bytes);  // gpad_duo.hip
 }
 extern "C" {
 int gpad_debug_res_stamps(unsigned long long* out, size_t bytes) {
     HIP_TRY(gpad::read_res_stamps(out, bytes));
+    return GPAD_OK;
+}
+int gpad_debug_duo_stamps(unsigned long long* out, size_t bytes) {
+    HIP_TRY(gpad::read_duo_stamps(out, bytes));
     return GPAD_OK;
 }
 // diagnostic builds only (not declared in gpad.h): the phase-anatomy stamps of the last panel-pair run
