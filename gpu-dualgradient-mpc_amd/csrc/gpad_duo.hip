@@ -48,7 +48,7 @@ template <int KB, int K>
 __device__ __forceinline__ void duo_refill(const SolveArgs<float>& a, const DuoCtx& c, DuoSlot& s, int p,
                                            float* w_l, float* gp_l, float* pd_l, float* z_l,
                                            const float (&r)[K]) {
-    s.pos = p;
+    s.pos = __builtin_amdgcn_readfirstlane(p);  // (uniform: scalar bookkeeping, see duo_step)
     s.vs = c.v0;
     s.need8d = false;
     s.th = a.theta[c.v0];
@@ -90,7 +90,7 @@ __device__ __forceinline__ void duo_claim(const SolveArgs<float>& a, const DuoCt
     const int p = s.nextp;
     if (c.tid == 0 && p < c.count) *claim_l = c.claim_base + atomicAdd(a.qctr, 1);
     duo_refill<KB, K>(a, c, s, p, w_l, gp_l, pd_l, z_l, r);  // (its barrier publishes *claim_l)
-    s.nextp = p < c.count ? *claim_l : c.count;
+    s.nextp = p < c.count ? __builtin_amdgcn_readfirstlane(*claim_l) : c.count;
 }
 
 // Step anatomy stamps (diagnostic builds only, -DGPAD_STAMP): shader clock of workgroup 0, every
@@ -120,18 +120,21 @@ __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx
                                          float* wa_l, float* zha_l, const float* gpa_l, float* wb_l,
                                          const float* zhb_l, float* gpb_l, float* pdb_l, CheckSlot* slots_b,
                                          CheckSlot* vslots, int* claim_b, float* z_l, const float (&r)[K]) {
+    // the slot bookkeeping is uniform and kept scalar (list positions via readfirstlane): the test
+    // period in vector registers cost an integer division per step (profiles/r03_duo_solo.txt)
     const bool runA = sa.pos < c.count && !sa.need8d;
     const bool runB = sb.need8d;
-    const bool chk = runB && c.use_tol && ((sb.vs + 1) % c.Kc) == 0;
+    const bool chk = runB && c.use_tol && ((__builtin_amdgcn_readfirstlane(sb.vs) + 1) % c.Kc) == 0;
     [[maybe_unused]] const int dsv = runA ? sa.vs : sb.vs;  // (stamp index)
     GPAD_DSTAMP(0);
     if (c.isA) {
         if (runA) {
             const float th = sa.th;
+            const float gpv = gpa_l[c.row];  // read before the chain: its LDS latency hides there
             const float acc = chain_regs<KA, K>(r, wa_l);
             GPAD_DSTAMP(1);
             if (c.live) {
-                const float zhv = acc - gpa_l[c.row];
+                const float zhv = acc - gpv;
                 sa.x0 = __builtin_fmaf(1.0f - th, sa.x0, th * zhv);
                 zha_l[c.row] = zhv;
                 sa.x1 = zhv;
@@ -142,10 +145,11 @@ __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx
         double gap = 0.0;
         if (runB) {
             const float th = sb.th, bn = sb.bn;
+            const float pdv = pdb_l[c.row];  // (before the chain, as gpv)
             const float cv = chain_regs<KB, K>(r, zhb_l);
             GPAD_DSTAMP(1);
             if (c.live) {
-                const float pdi = pdb_l[c.row], wi = sb.x1;
+                const float pdi = pdv, wi = sb.x1;
                 const float sv = (wi + pdi) + cv;                     // seq_functions.cpp:84
                 const float yp = (__builtin_fabsf(sv) + sv) * 0.5f;   // seq_functions.cpp:85
                 if (c.use_tol) sb.x2 = __builtin_fmaf(1.0f - th, sb.x2, th * cv);
@@ -263,8 +267,8 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs
     }
     __syncthreads();
     DuoSlot s0, s1;
-    s0.nextp = claim_l[0];
-    s1.nextp = claim_l[1];
+    s0.nextp = __builtin_amdgcn_readfirstlane(claim_l[0]);
+    s1.nextp = __builtin_amdgcn_readfirstlane(claim_l[1]);
     duo_refill<KB, K>(a, c, s0, blockIdx.x, w_l[0], gp_l[0], pd_l[0], z_l, r);
     duo_refill<KB, K>(a, c, s1, blockIdx.x + c.G, w_l[1], gp_l[1], pd_l[1], z_l, r);
     while (s0.pos < c.count || s1.pos < c.count) {
