@@ -1170,11 +1170,17 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
     static_assert(T > 8 && T <= 16, "panel pairs need 8 < T <= 16");
     constexpr int D = 2 * T - 16;  // double waves
     __shared__ Panel2Lds<T> L;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int count = a.count_in ? __builtin_amdgcn_readfirstlane(*a.count_in) : a.batch;
     if (a.count_in && count <= a.fin_thresh) return;  // the finisher has them
     const int panels = (count + 15) / 16;
     const bool pair = panels > (int)gridDim.x;
+    // Role index.  The SIMD issues MFMAs oldest wave first, so in the one-panel layout the roles
+    // are dealt from the last wave down: the relay pieces of tile T-1 (roles T, T+1) and its
+    // receiver run on the oldest waves of their SIMDs and the sequential relay is not starved --
+    // 5.92 -> 5.71 us per iteration at one panel per CU, 6.93 -> 6.75 at 4096 (r03_wave_order_ab.txt).
+    // In the pair layout the order measured neutral (the doubles' two chains keep their SIMD busy).
+    const int w0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int w = pair ? w0 : 15 - w0;
     const int items = pair ? (panels + 1) / 2 : panels;
     // hand-off (Handoff): both GEMMs run full-length chains on tiles T-2 and T-1
     const bool ho = Handoff<T>::on && (KQ > 0 || (16 * (T - 1) < a.n && 16 * (T - 1) < a.m &&

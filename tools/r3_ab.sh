@@ -1,9 +1,16 @@
-# round-3 call: finisher parity tests on the tree, duo anatomy and A/Bs
+# round-3 call: pair-layout wave order (role index reversed so the double waves are the youngest)
+# o1 = reversed in pair mode, o2 = reversed in pair and one-panel mode; parity on o1/o2, anatomy, A/Bs
 set -e
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_configs.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r3x_tests.log 2>&1 || { tail -30 gpurun_out/r3x_tests.log; exit 1; }
-tail -1 gpurun_out/r3x_tests.log
-for v in cur6 duo4 duo5; do GPAD_LIB=$PWD/tools/abl/$v.so timeout -k 10 120 python3 tools/duo_solo.py 2>/dev/null | sed "s/^/$v /"; done
-bash tools/ab.sh 3 "cur6|tools/abl/cur6.so|" "duo4|tools/abl/duo4.so|" "duo5|tools/abl/duo5.so|" > gpurun_out/r3x_ab.txt 2>&1
-cat gpurun_out/r3x_ab.txt
+for v in o1 o2; do
+  GPAD_LIB=$PWD/tools/abl/$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_configs.py tests/test_errors.py -x -q -k "panel or pair or c4 or c3 or handoff" --timeout 200 --timeout-method thread > gpurun_out/r3o_tests_$v.log 2>&1 || { tail -30 gpurun_out/r3o_tests_$v.log; exit 1; }
+  echo "$v: $(tail -1 gpurun_out/r3o_tests_$v.log)"
+done
+for v in stamp stamp_o1; do
+  GPAD_LIB=$PWD/tools/abl/$v.so timeout -k 10 120 python3 tools/stamp_panel.py --batch 8192 > gpurun_out/r3o_$v.txt 2>&1
+  cat gpurun_out/r3o_$v.txt
+done
+bash tools/ab.sh -t micro 3 "base|tools/abl/base.so|" "o1|tools/abl/o1.so|" "o2|tools/abl/o2.so|" > gpurun_out/r3o_ab.txt 2>&1
+bash tools/ab.sh 3 "base|tools/abl/base.so|" "o1|tools/abl/o1.so|" "o2|tools/abl/o2.so|" >> gpurun_out/r3o_ab.txt 2>&1
+cat gpurun_out/r3o_ab.txt
