@@ -38,11 +38,13 @@ def test_c5_batch1024_distinct_800x800_bitexact(gpu, oracle):
         np.testing.assert_array_equal(Y[b], yo, err_msg=f"y[{b}]")
 
 
-def test_c4_shard_certified_on_the_constraint(gpu, oracle):
+@pytest.mark.parametrize("quad", [0, 1])
+def test_c4_shard_certified_on_the_constraint(gpu, oracle, quad):
     """C4 shard (bench.py's workload: 8192 instances sharing ML/G, eps = 1e-4, phased panel
-    solve + finisher): every instance reported converged satisfies max(G z* - g) <= 1e-4
-    evaluated exactly (fp64) on the returned z* and the caller's f32 G, g; iteration counts
-    of a spread sample equal the oracle's."""
+    solve + finisher, duo or quad): every instance reported converged satisfies max(G z* - g) <=
+    1e-4 evaluated exactly (fp64) on the returned z* and the caller's f32 G, g; iteration counts
+    of a spread sample and of the longest solves (the finisher's) equal the oracle's.  The second
+    solve of the handle runs the phase plan made from the first one's counts."""
     import os
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -61,12 +63,16 @@ def test_c4_shard_certified_on_the_constraint(gpu, oracle):
     it = np.zeros(B, np.int32)
     with gpad_mpc.GpadSolver(0) as s:
         s.setup(t(ML32), t(G32), float(L32), n=n, m=m, batch=B, check_every=10)
-        st = s.run(z, y, t(M32), t(g32), N, tol, iters=it)
+        s.set_options(quad_finisher=quad)
+        for _ in range(2):  # the second solve is planned from the first one's counts
+            z.zero_()
+            y.zero_()
+            st = s.run(z, y, t(M32), t(g32), N, tol, iters=it)
     assert st["kernel"] == "panel" and st["converged"] == B
     Z = z.cpu().numpy().astype(np.float64)
     viol = (Z @ G32.astype(np.float64).T - g32.astype(np.float64)).max(axis=1)
     assert viol.max() <= tol, (viol.max(), int(viol.argmax()))
-    for b in range(0, B, 257):
+    for b in list(range(0, B, 257)) + [int(i) for i in np.argsort(-it, kind="stable")[:12]]:
         zo, yo, ito, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), ML32, M32[b], G32, g32[b], N, L32, tol)
         assert it[b] == ito, b
         np.testing.assert_array_equal(Z[b].astype(np.float32), zo)
