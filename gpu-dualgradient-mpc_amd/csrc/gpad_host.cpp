@@ -310,7 +310,6 @@ int gpad_set_option(gpad_handle_t h, int option, int value) {
         case GPAD_OPT_FLAT_A_LDS: return set(t.flat_a_lds, 0, 1, def.flat_a_lds);
         case GPAD_OPT_CONDENSED_PANEL: return set(t.cpanel, 0, 1, def.cpanel);
         case GPAD_OPT_DEBUG_DROP_HANDOFF: return set(t.debug_drop_handoff, 0, 1, def.debug_drop_handoff);
-        case GPAD_OPT_QUAD_FINISHER: h->plan.nph = 0; h->plan_key = 0; return set(t.quad, 0, 1, def.quad);
         default: return fail(GPAD_ERR_INVALID, "gpad_set_option: unknown option");
     }
 }

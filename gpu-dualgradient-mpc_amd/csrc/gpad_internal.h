@@ -29,7 +29,6 @@ struct Tuning {
     int flat_a_lds = 1;       // GPAD_OPT_FLAT_A_LDS: flat fragment image in LDS when it fits
     int cpanel = 1;           // GPAD_OPT_CONDENSED_PANEL: condensed batches on the MFMA panels
     int debug_drop_handoff = 0;  // GPAD_OPT_DEBUG_DROP_HANDOFF: test-only fault injection
-    int quad = 0;             // GPAD_OPT_QUAD_FINISHER: the four-column finisher (gpad_quad.hip)
 };
 
 // Device error word of a run (SolveArgs::err): kernels OR these bits in with a vector atomic;
@@ -118,8 +117,6 @@ hipError_t launch_resident(const SolveArgs<float>& a, hipStream_t s, bool* suppo
 // list is idx_in/count_in (a no-op unless *count_in <= a.fin_thresh) or 0..batch-1; needs a
 // zeroed a.qctr.  Persistent grid of `grid` workgroups (one per CU).
 hipError_t launch_duo(const SolveArgs<float>& a, int grid, hipStream_t s);
-// the same contract with four instances per slot on the matrix core (gpad_quad.hip)
-hipError_t launch_quad(const SolveArgs<float>& a, int grid, hipStream_t s);
 bool resident_supported(int n, int m);
 // GPAD_KERNEL_CONDENSED (gpad_condensed.hip): H = G_L (-ML) images for nmats matrix pairs, then
 // the one-chain-per-iteration latency kernel (m <= 208, n <= 256)

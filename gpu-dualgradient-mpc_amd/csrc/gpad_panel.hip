@@ -1244,8 +1244,7 @@ int panel_fin_thresh(int n, int m, int num_cus, const Tuning* t) {
     // the tail of a phased solve (survivors <= 2 per CU) goes to the latency kernel: one
     // instance per workgroup at ~1/6 of a panel's iteration time (when n, m fit it); measured
     // on C4: 2/CU 5.42e8 it/s, 4/CU 5.35e8, 8/CU 5.35e8, no finisher 5.04e8
-    // (the quad finisher holds 8 per CU: two slots of four columns)
-    int f = resident_supported(n, m) ? (t && t->quad ? 8 : 2) * num_cus : 0;
+    int f = resident_supported(n, m) ? 2 * num_cus : 0;
     if (t && t->finish_thresh >= 0 && f) f = t->finish_thresh;
     return f;
 }
@@ -1280,7 +1279,6 @@ struct PlanModel {
     int T, n, m, num_cus, grid;
     bool handoff;  // gpad_panel2_kernel's hand-off shapes (Handoff)
     bool relay;    // ... and its one-panel relay (T = 9, 13)
-    bool quad;     // the finisher is gpad_quad_kernel (Tuning::quad)
     double t_chain, t_res, t_launch = 5.0;
     double iter_time(long long panels) const {
         if (panels <= 0) return 0.0;
@@ -1311,10 +1309,8 @@ struct PlanModel {
         return 2 * t_launch + (v1 - v0 + 1) * it + (double)s0 * 16.0 * (n + m) / 5e6;
     }
     double finisher(int longest, long long work) const {
-        // quad: two slots of four columns per CU at ~3.5 us per slot-iteration while the queue
-        // lasts (4x4x1 MFMA chains, tools/lat/quad_bcast.hip), a slot's last column on the DPP chain
-        const double lat = longest * (quad ? 2.3 : 1.4) * t_res;
-        const double thr = (double)work * (quad ? 0.36 : 1.1) * t_res / num_cus;
+        const double lat = longest * 1.4 * t_res;
+        const double thr = (double)work * 1.1 * t_res / num_cus;
         return 2 * t_launch + (lat > thr ? lat : thr);
     }
 };
@@ -1360,7 +1356,6 @@ int panel_plan(const int* iters, int batch, int n, int m, int N, int check_every
     md.handoff = (T == 9 || T == 11 || T == 13) && n > 16 * (T - 1) && m > 16 * (T - 1) &&
                  (n + 15) / 16 == T && (m + 15) / 16 == T;
     md.relay = md.handoff && (T == 9 || T == 13);
-    md.quad = t && t->quad;
     md.t_chain = 0.055 * ((m + 15) / 16 + (n + 15) / 16) + 0.2;
     md.t_res = 0.0021 * (n + m) + 0.38;
     const bool fin_ok = resident_supported(n, m);
@@ -1632,7 +1627,7 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
             a.qctr = qctrs + ph;
             int g = a.fin_thresh < a.num_cus ? a.fin_thresh : a.num_cus;
             if (tn.duo_max_grid > 0 && tn.duo_max_grid < g) g = tn.duo_max_grid;  // more claims
-            if ((e = (tn.quad ? launch_quad : launch_duo)(a, g, s)) != hipSuccess) return e;
+            if ((e = launch_duo(a, g, s)) != hipSuccess) return e;
         }
         launch_panel_kernel<T>(a, grid, s);
         if ((e = hipGetLastError()) != hipSuccess) return e;

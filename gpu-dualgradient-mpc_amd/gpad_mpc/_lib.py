@@ -48,7 +48,6 @@ OPT_PANEL_MAX_GRID, OPT_DUO_MAX_GRID, OPT_FLAT_PANEL_MIN, OPT_FLAT_PANELS = 7, 8
 OPT_FLAT_WAVES, OPT_FLAT_A_LDS = 11, 12
 OPT_CONDENSED_PANEL = 14
 OPT_DEBUG_DROP_HANDOFF = 16  # test-only fault injection
-OPT_QUAD_FINISHER = 17
 OPT_RETIRED = (5, 13, 15)  # finisher kind, solo finisher workgroups, plan finisher cost (0.3)
 OPTIONS = {"phase_len": OPT_PHASE_LEN, "finish_thresh": OPT_FINISH_THRESH, "plan": OPT_PLAN,
            "phased": OPT_PHASED, "lpt": OPT_LPT,
@@ -56,7 +55,7 @@ OPTIONS = {"phase_len": OPT_PHASE_LEN, "finish_thresh": OPT_FINISH_THRESH, "plan
            "flat_panel_min": OPT_FLAT_PANEL_MIN, "flat_panels": OPT_FLAT_PANELS,
            "flat_waves": OPT_FLAT_WAVES, "flat_a_lds": OPT_FLAT_A_LDS,
            "condensed_panel": OPT_CONDENSED_PANEL,
-           "debug_drop_handoff": OPT_DEBUG_DROP_HANDOFF, "quad_finisher": OPT_QUAD_FINISHER}
+           "debug_drop_handoff": OPT_DEBUG_DROP_HANDOFF}
 
 FILE_ROWMAJOR, FILE_FLIPPED, FILE_FLAT = 0, 1, 2
 

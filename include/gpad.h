@@ -384,9 +384,6 @@ int gpad_schedule(int N, int kind, double* theta, double* beta);
                                     * GPAD_ERR_DEVICE; 0 (default) = off.  Honoured by the
                                     * 193..208-row shapes (the C3/C4 tiling, T = 13), which run
                                     * a separate test-only kernel instantiation while it is set */
-#define GPAD_OPT_QUAD_FINISHER 17 /* finisher of phased panel solves: 0 = duo (two instances per CU
-                                    * on DPP chains, default), 1 = quad (two slots of four instances
-                                    * per CU on 4x4x1 MFMA chains, DPP for a slot's last instance)  */
 int gpad_set_option(gpad_handle_t h, int option, int value);
 
 /* Synchronise the handle's stream (for callers using device memory + async runs). */

@@ -229,18 +229,16 @@ def test_bigpanel_bitexact(gpu, oracle, tol, N, nm, B, grid, phase):
         assert_bitexact(y[b], yo, f"instance {b} y")
 
 
-@pytest.mark.parametrize("quad", [0, 1])
 @pytest.mark.parametrize("grid", [1, 3, 5, 0])
 @pytest.mark.parametrize("nm,B,z0s", [((200, 200), 120, 0.0), ((40, 180), 200, 0.1), ((131, 64), 97, 0.1)])
-def test_finisher_queue_bitexact(gpu, oracle, grid, nm, B, z0s, quad):
+def test_finisher_queue_bitexact(gpu, oracle, grid, nm, B, z0s):
     """The tail of a phased panel solve on the duo finisher (two instances per workgroup in
     ping-pong, slots refilled from the survivor list through a device counter; grid capped to 1, 3
-    or 5 workgroups to force many claims) or the quad finisher (two slots of four columns on 4x4x1
-    MFMA chains, a slot's last live column on the DPP chain, columns refilled one by one).  The
-    finisher takes over after the first 10-iteration phase, so nearly the whole solve runs there;
-    every instance must match its own oracle solve, iteration count included."""
+    or 5 workgroups to force many claims).  The finisher takes over after the first 10-iteration
+    phase, so nearly the whole solve runs there; every instance must match its own oracle solve,
+    iteration count included."""
     from gpad_mpc import problems
-    opts = dict(phase_len=10, finish_thresh=100000, duo_max_grid=grid, quad_finisher=quad)
+    opts = dict(phase_len=10, finish_thresh=100000, duo_max_grid=grid)
     n, m = nm
     qp = problems.synthetic_qp(n, m, batch=B, seed=12)
     ML, G = qp.ML.astype(np.float32), qp.G.astype(np.float32)
