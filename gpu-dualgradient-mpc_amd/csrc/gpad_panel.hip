@@ -680,6 +680,7 @@ struct Panel2Lds {
     int hflag[3];          // hand-off generation per slot
     int herr;              // a wait expired (handoff_wait): reported to the run's error word at exit
     int hdrop;             // fault injection (kDebugDropHandoff) for this workgroup
+    int znz[16];           // per wave: a non-zero z_{-1} among its rows (fresh seed GEMM needed)
     float gred[16];        // per wave: max |g| over the rows it loaded (SolveArgs::gmax_part)
 };
 
@@ -844,16 +845,31 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             L.Wl[pq][slot] = make_float4(wv[0], wv[1], wv[2], wv[3]);
             if (fresh && use_tol) L.Zh[pq][slot] = make_float4(z[q][0], z[q][1], z[q][2], z[q][3]);
         }
-        if (fresh && use_tol) {  // u = G_L z_{-1}
-            __syncthreads();
+        if (fresh && use_tol) {  // u = G_L z_{-1} -- zero, and no GEMM, when every z_{-1} is zero
+            // (a cold start: every chain step fma(G_L, 0, +0) gives +0, so u = +0 exactly)
+            bool nz = false;
             if constexpr (NU > 0) {
-                f32x4 c0, c1;
-                panel_gemm2<T, NU == 2>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, c0, c1);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) u[0][r] = c0[r];
-                if constexpr (NU == 2) {
+                for (int q = 0; q < Q; ++q)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) u[Q - 1][r] = c1[r];
+                    for (int r = 0; r < 4; ++r) nz = nz || z[q][r] != 0.0f;
+            }
+            const bool wnz = __ballot(nz) != 0ull;
+            if (lane == 0) L.znz[threadIdx.x >> 6] = wnz ? 1 : 0;
+            __syncthreads();
+            int anynz = 0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) anynz |= L.znz[i];
+            if constexpr (NU > 0) {
+                if (anynz) {
+                    f32x4 c0, c1;
+                    panel_gemm2<T, NU == 2>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, c0, c1);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) u[0][r] = c0[r];
+                    if constexpr (NU == 2) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) u[Q - 1][r] = c1[r];
+                    }
                 }
             }
         }
