@@ -1467,6 +1467,7 @@ __device__ __forceinline__ int block_scan_1024(int* part, int tid, int v) {  // 
 }
 
 constexpr int kCompactMaxPanels = 8192;  // per-panel bases in LDS up to here (131072 instances)
+constexpr int kCompactU = 8;             // entries per thread and round: loads issued together
 __global__ __launch_bounds__(1024) void phase_compact_kernel(const int* __restrict__ seg_cnt,
                                                              const int* __restrict__ seg_idx, const int* count_prev,
                                                              int batch, int fin_prev, int* idx, int* count_out,
@@ -1475,6 +1476,7 @@ __global__ __launch_bounds__(1024) void phase_compact_kernel(const int* __restri
     __shared__ int ids[kSortMax];
     __shared__ int part[1024];
     __shared__ int pbase[kCompactMaxPanels];
+    __shared__ int pcnt[kCompactMaxPanels];
     __shared__ int total_l;
     const int tid = threadIdx.x;
     const int prev = count_prev ? *count_prev : batch;
@@ -1485,14 +1487,18 @@ __global__ __launch_bounds__(1024) void phase_compact_kernel(const int* __restri
     const int panels = (prev + 15) / 16;
     const int per = (panels + 1023) / 1024;
     const int p0 = tid * per < panels ? tid * per : panels, p1 = p0 + per < panels ? p0 + per : panels;
+    const bool lds_bases = panels <= kCompactMaxPanels;
     int sum = 0;
-    for (int p = p0; p < p1; ++p) sum += seg_cnt[p];
+    for (int p = p0; p < p1; ++p) {
+        const int c = seg_cnt[p];
+        if (lds_bases) pcnt[p] = c;
+        sum += c;
+    }
     int base = block_scan_1024(part, tid, sum);
     if (tid == 1023) total_l = base + sum;
-    const bool lds_bases = panels <= kCompactMaxPanels;
     if (lds_bases) {
         for (int p = p0; p < p1; ++p) {
-            const int c = seg_cnt[p];
+            const int c = pcnt[p];
             pbase[p] = c ? base : -1;
             base += c;
         }
@@ -1501,10 +1507,26 @@ __global__ __launch_bounds__(1024) void phase_compact_kernel(const int* __restri
     const int count = total_l;
     const bool sort = pred && count > 1 && count <= fin_cur && count <= kSortMax;
     int* dst = sort ? ids : idx;
-    if (lds_bases) {  // entry r of panel p by thread (16 p + r) mod 1024: coalesced, independent loads
-        for (int i = tid; i < 16 * panels; i += 1024) {
-            const int p = i >> 4, r = i & 15, b = pbase[p];
-            if (b >= 0 && r < seg_cnt[p]) dst[b + r] = seg_idx[i];
+    if (lds_bases) {  // entry r of panel p by thread (16 p + r) mod 1024: coalesced loads, kCompactU of
+        // them in flight per thread before any store (one L2 round trip per round, not per entry)
+        for (int i0 = tid; i0 < 16 * panels; i0 += 1024 * kCompactU) {
+            int v[kCompactU], at[kCompactU];
+#pragma unroll
+            for (int u = 0; u < kCompactU; ++u) {
+                const int i = i0 + 1024 * u;
+                at[u] = -1;
+                v[u] = 0;
+                if (i < 16 * panels) {
+                    const int p = i >> 4, r = i & 15, b = pbase[p];
+                    if (b >= 0 && r < pcnt[p]) {
+                        at[u] = b + r;
+                        v[u] = seg_idx[i];
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kCompactU; ++u)
+                if (at[u] >= 0) dst[at[u]] = v[u];
         }
     } else {
         for (int p = p0; p < p1; ++p) {
@@ -1515,14 +1537,25 @@ __global__ __launch_bounds__(1024) void phase_compact_kernel(const int* __restri
     }
     if (tid == 0) *count_out = count;
     if (!sort) return;
-    auto bin = [&](int id) {  // descending count -> ascending bin
-        const int q = pred[id];
-        const int k = q < 0 ? 0 : (q >= kSortBins ? kSortBins - 1 : q);
-        return kSortBins - 1 - k;
-    };
+    __syncthreads();  // ids complete
+    // the bins of this thread's entries (count <= kSortMax = 8 x 1024: one predicted count per entry,
+    // loaded once, used by the histogram and the scatter)
+    int bn[kSortMax / 1024];
+#pragma unroll
+    for (int u = 0; u < kSortMax / 1024; ++u) {
+        const int i = tid + 1024 * u;
+        bn[u] = 0;
+        if (i < count) {
+            const int q = pred[ids[i]];  // descending count -> ascending bin
+            const int k = q < 0 ? 0 : (q >= kSortBins ? kSortBins - 1 : q);
+            bn[u] = kSortBins - 1 - k;
+        }
+    }
     for (int i = tid; i < kSortBins; i += 1024) hist[i] = 0;
     __syncthreads();
-    for (int i = tid; i < count; i += 1024) atomicAdd(&hist[bin(ids[i])], 1);  // (LDS atomics)
+#pragma unroll
+    for (int u = 0; u < kSortMax / 1024; ++u)
+        if (tid + 1024 * u < count) atomicAdd(&hist[bn[u]], 1);  // (LDS atomics)
     __syncthreads();
     int local[4], hs = 0;  // thread tid owns bins 4 tid .. 4 tid + 3
 #pragma unroll
@@ -1534,9 +1567,10 @@ __global__ __launch_bounds__(1024) void phase_compact_kernel(const int* __restri
 #pragma unroll
     for (int q = 0; q < 4; ++q) hist[4 * tid + q] = hb + local[q];
     __syncthreads();
-    for (int i = tid; i < count; i += 1024) {
-        const int id = ids[i];
-        idx[atomicAdd(&hist[bin(id)], 1)] = id;
+#pragma unroll
+    for (int u = 0; u < kSortMax / 1024; ++u) {
+        const int i = tid + 1024 * u;
+        if (i < count) idx[atomicAdd(&hist[bn[u]], 1)] = ids[i];
     }
 }
 
