@@ -1190,13 +1190,17 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
     if (a.count_in && count <= a.fin_thresh) return;  // the finisher has them
     const int panels = (count + 15) / 16;
     const bool pair = panels > (int)gridDim.x;
-    // Role index.  The SIMD issues MFMAs oldest wave first, so in the one-panel layout the roles
-    // are dealt from the last wave down: the relay pieces of tile T-1 (roles T, T+1) and its
-    // receiver run on the oldest waves of their SIMDs and the sequential relay is not starved --
-    // 5.92 -> 5.71 us per iteration at one panel per CU, 6.93 -> 6.75 at 4096 (r03_wave_order_ab.txt).
-    // In the pair layout the order measured neutral (the doubles' two chains keep their SIMD busy).
+    // Role index.  The SIMD issues MFMAs oldest wave first, so a role's wave index sets its share
+    // of the SIMD while the SIMD is contended.  One-panel layout: the roles are dealt from the
+    // last wave down, so the relay pieces of tile T-1 (roles T, T+1) and its receiver run on the
+    // oldest waves of their SIMDs and the sequential relay is not starved -- 5.92 -> 5.71 us per
+    // iteration at one panel per CU, 6.93 -> 6.75 at 4096 (r03_wave_order_ab.txt).  Pairs: the
+    // two hand-off receivers (roles 12, 13, SIMDs 0, 1) swap waves with the doubles of roles 8, 9,
+    // so a receiver's chain -- which starts only when its piece arrives -- is not the youngest on
+    // its SIMD: -1 to -3 % per pair iteration, C4 -0.2 to -1.0 % (r03_pair_perm_ab.txt; helpers
+    // older than the singles, receivers oldest, or both, measured no better).
     const int w0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int w = pair ? w0 : 15 - w0;
+    const int w = pair ? ((w0 >> 1) == 4 ? w0 + 4 : ((w0 >> 1) == 6 ? w0 - 4 : w0)) : 15 - w0;
     const int items = pair ? (panels + 1) / 2 : panels;
     // hand-off (Handoff): both GEMMs run full-length chains on tiles T-2 and T-1
     const bool ho = Handoff<T>::on && (KQ > 0 || (16 * (T - 1) < a.n && 16 * (T - 1) < a.m &&
