@@ -38,7 +38,7 @@ struct DuoSlot {  // one instance slot; bookkeeping is uniform, the floats are t
     float x0, x1, x2;    // -ML lanes: z, zhat, -;  G/L lanes: y, w, u = G_L z (g_P, p_D in LDS)
 };
 struct DuoCtx {
-    int tid, count, G, v0, n, m, N, Kc, nA, nwaves, row, claim_base;
+    int tid, count, G, v0, n, m, N, Kc, nA, nwaves, row, claim_base, b0;  // b0: first G/L wave
     bool fresh, use_tol, isA, live;
 };
 
@@ -179,7 +179,7 @@ __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx
         sb.bn = a.beta[v + 1];
         int done = 0;
         if (chk) {
-            const int st1 = check_stage1<float>(slots_b + c.nA, c.nwaves - c.nA, a.L, a.tol, a.tol_gap);
+            const int st1 = check_stage1<float>(slots_b + c.b0, c.nwaves - c.nA, a.L, a.tol, a.tol_gap);
             bool verified = false;
             if (st1 & 1) {  // (A) nominated: decide on the direct chain G_L z, reset u to it
                 if (c.isA && c.live) z_l[c.row] = sb.x0;
@@ -195,7 +195,7 @@ __device__ __forceinline__ void duo_step(const SolveArgs<float>& a, const DuoCtx
                     check_publish<float>(vslots, vc, vc, vc, 0.0, mc);
                 }
                 __syncthreads();
-                verified = check_verify<float>(vslots + c.nA, c.nwaves - c.nA, a.L, a.tol);
+                verified = check_verify<float>(vslots + c.b0, c.nwaves - c.nA, a.L, a.tol);
             }
             done = check_code(st1, verified);
         }
@@ -243,8 +243,16 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs
     c.Kc = a.check_every;
     c.nA = (c.n + 63) >> 6;
     c.nwaves = blockDim.x >> 6;
-    c.isA = (c.tid >> 6) < c.nA;
-    c.row = c.isA ? c.tid : c.tid - 64 * c.nA;
+    {   // The G/L waves come first, i.e. are the older wave of each SIMD: the SIMD issues oldest
+        // first, so their 8d chain finishes first and its longer epilogue (8d, 8a, test partials)
+        // overlaps the tail of the -ML chain, whose short 8b/8c epilogue is what is left exposed
+        // before the barrier -- two slots 2.46 -> 2.31 us per slot-iteration, C4 -0.7 %
+        // (profiles/r03_duo_order_ab.txt).
+        const int nB = c.nwaves - c.nA;
+        c.isA = (c.tid >> 6) >= nB;
+        c.row = c.isA ? c.tid - 64 * nB : c.tid;
+        c.b0 = 0;
+    }
     c.live = c.isA ? c.row < c.n : c.row < c.m;
 
     float r[K];
