@@ -333,41 +333,59 @@ def c3_leg(dev, n=200, m=200, batch=4096, reps=3, max_iters=5000, tol=1e-4, ref=
     return out
 
 
-def condensed_leg(dev, n=200, m=200, batch=8192, reps=6, max_iters=5000, tol=1e-4, cpanel=1):
-    """The headline C4 shard on the opt-in condensed operator (GPAD_KERNEL_CONDENSED: one H GEMM
-    per iteration on the MFMA panels, gpad_cpanel.hip; NOT the reference's arithmetic) beside the
-    bit-exact panels on the same inputs: rate, the norm-wise distance of z* from the bit-exact z*,
-    and the fp64 constraint violation of the returned z* (Algorithm 1 decides on direct G_L z)."""
+def c4_global_leg(dev, n=200, m=200, batch=65536, steps=6, warmup=2, max_iters=5000, tol=1e-4, ref=None):
+    """BASELINE config C4 at its global size on ONE GPU: all 65536 instances (the batch the 8-GPU
+    run shards 8 x 8192) as one gpad_run per step, FRESH q/b every step as in the headline, steps
+    enqueued back to back (no host sync, work summed on the device), HIP events around them.  The
+    strong-scaling anchor for the driver's 1/2/4/8-GPU curve of the sharded batch (the headline
+    itself is weak scaling: 8192 per GPU).  tests/test_configs.py::test_c4_global_65536 checks the
+    same batch through gpad_solve_sharded over 8 shards against one handle and the oracle."""
     import torch
 
     import gpad_mpc
-    from gpad_mpc import _lib
-    ML, G, L, M, g = make_shard(n, m, batch, 0)
+    ML, G, L, _, _ = make_shard(n, m, 1, 0)
     f32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)  # noqa: E731
-    dML, dG, dM, dg = f32(ML), f32(G), f32(M), f32(g)
-    out = {"config": f"C4 shard: {batch} instances sharing ML/G, n={n}, m={m}, eps={tol}"}
-    zs = {}
-    for name, kern in (("condensed", _lib.KERNEL_CONDENSED), ("bit_exact", _lib.KERNEL_AUTO)):
-        z = torch.zeros(batch, n, device=dev)
-        y = torch.zeros(batch, m, device=dev)
-        with gpad_mpc.GpadSolver(dev.index or 0, stream=torch.cuda.current_stream(dev).cuda_stream) as s:
-            s.setup(dML, dG, float(np.float32(L)), n=n, m=m, batch=batch, shared=True, check_every=10, kernel=kern)
-            if kern == _lib.KERNEL_CONDENSED:
-                s.set_option("condensed_panel", cpanel)
-            best, st = 1e30, None
-            for _ in range(reps + 2):
-                r = s.run(z.zero_(), y.zero_(), dM, dg, max_iters, tol)
-                if r["kernel_ms"] < best:
-                    best, st = r["kernel_ms"], r
-        zs[name] = z.double()
-        out[name] = {"kernel": st["kernel"], "iters_per_s": st["total_iterations"] / (best / 1e3),
-                     "qp_solves_per_s": batch / (best / 1e3), "mean_iters_to_eps": st["total_iterations"] / batch,
-                     "solve_ms": best, "converged": st["converged"]}
-    zc, zb = zs["condensed"], zs["bit_exact"]
-    out["condensed"]["rel_dev_z_vs_bit_exact"] = float((zc - zb).norm() / zb.norm())
-    Gd, gd = dG.double(), dg.double()
-    out["condensed"]["max_constraint_violation"] = float((zc @ Gd.T - gd).max())
-    out["speedup"] = out["condensed"]["iters_per_s"] / out["bit_exact"]["iters_per_s"]
+    draws = make_stream(n, m, batch, warmup + steps, 99)
+    fresh = [(f32(a), f32(b)) for a, b in draws]
+    dML, dG = f32(ML), f32(G)
+    z = torch.zeros(batch, n, device=dev)
+    y = torch.zeros(batch, m, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    with gpad_mpc.GpadSolver(dev.index or 0, stream=stream.cuda_stream) as s:
+        s.setup(dML, dG, float(np.float32(L)), n=n, m=m, batch=batch, shared=True, check_every=10)
+        for k in range(warmup):
+            s.run(z.zero_(), y.zero_(), *fresh[k], max_iters, tol, stats=False)
+        torch.cuda.synchronize(dev)
+        acc = torch.zeros(1, dtype=torch.int64, device=dev)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for k in range(steps):
+            s.run(z.zero_(), y.zero_(), *fresh[warmup + k], max_iters, tol, stats=False)
+            s.accumulate_iterations(acc)
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        dev_ms = ev0.elapsed_time(ev1) / steps
+        st = s.last_stats()
+        total = int(acc.item())
+    out = {"config": f"C4 global batch on one GPU: {batch} instances sharing ML/G, n={n}, m={m}, eps={tol}, "
+                     f"fresh q/b every step ({steps} timed after {warmup})",
+           "kernel": st["kernel"], "converged_last": st["converged"],
+           "iters_per_s": total / dt, "qp_solves_per_s": batch * steps / dt, "ms_per_solve": dt / steps * 1e3,
+           "device_ms_per_solve": dev_ms, "mean_iters_to_eps": total / (batch * steps),
+           "achieved_tflops": total / steps * flops_per_iter(n, m) / (dev_ms / 1e3) / 1e12}
+    if ref is not None:
+        N = max(1, int(round(out["mean_iters_to_eps"])))
+        O = ref.O
+        L32 = np.float32(L)
+        k = min(batch, 64 * ref.info["threads"])
+        Mv, gv = (a[:k].astype(np.float32) for a in draws[-1])
+        MGneg, GL, _ = O.scale(ML.astype(np.float32), G.astype(np.float32), gv[0], L32)
+        c = ref.rate(MGneg, Mv, GL, O.scale_vec(gv, L32), N, shared=True,
+                     what=f"C4 instances (pool of {k}, shared ML/G), N = mean GPU iterations to eps")
+        c["qp_solves_per_s"] = c["value"] / N
+        out["cpu_baseline"] = c
     return out
 
 
@@ -573,8 +591,6 @@ def main():
     ap.add_argument("--kernel", default="auto", choices=["auto", "stream", "resident", "panel"])
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C2/C5 side legs")
-    ap.add_argument("--condensed", action="store_true",
-                    help="also time the frozen, not parity-compliant condensed operator (off by default)")
     ap.add_argument("--repeat-inputs", action="store_true",
                     help="headline on the SAME inputs every step (the planner then sees its own future); "
                          "default: fresh inputs per step, the repeated-input rate reported beside it")
@@ -773,31 +789,19 @@ def main():
                 "c1": (*[f32(a) for a in c1[:2]], f32(c1[2]).reshape(1, -1), f32(c1[3]).reshape(1, -1),
                        float(np.float32(qp1.L)), 1000)}.items():
             nn, mm = mML.shape
-            res = {}
-            for kk in ((_lib.KERNEL_AUTO, _lib.KERNEL_CONDENSED) if args.condensed else (_lib.KERNEL_AUTO,)):
-                with gpad_mpc.GpadSolver(dev.index, stream=stream.cuda_stream) as s1:
-                    s1.setup(mML, mG, mL, n=nn, m=mm, batch=1, kernel=kk)
-                    z1 = torch.zeros(1, nn, device=dev)
-                    y1 = torch.zeros(1, mm, device=dev)
-                    s1.run(z1, y1, mM, mg_, iters, 0.0)
-                    t = []
-                    for _ in range(5):
-                        st1 = s1.run(z1.zero_(), y1.zero_(), mM, mg_, iters, 0.0)
-                        t.append(st1["kernel_ms"])
-                res[kk] = (st1["kernel"], iters / (min(t) / 1e3), z1.double().cpu(), y1.double().cpu())
-            kb = res[_lib.KERNEL_AUTO]
-            rel = lambda a, b: float((a - b).norm() / b.norm())  # noqa: E731
+            with gpad_mpc.GpadSolver(dev.index, stream=stream.cuda_stream) as s1:
+                s1.setup(mML, mG, mL, n=nn, m=mm, batch=1)
+                z1 = torch.zeros(1, nn, device=dev)
+                y1 = torch.zeros(1, mm, device=dev)
+                s1.run(z1, y1, mM, mg_, iters, 0.0)
+                t = []
+                for _ in range(5):
+                    st1 = s1.run(z1.zero_(), y1.zero_(), mM, mg_, iters, 0.0)
+                    t.append(st1["kernel_ms"])
+            kb = (st1["kernel"], iters / (min(t) / 1e3))
             singles[name] = {"config": ("C2 single instance n=200 m=200" if name == "c2" else
                                         f"C1 single instance: battery n_u=4, N=10 (n={nn}, m={mm})"),
                              "kernel": kb[0], "iters_per_s": kb[1]}
-            if args.condensed:
-                kc = res[_lib.KERNEL_CONDENSED]
-                singles[name]["condensed"] = {
-                    "kernel": kc[0], "iters_per_s": kc[1],
-                    "rel_dev_z": rel(kc[2], kb[2]), "rel_dev_y": rel(kc[3], kb[3]),
-                    "note": "opt-in GPAD_KERNEL_CONDENSED (one m-long chain per iteration, not bit-exact, "
-                            "frozen); rel_dev_* = norm-wise distance from the bit-exact kernel's z/y after "
-                            "the same iterations"}
             if ref is not None:  # the reference's CPU steps on the same instance, one thread
                 O = ref.O
                 hm = [a.cpu().numpy() for a in (mML, mG, mM, mg_)]
@@ -814,8 +818,7 @@ def main():
             extra["hbm_bound_c5"] = hbm_leg(dev, ref=ref)
             extra["distinct_c2_batch"] = distinct_leg(dev, n, m, ref=ref)
             extra["c3_batch4096"] = c3_leg(dev, n, m, ref=ref)
-            if args.condensed:
-                extra["c4_condensed"] = condensed_leg(dev, n, m, batch=B)
+            extra["c4_global_1gpu"] = c4_global_leg(dev, n, m, ref=ref)
             extra["closed_loop_battery"] = closed_loop_leg(dev, cpu=not args.no_cpu)
             extra["closed_loop_battery_flat"] = closed_loop_leg(dev, cpu=False, flat=True)
             extra["flat_battery_c1"] = flat_leg(dev, ref=ref)

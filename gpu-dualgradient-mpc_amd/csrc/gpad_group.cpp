@@ -422,11 +422,11 @@ int gpad_group_run(gpad_group_t g, void* z0, void* y0, const void* M, const void
         if (g->count[d] > 0 && (rc = gpad_sync(g->h[d]))) return rc;
     if (st) {  // per-shard counters (host copies), aggregated; st->iters [batch] in global order
         gpad_stats_t tot{};
-        tot.iters = nullptr;
         for (int d = 0; d < nd; ++d) {
             if (g->count[d] == 0) continue;
             gpad_stats_t sd{};
             sd.iters = st->iters ? st->iters + g->start[d] : nullptr;
+            sd.codes = st->codes ? st->codes + g->start[d] : nullptr;
             if ((rc = gpad_last_stats(g->h[d], &sd))) return rc;
             tot.iterations = std::max(tot.iterations, sd.iterations);
             tot.converged += sd.converged;
@@ -437,8 +437,10 @@ int gpad_group_run(gpad_group_t g, void* z0, void* y0, const void* M, const void
             tot.flags |= sd.flags;
         }
         int* keep = st->iters;
+        int* keep_codes = st->codes;
         *st = tot;
         st->iters = keep;
+        st->codes = keep_codes;
     }
     return GPAD_OK;
 }

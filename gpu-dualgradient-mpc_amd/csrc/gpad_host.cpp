@@ -28,12 +28,18 @@ int fail(int code, const std::string& msg) {
     return code;
 }
 
+// "<what>: hipErrorName (code N): description" -- the name and number of the HIP status, so a
+// failure report says which runtime error it was (include/gpad.h gpad_last_error)
+std::string hip_detail(const std::string& what, hipError_t e) {
+    return what + ": " + hipGetErrorName(e) + " (code " + std::to_string((int)e) + "): " + hipGetErrorString(e);
+}
+
 #define HIP_TRY(expr)                                                                        \
     do {                                                                                     \
         hipError_t _e = (expr);                                                              \
         if (_e != hipSuccess) {                                                              \
             return fail(_e == hipErrorOutOfMemory ? GPAD_ERR_NOMEM : GPAD_ERR_HIP,           \
-                        std::string(#expr) + ": " + hipGetErrorString(_e));                   \
+                        hip_detail(#expr, _e));                                              \
         }                                                                                    \
     } while (0)
 
@@ -53,7 +59,7 @@ struct DevBuf {
         if (e != hipSuccess) {
             p = nullptr;
             return fail(e == hipErrorOutOfMemory ? GPAD_ERR_NOMEM : GPAD_ERR_HIP,
-                        std::string("hipMalloc: ") + hipGetErrorString(e));
+                        hip_detail("hipMalloc(" + std::to_string(want) + " bytes)", e));
         }
         bytes = want;
         return GPAD_OK;
@@ -86,8 +92,11 @@ void host_schedule(int N, int kind, double* theta, double* beta) {
 
 int gpad::set_last_error(int code, const std::string& msg) { return fail(code, msg); }
 
-// Run status block (gpad_handle_s::status), zeroed before a run's first launch: the device error
-// word, then the per-workgroup maxima of |g| (launch_absmax) from which the host takes gmax.
+// Run status block (gpad_handle_s::status): the device error word, then the per-workgroup maxima
+// of |g| (launch_absmax) from which the host takes gmax.  The maxima are zeroed before each run's
+// first launch; the error word is sticky -- zeroed only when the block is created and right after
+// gpad_sync / the stats collection copied it out -- so a fault of an asynchronous run still
+// reaches the next sync when further runs were queued behind it.
 struct RunStatus {
     int err;
     int pad;
@@ -105,10 +114,6 @@ struct gpad_handle_s {
     bool scaled = false;
     int ldn = 0, ldm = 0;
     DevBuf MGt, GLt, frag, stage;
-    DevBuf Hc;                 // GPAD_KERNEL_CONDENSED: H = G_L (-ML) images (gpad_condensed.hip)
-    bool Hc_ok = false;
-    DevBuf Hfrag;              // ... H in the panel fragment layout (gpad_cpanel.hip), shared f32
-    bool Hfrag_ok = false;
     bool frag_ok = false;      // frag holds the fragment image of the bound matrices
     bool keep_stage = false;   // gpad_solve's cached handle keeps its staging buffer
     // gpad_solve: host copy of the last bound (ML, G, L, dims) so a repeated one-shot call on
@@ -140,7 +145,6 @@ struct gpad_handle_s {
     gpad::PanelPlan plan;
     unsigned long long plan_key = 0;    // fingerprint of the counts the plan was built from
     int flat_vpred = 0;                 // flat panels: last iteration of the previous phased solve
-    int cond_vtake = 0;                 // condensed batches: finisher takeover iteration (0: none)
     // asynchronous runs (no stats): the counts of each phased solve are copied to pinned host
     // memory behind it; the next run re-plans from them once that copy has landed, so a pipeline
     // of back-to-back solves plans from its most recent completed solve without a host sync
@@ -163,27 +167,35 @@ struct gpad_handle_s {
 
 
 static int reset_status(gpad_handle_t h, double tol, double floor_scale) {
+    const bool fresh = h->status.p == nullptr;
     int rc = h->status.ensure(sizeof(RunStatus));
     if (rc) return rc;
-    HIP_TRY(hipMemsetAsync(h->status.p, 0, sizeof(RunStatus), h->stream));
+    if (fresh) HIP_TRY(hipMemsetAsync(h->status.p, 0, sizeof(RunStatus), h->stream));
+    else HIP_TRY(hipMemsetAsync((char*)h->status.p + offsetof(RunStatus, part), 0,
+                                sizeof(RunStatus) - offsetof(RunStatus, part), h->stream));
     h->last_tol = tol;
     h->last_floor_scale = floor_scale;
     return GPAD_OK;
 }
 
 // Enqueue the copy of the status block to *rs (the caller synchronises the stream): the error word,
-// and with `maxima` the per-workgroup |g| maxima of the run (RunStatus::part).
+// and with `maxima` the per-workgroup |g| maxima of the run (RunStatus::part).  The error word is
+// cleared behind the copy: every error bit is reported exactly once.
 static int fetch_status(gpad_handle_t h, RunStatus* rs, bool maxima = false) {
     rs->err = 0;
     if (!h->status.p) return GPAD_OK;
     const size_t bytes = maxima ? sizeof(RunStatus) : offsetof(RunStatus, part);
     HIP_TRY(hipMemcpyAsync(rs, h->status.p, bytes, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemsetAsync(h->status.p, 0, sizeof(int), h->stream));
     return GPAD_OK;
 }
 
 static double status_gmax(gpad_handle_t h, const RunStatus& rs) {
     double g = 0.0;
-    for (int b = 0; b < gpad::kAbsmaxMaxBlocks; ++b) g = std::max(g, rs.part[b]);
+    for (int b = 0; b < gpad::kAbsmaxMaxBlocks; ++b) {
+        if (std::isnan(rs.part[b])) return rs.part[b];  // a NaN in g (absmax_nan keeps it)
+        g = std::max(g, rs.part[b]);
+    }
     return g;
 }
 
@@ -197,11 +209,12 @@ static int status_error(const RunStatus& rs) {
 
 extern "C" {
 
-const char* gpad_version(void) { return "gpad-mi355x 0.3 (gfx950)"; }
+const char* gpad_version(void) { return "gpad-mi355x 0.4 (gfx950)"; }
 
 int gpad_device_count(void) {
     int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess) return fail(GPAD_ERR_NO_DEVICE, "gpad_device_count: no HIP runtime");
+    const hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess) return fail(GPAD_ERR_NO_DEVICE, hip_detail("gpad_device_count: hipGetDeviceCount", e));
     return count;
 }
 
@@ -225,9 +238,12 @@ int gpad_create(gpad_handle_t* out, int device, void* stream) {
     if (!out) return fail(GPAD_ERR_INVALID, "gpad_create: null handle pointer");
     *out = nullptr;
     int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
-        return fail(GPAD_ERR_NO_DEVICE, "gpad_create: no HIP device visible");
-    if (device < 0 || device >= count) return fail(GPAD_ERR_INVALID, "gpad_create: bad device index");
+    const hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess) return fail(GPAD_ERR_NO_DEVICE, hip_detail("gpad_create: hipGetDeviceCount", e));
+    if (count <= 0) return fail(GPAD_ERR_NO_DEVICE, "gpad_create: hipGetDeviceCount reported 0 devices");
+    if (device < 0 || device >= count)
+        return fail(GPAD_ERR_INVALID, "gpad_create: bad device index " + std::to_string(device) + " (" +
+                                          std::to_string(count) + " visible)");
     HIP_TRY(hipSetDevice(device));
     auto h = std::make_unique<gpad_handle_s>();
     h->device = device;
@@ -249,8 +265,6 @@ int gpad_destroy(gpad_handle_t h) {
     (void)hipStreamSynchronize(h->stream);
     h->MGt.release();
     h->GLt.release();
-    h->Hc.release();
-    h->Hfrag.release();
     h->GLx.release();
     h->Hq.release();
     h->frag.release();
@@ -308,7 +322,6 @@ int gpad_set_option(gpad_handle_t h, int option, int value) {
                 return fail(GPAD_ERR_INVALID, "gpad_set_option: flat waves must be 0, 8 or 16");
             return set(t.flat_waves, 0, 16, def.flat_waves);
         case GPAD_OPT_FLAT_A_LDS: return set(t.flat_a_lds, 0, 1, def.flat_a_lds);
-        case GPAD_OPT_CONDENSED_PANEL: return set(t.cpanel, 0, 1, def.cpanel);
         case GPAD_OPT_DEBUG_DROP_HANDOFF: return set(t.debug_drop_handoff, 0, 1, def.debug_drop_handoff);
         default: return fail(GPAD_ERR_INVALID, "gpad_set_option: unknown option");
     }
@@ -340,10 +353,8 @@ static int validate_dims(const gpad_dims_t* d) {
         return fail(GPAD_ERR_INVALID, "dims: bad memory kind");
     if (d->schedule != GPAD_SCHEDULE_MATLAB && d->schedule != GPAD_SCHEDULE_PAPER)
         return fail(GPAD_ERR_INVALID, "dims: bad schedule");
-    if ((d->kernel < GPAD_KERNEL_AUTO || d->kernel > GPAD_KERNEL_PANEL) && d->kernel != GPAD_KERNEL_CONDENSED)
+    if (d->kernel < GPAD_KERNEL_AUTO || d->kernel > GPAD_KERNEL_PANEL)
         return fail(GPAD_ERR_INVALID, "dims: bad kernel");
-    if (d->kernel == GPAD_KERNEL_CONDENSED && (d->dtype != GPAD_DTYPE_F32 || !gpad::condensed_supported(d->n, d->m)))
-        return fail(GPAD_ERR_UNSUPPORTED, "dims: the condensed kernel needs f32, m <= 208, n <= 256");
     if (!std::isfinite(d->tol_gap)) return fail(GPAD_ERR_INVALID, "dims: tol_gap must be finite");
     if (d->reserved != 0) return fail(GPAD_ERR_INVALID, "dims: reserved must be 0");
     return GPAD_OK;
@@ -363,7 +374,6 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
     h->hess_ok = false;
     h->plan.nph = 0;
     h->flat_vpred = 0;
-    h->cond_vtake = 0;
     h->plan_pending = false;
     h->last_phased = false;
     h->dims = *d;
@@ -403,16 +413,6 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
         HIP_TRY(gpad::launch_pack_kmajor<double>((const double*)dB, (double*)h->GLt.p, m, n, h->ldm, sb,
                                                  nmats, in_stride, (long long)b_elems, h->stream));
     }
-    // condensed operator H = G_L (-ML) (GPAD_KERNEL_CONDENSED only)
-    h->Hc_ok = false;
-    if (d->kernel == GPAD_KERNEL_CONDENSED) {
-        if ((rc = h->Hc.ensure(sizeof(float) * (size_t)m * h->ldm * nmats))) return rc;
-        HIP_TRY(gpad::launch_condense((const float*)h->GLt.p, (const float*)h->MGt.p, n, m, h->ldn, h->ldm, nmats,
-                                      d->shared ? 0 : (long long)a_elems, d->shared ? 0 : (long long)b_elems,
-                                      (float*)h->Hc.p, h->stream));
-        h->Hc_ok = true;
-    }
-    h->Hfrag_ok = false;
     // fragment image for the MFMA panel kernel (shared f32 matrices only); the buffer is kept
     // across setups and only grows
     h->frag_ok = false;
@@ -425,11 +425,6 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
                                             (float)sa, sb, h->frag.p, h->stream));
             h->frag_tiles = gpad::panel_tiles(n, m, d->batch);
             h->frag_ok = true;
-        }
-        if (h->Hc_ok && h->frag_ok && gpad::cpanel_supported(n, m)) {  // condensed batches on the MFMA pipe
-            if ((rc = h->Hfrag.ensure(gpad::cpanel_frag_bytes(n, m)))) return rc;
-            HIP_TRY(gpad::launch_pack_cpanel((const float*)h->Hc.p, n, m, h->ldm, h->Hfrag.p, h->stream));
-            h->Hfrag_ok = true;
         }
     }
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -487,8 +482,6 @@ int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* d, int n_u, const float*
     if (!(L > 0.0) || !std::isfinite(L)) return fail(GPAD_ERR_INVALID, "gpad_setup_flat: L must be > 0");
     if (d->dtype != GPAD_DTYPE_F32 || !d->shared)
         return fail(GPAD_ERR_UNSUPPORTED, "gpad_setup_flat: f32 and shared matrices only");
-    if (d->kernel == GPAD_KERNEL_CONDENSED)
-        return fail(GPAD_ERR_UNSUPPORTED, "gpad_setup_flat: no condensed kernel on the flat path");
     if (n_u <= 0 || d->n % n_u != 0 || d->m < 4 * d->n)
         return fail(GPAD_ERR_INVALID, "gpad_setup_flat: need n = n_u*N and m >= 4 n_u N");
     HIP_TRY(hipSetDevice(h->device));
@@ -498,7 +491,6 @@ int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* d, int n_u, const float*
     h->hess_ok = false;
     h->plan.nph = 0;
     h->flat_vpred = 0;
-    h->cond_vtake = 0;
     h->plan_pending = false;
     h->last_phased = false;
     h->dims = *d;
@@ -589,11 +581,6 @@ static int ensure_schedule(gpad_handle_t h, int N, const void* theta_in, const v
 // The phase plan is a pure function of the per-instance counts (and the shape): rebuild it only
 // when they changed (repeated solves of one batch skip the DP).
 static void update_plan(gpad_handle_t h, const int* counts, int batch, int N) {
-    if (h->dims.kernel == GPAD_KERNEL_CONDENSED) {
-        h->cond_vtake = gpad::cpanel_takeover(counts, batch, h->dims.n, h->dims.m, N, h->dims.check_every,
-                                              h->num_cus);
-        return;
-    }
     if (h->flat) {  // the flat panels' phases run to the previous solve's last iteration
         int mx = 0;
         for (int b = 0; b < batch; ++b) mx = std::max(mx, counts[b]);
@@ -644,6 +631,8 @@ static int collect_stats(gpad_handle_t h, gpad_stats_t* st) {
     if (h->timed && hipEventElapsedTime(&ms, h->ev0, h->ev1) == hipSuccess) st->kernel_ms = ms;
     st->tol_floor = h->last_tol > 0.0 ? h->last_floor_scale * status_gmax(h, rs) : 0.0;
     st->flags = (h->last_tol > 0.0 && h->last_tol < st->tol_floor) ? GPAD_FLAG_TOL_FLOOR : 0;
+    if (h->last_tol > 0.0 && !std::isfinite(st->tol_floor))  // NaN / inf in g: nothing certifies
+        st->flags |= GPAD_FLAG_TOL_FLOOR | GPAD_FLAG_NONFINITE_G;
     return status_error(rs);
 }
 
@@ -763,9 +752,6 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
     a.conv = conv;
     a.num_cus = h->num_cus;
     a.tune = &h->tune;
-    a.Hc = h->Hc_ok ? (const float*)h->Hc.p : nullptr;
-    a.hfrag = h->Hfrag_ok ? h->Hfrag.p : nullptr;
-    a.strideH = d.shared ? 0 : (long long)m * h->ldm;
     a.Hq = (h->hess_ok && tol > 0.0) ? (const T*)h->Hq.p : nullptr;
     a.strideHq = d.shared ? 0 : (long long)n * h->ldn;
     a.err = (int*)h->status.p;
@@ -829,57 +815,6 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
                 return fail(e == hipErrorInvalidValue ? GPAD_ERR_UNSUPPORTED : GPAD_ERR_HIP,
                             std::string("flat kernel: ") + hipGetErrorString(e));
             *kernel_out = GPAD_KERNEL_FLAT;
-            return finish(GPAD_OK);
-        }
-        if (kernel == GPAD_KERNEL_CONDENSED) {  // opt-in condensed operator (gpad_condensed.hip)
-            // shared-matrix batches beyond ~2 per CU on the MFMA pipe (gpad_cpanel.hip), else one
-            // workgroup per instance
-            if (d.shared && batch > 2 * h->num_cus && h->tune.cpanel) {
-                // eps mode: the panels run to the takeover iteration planned from the previous
-                // solve's counts (GPAD_OPT_PHASE_LEN forces one), the survivors finish one per
-                // workgroup on the latency kernel from the carried state
-                int vtake = N;
-                if (tol > 0.0 && h->tune.phased)
-                    vtake = h->tune.phase_len > 0 ? h->tune.phase_len : (h->cond_vtake > 0 ? h->cond_vtake : N);
-                a.v_begin = 0;
-                a.v_end = vtake < N ? vtake : N;
-                if (a.v_end < N) {
-                    const size_t pw = gpad::panel_work_bytes(m, batch) + 2 * sizeof(float) * (size_t)batch * m;
-                    int rc = h->pwork.ensure(pw);
-                    if (rc) return rc;
-                    int* idx0 = (int*)h->pwork.p;
-                    int* counts = idx0 + 2 * (size_t)batch;
-                    a.wc = reinterpret_cast<float*>(counts + 2 * gpad::kPanelMaxPhases);
-                    a.uc = a.wc + (size_t)batch * m;
-                    a.wbc = a.uc + (size_t)batch * m;
-                    a.cc = a.wbc + (size_t)batch * m;
-                    a.idx_out = idx0;
-                    a.count_out = counts;
-                    HIP_TRY(hipMemsetAsync(counts, 0, sizeof(int), h->stream));
-                }
-                e = gpad::launch_cpanel(a, h->stream, &ok);
-                if (e != hipSuccess) return fail(GPAD_ERR_HIP, std::string("condensed panel: ") + hipGetErrorString(e));
-                if (ok) {
-                    if (a.v_end < N) {  // the survivors on the latency kernel
-                        gpad::SolveArgs<T> f = a;
-                        f.v_begin = a.v_end;
-                        f.v_end = N;
-                        f.idx_in = a.idx_out;
-                        f.count_in = a.count_out;
-                        bool ok2 = false;
-                        e = gpad::launch_condensed(f, h->stream, &ok2);
-                        if (e != hipSuccess || !ok2)
-                            return fail(GPAD_ERR_HIP, std::string("condensed finisher: ") + hipGetErrorString(e));
-                    }
-                    h->last_phased = tol > 0.0 && h->tune.phased;  // its counts plan the next takeover
-                    *kernel_out = kernel;
-                    return finish(GPAD_OK);
-                }
-            }
-            e = gpad::launch_condensed(a, h->stream, &ok);
-            if (e != hipSuccess) return fail(GPAD_ERR_HIP, std::string("condensed: ") + hipGetErrorString(e));
-            if (!ok) return fail(GPAD_ERR_UNSUPPORTED, "condensed kernel: bind with dims.kernel = CONDENSED");
-            *kernel_out = kernel;
             return finish(GPAD_OK);
         }
         // shared matrices: panels once there are more instances than the latency kernel can
@@ -1013,8 +948,6 @@ static int run_impl(gpad_handle_t h, void* z0, void* y0, const void* M, const vo
     if (!z0 || !y0 || !M || !g) return fail(GPAD_ERR_INVALID, "gpad_run: null vector");
     if (N < 0) return fail(GPAD_ERR_INVALID, "gpad_run: N < 0");
     if (!(tol <= 0.0) && !std::isfinite(tol)) return fail(GPAD_ERR_INVALID, "gpad_run: bad tol");
-    if (h->dims.kernel == GPAD_KERNEL_CONDENSED && theta && N > 0 && ((const float*)theta)[0] != 1.0f)
-        return fail(GPAD_ERR_UNSUPPORTED, "gpad_run_scaled: the condensed kernel needs theta[0] = 1");
     HIP_TRY(hipSetDevice(h->device));
     if (h->dims.dtype == GPAD_DTYPE_F64)
         return run_typed<double>(h, (double*)z0, (double*)y0, (const double*)M, (const double*)g, N,

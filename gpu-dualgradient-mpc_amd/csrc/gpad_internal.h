@@ -27,7 +27,6 @@ struct Tuning {
     int flat_panels = 0;      // GPAD_OPT_FLAT_PANELS: panels per flat-panel workgroup (0: auto)
     int flat_waves = 0;       // GPAD_OPT_FLAT_WAVES: 0 auto, 8 or 16 waves per workgroup
     int flat_a_lds = 1;       // GPAD_OPT_FLAT_A_LDS: flat fragment image in LDS when it fits
-    int cpanel = 1;           // GPAD_OPT_CONDENSED_PANEL: condensed batches on the MFMA panels
     int debug_drop_handoff = 0;  // GPAD_OPT_DEBUG_DROP_HANDOFF: test-only fault injection
 };
 
@@ -44,6 +43,18 @@ constexpr int kDebugDropHandoff = 1;  // the first hand-off helper skips its fir
 template <typename T> struct ViolMargin;
 template <> struct ViolMargin<float> { static constexpr double value = 0x1p-20; };
 template <> struct ViolMargin<double> { static constexpr double value = 0x1p-49; };
+// max(acc, |x|) for acc >= 0 that keeps a NaN: as unsigned bit patterns the magnitudes order
+// finite < inf < NaN, so a NaN in g reaches the certification floor's max |g| (and the stats flag
+// it, GPAD_FLAG_NONFINITE_G) where fmax would drop it
+__device__ __forceinline__ float absmax_nan(float acc, float x) {
+    const unsigned a = __float_as_uint(acc), b = __float_as_uint(x) & 0x7fffffffu;
+    return __uint_as_float(a > b ? a : b);
+}
+__device__ __forceinline__ double absmax_nan(double acc, double x) {
+    const unsigned long long a = (unsigned long long)__double_as_longlong(acc),
+                             b = (unsigned long long)__double_as_longlong(x) & 0x7fffffffffffffffull;
+    return __longlong_as_double((long long)(a > b ? a : b));
+}
 // the decision itself, one expression everywhere (no contraction: -ffp-contract=off)
 __host__ __device__ inline bool viol_ok(double viol, double mag, double L, double tol, double margin) {
     return viol * L + margin * mag * L <= tol;
@@ -89,8 +100,6 @@ struct SolveArgs {
                            // every other path runs launch_absmax
     float* wc;             // carried w  [batch][m]
     float* uc;             // carried u = G_L z [batch][m]
-    float* wbc;            // condensed phases: carried wbar [batch][m]
-    float* cc;             // condensed phases: carried c = -G_L g_P [batch][m]
     int fin_thresh;        // survivors <= this: the resident finisher takes them (0: none)
     int* qctr;             // duo kernel: zeroed device counter of its work-list claims
     const int* pred;       // phased solves: per-instance iteration counts predicted from the
@@ -99,9 +108,6 @@ struct SolveArgs {
     int flat_staged;       // flat path: matrices staged in LDS (set by launch_flat)
     const struct PanelPlan* plan;  // panel phases: host-side plan from the previous solve (or null)
     const Tuning* tune;    // host-side tuning options (never null on a launch from gpad_host.cpp)
-    const float* Hc;       // condensed operator H = G_L (-ML), k-major [m][ldm] (gpad_condensed.hip)
-    const void* hfrag;     // H in the panel fragment layout (gpad_cpanel.hip), or null
-    long long strideH;     // elements between consecutive instances' H images (0 = shared)
     const T* Hq;           // QP Hessian H, k-major [n][ldn] (gpad_setup_hessian), or null: enables the
                            // value-function branches of the test (stream kernel only)
     long long strideHq;    // elements between consecutive instances' H images (0 = shared)
@@ -118,19 +124,6 @@ hipError_t launch_resident(const SolveArgs<float>& a, hipStream_t s, bool* suppo
 // zeroed a.qctr.  Persistent grid of `grid` workgroups (one per CU).
 hipError_t launch_duo(const SolveArgs<float>& a, int grid, hipStream_t s);
 bool resident_supported(int n, int m);
-// GPAD_KERNEL_CONDENSED (gpad_condensed.hip): H = G_L (-ML) images for nmats matrix pairs, then
-// the one-chain-per-iteration latency kernel (m <= 208, n <= 256)
-bool condensed_supported(int n, int m);
-hipError_t launch_condense(const float* GLt, const float* MGt, int n, int m, int ldn, int ldm, int nmats,
-                           long long strideA, long long strideB, float* Ht, hipStream_t s);
-hipError_t launch_condensed(const SolveArgs<float>& a, hipStream_t s, bool* supported);
-// ... and on the MFMA pipe for shared-matrix batches (gpad_cpanel.hip; T = ceil(max(n,m)/16) <= 16,
-// needs the panel fragment images and the H image)
-bool cpanel_supported(int n, int m);
-size_t cpanel_frag_bytes(int n, int m);
-hipError_t launch_pack_cpanel(const float* Ht, int n, int m, int ldm, void* hfrag, hipStream_t s);
-hipError_t launch_cpanel(const SolveArgs<float>& a, hipStream_t s, bool* supported);
-int cpanel_takeover(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus);
 hipError_t launch_panel(const SolveArgs<float>& a, hipStream_t s, bool* supported);
 // launch_panel at (n, m) runs the panel pairs, which fold max |g| into their loads (gmax_part)
 bool panel_folds_gmax(int n, int m);
@@ -140,7 +133,7 @@ bool panel_folds_gmax(int n, int m);
 // over.  With a.seg_cnt the panel writes its own slot -- seg_cnt[P], seg_idx[16 P + rank] -- and
 // phase_compact_kernel densifies the list at the boundary: no same-address atomics (hundreds of
 // panels appending to one counter serialise at L2, ~25 us per boundary at 512 panels measured).
-// Without it (flat / condensed panels) the survivors are appended through a.count_out.  Every
+// Without it (flat panels) the survivors are appended through a.count_out.  Every
 // panel of a phase calls it, parked or not, so no slot keeps a stale count.
 __device__ __forceinline__ void list_survivors(const SolveArgs<float>& a, int P, bool park, int inst, int lane,
                                                int j) {

@@ -831,7 +831,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 y[q][r] = okm ? a.y[b * m + i] : 0.0f;
                 const float gr = okm ? a.g[b * a.ld_g + i] : 0.0f;
                 pd[r] = (float)(a.gscale * (double)gr);
-                gmx = fmaxf(gmx, __builtin_fabsf(gr));
+                gmx = absmax_nan(gmx, gr);
                 if (fresh) {  // w_0 = y_0 + beta_0 (y_0 - y_{-1}), y_{-1} = y_0
                     wv[r] = __builtin_fmaf(a.beta[0], y[q][r] - y[q][r], y[q][r]);
                     u[q][r] = 0.0f;
@@ -1171,7 +1171,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
         __syncthreads();
     }
     if (a.gmax_part) {  // this wave's max |g| -> L.gred (reduced by the kernel at exit)
-        for (int o = 32; o > 0; o >>= 1) gmx = fmaxf(gmx, __shfl_xor(gmx, o, 64));
+        for (int o = 32; o > 0; o >>= 1) gmx = absmax_nan(gmx, __shfl_xor(gmx, o, 64));
         if (lane == 0) L.gred[threadIdx.x >> 6] = gmx;
     }
 }
@@ -1246,8 +1246,8 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
         if (Handoff<T>::on && threadIdx.x == 0 && L.herr) atomicOr(a.err, kDevErrHandoff);
         if (a.gmax_part && threadIdx.x == 0) {  // the run's max |g|: this workgroup's slot
             float g = 0.0f;
-            for (int i = 0; i < 16; ++i) g = fmaxf(g, L.gred[i]);
-            a.gmax_part[blockIdx.x] = fmax(a.gmax_part[blockIdx.x], (double)g);
+            for (int i = 0; i < 16; ++i) g = absmax_nan(g, L.gred[i]);
+            a.gmax_part[blockIdx.x] = absmax_nan(a.gmax_part[blockIdx.x], (double)g);
         }
     }
 }

@@ -146,14 +146,14 @@ __global__ __launch_bounds__(256) void absmax_kernel(const T* __restrict__ g, lo
             v[u] = i < count ? g[i] : T(0);
         }
 #pragma unroll
-        for (int u = 0; u < 16; ++u) mx = fmax(mx, fabs((double)v[u]));
+        for (int u = 0; u < 16; ++u) mx = absmax_nan(mx, (double)v[u]);
     }
-    for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+    for (int o = 32; o > 0; o >>= 1) mx = absmax_nan(mx, __shfl_xor(mx, o, 64));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
     __syncthreads();
     if (threadIdx.x == 0) {
-        mx = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
-        part[blockIdx.x] = fmax(part[blockIdx.x], mx);
+        mx = absmax_nan(absmax_nan(red[0], red[1]), absmax_nan(red[2], red[3]));
+        part[blockIdx.x] = absmax_nan(part[blockIdx.x], mx);
     }
 }
 

@@ -12,17 +12,18 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libgpad.so")
 
+VERSION_MAJOR, VERSION_MINOR = 0, 4  # include/gpad.h GPAD_VERSION_*: the layouts this binding declares
 GPAD_OK = 0
 ERR_INVALID, ERR_HIP, ERR_NOMEM, ERR_UNSUPPORTED, ERR_NOT_SETUP, ERR_NO_DEVICE = -1, -2, -3, -4, -5, -6
 ERR_DEVICE = -7  # a kernel reported a device-side failure (include/gpad.h)
 FLAG_TOL_FLOOR = 1  # gpad_stats_t.flags: tol below the certification floor
+FLAG_NONFINITE_G = 2  # ... g holds a NaN / infinity (tol_floor not finite)
 SCHEDULE_MATLAB, SCHEDULE_PAPER = 0, 1
 MEM_HOST, MEM_DEVICE = 0, 1
 DTYPE_F32, DTYPE_F64 = 0, 1
 KERNEL_AUTO, KERNEL_STREAM, KERNEL_RESIDENT, KERNEL_PANEL, KERNEL_FLAT = 0, 1, 2, 3, 4
-KERNEL_CONDENSED = 5  # opt-in, not bit-exact: the condensed operator (include/gpad.h)
 KERNEL_NAMES = {KERNEL_AUTO: "auto", KERNEL_STREAM: "stream", KERNEL_RESIDENT: "resident",
-                KERNEL_PANEL: "panel", KERNEL_FLAT: "flat", KERNEL_CONDENSED: "condensed"}
+                KERNEL_PANEL: "panel", KERNEL_FLAT: "flat"}
 
 # every symbol include/gpad.h declares (checked by tests/test_abi.py)
 EXPORTS = [
@@ -46,15 +47,14 @@ OPT_DEFAULT = -1
 OPT_PHASE_LEN, OPT_FINISH_THRESH, OPT_PLAN, OPT_PHASED, OPT_LPT = 1, 2, 3, 4, 6
 OPT_PANEL_MAX_GRID, OPT_DUO_MAX_GRID, OPT_FLAT_PANEL_MIN, OPT_FLAT_PANELS = 7, 8, 9, 10
 OPT_FLAT_WAVES, OPT_FLAT_A_LDS = 11, 12
-OPT_CONDENSED_PANEL = 14
 OPT_DEBUG_DROP_HANDOFF = 16  # test-only fault injection
-OPT_RETIRED = (5, 13, 15)  # finisher kind, solo finisher workgroups, plan finisher cost (0.3)
+OPT_RETIRED = (5, 13, 14, 15)  # finisher kind, solo finisher workgroups, plan finisher cost (0.3);
+# condensed panels (0.4, with the condensed operator)
 OPTIONS = {"phase_len": OPT_PHASE_LEN, "finish_thresh": OPT_FINISH_THRESH, "plan": OPT_PLAN,
            "phased": OPT_PHASED, "lpt": OPT_LPT,
            "panel_max_grid": OPT_PANEL_MAX_GRID, "duo_max_grid": OPT_DUO_MAX_GRID,
            "flat_panel_min": OPT_FLAT_PANEL_MIN, "flat_panels": OPT_FLAT_PANELS,
            "flat_waves": OPT_FLAT_WAVES, "flat_a_lds": OPT_FLAT_A_LDS,
-           "condensed_panel": OPT_CONDENSED_PANEL,
            "debug_drop_handoff": OPT_DEBUG_DROP_HANDOFF}
 
 FILE_ROWMAJOR, FILE_FLIPPED, FILE_FLAT = 0, 1, 2
@@ -91,9 +91,26 @@ class GpadError(RuntimeError):
 _LIB = None
 
 
+def _check_version(L) -> None:
+    """The library's gpad_version() ("gpad-mi355x MAJOR.MINOR ...") must be the version this binding
+    declares its structs for (Dims / Stats layouts change between minors)."""
+    txt = (L.gpad_version() or b"").decode(errors="replace")
+    parts = txt.split()
+    try:
+        major, minor = (int(x) for x in parts[1].split(".")[:2])
+    except (IndexError, ValueError):
+        raise ImportError(f"libgpad: unrecognised gpad_version() {txt!r}") from None
+    if (major, minor) != (VERSION_MAJOR, VERSION_MINOR):
+        raise ImportError(f"libgpad version {major}.{minor} does not match the binding's "
+                          f"{VERSION_MAJOR}.{VERSION_MINOR} (rebuild: make -C gpu-dualgradient-mpc_amd)")
+
+
 def load(path: str | None = None) -> C.CDLL:
-    """Load libgpad.so once.  Raises (loudly) when the HIP library is absent.
-    ``GPAD_LIB`` may point at another build of the same library (A/B benchmarking)."""
+    """Load libgpad.so once.  Raises (loudly) when the HIP library is absent or its version is not
+    the one this binding declares.  ``GPAD_LIB`` may point at another build of the same library;
+    ``GPAD_LIB_TOLERANT=1`` (A/B benchmarking of older builds only) binds what such a build
+    exports -- missing entry points become stubs returning ERR_UNSUPPORTED -- and skips the
+    version check."""
     global _LIB
     if _LIB is not None:
         return _LIB
@@ -102,7 +119,8 @@ def load(path: str | None = None) -> C.CDLL:
         raise ImportError(f"libgpad.so not built at {path}: run `make -C gpu-dualgradient-mpc_amd` "
                           "(or __graft_entry__.build()); there is no CPU fallback")
     L = C.CDLL(path)
-    if os.environ.get("GPAD_LIB"):  # A/B runs may load an older build: bind what it exports
+    tolerant = os.environ.get("GPAD_LIB_TOLERANT") == "1"
+    if tolerant:  # A/B runs may load an older build: bind what it exports
         class _Tolerant:
             def __init__(self, lib):
                 self.__dict__["_lib"] = lib
@@ -118,6 +136,8 @@ def load(path: str | None = None) -> C.CDLL:
         L = _Tolerant(L)
     vp, cvp, i, d = C.c_void_p, C.c_void_p, C.c_int, C.c_double
     L.gpad_version.restype = C.c_char_p
+    if not tolerant:
+        _check_version(L)
     L.gpad_strerror.restype = C.c_char_p
     L.gpad_strerror.argtypes = [i]
     L.gpad_last_error.restype = C.c_char_p

@@ -210,7 +210,8 @@ class GpadSolver:
         return dict(iterations=st.iterations, converged=st.converged,
                     total_iterations=st.total_iterations, kernel=_lib.KERNEL_NAMES.get(st.kernel),
                     kernel_ms=st.kernel_ms, tol_floor=st.tol_floor,
-                    below_tol_floor=bool(st.flags & _lib.FLAG_TOL_FLOOR))
+                    below_tol_floor=bool(st.flags & _lib.FLAG_TOL_FLOOR),
+                    nonfinite_g=bool(st.flags & _lib.FLAG_NONFINITE_G))
 
     def sync(self) -> None:
         check(self.lib.gpad_sync(self.h), "gpad_sync")
@@ -276,14 +277,18 @@ class GpadSolver:
         return self._stats_dict(st) if want else None
 
     def closed_loop(self, x, z, y, steps: int, N: int, tol: float = 0.0, *, warm: bool = False,
-                    xs=None, us=None, iters=None, stats: bool = True):
+                    xs=None, us=None, iters=None, codes=None, stats: bool = True):
         """gpad.m:79-95 on the device: ``steps`` receding-horizon MPC steps for every instance.
         x [batch][nx] is advanced in place; xs [steps][batch][nx] / us [steps][batch][nu]
-        receive the trajectories when given; ``iters`` (host int32 [steps*batch]) the counts."""
+        receive the trajectories when given; ``iters`` / ``codes`` (host int32 [steps*batch]) the
+        counts and termination codes."""
         st = Stats()
-        if iters is not None:
-            st.iters = iters.ctypes.data_as(C.POINTER(C.c_int))
-        want = stats or iters is not None or not _is_torch(z)
+        for arr, field in ((iters, "iters"), (codes, "codes")):
+            if arr is not None:
+                if arr.dtype != np.int32 or arr.size < steps * max(1, self.dims.batch if self.dims else 1):
+                    raise ValueError(f"{field} must be host int32 with steps * batch entries")
+                setattr(st, field, arr.ctypes.data_as(C.POINTER(C.c_int)))
+        want = stats or iters is not None or codes is not None or not _is_torch(z)
         opt = lambda a: _ptr(a) if a is not None else None  # noqa: E731
         check(self.lib.gpad_closed_loop(self.h, _ptr(x), _ptr(z), _ptr(y), int(steps), int(N),
                                         float(tol), int(bool(warm)), opt(xs), opt(us),
@@ -366,10 +371,12 @@ class GpadGroup:
         check(self.lib.gpad_group_setup(self.g, C.byref(self.dims), _ptr(ML), _ptr(G), float(L)),
               "gpad_group_setup")
 
-    def run(self, z, y, M, g, N: int, tol: float = 0.0, *, iters=None) -> dict:
+    def run(self, z, y, M, g, N: int, tol: float = 0.0, *, iters=None, codes=None) -> dict:
         st = Stats()
         if iters is not None:
             st.iters = iters.ctypes.data_as(C.POINTER(C.c_int))
+        if codes is not None:  # per-instance termination codes, [batch] in global order
+            st.codes = codes.ctypes.data_as(C.POINTER(C.c_int))
         check(self.lib.gpad_group_run(self.g, _ptr(z), _ptr(y), _ptr(M), _ptr(g), int(N), float(tol),
                                       C.byref(st)), "gpad_group_run")
         return GpadSolver._stats_dict(st)

@@ -26,8 +26,10 @@ extern "C" {
 #endif
 
 #define GPAD_VERSION_MAJOR 0
-#define GPAD_VERSION_MINOR 3 /* 0.3: gpad_stats_t gained tol_floor / flags, gpad_dims_t an explicit reserved
-                              * word (layouts changed: rebuild callers against this header) */
+#define GPAD_VERSION_MINOR 4 /* 0.3: gpad_stats_t gained tol_floor / flags, gpad_dims_t an explicit reserved
+                              * word (layouts changed: rebuild callers against this header);
+                              * 0.4: the condensed operator (kernel 5, option 14) removed, the device
+                              * error word sticky until reported; layouts as in 0.3 */
 
 /* status codes */
 #define GPAD_OK 0
@@ -41,7 +43,10 @@ extern "C" {
                                     * hand-off that never arrived): the run's z, y are invalid.
                                     * Returned by the call that collects the run's stats or
                                     * synchronises it (gpad_run with st, gpad_last_stats,
-                                    * gpad_sync, host-memory runs) -- never GPAD_OK            */
+                                    * gpad_sync, host-memory runs) -- never GPAD_OK; the error
+                                    * is kept on the device until one of those reports it, so
+                                    * asynchronous runs queued behind a failed one do not
+                                    * hide it                                                  */
 
 /* theta/beta schedule (acceldualgrad.m:18,27,55-56 vs paper eq. 8e) */
 #define GPAD_SCHEDULE_MATLAB 0 /* beta lagged one iteration, as the reference's MATLAB  */
@@ -59,17 +64,8 @@ extern "C" {
 #define GPAD_KERNEL_RESIDENT 2 /* matrix rows held in VGPRs; one workgroup/instance; n,m <= 208  */
 #define GPAD_KERNEL_PANEL 3    /* shared ML/G, f32 MFMA 16x16x4 panels; one wave per 16 instances */
 #define GPAD_KERNEL_FLAT 4     /* reported only: the flat battery path bound by gpad_setup_flat      */
-/* Opt-in, NOT bit-exact with the reference and NOT parity-compliant: the condensed operator
- * (z*, y* measured up to 7.8e-6 relative from the reference's at the C4 configuration to eps, above
- * the 1e-6 parity bar; kept for latency studies, no longer developed).  G_L zhat = H w + c with
- * H = G_L (-ML) (m x m, formed once per gpad_setup from an fp64 product) and c = -G_L gP, and
- * z = (-ML) wbar - gP with wbar the theta-averaged dual point -- one m-long chain per iteration
- * instead of the reference's m-long (8b) and n-long (8d) chains (C2 latency ~halved).  A
- * reassociation of the same iteration: z* and y* stay within the reference's own fp32-vs-MATLAB
- * spread (tests/test_condensed.py); Algorithm 1 is still decided on direct G_L z of the returned
- * point.  f32, one workgroup per instance, m <= 208, n <= 256; requires theta_0 = 1 (both
- * built-in schedules); custom theta tables of gpad_run_scaled must keep it. */
-#define GPAD_KERNEL_CONDENSED 5
+/* 5: the opt-in condensed operator (not the reference's arithmetic), removed in 0.4; dims.kernel = 5
+ * returns GPAD_ERR_INVALID */
 
 typedef struct gpad_dims {
     int n;           /* primal variables, n = n_u * N                                   */
@@ -92,11 +88,13 @@ typedef struct gpad_stats {
     long long total_iterations;  /* sum of per-instance iterations                      */
     int kernel;                  /* GPAD_KERNEL_* that ran                               */
     double kernel_ms;            /* device time of the solve launch (HIP events)        */
-    int* iters;                  /* optional caller array [batch] (host) or NULL        */
+    int* iters;                  /* optional caller array (host) or NULL: [batch]; gpad_closed_loop:
+                                  * [steps][batch]                                        */
     double tol_floor;            /* tol > 0: the certification floor of this run's data, see
                                   * gpad_run (0 when tol <= 0)                             */
     int flags;                   /* GPAD_FLAG_* of the run                                  */
-    int* codes;                  /* optional caller array [batch] (host) or NULL: per-instance
+    int* codes;                  /* optional caller array (host) or NULL, sized as iters:
+                                  * [batch]; gpad_closed_loop: [steps][batch].  Per-instance
                                   * termination code, 0 = ran to N, 1..4 = the test that
                                   * stopped it (gpad_run)                                   */
 } gpad_stats_t;
@@ -104,6 +102,8 @@ typedef struct gpad_stats {
 /* gpad_stats_t.flags */
 #define GPAD_FLAG_TOL_FLOOR 1 /* 0 < tol < tol_floor: no instance with an active constraint can be
                                * certified; expect converged == 0 (use f64 or a larger tol)   */
+#define GPAD_FLAG_NONFINITE_G 2 /* tol > 0 and g holds a NaN or an infinity: tol_floor is not
+                                 * finite (NaN when g has a NaN) and TOL_FLOOR is set too        */
 
 typedef struct gpad_handle_s* gpad_handle_t;
 
@@ -112,7 +112,9 @@ const char* gpad_version(void);
  * of gpad_group_create / gpad_solve_sharded (main.cu picks device 0, :116) */
 int gpad_device_count(void);
 const char* gpad_strerror(int status);
-const char* gpad_last_error(void); /* thread-local detail of the last failure */
+/* thread-local detail of the last failure; HIP runtime failures carry the HIP status name and
+ * number ("hipErrorNoDevice (code 100): ...") */
+const char* gpad_last_error(void);
 
 /* Handle bound to one device and one HIP stream; every launch and copy of the handle is
  * ordered on that stream.  NULL = the device's default (null) stream, as in every HIP API.
@@ -225,8 +227,9 @@ int gpad_run_state(gpad_handle_t h, const void* x, void* z0, void* y0, int N, do
  *                   xs[t] = x;  us[t] = u = z*[0:nu];  x <- A x + B u
  * x [batch][nx]: in x_0, out x_steps.  z [batch][n], y [batch][m]: the last step's solution.
  * xs [steps][batch][nx], us [steps][batch][nu]: optional trajectories (NULL to skip).
- * st->iters, when given, receives [steps][batch] iteration counts; the other stats aggregate
- * over every (step, instance); kernel_ms times the whole loop. */
+ * st->iters and st->codes, when given, receive [steps][batch] iteration counts and termination
+ * codes (size both arrays steps * batch); the other stats aggregate over every (step, instance);
+ * kernel_ms times the whole loop. */
 int gpad_closed_loop(gpad_handle_t h, void* x, void* z, void* y, int steps, int N, double tol, int warm,
                      void* xs, void* us, gpad_stats_t* st);
 
@@ -361,14 +364,14 @@ int gpad_schedule(int N, int kind, double* theta, double* beta);
 #define GPAD_OPT_DEFAULT (-1)
 #define GPAD_OPT_PHASE_LEN 1       /* panel phase length in iterations (default 4 * check_every,
                                     * doubling after the 10th phase; set: uniform, with PLAN 0);
-                                    * flat panels: the first phase; condensed batches: the finisher
-                                    * takeover iteration (default planned from the previous solve) */
+                                    * flat panels: the first phase                                  */
 #define GPAD_OPT_FINISH_THRESH 2   /* survivors at which the finisher takes over (default 2/CU)    */
 #define GPAD_OPT_PLAN 3            /* 1: plan phases from the previous solve's counts (default)    */
 #define GPAD_OPT_PHASED 4          /* 1: phased compaction of tol > 0 panel solves (default; flat
                                     * panels: from 4 panels per CU), 2: always, 0: one launch       */
 /* 5 (finisher kind), 13 (solo finisher workgroups), 15 (plan finisher cost): retired in 0.3 after
- * measuring no gain; setting them returns GPAD_ERR_INVALID                         */
+ * measuring no gain; 14 (condensed panels): removed with the condensed operator in
+ * 0.4; setting them returns GPAD_ERR_INVALID                                                    */
 #define GPAD_OPT_LPT 6             /* 1: longest-predicted-first finisher queue (default)          */
 #define GPAD_OPT_PANEL_MAX_GRID 7  /* cap on the panel grid, workgroups (0 = none, default)        */
 #define GPAD_OPT_DUO_MAX_GRID 8    /* cap on the finisher grid (0 = none, default)                 */
@@ -376,8 +379,6 @@ int gpad_schedule(int N, int kind, double* theta, double* beta);
 #define GPAD_OPT_FLAT_PANELS 10    /* panels per flat-panel workgroup, 1..4 (0 = auto, default)    */
 #define GPAD_OPT_FLAT_WAVES 11     /* flat-panel workgroup waves: 0 auto (default), 8 or 16         */
 #define GPAD_OPT_FLAT_A_LDS 12     /* 1: flat fragment image staged in LDS when it fits (default)  */
-#define GPAD_OPT_CONDENSED_PANEL 14 /* 1: GPAD_KERNEL_CONDENSED batches (shared, > 2/CU) on the MFMA
-                                     * panels (default); 0: one workgroup per instance             */
 #define GPAD_OPT_DEBUG_DROP_HANDOFF 16 /* test only (fault injection): 1 = every panel solve that
                                     * uses the chain hand-off withholds its first post, so the
                                     * receiver's bounded wait expires and the run ends in

@@ -283,113 +283,6 @@ static int orc_solve_f32_h(float* z, float* y, const float* MGneg, const float* 
     return it;
 }
 
-/* ---- condensed operator (GPAD_KERNEL_CONDENSED: opt-in, NOT the reference's arithmetic) ----
- * The same GPAD iteration (main.cu:160-172 / acceldualgrad.m:29-64) with zhat eliminated:
- *   G_L zhat_v = G_L (MGneg w_v - gP) = H w_v + c,   H = G_L MGneg (m x m),  c = -G_L gP,
- * and, because theta_0 = 1 (both schedules), z_v = MGneg wbar_v - gP with the averaged dual
- * point wbar_v = (1 - theta_v) wbar_{v-1} + theta_v w_v (8c moved through the linear map).  One
- * m-long chain per iteration instead of an m-long (8b) and an n-long (8d) one; z is formed only
- * when a test is decided and at the end.  Equal to the reference in exact arithmetic; in fp32 it
- * is a reassociation (H rounded once from fp64), as far from the reference as any other
- * summation order (tests/test_condensed.py measures it against the reference's own fp32-vs-fp64
- * spread).  Algorithm 1 stays certified on the returned point: both tests are only nominated
- * by the condensed quantities and decided on direct chains of the z / zhat that is returned. */
-void orc_condense_f32(const float* GL, const float* MGneg, int n, int m, float* H) {
-    for (int i = 0; i < m; i++)
-        for (int j = 0; j < m; j++) {
-            double acc = 0.0;
-            for (int k = 0; k < n; k++) acc = fma((double)GL[(size_t)i * n + k], (double)MGneg[(size_t)k * m + j], acc);
-            H[(size_t)i * m + j] = (float)acc;
-        }
-}
-
-/* direct chains: x = MGneg v - gP (n), then a = GL x (m) */
-static void orc_direct(const float* MGneg, const float* gP, const float* GL, const float* v, float* x,
-                       float* a, int n, int m) {
-    orc_step2_f32(MGneg, v, gP, x, n, m);
-    for (int i = 0; i < m; i++) a[i] = orc_chain(GL + (size_t)i * n, x, n);
-}
-
-int orc_solve_condensed_f32(float* z, float* y, const float* MGneg, const float* gP, const float* GL,
-                            const float* pD, const float* H, int n, int m, int N, float L, double tol,
-                            double tol_gap, int check_every, const float* theta, const float* beta,
-                            int* converged) {
-    const int mm = m > 0 ? m : 1;
-    float* base = (float*)malloc(sizeof(float) * (size_t)mm * 9);
-    float* ycur = base;
-    float* yprev = ycur + mm;
-    float* w = yprev + mm;
-    float* ynew = w + mm;
-    float* u = ynew + mm;     /* G_L z estimate: (1-theta) u + theta s */
-    float* s = u + mm;        /* H w + c: G_L zhat by the condensed operator */
-    float* c = s + mm;
-    float* wbar = c + mm;
-    float* a = wbar + mm;     /* direct G_L x of a decided test */
-    float* x = (float*)malloc(sizeof(float) * (size_t)(n > 0 ? n : 1));
-    if (check_every <= 0) check_every = 10;
-    memcpy(ycur, y, sizeof(float) * m);
-    memcpy(yprev, y, sizeof(float) * m);
-    for (int i = 0; i < m; i++) {
-        c[i] = -orc_chain(GL + (size_t)i * n, gP, n);
-        wbar[i] = 0.0f;
-        u[i] = 0.0f;  /* theta_0 = 1: u_0 = fmaf(0, u, s) = s whatever the seed */
-    }
-    const int use_tol = tol > 0.0;
-    const double tgap = orc_tol_gap(tol, tol_gap);
-    int it = 0, conv = 0;
-    for (int v = 0; v < N; v++) {
-        const float th = theta[v], omt = 1.0f - th;
-        orc_step1_f32(ycur, yprev, w, beta[v], m);
-        for (int i = 0; i < m; i++) {
-            s[i] = orc_chain(H + (size_t)i * m, w, m) + c[i];
-            wbar[i] = fmaf(omt, wbar[i], th * w[i]);
-            const float sv = (w[i] + pD[i]) + s[i];
-            ynew[i] = (fabsf(sv) + sv) * 0.5f;
-        }
-        float* t = yprev; yprev = ycur; ycur = ynew; ynew = t;
-        it = v + 1;
-        if (!use_tol) continue;
-        for (int i = 0; i < m; i++) u[i] = fmaf(omt, u[i], th * s[i]);
-        if ((it % check_every) != 0) continue;
-        float viol = -INFINITY;
-        for (int i = 0; i < m; i++) viol = fmaxf(viol, u[i] + pD[i]);
-        if ((double)viol * L <= tol) {  /* (A) nominated: decide on G_L z of z = MGneg wbar - gP */
-            orc_direct(MGneg, gP, GL, wbar, x, a, n, m);
-            float vc = -INFINITY, mag = 0.0f;
-            for (int i = 0; i < m; i++) {
-                u[i] = a[i];
-                vc = fmaxf(vc, a[i] + pD[i]);
-                mag = fmaxf(mag, fabsf(a[i]) + fabsf(pD[i]));
-            }
-            if ((double)vc * L + ORC_MARGIN_F32 * (double)mag * L <= tol) { conv = 1; break; }
-        }
-        /* (B) nominated on s = H w + c, decided on G_L zhat of zhat = MGneg w - gP */
-        int pass = 1;
-        for (int k = 0; k < 2 && pass; k++) {
-            const float* ch = k == 0 ? s : a;
-            if (k == 1) orc_direct(MGneg, gP, GL, w, x, a, n, m);
-            float violh = -INFINITY, magh = 0.0f, wmin = INFINITY;
-            double gap = 0.0;
-            for (int i = 0; i < m; i++) {
-                const float tt = ch[i] + pD[i];
-                violh = fmaxf(violh, tt);
-                magh = fmaxf(magh, fabsf(ch[i]) + fabsf(pD[i]));
-                wmin = fminf(wmin, w[i]);
-                gap -= (double)w[i] * (double)tt;
-            }
-            pass = ((double)violh * L + ORC_MARGIN_F32 * (double)magh * L <= tol) && (wmin >= 0.0f) &&
-                   (gap * L <= tgap);
-        }
-        if (pass) { memcpy(z, x, sizeof(float) * n); conv = 2; break; }
-    }
-    if (it > 0 && conv != 2) orc_step2_f32(MGneg, wbar, gP, z, n, m);  /* z = MGneg wbar - gP */
-    memcpy(y, ycur, sizeof(float) * m);
-    free(base);
-    free(x);
-    if (converged) *converged = conv;
-    return it;
-}
-
 /* ---- fp64, acceldualgrad.m operation order ------------------------------------- */
 /* the fp64 twin of orc_check_f32 (margin ORC_MARGIN_F64 = 16 units of 2^-53) */
 /* fp64 twins of the value functions (orc_valuefcn's sums; ML is +H^-1 G' here) */

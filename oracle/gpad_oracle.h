@@ -79,15 +79,6 @@ int orc_solve_value_f64(double* z, double* y, const double* ML, const double* gP
                         double tol_gap, int check_every, int schedule, int* converged);
 
 /* fp64 solve in acceldualgrad.m:43-64 order: inputs are ML (+H^-1 G^T), gP, G, g, L. */
-/* condensed operator (opt-in GPAD_KERNEL_CONDENSED; not the reference's arithmetic):
- * H = fl32(G_L MGneg) by an fp64 fma chain over k; the solve as orc_solve_f32's semantics with
- * G_L zhat = H w + c, z = MGneg wbar - gP (gpad_oracle.c) */
-void orc_condense_f32(const float* GL, const float* MGneg, int n, int m, float* H);
-int orc_solve_condensed_f32(float* z, float* y, const float* MGneg, const float* gP, const float* GL,
-                            const float* pD, const float* H, int n, int m, int N, float L, double tol,
-                            double tol_gap, int check_every, const float* theta, const float* beta,
-                            int* converged);
-
 int orc_solve_f64(double* z, double* y, const double* ML, const double* gP, const double* G,
                   const double* g, int n, int m, int N, double L, double tol, double tol_gap,
                   int check_every, int schedule, int* converged);

@@ -81,10 +81,6 @@ class Oracle:
         L.orc_solve_flat_f32.argtypes = [_f, _f, _f, _f, _f, _f, C.c_int, C.c_int, C.c_int, C.c_int,
                                          C.c_float, C.c_double, C.c_double, C.c_int, _f, _f, _i]
         L.orc_solve_flat_f32.restype = C.c_int
-        L.orc_condense_f32.argtypes = [_f, _f, C.c_int, C.c_int, _f]
-        L.orc_solve_condensed_f32.argtypes = [_f, _f, _f, _f, _f, _f, _f, C.c_int, C.c_int, C.c_int,
-                                              C.c_float, C.c_double, C.c_double, C.c_int, _f, _f, _i]
-        L.orc_solve_condensed_f32.restype = C.c_int
         self.lib = L
 
     # -- steps ------------------------------------------------------------------
@@ -164,32 +160,6 @@ class Oracle:
                                     np.float32(L), float(tol), float(tol_gap), check_every, _fp(theta),
                                     _fp(beta), C.byref(conv))
         return z, y, it, bool(conv.value)
-
-    # -- condensed operator (GPAD_KERNEL_CONDENSED; gpad_oracle.c orc_solve_condensed_f32) ----
-    def condense(self, GL, MGneg):
-        """H = fl32(G_L MGneg), fp64 fma chain over k (m x m)."""
-        GL = np.ascontiguousarray(GL, np.float32); MGneg = np.ascontiguousarray(MGneg, np.float32)
-        m, n = GL.shape
-        H = np.empty((m, m), np.float32)
-        self.lib.orc_condense_f32(_fp(GL), _fp(MGneg), n, m, _fp(H))
-        return H
-
-    def solve_condensed_f32(self, z0, y0, ML, M, G, g, N, L, tol=0.0, check_every=10,
-                            schedule=SCHEDULE_MATLAB, tol_gap=0.0, H=None):
-        MGneg, GL, pD = self.scale(ML, G, g, L)
-        if H is None:
-            H = self.condense(GL, MGneg)
-        n, m = MGneg.shape
-        z = np.array(z0, np.float32, copy=True).reshape(n)
-        y = np.array(y0, np.float32, copy=True).reshape(m)
-        theta, beta = self.schedule_f32(max(N, 1), schedule)
-        conv = C.c_int(0)
-        gP = np.ascontiguousarray(M, np.float32).reshape(n)
-        it = self.lib.orc_solve_condensed_f32(_fp(z), _fp(y), _fp(MGneg), _fp(gP), _fp(GL), _fp(pD),
-                                              _fp(np.ascontiguousarray(H, np.float32)), n, m, N,
-                                              np.float32(L), float(tol), float(tol_gap), check_every,
-                                              _fp(theta), _fp(beta), C.byref(conv))
-        return z, y, it, conv.value
 
     def solve_f64(self, z0, y0, ML, M, G, g, N, L, tol=0.0, check_every=10,
                   schedule=SCHEDULE_MATLAB, tol_gap=0.0):

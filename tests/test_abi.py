@@ -104,6 +104,37 @@ def test_create_without_gpu_reports_no_device():
     rc = L.gpad_create(C.byref(h), 0, None)
     assert rc in (_lib.ERR_NO_DEVICE, _lib.ERR_HIP)
     assert not h.value
+    # the failure names the HIP status it came from (name and number), or says
+    # the runtime reported zero devices -- never a bare "no device"
+    msg = L.gpad_last_error().decode()
+    assert msg.startswith("gpad_create: hipGetDeviceCount"), msg
+    assert ("hipError" in msg and "(code " in msg) or "reported 0 devices" in msg, msg
+    n = L.gpad_device_count()
+    if n < 0:
+        assert "hipError" in L.gpad_last_error().decode()
+
+
+def test_binding_checks_library_version():
+    """the ctypes binding refuses a library whose gpad_version() is not the version
+    its Dims / Stats layouts are declared for (GPAD_VERSION_MINOR of include/gpad.h)."""
+    import re as _re
+
+    from gpad_mpc import _lib
+    hdr = open(HEADER).read()
+    minor = int(_re.search(r"#define GPAD_VERSION_MINOR (\d+)", hdr).group(1))
+    assert (_lib.VERSION_MAJOR, _lib.VERSION_MINOR) == (0, minor)
+    assert f"0.{minor}".encode() in _lib.load().gpad_version()
+
+    class Fake:
+        def __init__(self, v):
+            self.v = v
+
+        def gpad_version(self):
+            return self.v
+    _lib._check_version(Fake(f"gpad-mi355x 0.{minor} (gfx950)".encode()))
+    for bad in (b"gpad-mi355x 0.3 (gfx950)", b"garbage"):
+        with pytest.raises(ImportError):
+            _lib._check_version(Fake(bad))
 
 
 def test_product_path_has_no_oracle_dependency():

@@ -61,6 +61,51 @@ def test_dropped_handoff_fails_the_run(gpu, oracle, batch):
         assert_bitexact(y[b].cpu().numpy(), yo, f"y[{b}]")
 
 
+def test_device_error_is_sticky_across_async_runs(gpu):
+    """a faulty asynchronous run followed by a clean one, then one gpad_sync: the sync
+    reports the first run's GPAD_ERR_DEVICE (the second run's status reset must not wipe it), and
+    the error is reported once -- the next sync is clean."""
+    import torch
+
+    import gpad_mpc
+    from gpad_mpc import _lib
+    ML, G, L, M, g = _shard(64)
+    dev = torch.device("cuda:0")
+    t = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
+    with gpad_mpc.GpadSolver(0) as s:
+        s.setup(t(ML), t(G), L, n=200, m=200, batch=64, kernel=_lib.KERNEL_PANEL)
+        z = torch.zeros(64, 200, device=dev)
+        y = torch.zeros(64, 200, device=dev)
+        dM, dg = t(M), t(g)
+        s.set_option("debug_drop_handoff", 1)
+        s.run(z, y, dM, dg, 20, 0.0, stats=False)          # faulty, asynchronous
+        s.set_option("debug_drop_handoff", 0)
+        s.run(z.zero_(), y.zero_(), dM, dg, 20, 0.0, stats=False)  # clean, queued behind it
+        with pytest.raises(_lib.GpadError) as ei:
+            s.sync()
+        assert ei.value.code == _lib.ERR_DEVICE
+        s.sync()  # reported once
+        st = s.run(z.zero_(), y.zero_(), dM, dg, 20, 0.0)
+        assert st["kernel"] == "panel"
+
+
+@pytest.mark.parametrize("bad", [np.nan, np.inf])
+def test_nonfinite_g_is_flagged(gpu, bad):
+    """max |g| of the certification floor keeps a NaN / infinity of g (panel pairs fold
+    it into their loads, every other path runs the absmax kernel): the stats flag it."""
+    import gpad_mpc
+    for batch in (8, 4400):  # resident kernel + absmax launch; panel pairs' folded max
+        ML, G, L, M, g = _shard(batch)
+        g[batch // 2, 7] = bad
+        with gpad_mpc.GpadSolver(0) as s:
+            s.setup(ML, G, L, n=200, m=200, batch=batch)
+            z = np.zeros((batch, 200), np.float32)
+            y = np.zeros((batch, 200), np.float32)
+            st = s.run(z, y, M, g, 60, 1e-4)
+        assert st["nonfinite_g"] and st["below_tol_floor"], (batch, st)
+        assert (np.isnan(st["tol_floor"]) if np.isnan(bad) else np.isinf(st["tol_floor"])), st
+
+
 def test_dropped_handoff_fails_host_memory_run(gpu):
     """Host-memory runs synchronise inside gpad_run: the error comes back from gpad_run itself,
     with or without a stats struct."""

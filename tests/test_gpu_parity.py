@@ -475,11 +475,14 @@ def test_error_paths(gpu):
         s.run(np.zeros(300, np.float32), np.zeros(300, np.float32), np.zeros(300, np.float32),
               np.zeros(300, np.float32), 10, 0.0)
     assert e.value.code == _lib.ERR_UNSUPPORTED
-    for name, bad in (("condensed_panel", 2), ("lpt", 2), (99, 1)) + tuple((r, 0) for r in _lib.OPT_RETIRED):
+    for name, bad in (("lpt", 2), (99, 1)) + tuple((r, 0) for r in _lib.OPT_RETIRED):
         with pytest.raises(gpad_mpc.GpadError) as e:  # out of range / unknown / retired
             s.set_option(name, bad)
         assert e.value.code == _lib.ERR_INVALID
-    s.set_option("condensed_panel", _lib.OPT_DEFAULT)
+    s.set_option("lpt", _lib.OPT_DEFAULT)
+    with pytest.raises(gpad_mpc.GpadError) as e:  # the removed condensed operator (0.4)
+        s.setup(np.zeros((8, 8), np.float32), np.zeros((8, 8), np.float32), 1.0, n=8, m=8, kernel=5)
+    assert e.value.code == _lib.ERR_INVALID
     s.close()
 
 

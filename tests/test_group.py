@@ -29,7 +29,7 @@ def _qp(n, m, B, seed, shared=True):
     return ML, f(qp.M).reshape(B, n), G, f(qp.g).reshape(B, m), np.float32(qp.L)
 
 
-def _single(ML, M, G, g, L, N, tol, shared):
+def _single(ML, M, G, g, L, N, tol, shared, codes=None):
     import gpad_mpc
     B, n = M.shape
     m = g.shape[1]
@@ -38,7 +38,7 @@ def _single(ML, M, G, g, L, N, tol, shared):
     it = np.zeros(B, np.int32)
     with gpad_mpc.GpadSolver(0) as s:
         s.setup(ML, G, float(L), n=n, m=m, batch=B, shared=shared)
-        s.run(z, y, M, g, N, tol, iters=it)
+        s.run(z, y, M, g, N, tol, iters=it, codes=codes)
     return z, y, it
 
 
@@ -52,22 +52,26 @@ def test_group_shards_equal_single_handle(gpu, devices, transport, memory, share
     import gpad_mpc
     n, m = 40, 72
     ML, M, G, g, L = _qp(n, m, B, seed=B + 3, shared=shared)
-    zr, yr, itr = _single(ML, M, G, g, L, N, tol, shared)
+    cr = np.full(B, -1, np.int32)
+    zr, yr, itr = _single(ML, M, G, g, L, N, tol, shared, codes=cr)
     Z = np.zeros((B, n), np.float32)
     Y = np.zeros((B, m), np.float32)
     it = np.zeros(B, np.int32)
+    codes = np.full(B, -1, np.int32)  # the group forwards st->codes to every shard
     with gpad_mpc.GpadGroup(devices) as grp:
         assert grp.transport == transport
         if memory == "device":
             t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)  # noqa: E731
             dZ, dY = t(Z), t(Y)
             grp.setup(t(ML), t(G), float(L), n=n, m=m, batch=B, shared=shared)
-            st = grp.run(dZ, dY, t(M), t(g), N, tol, iters=it)
+            st = grp.run(dZ, dY, t(M), t(g), N, tol, iters=it, codes=codes)
             Z, Y = dZ.cpu().numpy(), dY.cpu().numpy()
         else:
             grp.setup(ML, G, float(L), n=n, m=m, batch=B, shared=shared)
-            st = grp.run(Z, Y, M, g, N, tol, iters=it)
+            st = grp.run(Z, Y, M, g, N, tol, iters=it, codes=codes)
     np.testing.assert_array_equal(it, itr)
+    np.testing.assert_array_equal(codes, cr)
+    assert (cr >= 0).all() and ((cr > 0).sum() == st["converged"])
     np.testing.assert_array_equal(Z, zr)
     np.testing.assert_array_equal(Y, yr)
     assert st["total_iterations"] == int(itr.sum()) and st["iterations"] == int(itr.max())

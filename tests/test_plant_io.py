@@ -168,7 +168,17 @@ def test_closed_loop_bitexact(gpu, oracle, batch, warm, tol, kernel):
     XS = np.zeros((steps, batch, 3), np.float32)
     US = np.zeros((steps, batch, 3), np.float32)
     IT = np.zeros(steps * batch, np.int32)
-    st = s.closed_loop(X, Z, Y, steps, N, tol, warm=warm, xs=XS, us=US, iters=IT)
+    # codes are [steps][batch] like iters (a [batch]-sized array overflowed); a guard
+    # tail past steps * batch must stay untouched
+    CD = np.full(steps * batch + 16, -7, np.int32)
+    st = s.closed_loop(X, Z, Y, steps, N, tol, warm=warm, xs=XS, us=US, iters=IT, codes=CD)
+    assert (CD[steps * batch:] == -7).all()
+    CD = CD[:steps * batch].reshape(steps, batch)
+    assert ((CD > 0).sum() == st["converged"]) and (CD >= 0).all()
+    if tol <= 0:
+        assert (CD == 0).all()
+    else:  # converged exactly where the step stopped before N
+        np.testing.assert_array_equal(CD > 0, IT.reshape(steps, batch) < N)
     IT = IT.reshape(steps, batch)
     L = np.float32(qp.L)
     MGneg, GL, _ = oracle.scale(F32(qp.ML), F32(qp.G), F32(qp.g), L)
