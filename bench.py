@@ -29,6 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "gpu-dualgradient-mpc_amd"))
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X dense fp32 (VALU = f32 MFMA rate), MI355X_MICROARCH.md
+FP64_MFMA_PEAK_TFLOPS = 78.6  # MI355X f64 matrix (spec; measured 70 TF/s back-to-back, profiles/r04_mfma_f64.txt)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -386,6 +387,64 @@ def c4_global_leg(dev, n=200, m=200, batch=65536, steps=6, warmup=2, max_iters=5
                      what=f"C4 instances (pool of {k}, shared ML/G), N = mean GPU iterations to eps")
         c["qp_solves_per_s"] = c["value"] / N
         out["cpu_baseline"] = c
+    return out
+
+
+def f64_value_leg(dev, n=200, m=200, batch=8192, tol=1e-6, max_iters=20000, ref=None):
+    """The reference's own termination regime (acceldualgrad.m:12-13: e_g = e_V = 1e-6, below the
+    f32 certification floor, so f64) with the QP Hessian bound -- Algorithm 1's value-function
+    branches (:73, :76) evaluated -- on C4-shaped value problems (n = m = 200 sharing H, ML, G;
+    constraints active at optima with positive objective values: tests/test_value.py's generator):
+    the f64 MFMA panels (gpad_panel64.hip) beside the one-instance-per-workgroup f64 stream kernel
+    on the same batch (bit-identical results, tests/test_panel64.py).  CPU: the oracle's fp64
+    restatement of acceldualgrad.m (the reference's f64 path is MATLAB, not runnable here)."""
+    import torch
+
+    import gpad_mpc
+    from gpad_mpc import _lib
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_value import value_problem
+    H, ML, M, G, g, L, _ = value_problem(n, m, 7, 1.0, batch=batch)
+    f64 = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float64)).to(dev)  # noqa: E731
+    dH, dML, dG, dM, dg = f64(H), f64(ML), f64(G), f64(M), f64(g)
+    out = {"config": f"{batch} value problems sharing H, ML, G, n={n}, m={m}, f64, e_g = e_V = {tol}, "
+                     "H bound (value-function branches)"}
+    for name, kern in (("panel64", _lib.KERNEL_PANEL), ("stream", _lib.KERNEL_STREAM)):
+        z = torch.zeros(batch, n, dtype=torch.float64, device=dev)
+        y = torch.zeros(batch, m, dtype=torch.float64, device=dev)
+        codes = np.zeros(batch, np.int32)
+        with gpad_mpc.GpadSolver(dev.index or 0, stream=torch.cuda.current_stream(dev).cuda_stream) as s:
+            s.setup(dML, dG, float(L), n=n, m=m, batch=batch, shared=True, check_every=10, kernel=kern,
+                    tol_gap=tol)
+            s.setup_hessian(dH)
+            best, st = 1e30, None
+            for _ in range(2 if name == "panel64" else 1):
+                r = s.run(z.zero_(), y.zero_(), dM, dg, max_iters, tol, codes=codes)
+                if r["kernel_ms"] < best:
+                    best, st = r["kernel_ms"], r
+        out[name] = {"kernel": st["kernel"], "iters_per_s": st["total_iterations"] / (best / 1e3),
+                     "qp_solves_per_s": batch / (best / 1e3), "solve_ms": best,
+                     "mean_iters_to_eps": st["total_iterations"] / batch, "converged": st["converged"],
+                     "codes": {str(k): int((codes == k).sum()) for k in range(5) if (codes == k).any()}}
+    out["speedup_vs_stream"] = out["panel64"]["iters_per_s"] / out["stream"]["iters_per_s"]
+    achieved = out["panel64"]["iters_per_s"] * 4.0 * n * m / 1e12
+    out["roofline"] = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                       "frac": achieved / FP64_MFMA_PEAK_TFLOPS,
+                       "note": "4nm flop per instance-iteration (the two mat-vecs); peak = f64 MFMA spec"}
+    if ref is not None:  # the oracle's fp64 solve (acceldualgrad.m order) on a bounded sample, one thread
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle
+        O = pyoracle.Oracle()
+        t0, its, k = time.perf_counter(), 0, 0
+        while time.perf_counter() - t0 < 3.0 and k < batch:
+            _, _, it, _ = O.solve_value_f64(np.zeros(n), np.zeros(m), ML, M[k], G, g[k], H, max_iters, L, tol,
+                                            tol_gap=tol)
+            its += it
+            k += 1
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": its / dt, "unit": "GPAD iterations/s", "cores": 1, "kind": "port",
+                               "sample": f"{k} instances to e_g = e_V = {tol} (value branches), fp64 oracle "
+                                         "(acceldualgrad.m order), one thread", "seconds": round(dt, 3)}
     return out
 
 
@@ -819,6 +878,7 @@ def main():
             extra["distinct_c2_batch"] = distinct_leg(dev, n, m, ref=ref)
             extra["c3_batch4096"] = c3_leg(dev, n, m, ref=ref)
             extra["c4_global_1gpu"] = c4_global_leg(dev, n, m, ref=ref)
+            extra["f64_value_c4"] = f64_value_leg(dev, n, m, ref=ref)
             extra["closed_loop_battery"] = closed_loop_leg(dev, cpu=not args.no_cpu)
             extra["closed_loop_battery_flat"] = closed_loop_leg(dev, cpu=False, flat=True)
             extra["flat_battery_c1"] = flat_leg(dev, ref=ref)

@@ -125,6 +125,11 @@ struct gpad_handle_s {
     DevBuf GLx;  // flat path: flat G_L expanded to the full k-major image (flat resident kernel)
     DevBuf Hq;           // gpad_setup_hessian: H, k-major [n][ldn] per matrix (value-function branches)
     bool hess_ok = false;
+    DevBuf frag64;       // f64 panels (gpad_panel64.hip): -ML | G_L fragment images, shared f64 matrices
+    bool frag64_ok = false;
+    int frag64_tiles = 0;
+    DevBuf hfrag64;      // ... and H's, bound by gpad_setup_hessian (value branches on the f64 panels)
+    bool hfrag64_ok = false;
     int frag_tiles = 0;
     DevBuf theta, beta;
     int sched_len = 0, sched_kind = -1, sched_dtype = -1;
@@ -267,6 +272,8 @@ int gpad_destroy(gpad_handle_t h) {
     h->GLt.release();
     h->GLx.release();
     h->Hq.release();
+    h->frag64.release();
+    h->hfrag64.release();
     h->frag.release();
     h->stage.release();
     h->theta.release();
@@ -372,6 +379,8 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
     h->flat = false;
     h->shadow_ok = false;
     h->hess_ok = false;
+    h->frag64_ok = false;
+    h->hfrag64_ok = false;
     h->plan.nph = 0;
     h->flat_vpred = 0;
     h->plan_pending = false;
@@ -415,6 +424,16 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
     }
     // fragment image for the MFMA panel kernel (shared f32 matrices only); the buffer is kept
     // across setups and only grows
+    // f64 panels: -ML | G_L in the f64 MFMA fragment layout (gpad_panel64.hip)
+    if (d->shared && d->dtype == GPAD_DTYPE_F64 && gpad::panel64_supported(n, m)) {
+        const int T = gpad::panel64_tiles(n, m);
+        const size_t ob = gpad::panel64_frag_bytes(n, m);
+        if ((rc = h->frag64.ensure(2 * ob))) return rc;
+        HIP_TRY(gpad::launch_pack_panel64((const double*)dA, n, m, sa, T, h->frag64.p, h->stream));
+        HIP_TRY(gpad::launch_pack_panel64((const double*)dB, m, n, sb, T, (char*)h->frag64.p + ob, h->stream));
+        h->frag64_tiles = T;
+        h->frag64_ok = true;
+    }
     h->frag_ok = false;
     h->frag_tiles = 0;
     if (d->shared && d->dtype == GPAD_DTYPE_F32) {
@@ -447,6 +466,7 @@ int gpad_setup_hessian(gpad_handle_t h, const void* H) {
     if (!h->ready) return fail(GPAD_ERR_NOT_SETUP, "gpad_setup_hessian: call gpad_setup first");
     if (h->flat) return fail(GPAD_ERR_UNSUPPORTED, "gpad_setup_hessian: not on the flat battery path");
     h->hess_ok = false;
+    h->hfrag64_ok = false;
     if (!H) return GPAD_OK;
     HIP_TRY(hipSetDevice(h->device));
     const gpad_dims_t& d = h->dims;
@@ -468,6 +488,11 @@ int gpad_setup_hessian(gpad_handle_t h, const void* H) {
     else
         HIP_TRY(gpad::launch_pack_kmajor<double>((const double*)dH, (double*)h->Hq.p, n, n, h->ldn, 1.0, nmats,
                                                  in_stride, out_stride, h->stream));
+    if (h->frag64_ok) {  // shared f64: H for the f64 panels' value branches
+        if ((rc = h->hfrag64.ensure(gpad::panel64_frag_bytes(n, d.m)))) return rc;
+        HIP_TRY(gpad::launch_pack_panel64((const double*)dH, n, n, 1.0, h->frag64_tiles, h->hfrag64.p, h->stream));
+        h->hfrag64_ok = true;
+    }
     HIP_TRY(hipStreamSynchronize(h->stream));
     h->hess_ok = true;
     return GPAD_OK;
@@ -780,9 +805,25 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
         *kernel_out = d.kernel == GPAD_KERNEL_AUTO ? GPAD_KERNEL_STREAM : d.kernel;
         return finish(GPAD_OK);
     }
-    if (a.Hq) {  // value-function branches: evaluated by the stream kernel family only
+    if constexpr (sizeof(T) == sizeof(double)) {
+        // f64 panels on the f64 MFMA pipe (shared matrices, n, m <= 256; value branches included):
+        // forced, or from one panel per CU on (below that the one-instance-per-workgroup stream
+        // kernel has the shorter iteration)
+        if (h->frag64_ok && (kernel == GPAD_KERNEL_PANEL || (kernel == GPAD_KERNEL_AUTO && batch >= 16 * h->num_cus))) {
+            a.frag = h->frag64.p;
+            a.frag_tiles = h->frag64_tiles;
+            a.hfrag64 = (a.Hq && h->hfrag64_ok) ? h->hfrag64.p : nullptr;
+            a.Hq = nullptr;
+            e = gpad::launch_panel64(a, h->stream);
+            if (e != hipSuccess) return fail(GPAD_ERR_HIP, hip_detail("f64 panel", e));
+            *kernel_out = GPAD_KERNEL_PANEL;
+            return finish(GPAD_OK);
+        }
+    }
+    if (a.Hq) {  // value-function branches: the stream kernel family (and the f64 panels, above)
         if (kernel != GPAD_KERNEL_AUTO && kernel != GPAD_KERNEL_STREAM)
-            return fail(GPAD_ERR_UNSUPPORTED, "the value-function test (gpad_setup_hessian) runs on the stream kernel");
+            return fail(GPAD_ERR_UNSUPPORTED, "the value-function test (gpad_setup_hessian) runs on the stream kernel "
+                                              "(f32) or the stream / f64 panel kernels (f64)");
         kernel = GPAD_KERNEL_STREAM;
     }
     if constexpr (sizeof(T) == sizeof(float)) {
@@ -846,7 +887,8 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
         }
     } else {
         if (kernel == GPAD_KERNEL_PANEL || kernel == GPAD_KERNEL_RESIDENT)
-            return fail(GPAD_ERR_UNSUPPORTED, "f64 runs on the stream kernel only");
+            return fail(GPAD_ERR_UNSUPPORTED, "f64: the resident kernel is f32 only; the f64 panels need shared "
+                                              "matrices with n, m <= 256");
     }
     if (!ok) {
         kernel = GPAD_KERNEL_STREAM;

@@ -111,6 +111,8 @@ struct SolveArgs {
     const T* Hq;           // QP Hessian H, k-major [n][ldn] (gpad_setup_hessian), or null: enables the
                            // value-function branches of the test (stream kernel only)
     long long strideHq;    // elements between consecutive instances' H images (0 = shared)
+    const void* hfrag64;   // f64 panels (gpad_panel64.hip): H in their fragment layout, or null (no value
+                           // branches)
     int* err;              // device error word (kDevErr* bits), never null on a solve launch
     int debug;             // kDebug* fault-injection bits (tests only)
 };
@@ -125,6 +127,14 @@ hipError_t launch_resident(const SolveArgs<float>& a, hipStream_t s, bool* suppo
 hipError_t launch_duo(const SolveArgs<float>& a, int grid, hipStream_t s);
 bool resident_supported(int n, int m);
 hipError_t launch_panel(const SolveArgs<float>& a, hipStream_t s, bool* supported);
+// f64 panels on the f64 MFMA pipe (gpad_panel64.hip): shared matrices, n, m <= 256, one panel of 16
+// instances per workgroup, value-function branches when a.hfrag64 is set; a.frag = the -ML | G_L
+// images of launch_pack_panel64, a.frag_tiles = panel64_tiles(n, m)
+bool panel64_supported(int n, int m);
+int panel64_tiles(int n, int m);
+size_t panel64_frag_bytes(int n, int m);  // one T x T operand image
+hipError_t launch_pack_panel64(const double* src, int rows, int cols, double scale, int T, void* dst, hipStream_t s);
+hipError_t launch_panel64(const SolveArgs<double>& a, hipStream_t s);
 // launch_panel at (n, m) runs the panel pairs, which fold max |g| into their loads (gmax_part)
 bool panel_folds_gmax(int n, int m);
 

@@ -1,0 +1,415 @@
+// gpad_panel64.hip -- shared-matrix f64 batches on the f64 MFMA pipe (gfx950), with the
+// value-function branches of Algorithm 1.
+//
+// The reference's own termination regime (acceldualgrad.m:12-13: e_g = e_V = 1e-6) lies below the
+// f32 certification floor (include/gpad.h gpad_run), so it needs f64; with the QP Hessian bound
+// (gpad_setup_hessian) the test also evaluates valuefcn / dualfcn (acceldualgrad.m:30-33, 73, 76).
+// Until round 4 only the one-workgroup-per-instance stream kernel ran f64, streaming the shared
+// matrices from L2 for every instance.  Here a workgroup owns a panel of 16 instances and wave t
+// owns row tile t of both GEMMs, as gpad_panel_kernel does in f32:
+//   Zhat[n x 16] = (-ML) W[m x 16],   C[m x 16] = G_L Zhat[n x 16]
+// on v_mfma_f64_16x16x4_f64, whose result is bitwise the ascending-k fma chain
+// (profiles/r04_mfma_f64.txt: 0 of 256 outputs differ over K = 200) -- so every chain here is the
+// f64 stream kernel's chain4 (fma, ascending k), and the epilogues are its epilogues: z, y, w, u and
+// the iteration counts equal the stream kernel's bit for bit, and the fp64 oracle's
+// (orc_solve_value_f64, acceldualgrad.m's mul/add order) to rounding (tests/test_panel64.py).
+//
+// Layouts (f64 16x16x4: lane l supplies A[l&15][k = l>>4] and B[k = l>>4][l&15], accumulator
+// register r holds D[(l>>4) + 4r][l&15]):
+//   PA[b][t][lane][q] = M[16t + (lane&15)][16b + 4q + (lane>>4)]   (4 doubles = 32 B per lane)
+// so accumulator register q of lane l in wave t is row 16t + 4q + (l>>4): exactly the B operand of
+// k-step q of k-block t of the next GEMM.  No row permutation is needed (the f32 kernels need one,
+// their accumulator layout is row 4(l>>4) + r).  Vectors cross between the GEMMs through LDS in
+// that fragment order, [tile][lane][4] doubles; each lane keeps its own rows' z, y, u, g_P, p_D in
+// registers.  Images: -ML, G_L and (value branches) H, each T x T tiles of 2 KiB.
+//
+// Value branches, per column, where the MATLAB test reaches them (test (B)'s violation part passed,
+// the rest of (B) did not): V(zhat) from one H-GEMM over the panel; for columns with w not >= 0
+// also D(y+) = V(z(y+)) + L y+'(G_L z(y+) + p_D), z(y+) = -ML y+ - M: three more GEMMs.  Sums over
+// rows are fp64 trees (lane rows, lane groups, tiles) -- the stream kernel sums in another tree
+// order, the oracle sequentially (the same values to ~1e-16 relative).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "gpad_internal.h"
+
+namespace gpad {
+
+namespace {
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kP64MaxTiles = 16;  // n, m <= 256 (16 waves)
+
+int p64_tiles(int n, int m) {
+    const int t = ((n > m ? n : m) + 15) / 16;
+    return t <= kP64MaxTiles ? t : 0;
+}
+
+__global__ void pack_panel64_kernel(const double* __restrict__ src, int rows, int cols, double scale, int T,
+                                    double* __restrict__ dst) {
+    // dst[((b*T + t)*64 + lane)*4 + q] for k-block b < T, row tile t < T
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= T * T * 64) return;
+    const int lane = idx & 63, t = (idx >> 6) % T, b = (idx >> 6) / T;
+    const int row = 16 * t + (lane & 15);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int col = 16 * b + 4 * q + (lane >> 4);
+        dst[(size_t)idx * 4 + q] = (row < rows && col < cols) ? scale * src[(size_t)row * cols + col] : 0.0;
+    }
+}
+
+__device__ __forceinline__ f64x4 ld_a(__amdgpu_buffer_rsrc_t PA, int voff, int soff) {
+    const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(PA, voff, soff, 0);
+    const u32x4 hi = __builtin_amdgcn_raw_buffer_load_b128(PA, voff + 16, soff, 0);
+    f64x4 r;
+    r[0] = __hiloint2double((int)lo.y, (int)lo.x);
+    r[1] = __hiloint2double((int)lo.w, (int)lo.z);
+    r[2] = __hiloint2double((int)hi.y, (int)hi.x);
+    r[3] = __hiloint2double((int)hi.w, (int)hi.z);
+    return r;
+}
+
+// acc = A[tile t] x B over k-blocks [0, nkb) (ascending k: the fma chain), A streamed from L2 one
+// block ahead, B (fragment order) from LDS one block ahead.  Zero-padded k-steps add +0 only.
+template <int T>
+__device__ __forceinline__ f64x4 gemm64(__amdgpu_buffer_rsrc_t PA, const f64x4* __restrict__ Bl, int voff, int lane,
+                                        int nkb) {
+    f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+    f64x4 a[2], b[2];
+    a[0] = ld_a(PA, voff, 0);
+    b[0] = Bl[lane];
+#pragma unroll
+    for (int kb = 0; kb < T; ++kb) {
+        const int cur = kb & 1, nxt = cur ^ 1;
+        if (kb < nkb) {  // uniform (nkb < T only when n != m)
+            if (kb + 1 < nkb) {
+                a[nxt] = ld_a(PA, voff, (kb + 1) * T * 2048);
+                b[nxt] = Bl[(kb + 1) * 64 + lane];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[cur][0], b[cur][0], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[cur][1], b[cur][1], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[cur][2], b[cur][2], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[cur][3], b[cur][3], acc, 0, 0, 0);
+            asm volatile("" ::: "memory");
+        }
+    }
+    return acc;
+}
+
+struct P64Slot {  // per tile and column: the test partials / the value-function sums
+    double violz[16], violh[16], wmin[16], gap[16], magh[16];
+};
+
+// max / min / sum of this lane's 4 rows over the 4 lane groups of its column (xor 16, 32)
+__device__ __forceinline__ double col_max(double v) {
+    v = fmax(v, __shfl_xor(v, 16, 64));
+    return fmax(v, __shfl_xor(v, 32, 64));
+}
+__device__ __forceinline__ double col_min(double v) {
+    v = fmin(v, __shfl_xor(v, 16, 64));
+    return fmin(v, __shfl_xor(v, 32, 64));
+}
+__device__ __forceinline__ double col_sum(double v) {
+    v += __shfl_xor(v, 16, 64);
+    return v + __shfl_xor(v, 32, 64);
+}
+
+}  // namespace
+
+template <int T>
+__global__ __launch_bounds__(64 * T) void gpad_panel64_kernel(SolveArgs<double> a) {
+    __shared__ f64x4 Wl[T * 64];  // w    (B of GEMM 1), fragment order
+    __shared__ f64x4 Zh[T * 64];  // zhat (B of GEMM 2)
+    __shared__ f64x4 Xv[T * 64];  // z for the (A) verification; the value branches' operands
+    __shared__ f64x4 Gp[T * 64];  // g_P of this lane's rows (in LDS: registers are the limit)
+    __shared__ P64Slot slots[T];
+    __shared__ double vsum[2][T][16];  // value branches: per tile and column, V / dual sums
+
+    const int lane = threadIdx.x & 63;
+    const int t = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int j = lane >> 4, c = lane & 15;
+    const int n = a.n, m = a.m, N = a.N, K = a.check_every;
+    const int nkb1 = (m + 15) / 16, nkb2 = (n + 15) / 16;  // k-blocks of GEMM 1 (K = m), GEMM 2 / H (K = n)
+    const bool on1 = 16 * t < n, on2 = 16 * t < m;         // this tile has output rows in GEMM 1 / 2
+    const int abytes = T * T * 2048;
+    const __amdgpu_buffer_rsrc_t PA1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.frag), 0, abytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t PA2 =
+        __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)a.frag + abytes), 0, abytes, 0x00020000);
+    const bool value = a.hfrag64 != nullptr && a.tol > 0.0;
+    const __amdgpu_buffer_rsrc_t PH =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(value ? a.hfrag64 : a.frag), 0, abytes, 0x00020000);
+    const int voff = t * 2048 + lane * 32;
+    const int slot = t * 64 + lane;
+    const bool use_tol = a.tol > 0.0;
+    const double eV = a.tol_gap;
+    const int panels = (a.batch + 15) / 16;
+
+    for (int p = blockIdx.x; p < panels; p += gridDim.x) {
+        const int inst = 16 * p + c;
+        bool active = inst < a.batch;
+        // register r <-> row 16t + 4r + j of the column's instance
+        double z[4], y[4], u[4], pd[4];
+        {
+            f64x4 w, gp;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 * t + 4 * r + j;
+                const bool okn = active && i < n, okm = active && i < m;
+                z[r] = okn ? a.z[(size_t)inst * n + i] : 0.0;
+                gp[r] = okn ? a.gP[(size_t)inst * a.ld_gP + i] : 0.0;
+                y[r] = okm ? a.y[(size_t)inst * m + i] : 0.0;
+                pd[r] = okm ? a.gscale * a.g[(size_t)inst * a.ld_g + i] : 0.0;
+                w[r] = __builtin_fma(a.beta[0], y[r] - y[r], y[r]);  // 8a with y_0 = y_{-1}
+                u[r] = 0.0;
+            }
+            Wl[slot] = w;
+            Gp[slot] = gp;
+            Xv[slot] = f64x4{z[0], z[1], z[2], z[3]};
+        }
+        __syncthreads();
+        if (use_tol && on2) {  // u = G_L z_{-1}, then the 8c recursion
+            const f64x4 cz = gemm64<T>(PA2, Xv, voff, lane, nkb2);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) u[r] = cz[r];
+        }
+        __syncthreads();
+
+        int v = 0;
+        while (true) {
+            const double th = a.theta[v], bn = a.beta[v + 1];
+            ++v;
+            const bool chk = use_tol && (v % K) == 0;
+            const double omt = 1.0 - th;
+            // ---- GEMM 1 + epilogue: zhat = -ML w - g_P (8b), z = (1-th) z + th zhat (8c) ----
+            {
+                const f64x4 acc = on1 ? gemm64<T>(PA1, Wl, voff, lane, nkb1) : f64x4{0.0, 0.0, 0.0, 0.0};
+                const f64x4 gp = Gp[slot];
+                f64x4 zh;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    zh[r] = acc[r] - gp[r];
+                    const double zn = __builtin_fma(omt, z[r], th * zh[r]);
+                    if (active) z[r] = zn;
+                }
+                Zh[slot] = zh;
+            }
+            __syncthreads();
+            // ---- GEMM 2 + epilogue: y+ = [w + G_L zhat + p_D]+ (8d), next w (8a), test partials ----
+            double violz = -INFINITY, violh = -INFINITY, wmin = INFINITY, magh = 0.0, gap = 0.0;
+            {
+                const f64x4 acc = on2 ? gemm64<T>(PA2, Zh, voff, lane, nkb2) : f64x4{0.0, 0.0, 0.0, 0.0};
+                const f64x4 wv = Wl[slot];
+                f64x4 wn;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const double cv = acc[r];
+                    const double sv = (wv[r] + pd[r]) + cv;  // seq_functions.cpp:84
+                    const double yp = (fabs(sv) + sv) * 0.5;  // seq_functions.cpp:85
+                    wn[r] = __builtin_fma(bn, yp - y[r], yp);
+                    if (use_tol) {
+                        const double un = __builtin_fma(omt, u[r], th * cv);
+                        if (active) u[r] = un;
+                        if (chk && active && (16 * t + 4 * r + j) < m) {
+                            const double tt = cv + pd[r];
+                            violh = fmax(violh, tt);
+                            magh = fmax(magh, fabs(cv) + fabs(pd[r]));
+                            wmin = fmin(wmin, wv[r]);
+                            gap -= wv[r] * tt;
+                            violz = fmax(violz, u[r] + pd[r]);
+                        }
+                    }
+                    if (active) y[r] = yp;
+                }
+                if (active) Wl[slot] = wn;  // (GEMM 2 reads Zh; the next GEMM 1 reads w after the barrier)
+            }
+            if (chk) {
+                violz = col_max(violz);
+                violh = col_max(violh);
+                magh = col_max(magh);
+                wmin = col_min(wmin);
+                gap = col_sum(gap);
+                if (j == 0) {
+                    slots[t].violz[c] = violz;
+                    slots[t].violh[c] = violh;
+                    slots[t].magh[c] = magh;
+                    slots[t].wmin[c] = wmin;
+                    slots[t].gap[c] = gap;
+                }
+            }
+            __syncthreads();
+            if (!chk && v < N) continue;
+
+            // ---- Algorithm 1, per column (lane c's column; every wave reads every tile) ----------
+            int code = 0;
+            if (chk) {
+                int st1 = 0;
+                bool vh_ok = false, w_ok = false;
+                double gq = 0.0;
+                if (active) {
+                    double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, mh = 0.0;
+#pragma unroll
+                    for (int s2 = 0; s2 < T; ++s2) {
+                        vz = fmax(vz, slots[s2].violz[c]);
+                        vh = fmax(vh, slots[s2].violh[c]);
+                        mh = fmax(mh, slots[s2].magh[c]);
+                        wm = fmin(wm, slots[s2].wmin[c]);
+                        gq += slots[s2].gap[c];
+                    }
+                    vh_ok = viol_ok(vh, mh, a.L, a.tol, ViolMargin<double>::value);
+                    w_ok = wm >= 0.0;
+                    st1 = (vz * a.L <= a.tol ? 1 : 0) | ((vh_ok && w_ok && (gq * a.L <= a.tol_gap)) ? 2 : 0);
+                }
+                bool verified = false;
+                if (__syncthreads_or(st1 & 1)) {  // (A) nominated somewhere: G_L z for the panel
+                    Xv[slot] = f64x4{z[0], z[1], z[2], z[3]};
+                    __syncthreads();
+                    const f64x4 cz = on2 ? gemm64<T>(PA2, Xv, voff, lane, nkb2) : f64x4{0.0, 0.0, 0.0, 0.0};
+                    double vc = -INFINITY, mc = 0.0;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        if ((st1 & 1) && (16 * t + 4 * r + j) < m) {
+                            u[r] = cz[r];  // the recursion restarts from the direct value
+                            vc = fmax(vc, cz[r] + pd[r]);
+                            mc = fmax(mc, fabs(cz[r]) + fabs(pd[r]));
+                        }
+                    }
+                    vc = col_max(vc);
+                    mc = col_max(mc);
+                    if (j == 0) {  // every wave read the stage-1 slots before the barrier above
+                        slots[t].violz[c] = vc;
+                        slots[t].magh[c] = mc;
+                    }
+                    __syncthreads();
+                    if (st1 & 1) {
+                        double vcc = -INFINITY, mcc = 0.0;
+#pragma unroll
+                        for (int s2 = 0; s2 < T; ++s2) {
+                            vcc = fmax(vcc, slots[s2].violz[c]);
+                            mcc = fmax(mcc, slots[s2].magh[c]);
+                        }
+                        verified = viol_ok(vcc, mcc, a.L, a.tol, ViolMargin<double>::value);
+                    }
+                }
+                code = ((st1 & 1) && verified) ? 1 : ((st1 & 2) ? 2 : 0);
+                // value-function branches (acceldualgrad.m:73, 76) where the MATLAB test reaches them
+                const bool need = value && active && code == 0 && vh_ok;
+                if (value && __syncthreads_or(need)) {
+                    // V(zhat) = sum_i (zhat_i / 2 + M_i) (H zhat)_i  (zhat: this iteration's, in Zh)
+                    const f64x4 gp = Gp[slot], zk = Zh[slot];
+                    double vp = 0.0;
+                    if (on1) {
+                        const f64x4 hx = gemm64<T>(PH, Zh, voff, lane, nkb2);
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            if (16 * t + 4 * r + j < n) vp += (0.5 * zk[r] + gp[r]) * hx[r];
+                    }
+                    vp = col_sum(vp);
+                    if (j == 0) vsum[0][t][c] = vp;
+                    __syncthreads();
+                    double V = 0.0;
+#pragma unroll
+                    for (int s2 = 0; s2 < T; ++s2) V += vsum[0][s2][c];
+                    if (need && w_ok) code = gq * a.L <= V * eV / (1.0 + eV) ? 3 : 0;  // :73
+                    const bool needd = need && !w_ok;
+                    if (__syncthreads_or(needd)) {
+                        // z(y+) = -ML y+ - M (GEMM 1 on y+), then V(z(y+)) and y+'(G_L z(y+) + p_D)
+                        // (the barrier of the vote: Xv is free, every (A) verification GEMM is done)
+                        Xv[slot] = f64x4{y[0], y[1], y[2], y[3]};
+                        __syncthreads();
+                        f64x4 zp = {0.0, 0.0, 0.0, 0.0};
+                        if (on1) {
+                            const f64x4 acc = gemm64<T>(PA1, Xv, voff, lane, nkb1);
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) zp[r] = acc[r] - gp[r];
+                        }
+                        __syncthreads();
+                        Xv[slot] = zp;
+                        __syncthreads();
+                        double vq = 0.0, lin = 0.0;
+                        if (on1) {
+                            const f64x4 hx = gemm64<T>(PH, Xv, voff, lane, nkb2);
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+                                if (16 * t + 4 * r + j < n) vq += (0.5 * zp[r] + gp[r]) * hx[r];
+                        }
+                        if (on2) {
+                            const f64x4 cc = gemm64<T>(PA2, Xv, voff, lane, nkb2);
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+                                if (16 * t + 4 * r + j < m) lin += y[r] * (cc[r] + pd[r]);
+                        }
+                        vq = col_sum(vq);
+                        lin = col_sum(lin);
+                        if (j == 0) {
+                            vsum[0][t][c] = vq;
+                            vsum[1][t][c] = lin;
+                        }
+                        __syncthreads();
+                        double Vp = 0.0, ls = 0.0;
+#pragma unroll
+                        for (int s2 = 0; s2 < T; ++s2) {
+                            Vp += vsum[0][s2][c];
+                            ls += vsum[1][s2][c];
+                        }
+                        const double D = Vp + a.L * ls;
+                        if (needd) code = V - D <= eV * (D > 1.0 ? D : 1.0) ? 4 : 0;  // :76
+                    }
+                }
+            }
+            // ---- finished columns: results out (tests (B), (B'), (B'') certify zhat) -----------
+            if (active && (code != 0 || v >= N)) {
+                const f64x4 zk = Zh[slot];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 16 * t + 4 * r + j;
+                    if (i < n) a.z[(size_t)inst * n + i] = code >= 2 ? zk[r] : z[r];
+                    if (i < m) a.y[(size_t)inst * m + i] = y[r];
+                }
+                if (t == 0 && j == 0) {
+                    a.iters[inst] = v;
+                    a.conv[inst] = code;
+                }
+                active = false;
+            }
+            if (!__syncthreads_or(active ? 1 : 0)) break;
+        }
+        __syncthreads();  // the next panel reuses the LDS tiles
+    }
+}
+
+bool panel64_supported(int n, int m) { return p64_tiles(n, m) > 0; }
+int panel64_tiles(int n, int m) { return p64_tiles(n, m); }
+size_t panel64_frag_bytes(int n, int m) {
+    const int T = p64_tiles(n, m);
+    return (size_t)T * T * 2048;  // one operand
+}
+
+hipError_t launch_pack_panel64(const double* src, int rows, int cols, double scale, int T, void* dst, hipStream_t s) {
+    const int tot = T * T * 64;
+    hipLaunchKernelGGL(pack_panel64_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, src, rows, cols, scale, T,
+                       (double*)dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_panel64(const SolveArgs<double>& a, hipStream_t s) {
+    const int T = p64_tiles(a.n, a.m);
+    if (!T || !a.frag || a.frag_tiles != T || a.strideA || a.strideB) return hipErrorInvalidValue;
+    const int panels = (a.batch + 15) / 16;
+    const int grid = panels < a.num_cus ? panels : a.num_cus;
+    switch (T) {
+#define GPAD_P64(TT) \
+    case TT: hipLaunchKernelGGL((gpad_panel64_kernel<TT>), dim3(grid), dim3(64 * TT), 0, s, a); break;
+        GPAD_P64(1) GPAD_P64(2) GPAD_P64(3) GPAD_P64(4) GPAD_P64(5) GPAD_P64(6) GPAD_P64(7) GPAD_P64(8)
+        GPAD_P64(9) GPAD_P64(10) GPAD_P64(11) GPAD_P64(12) GPAD_P64(13) GPAD_P64(14) GPAD_P64(15) GPAD_P64(16)
+#undef GPAD_P64
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace gpad

@@ -1,0 +1,133 @@
+"""f64 panels on the f64 MFMA pipe (csrc/gpad_panel64.hip): shared-matrix f64 batches, with the
+value-function branches of Algorithm 1 (acceldualgrad.m:30-33, 73, 76) when H is bound -- the
+reference's own termination regime e_g = e_V = 1e-6 (acceldualgrad.m:12-13), which lies below the
+f32 certification floor.
+
+Pins: (1) the f64 stream kernel on the same inputs, bit for bit (z, y, iteration counts, codes):
+v_mfma_f64_16x16x4_f64 is the ascending-k fma chain (profiles/r04_mfma_f64.txt) and the epilogues
+are the stream kernel's; (2) the fp64 oracle (orc_solve_value_f64 / orc_solve_f64, the mul/add
+order of acceldualgrad.m): iteration counts and termination codes equal, z within 1e-12.  The
+oracle itself is pinned to a literal restatement of the commented MATLAB test (test_value.py).
+Iteration counts to eps are parity unpinned against the reference, which never runs its test.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from test_value import value_problem
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(ML, G, L, M, g, N, tol, *, kernel, H=None, tol_gap=0.0, K=10, dev=True):
+    import torch
+
+    import gpad_mpc
+    from gpad_mpc import _lib
+    B, n = M.shape
+    m = g.shape[1]
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float64)).cuda()  # noqa: E731
+    z = torch.zeros(B, n, dtype=torch.float64, device="cuda")
+    y = torch.zeros(B, m, dtype=torch.float64, device="cuda")
+    it = np.zeros(B, np.int32)
+    codes = np.full(B, -1, np.int32)
+    kern = {"panel": _lib.KERNEL_PANEL, "stream": _lib.KERNEL_STREAM, "auto": _lib.KERNEL_AUTO}[kernel]
+    with gpad_mpc.GpadSolver(0) as s:
+        s.setup(t(ML), t(G), float(L), n=n, m=m, batch=B, check_every=K, kernel=kern, tol_gap=tol_gap)
+        if H is not None:
+            s.setup_hessian(t(H))
+        st = s.run(z, y, t(M), t(g), N, tol, iters=it, codes=codes)
+    return z.cpu().numpy(), y.cpu().numpy(), it, codes, st
+
+
+@pytest.mark.parametrize("shift,tol,tol_gap,K", [(1.0, 1e-2, 1e-1, 1), (1.0, 1e-3, 1e-2, 1),
+                                                 (3.0, 1e-3, 1e-2, 10), (3.0, 1e-2, 1e-1, 1)])
+def test_panel64_value_branches_small(gpu, oracle, shift, tol, tol_gap, K):
+    """n = 20, m = 40 (T = 3), 64 instances, H bound: the f64 panel equals the f64 stream kernel bit
+    for bit and the fp64 oracle (counts, codes, z to 1e-12); codes 3 / 4 occur in the sweep."""
+    B = 64
+    H, ML, M, G, g, L = (np.asarray(a) for a in value_problem(20, 40, 7, shift, batch=B)[:6])
+    zp, yp, itp, cp, stp = _run(ML, G, L, M, g, 5000, tol, kernel="panel", H=H, tol_gap=tol_gap, K=K)
+    zs, ys, its, cs, sts = _run(ML, G, L, M, g, 5000, tol, kernel="stream", H=H, tol_gap=tol_gap, K=K)
+    assert stp["kernel"] == "panel" and sts["kernel"] == "stream"
+    np.testing.assert_array_equal(itp, its)
+    np.testing.assert_array_equal(cp, cs)
+    np.testing.assert_array_equal(zp, zs)
+    np.testing.assert_array_equal(yp, ys)
+    for b in range(B):
+        zo, yo, ito, co = oracle.solve_value_f64(np.zeros(20), np.zeros(40), ML, M[b], G, g[b], H, 5000, L, tol,
+                                                 check_every=K, tol_gap=tol_gap)
+        assert (itp[b], cp[b]) == (ito, co), b
+        np.testing.assert_allclose(zp[b], zo, rtol=1e-12, atol=1e-14)
+    TestCodes.seen.update(cp.tolist())
+
+
+class TestCodes:
+    seen: set = set()
+
+    def test_value_codes_exercised(self, gpu, oracle):
+        if not self.seen:
+            for case in [(1.0, 1e-2, 1e-1, 1), (3.0, 1e-2, 1e-1, 1)]:
+                test_panel64_value_branches_small(gpu, oracle, *case)
+        assert {3, 4} & self.seen, self.seen
+
+
+def test_panel64_reference_tolerance_c4_shape(gpu, oracle):
+    """C4 shape (n = m = 200, T = 13), the reference's e_g = e_V = 1e-6 with H bound, 512 instances
+    (value problems: constraints active at an optimum with a positive objective): bit-exact with the
+    f64 stream kernel on every instance, and a spread sample equal to the fp64 oracle (counts,
+    codes, z to 1e-12); every instance converged (codes 2 / 3)."""
+    B, tol = 512, 1e-6
+    H, ML, M, G, g, L = (np.asarray(a) for a in value_problem(200, 200, 7, 1.0, batch=B)[:6])
+    zp, yp, itp, cp, stp = _run(ML, G, L, M, g, 20000, tol, kernel="panel", H=H, tol_gap=tol)
+    zs, ys, its, cs, _ = _run(ML, G, L, M, g, 20000, tol, kernel="stream", H=H, tol_gap=tol)
+    assert stp["kernel"] == "panel" and stp["converged"] == B
+    np.testing.assert_array_equal(itp, its)
+    np.testing.assert_array_equal(cp, cs)
+    np.testing.assert_array_equal(zp, zs)
+    np.testing.assert_array_equal(yp, ys)
+    assert 3 in set(cp.tolist())
+    for b in list(range(0, B, 37)) + [int(np.argmax(itp))]:
+        zo, yo, ito, co = oracle.solve_value_f64(np.zeros(200), np.zeros(200), ML, M[b], G, g[b], H, 20000, L, tol,
+                                                 tol_gap=tol)
+        assert (itp[b], cp[b]) == (ito, co), b
+        np.testing.assert_allclose(zp[b], zo, rtol=1e-12, atol=1e-14)
+
+
+@pytest.mark.parametrize("n,m", [(37, 53), (200, 180), (256, 256), (5, 129), (160, 200)])
+def test_panel64_fixed_n_ragged(gpu, n, m):
+    """Fixed N = 60 (no test) and eps = 1e-6 without H on ragged shapes: bit-exact with the f64
+    stream kernel (zero-padded k-steps and skipped tiles)."""
+    from gpad_mpc import problems
+    B = 40
+    qp = problems.synthetic_qp(n, m, batch=B, seed=n + m)
+    ML, G = np.asarray(qp.ML), np.asarray(qp.G)
+    M, g = np.asarray(qp.M).reshape(B, n), np.asarray(qp.g).reshape(B, m)
+    for N, tol in ((60, 0.0), (3000, 1e-6)):
+        a = _run(ML, G, qp.L, M, g, N, tol, kernel="panel")
+        b = _run(ML, G, qp.L, M, g, N, tol, kernel="stream")
+        assert a[4]["kernel"] == "panel"
+        for x, y_ in zip(a[:4], b[:4]):
+            np.testing.assert_array_equal(x, y_)
+
+
+def test_panel64_auto_c4_batch_certified(gpu, oracle):
+    """AUTO picks the f64 panels for a C4-generator batch of 8192 in f64 at eps = 1e-6 (the f32 path's
+    floor is ~2^-20 max|g|): every instance converges with fp64 max(G z* - g) <= eps on the returned
+    z*; a sample and the longest instances equal the fp64 oracle (counts, z to 1e-12)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    n = m = 200
+    B, tol = 8192, 1e-6
+    ML, G, L, M, g = bench.make_shard(n, m, B, 0)
+    z, y, it, codes, st = _run(ML, G, L, M, g, 20000, tol, kernel="auto", tol_gap=tol)
+    assert st["kernel"] == "panel" and st["converged"] == B
+    viol = (z @ G.T - g).max(axis=1)
+    assert viol.max() <= tol, (viol.max(), int(viol.argmax()))
+    for b in list(range(0, B, 1021)) + [int(i) for i in np.argsort(-it, kind="stable")[:4]]:
+        zo, yo, ito, co = oracle.solve_f64(np.zeros(n), np.zeros(m), ML, M[b], G, g[b], 20000, L, tol, tol_gap=tol)
+        assert it[b] == ito and co and codes[b] in (1, 2), b
+        np.testing.assert_allclose(z[b], zo, rtol=1e-12, atol=1e-14)
