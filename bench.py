@@ -222,8 +222,10 @@ def traffic_from_profile(kernel_name):
         solves = 2 * (int(args[args.index("--steps") + 1]) + int(args[args.index("--warmup") + 1]))
     except (ValueError, IndexError):
         return None, None
+    names = kernel_name if isinstance(kernel_name, (list, tuple)) else [kernel_name]
     tot = [v["hbm_bytes_total"] for k, v in d.get("pmc_per_launch", {}).items()
-           if (k == kernel_name or k.startswith(kernel_name[:-1] + ", ")) and "hbm_bytes_total" in v]
+           if any(k == kn or (kn.endswith(">") and k.startswith(kn[:-1] + ", ")) for kn in names)
+           and "hbm_bytes_total" in v]
     if not tot or solves <= 0:
         return None, None
     return sum(tot) / solves, os.path.relpath(path, ROOT)
@@ -835,7 +837,10 @@ def main():
         T = (max(n, m) + 15) // 16
         kname = (f"gpad::gpad_panel2_kernel<{T}>" if T > 8 else f"gpad::gpad_panel_kernel<{T}>") \
             if st["kernel"] == "panel" else f"gpad::gpad_{st['kernel']}_kernel"
-        traffic, traffic_src = traffic_from_profile(kname)
+        # n = m = 200: the pair phases run on the W32 layout (gpad_pair32_kernel), the one-panel
+        # phases on gpad_panel2_kernel -- the solve's panel traffic is both
+        knames = [kname, "gpad::gpad_pair32_kernel"] if (n, m) == (200, 200) and st["kernel"] == "panel" else [kname]
+        traffic, traffic_src = traffic_from_profile(knames)
         launches = util["launches_per_solve"] if st["kernel"] == "panel" else 1
         # single instances (configs C1 and C2): latency kernels, fixed iteration counts
         singles = {}
