@@ -837,10 +837,7 @@ def main():
         T = (max(n, m) + 15) // 16
         kname = (f"gpad::gpad_panel2_kernel<{T}>" if T > 8 else f"gpad::gpad_panel_kernel<{T}>") \
             if st["kernel"] == "panel" else f"gpad::gpad_{st['kernel']}_kernel"
-        # n = m = 200: the pair phases run on the W32 layout (gpad_pair32_kernel), the one-panel
-        # phases on gpad_panel2_kernel -- the solve's panel traffic is both
-        knames = [kname, "gpad::gpad_pair32_kernel"] if (n, m) == (200, 200) and st["kernel"] == "panel" else [kname]
-        traffic, traffic_src = traffic_from_profile(knames)
+        traffic, traffic_src = traffic_from_profile(kname)
         launches = util["launches_per_solve"] if st["kernel"] == "panel" else 1
         # single instances (configs C1 and C2): latency kernels, fixed iteration counts
         singles = {}

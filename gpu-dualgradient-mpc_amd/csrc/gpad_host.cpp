@@ -115,8 +115,6 @@ struct gpad_handle_s {
     int ldn = 0, ldm = 0;
     DevBuf MGt, GLt, frag, stage;
     bool frag_ok = false;      // frag holds the fragment image of the bound matrices
-    DevBuf frag32;             // n = m = 200: the W32 pair images (gpad_pair32.hip)
-    bool frag32_ok = false;
     bool keep_stage = false;   // gpad_solve's cached handle keeps its staging buffer
     // gpad_solve: host copy of the last bound (ML, G, L, dims) so a repeated one-shot call on
     // the same host matrices skips the H2D copy and repack
@@ -276,7 +274,6 @@ int gpad_destroy(gpad_handle_t h) {
     h->Hq.release();
     h->frag64.release();
     h->hfrag64.release();
-    h->frag32.release();
     h->frag.release();
     h->stage.release();
     h->theta.release();
@@ -333,7 +330,6 @@ int gpad_set_option(gpad_handle_t h, int option, int value) {
             return set(t.flat_waves, 0, 16, def.flat_waves);
         case GPAD_OPT_FLAT_A_LDS: return set(t.flat_a_lds, 0, 1, def.flat_a_lds);
         case GPAD_OPT_DEBUG_DROP_HANDOFF: return set(t.debug_drop_handoff, 0, 1, def.debug_drop_handoff);
-        case GPAD_OPT_PAIR32: return set(t.pair32, 0, 1, def.pair32);
         default: return fail(GPAD_ERR_INVALID, "gpad_set_option: unknown option");
     }
 }
@@ -439,7 +435,6 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
         h->frag64_ok = true;
     }
     h->frag_ok = false;
-    h->frag32_ok = false;
     h->frag_tiles = 0;
     if (d->shared && d->dtype == GPAD_DTYPE_F32) {
         const size_t fb = gpad::panel_frag_bytes(n, m, d->batch);
@@ -449,12 +444,6 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
                                             (float)sa, sb, h->frag.p, h->stream));
             h->frag_tiles = gpad::panel_tiles(n, m, d->batch);
             h->frag_ok = true;
-        }
-        h->frag32_ok = false;
-        if (h->frag_ok && gpad::pair32_supported(n, m)) {  // the W32 pair layout of the C3/C4 shape
-            if ((rc = h->frag32.ensure(gpad::pair32_frag_bytes()))) return rc;
-            HIP_TRY(gpad::launch_pack_pair32((const float*)dA, (const float*)dB, (float)sa, sb, h->frag32.p, h->stream));
-            h->frag32_ok = true;
         }
     }
     HIP_TRY(hipStreamSynchronize(h->stream));
@@ -555,7 +544,6 @@ int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* d, int n_u, const float*
                                             h->stream));
     }
     h->frag_ok = false;
-    h->frag32_ok = false;
     h->frag_tiles = 0;
     {  // MFMA panels over the flat data (gpad_flatpanel.hip)
         const size_t fb = gpad::flatpanel_frag_bytes(d->n, m, n_u);
@@ -766,7 +754,6 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
     a.strideB = d.shared ? 0 : (long long)n * h->ldm;
     a.frag = h->frag_ok ? h->frag.p : nullptr;
     a.frag_tiles = h->frag_tiles;
-    a.frag32 = (h->frag32_ok && h->tune.pair32) ? h->frag32.p : nullptr;
     a.gP = dM;
     a.g = dg;
     a.ld_gP = n;

@@ -28,7 +28,6 @@ struct Tuning {
     int flat_waves = 0;       // GPAD_OPT_FLAT_WAVES: 0 auto, 8 or 16 waves per workgroup
     int flat_a_lds = 1;       // GPAD_OPT_FLAT_A_LDS: flat fragment image in LDS when it fits
     int debug_drop_handoff = 0;  // GPAD_OPT_DEBUG_DROP_HANDOFF: test-only fault injection
-    int pair32 = 1;           // GPAD_OPT_PAIR32: the W32 pair layout for n = m = 200 (gpad_pair32.hip)
 };
 
 // Device error word of a run (SolveArgs::err): kernels OR these bits in with a vector atomic;
@@ -112,10 +111,6 @@ struct SolveArgs {
     const T* Hq;           // QP Hessian H, k-major [n][ldn] (gpad_setup_hessian), or null: enables the
                            // value-function branches of the test (stream kernel only)
     long long strideHq;    // elements between consecutive instances' H images (0 = shared)
-    const void* frag32;    // C3/C4 shape (n = m = 200): the W32 pair images (gpad_pair32.hip), or null
-    int pair32;            // 1: gpad_pair32_kernel runs this solve's pair phases (gpad_panel2_kernel
-                           // returns in them), phases of more than pair32_min panels
-    int pair32_min;
     const void* hfrag64;   // f64 panels (gpad_panel64.hip): H in their fragment layout, or null (no value
                            // branches)
     int* err;              // device error word (kDevErr* bits), never null on a solve launch
@@ -135,12 +130,6 @@ hipError_t launch_panel(const SolveArgs<float>& a, hipStream_t s, bool* supporte
 // f64 panels on the f64 MFMA pipe (gpad_panel64.hip): shared matrices, n, m <= 256, one panel of 16
 // instances per workgroup, value-function branches when a.hfrag64 is set; a.frag = the -ML | G_L
 // images of launch_pack_panel64, a.frag_tiles = panel64_tiles(n, m)
-// W32 panel pairs (gpad_pair32.hip): n = m = 200, 32 instances per workgroup on 32x32x2 chains
-bool pair32_supported(int n, int m);
-size_t pair32_frag_bytes();
-hipError_t launch_pack_pair32(const float* ML, const float* G, float mg_sign, double g_scale, void* frag,
-                              hipStream_t s);
-hipError_t launch_pair32(const SolveArgs<float>& a, int grid, hipStream_t s);
 bool panel64_supported(int n, int m);
 int panel64_tiles(int n, int m);
 size_t panel64_frag_bytes(int n, int m);  // one T x T operand image

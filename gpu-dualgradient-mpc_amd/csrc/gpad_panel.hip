@@ -1190,7 +1190,6 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
     if (a.count_in && count <= a.fin_thresh) return;  // the finisher has them
     const int panels = (count + 15) / 16;
     const bool pair = panels > (int)gridDim.x;
-    if (pair && a.pair32) return;  // gpad_pair32_kernel runs the pair phases of this solve
     // Role index.  The SIMD issues MFMAs oldest wave first, so a role's wave index sets its share
     // of the SIMD while the SIMD is contended.  One-panel layout: the roles are dealt from the
     // last wave down, so the relay pieces of tile T-1 (roles T, T+1) and its receiver run on the
@@ -1588,52 +1587,28 @@ hipError_t launch_phase_compact(const int* seg_cnt, const int* seg_idx, const in
 }
 
 template <int T>
-static void launch_panel2(const SolveArgs<float>& a, int grid, hipStream_t s) {
-    // the C3/C4 shapes (T = 13) with full-length chains and one last-block length in both
-    // GEMMs: the compile-time variant (panel2_run KQ)
-    const int nkb1 = (a.m + 15) / 16, nkb2 = (a.n + 15) / 16;
-    const int kq1 = (a.m - 16 * (nkb1 - 1) + 3) / 4, kq2 = (a.n - 16 * (nkb2 - 1) + 3) / 4;
-    const bool full = nkb1 == T && nkb2 == T && kq1 == kq2;
-    if constexpr (T == 13) {
-        if (a.debug & kDebugDropHandoff) {  // tests only: the fault-injection instantiations
-            if (full && kq1 == 2) hipLaunchKernelGGL((gpad_panel2_kernel<T, 2, true>), dim3(grid), dim3(1024), 0, s, a);
-            else hipLaunchKernelGGL((gpad_panel2_kernel<T, 0, true>), dim3(grid), dim3(1024), 0, s, a);
-            return;
-        }
-        if (full && kq1 == 1) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 1>), dim3(grid), dim3(1024), 0, s, a); return; }
-        if (full && kq1 == 2) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 2>), dim3(grid), dim3(1024), 0, s, a); return; }
-        if (full && kq1 == 3) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 3>), dim3(grid), dim3(1024), 0, s, a); return; }
-        if (full && kq1 == 4) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 4>), dim3(grid), dim3(1024), 0, s, a); return; }
-    }
-    (void)full;
-    hipLaunchKernelGGL((gpad_panel2_kernel<T, 0>), dim3(grid), dim3(1024), 0, s, a);
-}
-
-template <int T>
 static void launch_panel_kernel(const SolveArgs<float>& a, int grid, hipStream_t s) {
     if constexpr (T == 0) {
         (void)launch_bigpanel(a, grid, s);
     } else if constexpr (T > 8) {
-        // n = m = 200 pairs on the W32 layout (gpad_pair32.hip), launched first: it takes a phase that
-        // holds more panels than this grid, and the panel-pair kernel then returns at once (it runs the
-        // one-panel layout otherwise).  Phase 0 (count = batch) is decided here, with one launch.
-        if (T == 13 && a.frag32 && !(a.debug & kDebugDropHandoff)) {
-            SolveArgs<float> b = a;
-            b.pair32 = 1;
-            b.pair32_min = grid;
-            const int panels0 = (a.batch + 15) / 16;
-            const int items = (panels0 + 1) / 2;
-            const int g32 = items < a.num_cus ? items : a.num_cus;
-            const bool known = a.count_in == nullptr;  // phase 0: the count is the batch
-            if (known && panels0 <= grid) {            // one panel per workgroup: the 16x16x4 layout
-                launch_panel2<T>(a, grid, s);
+        // the C3/C4 shapes (T = 13) with full-length chains and one last-block length in both
+        // GEMMs: the compile-time variant (panel2_run KQ)
+        const int nkb1 = (a.m + 15) / 16, nkb2 = (a.n + 15) / 16;
+        const int kq1 = (a.m - 16 * (nkb1 - 1) + 3) / 4, kq2 = (a.n - 16 * (nkb2 - 1) + 3) / 4;
+        const bool full = nkb1 == T && nkb2 == T && kq1 == kq2;
+        if constexpr (T == 13) {
+            if (a.debug & kDebugDropHandoff) {  // tests only: the fault-injection instantiations
+                if (full && kq1 == 2) hipLaunchKernelGGL((gpad_panel2_kernel<T, 2, true>), dim3(grid), dim3(1024), 0, s, a);
+                else hipLaunchKernelGGL((gpad_panel2_kernel<T, 0, true>), dim3(grid), dim3(1024), 0, s, a);
                 return;
             }
-            (void)launch_pair32(b, g32, s);
-            if (!known) launch_panel2<T>(b, grid, s);
-            return;
+            if (full && kq1 == 1) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 1>), dim3(grid), dim3(1024), 0, s, a); return; }
+            if (full && kq1 == 2) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 2>), dim3(grid), dim3(1024), 0, s, a); return; }
+            if (full && kq1 == 3) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 3>), dim3(grid), dim3(1024), 0, s, a); return; }
+            if (full && kq1 == 4) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 4>), dim3(grid), dim3(1024), 0, s, a); return; }
         }
-        launch_panel2<T>(a, grid, s);
+        (void)full;
+        hipLaunchKernelGGL((gpad_panel2_kernel<T, 0>), dim3(grid), dim3(1024), 0, s, a);
     } else
         hipLaunchKernelGGL((gpad_panel_kernel<T>), dim3(grid), dim3(64 * T), 0, s, a);
 }

@@ -385,8 +385,6 @@ int gpad_schedule(int N, int kind, double* theta, double* beta);
                                     * GPAD_ERR_DEVICE; 0 (default) = off.  Honoured by the
                                     * 193..208-row shapes (the C3/C4 tiling, T = 13), which run
                                     * a separate test-only kernel instantiation while it is set */
-#define GPAD_OPT_PAIR32 17         /* 1 (default): n = m = 200 panel pairs on 32x32x2 MFMA chains (32
-                                    * instances per chain, gpad_pair32.hip); 0: the 16x16x4 pairs     */
 int gpad_set_option(gpad_handle_t h, int option, int value);
 
 /* Synchronise the handle's stream (for callers using device memory + async runs). */
