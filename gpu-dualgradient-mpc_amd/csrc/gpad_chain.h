@@ -24,23 +24,84 @@ template <typename T> struct V4;
 template <> struct V4<float> { using type = float4; };
 template <> struct V4<double> { using type = double4; };
 
-// ---- wave64 reductions (DPP/permute lowered by the compiler) ---------------------------
-template <typename T>
-__device__ __forceinline__ T wave_max(T v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-    return v;
+// ---- wave64 butterflies on the VALU ------------------------------------------------------
+// __shfl_xor lowers to ds_bpermute: an LDS round trip per level, and with the latency kernels'
+// register-resident rows leaving few VGPRs the levels of the test's five reductions serialize
+// (~40 dependent permutes per Algorithm-1 test).  The same butterfly partners without LDS:
+// xor 32 / 16 by gfx950's v_permlane32_swap / v_permlane16_swap, xor 8 by DPP row_ror:8, xor 4
+// by DPP row_shl:4 into banks 0, 2 and row_shr:4 into banks 1, 3, xor 2 / 1 by DPP quad_perm.
+// Each level combines the same two partials as the __shfl_xor butterfly (op(own, partner), op
+// commutative), so sums are bit-identical to it and every lane ends with the same value.
+template <int O>
+__device__ __forceinline__ unsigned bfly_u32(unsigned x) {
+    if constexpr (O == 8) return __builtin_amdgcn_update_dpp(x, x, 0x128, 0xf, 0xf, false);  // row_ror:8
+    if constexpr (O == 4) {
+        const unsigned t = __builtin_amdgcn_update_dpp(x, x, 0x104, 0xf, 0x5, false);      // row_shl:4
+        return __builtin_amdgcn_update_dpp(t, x, 0x114, 0xf, 0xa, false);                 // row_shr:4
+    }
+    if constexpr (O == 2) return __builtin_amdgcn_update_dpp(x, x, 0x4e, 0xf, 0xf, false);  // [2,3,0,1]
+    if constexpr (O == 1) return __builtin_amdgcn_update_dpp(x, x, 0xb1, 0xf, 0xf, false);  // [1,0,3,2]
+    static_assert(O == 1 || O == 2 || O == 4 || O == 8, "DPP levels");
+    return x;
 }
-template <typename T>
-__device__ __forceinline__ T wave_min(T v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
-    return v;
+// one butterfly level of op: lanes l and l ^ O both get op(v_l, v_(l^O))
+template <int O, typename Op>
+__device__ __forceinline__ float bfly(float v, Op op) {
+    const unsigned x = __float_as_uint(v);
+    if constexpr (O == 32 || O == 16) {
+        const auto r = O == 32 ? __builtin_amdgcn_permlane32_swap(x, x, false, false)
+                               : __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        return op(__uint_as_float(r[0]), __uint_as_float(r[1]));  // (own, partner) in either order
+    } else {
+        return op(v, __uint_as_float(bfly_u32<O>(x)));
+    }
 }
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+template <int O, typename Op>
+__device__ __forceinline__ double bfly(double v, Op op) {
+    const unsigned long long b = __double_as_longlong(v);
+    const unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32);
+    if constexpr (O == 32 || O == 16) {
+        const auto rl = O == 32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
+                                : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+        const auto rh = O == 32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
+                                : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+        const double a = __longlong_as_double((long long)(((unsigned long long)rh[0] << 32) | rl[0]));
+        const double c = __longlong_as_double((long long)(((unsigned long long)rh[1] << 32) | rl[1]));
+        return op(a, c);
+    } else {
+        const unsigned pl = bfly_u32<O>(lo), ph = bfly_u32<O>(hi);
+        return op(v, __longlong_as_double((long long)(((unsigned long long)ph << 32) | pl)));
+    }
+}
+template <typename T, typename Op>
+__device__ __forceinline__ T wave_reduce(T v, Op op) {  // levels 32, 16, ..., 1 (the shfl_xor order)
+    v = bfly<32>(v, op);
+    v = bfly<16>(v, op);
+    v = bfly<8>(v, op);
+    v = bfly<4>(v, op);
+    v = bfly<2>(v, op);
+    return bfly<1>(v, op);
+}
+struct OpMax { template <typename T> __device__ T operator()(T a, T b) const { return fmax(a, b); } };
+struct OpMin { template <typename T> __device__ T operator()(T a, T b) const { return fmin(a, b); } };
+struct OpAdd { template <typename T> __device__ T operator()(T a, T b) const { return a + b; } };
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) { return wave_reduce(v, OpMax{}); }
+template <typename T>
+__device__ __forceinline__ T wave_min(T v) { return wave_reduce(v, OpMin{}); }
+__device__ __forceinline__ double wave_sum(double v) { return wave_reduce(v, OpAdd{}); }
+
+// max / min over lanes 0..7 (the test slots of up to 8 waves, one per lane)
+template <typename Op>
+__device__ __forceinline__ double lanes8_reduce(double v, Op op) {
+    v = bfly<1>(v, op);
+    v = bfly<2>(v, op);
+    return bfly<4>(v, op);
+}
+__device__ __forceinline__ double lane_read(double v, int l) {  // lane l's value, wave-uniform
+    const unsigned long long b = __double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l), hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
 // Per-wave partials of the Algorithm-1 test -> LDS slot of the wave.
@@ -68,20 +129,27 @@ __device__ __forceinline__ void check_publish(CheckSlot* slots, T violz, T violh
 }
 
 // Every thread evaluates the decision from the same LDS words -> uniform, no extra barrier.
+// Lane i < nwaves (<= 8) reads slot i -- one LDS round trip instead of one per slot -- the maxima
+// and minima meet over lanes 0..7 by DPP (order-free), and the fp64 gap is summed in wave order
+// (((0 + g_0) + g_1) + ...) from lane reads, as the sequential loop summed it.
 // Returns bit 1: test (A) nominated by the recursion (L*max(u + pD) <= tol; decided later on
 // the direct G_L z by check_verify), bit 2: test (B) passed
 //   L*max(G_L zhat + pD) + margin L*max(|G_L zhat| + |pD|) <= tol, w >= 0, -L w't <= tol_gap.
 template <typename T>
 __device__ __forceinline__ int check_stage1(const CheckSlot* slots, int nwaves, double L, double tol,
                                             double tol_gap) {
-    double vz = -INFINITY, vh = -INFINITY, wm = INFINITY, gap = 0.0, mh = 0.0;
-    for (int i = 0; i < nwaves; ++i) {
-        vz = fmax(vz, slots[i].violz);
-        vh = fmax(vh, slots[i].violh);
-        wm = fmin(wm, slots[i].wmin);
-        gap += slots[i].gap;
-        mh = fmax(mh, slots[i].magh);
-    }
+    const int lane = threadIdx.x & 63;
+    const bool own = lane < nwaves;
+    double vz = own ? slots[lane].violz : -INFINITY, vh = own ? slots[lane].violh : -INFINITY;
+    double wm = own ? slots[lane].wmin : INFINITY, mh = own ? slots[lane].magh : 0.0;
+    const double g = own ? slots[lane].gap : 0.0;
+    // (folded into the loop's initial values, so an all-NaN column reduces as the loop did)
+    vz = fmax(-INFINITY, lane_read(lanes8_reduce(vz, OpMax{}), 0));
+    vh = fmax(-INFINITY, lane_read(lanes8_reduce(vh, OpMax{}), 0));
+    mh = fmax(0.0, lane_read(lanes8_reduce(mh, OpMax{}), 0));
+    wm = fmin(INFINITY, lane_read(lanes8_reduce(wm, OpMin{}), 0));
+    double gap = 0.0;
+    for (int i = 0; i < nwaves; ++i) gap += lane_read(g, i);
     const bool a = vz * L <= tol;
     const bool b = viol_ok(vh, mh, L, tol, ViolMargin<T>::value) && (wm >= 0.0) && (gap * L <= tol_gap);
     return (a ? 1 : 0) | (b ? 2 : 0);
@@ -90,11 +158,10 @@ __device__ __forceinline__ int check_stage1(const CheckSlot* slots, int nwaves, 
 // Test (A) on the direct chain c = G_L z: slots hold max(c + pD) in violz, max(|c| + |pD|) in magh.
 template <typename T>
 __device__ __forceinline__ bool check_verify(const CheckSlot* slots, int nwaves, double L, double tol) {
-    double vc = -INFINITY, mc = 0.0;
-    for (int i = 0; i < nwaves; ++i) {
-        vc = fmax(vc, slots[i].violz);
-        mc = fmax(mc, slots[i].magh);
-    }
+    const int lane = threadIdx.x & 63;
+    const bool own = lane < nwaves;
+    const double vc = fmax(-INFINITY, lane_read(lanes8_reduce(own ? slots[lane].violz : -INFINITY, OpMax{}), 0));
+    const double mc = fmax(0.0, lane_read(lanes8_reduce(own ? slots[lane].magh : 0.0, OpMax{}), 0));
     return viol_ok(vc, mc, L, tol, ViolMargin<T>::value);
 }
 

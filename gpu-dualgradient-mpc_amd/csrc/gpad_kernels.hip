@@ -451,21 +451,30 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
     int it = 0;
     int done = 0;
     float zhi = 0.0f;
-    // theta/beta are prefetched one iteration ahead (tables hold N + 2 entries)
+    // theta/beta are fetched one iteration ahead, by each role in its idle half (the A waves while
+    // the 8d chains run, the B waves while the 8b chains run), and the test period is a countdown:
+    // between barrier 2 and the next 8b chain only the loop branch remains (tables hold N + 2
+    // entries).
     float th = a.theta[0], bn = a.beta[1];
+    float th_next = 0.0f, bn_next = 0.0f;
+    const int Kc = a.check_every;
+    int kc = Kc;  // iterations to the next test: chk <=> (v + 1) % Kc == 0
     for (int v = 0; v < a.N; ++v) {
-        const float th_next = a.theta[v + 1], bn_next = a.beta[v + 2];
-        const bool chk = a.tol > 0.0 && ((v + 1) % a.check_every) == 0;
+        const bool chk = use_tol && --kc == 0;
+        if (chk) kc = Kc;
         GPAD_RSTAMP(0);
         if (isA) {  // ---- 8b + 8c --------------------------------------------------------
             const float acc = chain_regs<KA, K>(r, wvec);
             GPAD_RSTAMP(1);
             if (live) {
                 const float zhv = acc - gpi;
+                zh_l[row] = zhv;  // (the exchange first: 8c is off the critical path)
                 zi = __builtin_fmaf(1.0f - th, zi, th * zhv);
-                zh_l[row] = zhv;
                 zhi = zhv;
             }
+        } else {
+            th_next = a.theta[v + 1];
+            bn_next = a.beta[v + 2];
         }
         __syncthreads();
         GPAD_RSTAMP(2);
@@ -483,6 +492,8 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
                     sv = (wi + pdi) + c;             // seq_functions.cpp:84
                     yp = (__builtin_fabsf(sv) + sv) * 0.5f;
                 }
+                const float wn = __builtin_fmaf(bn, yp - yi, yp);
+                put_w(wn);  // (the exchange first: u and the test partials are off the critical path)
                 if (use_tol) ui = __builtin_fmaf(1.0f - th, ui, th * c);
                 if (chk) {
                     const float t = c + pdi;
@@ -492,10 +503,12 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_resident_kernel(Solv
                     gap = -((double)wi * (double)t);
                     violz = ui + pdi;
                 }
-                wi = __builtin_fmaf(bn, yp - yi, yp);
+                wi = wn;
                 yi = yp;
-                put_w(wi);
             }
+        } else {
+            th_next = a.theta[v + 1];
+            bn_next = a.beta[v + 2];
         }
         if (chk) check_publish<float>(slots[0], violz, violh, wmin, gap, magh);
         GPAD_RSTAMP(4);

@@ -13,8 +13,10 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "gpu-dualgradient-mpc_amd"))
 
 
-def stamps():
-    """Step anatomy of the duo with one live slot (diagnostic build: GPAD_LIB=tools/abl/stamp.so)."""
+def stamps(two=False):
+    """Step anatomy of the duo (diagnostic build: GPAD_LIB=tools/abl/stamp.so): one live slot, or
+    two (--two); steps 200..207 of workgroup 0, per wave: chain, epilogue, barrier wait, post-barrier
+    bookkeeping, gap to the next step (cycles of the shader clock)."""
     import ctypes as C
 
     import torch
@@ -23,37 +25,40 @@ def stamps():
     import gpad_mpc
     from gpad_mpc import _lib
     dev = torch.device("cuda:0")
-    ML, G, L, M, g = bench.make_shard(200, 200, 1, 0)
+    B = 2 if two else 1
+    ML, G, L, M, g = bench.make_shard(200, 200, B, 0)
     f32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)  # noqa: E731
     with gpad_mpc.GpadSolver(0) as s:
-        s.setup(f32(ML), f32(G), float(np.float32(L)), n=200, m=200, batch=1, kernel=_lib.KERNEL_PANEL)
-        s.set_options(phase_len=10, finish_thresh=100000)
-        z = torch.zeros(1, 200, device=dev)
-        y = torch.zeros(1, 200, device=dev)
+        s.setup(f32(ML), f32(G), float(np.float32(L)), n=200, m=200, batch=B, kernel=_lib.KERNEL_PANEL)
+        s.set_options(phase_len=10, finish_thresh=100000, **({"duo_max_grid": 1} if two else {}))
+        z = torch.zeros(B, 200, device=dev)
+        y = torch.zeros(B, 200, device=dev)
         s.run(z, y, f32(M), f32(g), 300, 1e-12)
     L_ = _lib.load()
-    buf = (C.c_ulonglong * (8 * 4 * 2 * 5))()
+    buf = (C.c_ulonglong * (8 * 8 * 5))()
     f = L_._lib.gpad_debug_duo_stamps if hasattr(L_, "_lib") else L_.gpad_debug_duo_stamps
     f.argtypes = [C.c_void_p, C.c_size_t]
     assert f(buf, C.sizeof(buf)) == 0
-    st = np.array(buf, dtype=np.int64).reshape(8, 4, 2, 5)
+    st = np.array(buf, dtype=np.int64).reshape(8, 8, 5)
+    print(f"duo, {'two live slots' if two else 'one live slot'}: steps 200..206, cycles (shader clock)")
     for w in range(8):
-        seg = []
-        for i in range(3):
-            a_, b_ = st[w, i, 0].copy(), st[w, i, 1].copy()
-            for x in (a_, b_):  # a wave without this step's chain stamps no point 1
-                if x[1] == 0:
-                    x[1] = x[0]
-            seg.append([a_[1] - a_[0], a_[2] - a_[1], a_[3] - a_[2], a_[4] - a_[3], b_[0] - a_[4],
-                        b_[1] - b_[0], b_[2] - b_[1], b_[3] - b_[2], b_[4] - b_[3], st[w, i + 1, 0, 0] - b_[4]])
-        d = np.mean(seg, axis=0).astype(int)
-        print(f"wave {w} ({'A' if w < 4 else 'B'}): 8b-step chain {d[0]} epi {d[1]} bar {d[2]} post {d[3]} gap {d[4]} | "
-              f"8d-step chain {d[5]} epi {d[6]} bar {d[7]} post {d[8]} gap {d[9]} | iteration {int(d.sum())}")
+        rows = []
+        for i in range(7):
+            x = st[w, i].copy()
+            if x[1] == 0:  # no chain on this wave this step
+                x[1] = x[0]
+            rows.append([x[1] - x[0], x[2] - x[1], x[3] - x[2], x[4] - x[3], st[w, i + 1, 0] - x[4],
+                         st[w, i + 1, 0] - x[0]])
+        rows = np.array(rows)
+        for par in (0, 1):
+            d = rows[par::2].mean(axis=0).astype(int)
+            print(f"wave {w} ({'B' if w < 4 else 'A'}) steps {'even' if par == 0 else 'odd '}: chain {d[0]:5d} "
+                  f"epi {d[1]:4d} bar {d[2]:5d} post {d[3]:4d} gap {d[4]:4d} | step {d[5]}")
 
 
 def main():
     if "--stamps" in sys.argv:
-        stamps()
+        stamps(two="--two" in sys.argv)
         return
     import torch
 
