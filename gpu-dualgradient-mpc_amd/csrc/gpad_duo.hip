@@ -191,15 +191,23 @@ __device__ __forceinline__ void duo_half_b(const DuoCtx& c, DuoSlot& sb, bool ch
 
 // after the barrier that closes slot sb's 8d half (every wave): iteration count, schedule, the
 // test's decision, and on termination the results out and the slot refilled from the queue
-template <int KB, int K>
+// PRE: the schedule of the next iteration was fetched ahead (th_n, bn_n; duo_solo), else it is
+// loaded here
+template <int KB, int K, bool PRE = false>
 __device__ __forceinline__ void duo_post_b(const SolveArgs<float>& a, const DuoCtx& c, DuoSlot& sb, bool chk,
                                            float* wb_l, float* gpb_l, float* pdb_l, CheckSlot* slots_b,
-                                           CheckSlot* vslots, int* claim_b, float* z_l, const float (&r)[K]) {
+                                           CheckSlot* vslots, int* claim_b, float* z_l, const float (&r)[K],
+                                           float th_n = 0.0f, float bn_n = 0.0f) {
     sb.need8d = false;
     sb.kc = chk ? c.Kc : sb.kc - 1;
     const int v = ++sb.vs;
-    sb.th = sched(a.theta, v);  // next iteration's schedule (tables hold N + 2 entries)
-    sb.bn = sched(a.beta, v + 1);
+    if constexpr (PRE) {
+        sb.th = th_n;
+        sb.bn = bn_n;
+    } else {
+        sb.th = sched(a.theta, v);  // next iteration's schedule (tables hold N + 2 entries)
+        sb.bn = sched(a.beta, v + 1);
+    }
     int done = 0;
     if (chk) {
         const int st1 = check_stage1<float>(slots_b + c.b0, c.nwaves - c.nA, a.L, a.tol, a.tol_gap);
@@ -279,10 +287,18 @@ template <int KA, int KB, int K>
 __device__ __forceinline__ void duo_solo(const SolveArgs<float>& a, const DuoCtx& c, DuoSlot& s, float* w_l,
                                          float* zh_l, float* gp_l, float* pd_l, CheckSlot* slots,
                                          CheckSlot* vslots, int* claim, float* z_l, const float (&r)[K]) {
+    // the next iteration's theta / beta by vector loads, each role in its idle half (as the
+    // resident kernel): no scalar-load latency in front of the next chain's first LDS read
+    float th_n = a.theta[s.vs + 1], bn_n = a.beta[s.vs + 2];
     while (s.pos < c.count) {
         if (!s.need8d) {  // (a slot that enters after its 8b half starts at 8d)
             GPAD_DSTAMP(0);
-            if (c.isA) duo_half_a<KA, K>(c, s, w_l, zh_l, gp_l, r);
+            if (c.isA) {
+                duo_half_a<KA, K>(c, s, w_l, zh_l, gp_l, r);
+            } else {
+                th_n = a.theta[s.vs + 1];
+                bn_n = a.beta[s.vs + 2];
+            }
             GPAD_DSTAMP(2);
             __syncthreads();
             GPAD_DSTAMP(3);
@@ -291,11 +307,16 @@ __device__ __forceinline__ void duo_solo(const SolveArgs<float>& a, const DuoCtx
         }
         const bool chk = c.use_tol && s.kc == 1;
         GPAD_DSTAMP(0);
-        if (!c.isA) duo_half_b<KB, K>(c, s, chk, zh_l, w_l, pd_l, slots, r);
+        if (!c.isA) {
+            duo_half_b<KB, K>(c, s, chk, zh_l, w_l, pd_l, slots, r);
+        } else {
+            th_n = a.theta[s.vs + 1];
+            bn_n = a.beta[s.vs + 2];
+        }
         GPAD_DSTAMP(2);
         __syncthreads();
         GPAD_DSTAMP(3);
-        duo_post_b<KB, K>(a, c, s, chk, w_l, gp_l, pd_l, slots, vslots, claim, z_l, r);
+        duo_post_b<KB, K, true>(a, c, s, chk, w_l, gp_l, pd_l, slots, vslots, claim, z_l, r, th_n, bn_n);
         GPAD_DSTAMP(4);
         GPAD_DSTEP();
     }

@@ -96,6 +96,35 @@ def parse(args):
             print(f"survivors past iteration {v:>4}: {(it > v).sum()}")
 
 
+def stats(args):
+    """Per-kernel durations over every solve of the trace, and the solve spans (A/B of a phase)."""
+    files = glob.glob(os.path.join(args.dir, "**", "*kernel_trace.csv"), recursive=True)
+    if not files:
+        sys.exit(f"no kernel_trace.csv under {args.dir}")
+    with open(files[0]) as f:
+        rows = sorted(csv.DictReader(f), key=lambda r: int(r["Start_Timestamp"]))
+    gpad = [r for r in rows if "gpad" in r["Kernel_Name"] and "pack" not in r["Kernel_Name"]]
+    solves, cur = [], []
+    for r in gpad:
+        if cur and int(r["Start_Timestamp"]) - int(cur[-1]["End_Timestamp"]) > 200_000:
+            solves.append(cur)
+            cur = []
+        cur.append(r)
+    solves.append(cur)
+    solves = solves[1:]  # (the first solve warms up)
+    spans = [(int(s[-1]["End_Timestamp"]) - int(s[0]["Start_Timestamp"])) / 1e3 for s in solves]
+    per = {}
+    for s in solves:
+        for r in s:
+            k = r["Kernel_Name"].split("(")[0][-34:]
+            per.setdefault(k, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    print(f"{args.label} solves {len(solves)}: span mean {np.mean(spans):.1f} median {np.median(spans):.1f} "
+          f"min {np.min(spans):.1f} us")
+    for k, d in sorted(per.items(), key=lambda kv: -sum(kv[1])):
+        print(f"{args.label}   {k:<34} n {len(d):>3} per solve {sum(d) / len(solves):8.1f} us  "
+              f"mean {np.mean(d):7.1f}  min {np.min(d):7.1f}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -107,8 +136,11 @@ def main():
     b = sub.add_parser("parse")
     b.add_argument("dir")
     b.add_argument("--iters", default="gpurun_out/tl_iters.npy")
+    c = sub.add_parser("stats")
+    c.add_argument("dir")
+    c.add_argument("--label", default="")
     args = ap.parse_args()
-    run(args) if args.cmd == "run" else parse(args)
+    {"run": run, "parse": parse, "stats": stats}[args.cmd](args)
 
 
 if __name__ == "__main__":
