@@ -672,7 +672,7 @@ struct Panel2Lds {
     float4 Pd[2][T * 64];  //                            p_D rows
     PanelSlot2 slots[2][T];
     float4 TA[2][8][4][T];  // tail layout (TailPair): rows 16 (T-1) + r of each GEMM's matrix, [r][j][kb] =
-                            // fragment (kb, tile T-1, lane 16 j + r), components q -> k = 16 kb + 4 q + j
+                            // fragment (kb, tile T-1, lane 16 j + pi16(r)), components q -> k = 16 kb + 4 q + j
     float4 hand[3][64];    // hand-off accumulators
     int hflag[3];          // hand-off generation per slot
     int herr;              // a wait expired (handoff_wait): reported to the run's error word at exit
@@ -808,15 +808,58 @@ __device__ __forceinline__ void tail_chain(const float4 (&TA)[8][4][T], const fl
 }
 
 // the relay piece TP of one GEMM (g = 0: -ML, B = w; g = 1: G_L, B = zhat); the last piece returns
-// the finished accumulator to its wave
+// the finished accumulator to its wave.  The relay is the sequential path of the layout (its MFMAs
+// wait behind the other waves' 16x16x4 ones), so a piece loads its first k-block's operands before
+// it waits for its predecessor, keeps one k-block of operands in flight, and spins on the flag
+// without sleeping.
 template <int T, int KQ, int TP>
 __device__ __forceinline__ f32x4 tail_piece(Panel2Lds<T>& L, int g, const float4* B, int lane, int gen) {
     constexpr int KB0 = TP == 0 ? 0 : (TP == 1 ? 4 : (TP == 2 ? 7 : 10));
     constexpr int KB1 = TP == 0 ? 4 : (TP == 1 ? 7 : (TP == 2 ? 10 : T));
+    const int r8 = 4 * (lane >> 5) + (lane & 3);
+    const float4* Bp = B + ((lane >> 4) & 1) * (T * 64) + (lane & 15);
+    const float4 (&TA)[8][4][T] = L.TA[g];
+    float4 a4[2][4], b4[2][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        a4[0][j] = TA[r8][j][KB0];
+        b4[0][j] = Bp[KB0 * 64 + 16 * j];
+    }
     f32x4 acc = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    if constexpr (TP > 0) acc = handoff_wait(L, TP - 1, gen, lane);
+    if constexpr (TP > 0) {
+        for (int s = 0;; ++s) {
+            if (__hip_atomic_load(&L.hflag[TP - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == gen) break;
+            if (s == (1 << 22)) {  // (bounded as handoff_wait: an expired wait fails the run)
+                L.herr = 1;
+                break;
+            }
+        }
+        asm volatile("" ::: "memory");
+        const float4 hv = L.hand[TP - 1][lane];
+        acc = f32x4{hv.x, hv.y, hv.z, hv.w};
+    }
     __builtin_amdgcn_s_setprio(3);
-    tail_chain<T, KQ, KB0, KB1>(L.TA[g], B, lane, acc);
+#pragma unroll
+    for (int kb = KB0; kb < KB1; ++kb) {
+        const int cur = (kb - KB0) & 1, nxt = cur ^ 1;
+        if (kb + 1 < KB1) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                a4[nxt][j] = TA[r8][j][kb + 1];
+                b4[nxt][j] = Bp[(kb + 1) * 64 + 16 * j];
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (kb + 1 < T || q < KQ) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(f4c(a4[cur][j], q), f4c(b4[cur][j], q), acc, 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
     if constexpr (TP < 3) handoff_post(L, TP, gen, lane, acc);
     __builtin_amdgcn_s_setprio(0);
     return acc;
@@ -846,14 +889,14 @@ __device__ __forceinline__ float* tail_slot(float4* V, int lane, int i) {
 // GEMMs (16 (T-1) < n, m <= 16 T) whose last k-block issues KQ steps in both: no runtime kq tests
 // (scalar branches whose conditions the compiler spilled to VGPR lanes) and no short-chain paths.
 // DROP: the fault-injection instantiation (handoff_piece).
-// TP >= 0: TailPair layout, this single wave also runs relay piece TP of the 4x4x1 tail chain (TP = 3:
-// and owns the tail rows).
+// TP >= 0: TailPair layout, this wave (no sixteen-row chain) runs relay piece TP of the 4x4x1 tail
+// chain (TP = 3: and owns the tail rows).
 template <int T, int NU, int ROLE = 0, int KB0 = 0, int KB1 = 0, bool PRIO = false, int KQ = 0, bool DROP = false,
           int TP = -1>
 __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<T>& L, int t, int p0,
                                            bool pair, int items, int count, HoSlots hs = HoSlots{-1, -1}) {
     static_assert(ROLE == 0 || (Handoff<T>::on && (ROLE == 3 ? NU == 0 : NU == 1)), "hand-off roles");
-    static_assert(TP < 0 || (NU == 1 && ROLE == 0 && T == 13 && KQ > 0 && KQ <= 2), "tail pieces");
+    static_assert(TP < 0 || (NU == 0 && ROLE == 0 && T == 13 && KQ > 0 && KQ <= 2), "tail pieces");
     constexpr bool OWN = TP == 3;  // the tail owner
     const int lane = threadIdx.x & 63;
     const int j = lane >> 4, c = lane & 15;
@@ -976,6 +1019,13 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             int anynz = 0;
 #pragma unroll
             for (int i = 0; i < 16; ++i) anynz |= L.znz[i];
+            if constexpr (OWN) {
+                if (anynz) {
+                    const f32x4 cu = tail_full<T, KQ>(L, 1, L.Zh[0], lane);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) tr.u[i] = cu[i];
+                }
+            }
             if constexpr (NU > 0) {
                 if (anynz) {
                     f32x4 c0, c1;
@@ -985,11 +1035,6 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                     if constexpr (NU == 2) {
 #pragma unroll
                         for (int r = 0; r < 4; ++r) u[Q - 1][r] = c1[r];
-                    }
-                    if constexpr (OWN) {
-                        const f32x4 cu = tail_full<T, KQ>(L, 1, L.Zh[0], lane);
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) tr.u[i] = cu[i];
                     }
                 }
             }
@@ -1017,21 +1062,21 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             const float omt = 1.0f - th;
             GPAD_STAMP_AT(0);
             // ---- GEMM 1 + epilogue: zhat = -ML w - g_P (8b), z = (1-th) z + th zhat (8c) ----
+            if constexpr (TP >= 0) {  // the tail relay's piece
+                ++tgen;
+                const f32x4 ta = tail_piece<T, KQ, TP>(L, 0, L.Wl[0], lane, tgen);
+                if constexpr (OWN) {  // 8b / 8c of the tail rows
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const float h = ta[i] - tr.gp[i];
+                        *tail_slot<T>(L.Zh[0], lane, i) = h;
+                        tr.z[i] = __builtin_fmaf(omt, tr.z[i], th * h);
+                    }
+                }
+            }
             if constexpr (NU > 0) {
                 f32x4 acc[2];
                 ++hgen;
-                if constexpr (TP >= 0) {  // the tail relay's piece first (its wave is the SIMD's oldest)
-                    ++tgen;
-                    const f32x4 ta = tail_piece<T, KQ, TP>(L, 0, L.Wl[0], lane, tgen);
-                    if constexpr (OWN) {  // 8b / 8c of the tail rows
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            const float h = ta[i] - tr.gp[i];
-                            *tail_slot<T>(L.Zh[0], lane, i) = h;
-                            tr.z[i] = __builtin_fmaf(omt, tr.z[i], th * h);
-                        }
-                    }
-                }
                 if constexpr (ROLE == 1)
                     handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA1, L.Wl[p0], voff_r, lane, aph, hs, hgen);
                 if constexpr (ROLE == 2)
@@ -1081,49 +1126,49 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 magh[q] = 0.0f;
                 gap[q] = 0.0;
             }
-            if constexpr (NU > 0) {
-                f32x4 acc[2];
-                ++hgen;
-                if constexpr (TP >= 0) {
-                    ++tgen;
-                    const f32x4 tc = tail_piece<T, KQ, TP>(L, 1, L.Zh[0], lane, tgen);
-                    if constexpr (OWN) {  // 8d / 8a of the tail rows, and their test partials
-                        float tvz = -INFINITY, tvh = -INFINITY, twm = INFINITY, tmh = 0.0f;
-                        double tgap = 0.0;
+            if constexpr (TP >= 0) {
+                ++tgen;
+                const f32x4 tc = tail_piece<T, KQ, TP>(L, 1, L.Zh[0], lane, tgen);
+                if constexpr (OWN) {  // 8d / 8a of the tail rows, and their test partials
+                    float tvz = -INFINITY, tvh = -INFINITY, twm = INFINITY, tmh = 0.0f;
+                    double tgap = 0.0;
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            float* wp = tail_slot<T>(L.Wl[0], lane, i);
-                            const float wv = *wp, cv = tc[i];
-                            const float sv = (wv + tr.pd[i]) + cv;
-                            const float yp = (__builtin_fabsf(sv) + sv) * 0.5f;
-                            *wp = __builtin_fmaf(bn, yp - tr.y[i], yp);
-                            tr.y[i] = yp;
-                            if (use_tol) {
-                                tr.u[i] = __builtin_fmaf(omt, tr.u[i], th * cv);
-                                if (chk && tr.act && 16 * (T - 1) + 4 * (lane >> 5) + i < m) {
-                                    const float tt = cv + tr.pd[i];
-                                    tvh = fmaxf(tvh, tt);
-                                    tmh = fmaxf(tmh, __builtin_fabsf(cv) + __builtin_fabsf(tr.pd[i]));
-                                    twm = fminf(twm, wv);
-                                    tgap -= (double)wv * (double)tt;
-                                    tvz = fmaxf(tvz, tr.u[i] + tr.pd[i]);
-                                }
-                            }
-                        }
-                        if (chk) {  // the two row groups (lanes l, l ^ 32) of each column
-                            tvz = bfly<32>(tvz, OpMax{});
-                            tvh = bfly<32>(tvh, OpMax{});
-                            tmh = bfly<32>(tmh, OpMax{});
-                            twm = bfly<32>(twm, OpMin{});
-                            tgap = bfly<32>(tgap, OpAdd{});
-                            if (lane < 32) {
-                                PanelSlot2& S = L.slots[(lane >> 4) & 1][T - 1];
-                                S.f[lane & 15] = make_float4(tvz, tvh, tmh, twm);
-                                S.gap[lane & 15] = tgap;
+                    for (int i = 0; i < 4; ++i) {
+                        float* wp = tail_slot<T>(L.Wl[0], lane, i);
+                        const float wv = *wp, cv = tc[i];
+                        const float sv = (wv + tr.pd[i]) + cv;
+                        const float yp = (__builtin_fabsf(sv) + sv) * 0.5f;
+                        *wp = __builtin_fmaf(bn, yp - tr.y[i], yp);
+                        tr.y[i] = yp;
+                        if (use_tol) {
+                            tr.u[i] = __builtin_fmaf(omt, tr.u[i], th * cv);
+                            if (chk && tr.act && 16 * (T - 1) + 4 * (lane >> 5) + i < m) {
+                                const float tt = cv + tr.pd[i];
+                                tvh = fmaxf(tvh, tt);
+                                tmh = fmaxf(tmh, __builtin_fabsf(cv) + __builtin_fabsf(tr.pd[i]));
+                                twm = fminf(twm, wv);
+                                tgap -= (double)wv * (double)tt;
+                                tvz = fmaxf(tvz, tr.u[i] + tr.pd[i]);
                             }
                         }
                     }
+                    if (chk) {  // the two row groups (lanes l, l ^ 32) of each column
+                        tvz = bfly<32>(tvz, OpMax{});
+                        tvh = bfly<32>(tvh, OpMax{});
+                        tmh = bfly<32>(tmh, OpMax{});
+                        twm = bfly<32>(twm, OpMin{});
+                        tgap = bfly<32>(tgap, OpAdd{});
+                        if (lane < 32) {
+                            PanelSlot2& S = L.slots[(lane >> 4) & 1][T - 1];
+                            S.f[lane & 15] = make_float4(tvz, tvh, tmh, twm);
+                            S.gap[lane & 15] = tgap;
+                        }
+                    }
                 }
+            }
+            if constexpr (NU > 0) {
+                f32x4 acc[2];
+                ++hgen;
                 if constexpr (ROLE == 1)
                     handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA2, L.Zh[p0], voff_r, lane, aph, hs, hgen);
                 if constexpr (ROLE == 2)
@@ -1440,29 +1485,25 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
         L.hdrop = DROP && blockIdx.x == 0;  // tests: workgroup 0 drops one post
     }
     if (threadIdx.x < 16) L.gred[threadIdx.x] = 0.0f;
-    if constexpr (TL) {  // the tail rows' A operands: fragment (kb, T-1, 16 j + r) -> TA[g][r][j][kb]
+    if constexpr (TL) {  // the tail rows' A operands: row 16 (T-1) + r sits in fragment lane 16 j + pi16(r)
         if (pair) {
             const float4* F = static_cast<const float4*>(a.frag);
             for (int e = threadIdx.x; e < 2 * 8 * 4 * T; e += blockDim.x) {
                 const int g = e / (8 * 4 * T), r = (e / (4 * T)) % 8, j = (e / T) % 4, kb = e % T;
-                L.TA[g][r][j][kb] = F[(size_t)g * T * T * 64 + ((size_t)kb * T + (T - 1)) * 64 + 16 * j + r];
+                L.TA[g][r][j][kb] = F[(size_t)g * T * T * 64 + ((size_t)kb * T + (T - 1)) * 64 + 16 * j + pi16(r)];
             }
         }
     }
     __syncthreads();
     if constexpr (TL) {
-        if (pair) {  // 24 chains, 6 per SIMD: waves 0..3 singles of tiles T-5, T-4 with the tail relay
-            // pieces (the oldest wave of each SIMD), 4..7 singles of tiles T-3, T-2, 8..15 doubles of
-            // tiles 0..T-6 (TailPair)
-            constexpr int S0 = T - 5;
+        if (pair) {  // waves 0..3 (the oldest of each SIMD): the tail relay pieces, no sixteen-row chain;
+            // 4..15: doubles of tiles 0..T-2 (24 chains, 6 per SIMD; TailPair)
             switch (w0) {
-                case 0: panel2_run<T, 1, 0, 0, 0, false, KQ, false, 0>(a, L, S0, 0, true, items, count); break;
-                case 1: panel2_run<T, 1, 0, 0, 0, false, KQ, false, 1>(a, L, S0, 1, true, items, count); break;
-                case 2: panel2_run<T, 1, 0, 0, 0, false, KQ, false, 2>(a, L, S0 + 1, 0, true, items, count); break;
-                case 3: panel2_run<T, 1, 0, 0, 0, false, KQ, false, 3>(a, L, S0 + 1, 1, true, items, count); break;
-                default:
-                    if (w0 < 8) panel2_run<T, 1, 0, 0, 0, false, KQ>(a, L, S0 + 2 + ((w0 - 4) >> 1), w0 & 1, true, items, count);
-                    else panel2_run<T, 2, 0, 0, 0, false, KQ>(a, L, w0 - 8, 0, true, items, count);
+                case 0: panel2_run<T, 0, 0, 0, 0, false, KQ, false, 0>(a, L, 0, 0, true, items, count); break;
+                case 1: panel2_run<T, 0, 0, 0, 0, false, KQ, false, 1>(a, L, 0, 0, true, items, count); break;
+                case 2: panel2_run<T, 0, 0, 0, 0, false, KQ, false, 2>(a, L, 0, 0, true, items, count); break;
+                case 3: panel2_run<T, 0, 0, 0, 0, false, KQ, false, 3>(a, L, 0, 0, true, items, count); break;
+                default: panel2_run<T, 2, 0, 0, 0, false, KQ>(a, L, w0 - 4, 0, true, items, count);
             }
         } else {  // one panel: the relay layout of tile T-1 (as the hand-off branch below)
             using H = Handoff<T>;
