@@ -330,7 +330,6 @@ int gpad_set_option(gpad_handle_t h, int option, int value) {
             return set(t.flat_waves, 0, 16, def.flat_waves);
         case GPAD_OPT_FLAT_A_LDS: return set(t.flat_a_lds, 0, 1, def.flat_a_lds);
         case GPAD_OPT_DEBUG_DROP_HANDOFF: return set(t.debug_drop_handoff, 0, 1, def.debug_drop_handoff);
-        case GPAD_OPT_PAIR_TAIL: return set(t.pair_tail, 0, 1, def.pair_tail);
         default: return fail(GPAD_ERR_INVALID, "gpad_set_option: unknown option");
     }
 }

@@ -671,8 +671,6 @@ struct Panel2Lds {
     float4 Gp[2][T * 64];  //                            g_P rows
     float4 Pd[2][T * 64];  //                            p_D rows
     PanelSlot2 slots[2][T];
-    float4 TA[2][8][4][T];  // tail layout (TailPair): rows 16 (T-1) + r of each GEMM's matrix, [r][j][kb] =
-                            // fragment (kb, tile T-1, lane 16 j + pi16(r)), components q -> k = 16 kb + 4 q + j
     float4 hand[3][64];    // hand-off accumulators
     int hflag[3];          // hand-off generation per slot
     int herr;              // a wait expired (handoff_wait): reported to the run's error word at exit
@@ -757,130 +755,6 @@ __device__ __forceinline__ void handoff_take(Panel2Lds<T>& L, __amdgpu_buffer_rs
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Tail pair layout (TailPair; T = 13, 192 < n, m <= 200, last k-block KQ <= 2).  The pairs' 16x16x4
-// tiles cover 208 rows; tile T-1 holds only 200 - 192 = 8 real rows, so two of the 26 chains per
-// GEMM are half padding.  Here tiles 0..T-2 run as before (24 chains: 6 per SIMD, no hand-off) and
-// the last 8 rows of BOTH panels run as one v_mfma_f32_4x4x1_16b_f32 chain, 16 blocks of 4 rows x 4
-// instances, no padding:
-//     D[lane][i] += A[r8(lane)][k] * x[P, C][k],   lane -> panel P = (lane >> 4) & 1, column
-//     C = lane & 15, row group rb = lane >> 5; register i <-> row 16 (T-1) + 4 rb + i
-// (A_b[i] comes from lane 4 b + i, B_b[j] from lane 4 b + j, b = 8 rb + 4 P + (C >> 2)).  Each step
-// is one fused multiply-add per output, ascending k: bitwise the sequential fmaf chain, as the
-// 16x16x4 chains (profiles/r01_mfma4x4.txt: 0 of 256 differ).  The chain costs 200 x ~10 MFMA-pipe
-// cycles against 2 x 52 x ~36 for the two half-empty 16x16x4 chains; it runs as a relay of four
-// pieces, one per SIMD (k-blocks [0,4) [4,7) [7,10) [10,T)), on the oldest wave of each SIMD at
-// raised priority, handed on through the LDS hand-off slots; the last piece's wave keeps the tail
-// rows' state (z, y, u, g_P, p_D of its four outputs) and runs their epilogues, test partials,
-// verification chains and carries.  A operands come from LDS (TA, filled from the fragment image at
-// kernel start), B operands straight from the panels' fragment vectors.
-__device__ __forceinline__ float f4c(const float4& v, int q) {  // component q (q constant once unrolled)
-    return q == 0 ? v.x : (q == 1 ? v.y : (q == 2 ? v.z : v.w));
-}
-struct TailRows {  // the tail owner's per-lane state: rows 16 (T-1) + 4 rb + i of instance (P, C)
-    float z[4], y[4], u[4], gp[4], pd[4];
-    int inst;
-    bool act;
-};
-
-template <int T, int KQ, int KB0, int KB1>
-__device__ __forceinline__ void tail_chain(const float4 (&TA)[8][4][T], const float4* B, int lane, f32x4& acc) {
-    const int r8 = 4 * (lane >> 5) + (lane & 3);
-    const float4* Bp = B + ((lane >> 4) & 1) * (T * 64) + (lane & 15);
-#pragma unroll
-    for (int kb = KB0; kb < KB1; ++kb) {
-        float4 a4[4], b4[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            a4[j] = TA[r8][j][kb];
-            b4[j] = Bp[kb * 64 + 16 * j];
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            if (kb + 1 < T || q < KQ) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(f4c(a4[j], q), f4c(b4[j], q), acc, 0, 0, 0);
-            }
-        }
-        asm volatile("" : "+v"(acc)::"memory");
-    }
-}
-
-// the relay piece TP of one GEMM (g = 0: -ML, B = w; g = 1: G_L, B = zhat); the last piece returns
-// the finished accumulator to its wave.  The relay is the sequential path of the layout (its MFMAs
-// wait behind the other waves' 16x16x4 ones), so a piece loads its first k-block's operands before
-// it waits for its predecessor, keeps one k-block of operands in flight, and spins on the flag
-// without sleeping.
-template <int T, int KQ, int TP>
-__device__ __forceinline__ f32x4 tail_piece(Panel2Lds<T>& L, int g, const float4* B, int lane, int gen) {
-    constexpr int KB0 = TP == 0 ? 0 : (TP == 1 ? 4 : (TP == 2 ? 7 : 10));
-    constexpr int KB1 = TP == 0 ? 4 : (TP == 1 ? 7 : (TP == 2 ? 10 : T));
-    const int r8 = 4 * (lane >> 5) + (lane & 3);
-    const float4* Bp = B + ((lane >> 4) & 1) * (T * 64) + (lane & 15);
-    const float4 (&TA)[8][4][T] = L.TA[g];
-    float4 a4[2][4], b4[2][4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        a4[0][j] = TA[r8][j][KB0];
-        b4[0][j] = Bp[KB0 * 64 + 16 * j];
-    }
-    f32x4 acc = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    if constexpr (TP > 0) {
-        for (int s = 0;; ++s) {
-            if (__hip_atomic_load(&L.hflag[TP - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == gen) break;
-            if (s == (1 << 22)) {  // (bounded as handoff_wait: an expired wait fails the run)
-                L.herr = 1;
-                break;
-            }
-        }
-        asm volatile("" ::: "memory");
-        const float4 hv = L.hand[TP - 1][lane];
-        acc = f32x4{hv.x, hv.y, hv.z, hv.w};
-    }
-    __builtin_amdgcn_s_setprio(3);
-#pragma unroll
-    for (int kb = KB0; kb < KB1; ++kb) {
-        const int cur = (kb - KB0) & 1, nxt = cur ^ 1;
-        if (kb + 1 < KB1) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                a4[nxt][j] = TA[r8][j][kb + 1];
-                b4[nxt][j] = Bp[(kb + 1) * 64 + 16 * j];
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            if (kb + 1 < T || q < KQ) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    acc = __builtin_amdgcn_mfma_f32_4x4x1f32(f4c(a4[cur][j], q), f4c(b4[cur][j], q), acc, 0, 0, 0);
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    if constexpr (TP < 3) handoff_post(L, TP, gen, lane, acc);
-    __builtin_amdgcn_s_setprio(0);
-    return acc;
-}
-
-// the whole tail chain on the owner alone (the seed and verification GEMMs)
-template <int T, int KQ>
-__device__ __forceinline__ f32x4 tail_full(Panel2Lds<T>& L, int g, const float4* B, int lane) {
-    f32x4 acc = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    tail_chain<T, KQ, 0, T>(L.TA[g], B, lane, acc);
-    return acc;
-}
-
-// one component of a fragment vector: row 16 (T-1) + 4 q + j of panel P's column C sits in
-// component q of float4 (T-1) 64 + 16 j + C; the tail owner's row 4 rb + i is (q, j) = (rb, i)
-template <int T>
-__device__ __forceinline__ float* tail_slot(float4* V, int lane, int i) {
-    return reinterpret_cast<float*>(V + ((lane >> 4) & 1) * (T * 64) + (T - 1) * 64 + 16 * i + (lane & 15)) +
-           (lane >> 5);
-}
-
 // Hand-off roles (Handoff): 0 none; 1 pair helper (NU = 1: blocks [KB0, KB1) of tile t-1 into
 // slot hs.out, then its own chain); 2 receiver (NU = 1: its own chain from block KB0, slot hs.in);
 // 3 relay (NU = 0: blocks [KB0, KB1) of tile t from slot hs.in, or zero, into slot hs.out).
@@ -889,15 +763,10 @@ __device__ __forceinline__ float* tail_slot(float4* V, int lane, int i) {
 // GEMMs (16 (T-1) < n, m <= 16 T) whose last k-block issues KQ steps in both: no runtime kq tests
 // (scalar branches whose conditions the compiler spilled to VGPR lanes) and no short-chain paths.
 // DROP: the fault-injection instantiation (handoff_piece).
-// TP >= 0: TailPair layout, this wave (no sixteen-row chain) runs relay piece TP of the 4x4x1 tail
-// chain (TP = 3: and owns the tail rows).
-template <int T, int NU, int ROLE = 0, int KB0 = 0, int KB1 = 0, bool PRIO = false, int KQ = 0, bool DROP = false,
-          int TP = -1>
+template <int T, int NU, int ROLE = 0, int KB0 = 0, int KB1 = 0, bool PRIO = false, int KQ = 0, bool DROP = false>
 __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<T>& L, int t, int p0,
                                            bool pair, int items, int count, HoSlots hs = HoSlots{-1, -1}) {
     static_assert(ROLE == 0 || (Handoff<T>::on && (ROLE == 3 ? NU == 0 : NU == 1)), "hand-off roles");
-    static_assert(TP < 0 || (NU == 0 && ROLE == 0 && T == 13 && KQ > 0 && KQ <= 2), "tail pieces");
-    constexpr bool OWN = TP == 3;  // the tail owner
     const int lane = threadIdx.x & 63;
     const int j = lane >> 4, c = lane & 15;
     const int n = a.n, m = a.m, N = a.N, K = a.check_every;
@@ -921,8 +790,6 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
     const bool on1 = FULL || 16 * t < n, on2 = FULL || 16 * t < m;
     const int voff_r = voff - 1024;  // helper: the receiver's tile t - 1 (Handoff)
     int hgen = 0;                    // hand-off generation, counted alike by helper and receiver
-    int tgen = 0;                    // tail relay generation (one per GEMM), counted alike by the pieces
-    TailRows tr;                     // OWN: the tail rows' state
     float gmx = 0.0f;                // max |g| over the rows this lane loads (gmax_part)
 
     for (int it = blockIdx.x; it < items; it += gridDim.x) {
@@ -973,33 +840,6 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             L.Wl[pq][slot] = make_float4(wv[0], wv[1], wv[2], wv[3]);
             if (fresh && use_tol) L.Zh[pq][slot] = make_float4(z[q][0], z[q][1], z[q][2], z[q][3]);
         }
-        if constexpr (OWN) {  // the tail rows of both panels' columns: lane -> (P, C, rb)
-            const int k = 16 * (2 * it + ((lane >> 4) & 1)) + (lane & 15);
-            tr.act = k < count;
-            tr.inst = tr.act ? (a.idx_in ? a.idx_in[k] : k) : 0;
-            const size_t b = (size_t)tr.inst;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int row = 16 * (T - 1) + 4 * (lane >> 5) + i;
-                const bool okn = tr.act && row < n, okm = tr.act && row < m;
-                tr.z[i] = okn ? a.z[b * n + row] : 0.0f;
-                tr.gp[i] = okn ? a.gP[b * a.ld_gP + row] : 0.0f;
-                tr.y[i] = okm ? a.y[b * m + row] : 0.0f;
-                const float gr = okm ? a.g[b * a.ld_g + row] : 0.0f;
-                tr.pd[i] = (float)(a.gscale * (double)gr);
-                gmx = absmax_nan(gmx, gr);
-                float wv;
-                if (fresh) {
-                    wv = __builtin_fmaf(a.beta[0], tr.y[i] - tr.y[i], tr.y[i]);
-                    tr.u[i] = 0.0f;
-                } else {
-                    wv = okm ? a.wc[b * m + row] : 0.0f;
-                    tr.u[i] = okm && use_tol ? a.uc[b * m + row] : 0.0f;
-                }
-                *tail_slot<T>(L.Wl[0], lane, i) = wv;
-                if (fresh && use_tol) *tail_slot<T>(L.Zh[0], lane, i) = tr.z[i];
-            }
-        }
         if (fresh && use_tol) {  // u = G_L z_{-1} -- zero, and no GEMM, when every z_{-1} is zero
             // (a cold start: every chain step fma(G_L, 0, +0) gives +0, so u = +0 exactly)
             bool nz = false;
@@ -1009,23 +849,12 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
 #pragma unroll
                     for (int r = 0; r < 4; ++r) nz = nz || z[q][r] != 0.0f;
             }
-            if constexpr (OWN) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) nz = nz || tr.z[i] != 0.0f;
-            }
             const bool wnz = __ballot(nz) != 0ull;
             if (lane == 0) L.znz[threadIdx.x >> 6] = wnz ? 1 : 0;
             __syncthreads();
             int anynz = 0;
 #pragma unroll
             for (int i = 0; i < 16; ++i) anynz |= L.znz[i];
-            if constexpr (OWN) {
-                if (anynz) {
-                    const f32x4 cu = tail_full<T, KQ>(L, 1, L.Zh[0], lane);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) tr.u[i] = cu[i];
-                }
-            }
             if constexpr (NU > 0) {
                 if (anynz) {
                     f32x4 c0, c1;
@@ -1062,18 +891,6 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             const float omt = 1.0f - th;
             GPAD_STAMP_AT(0);
             // ---- GEMM 1 + epilogue: zhat = -ML w - g_P (8b), z = (1-th) z + th zhat (8c) ----
-            if constexpr (TP >= 0) {  // the tail relay's piece
-                ++tgen;
-                const f32x4 ta = tail_piece<T, KQ, TP>(L, 0, L.Wl[0], lane, tgen);
-                if constexpr (OWN) {  // 8b / 8c of the tail rows
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const float h = ta[i] - tr.gp[i];
-                        *tail_slot<T>(L.Zh[0], lane, i) = h;
-                        tr.z[i] = __builtin_fmaf(omt, tr.z[i], th * h);
-                    }
-                }
-            }
             if constexpr (NU > 0) {
                 f32x4 acc[2];
                 ++hgen;
@@ -1125,46 +942,6 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 wmin[q] = INFINITY;
                 magh[q] = 0.0f;
                 gap[q] = 0.0;
-            }
-            if constexpr (TP >= 0) {
-                ++tgen;
-                const f32x4 tc = tail_piece<T, KQ, TP>(L, 1, L.Zh[0], lane, tgen);
-                if constexpr (OWN) {  // 8d / 8a of the tail rows, and their test partials
-                    float tvz = -INFINITY, tvh = -INFINITY, twm = INFINITY, tmh = 0.0f;
-                    double tgap = 0.0;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        float* wp = tail_slot<T>(L.Wl[0], lane, i);
-                        const float wv = *wp, cv = tc[i];
-                        const float sv = (wv + tr.pd[i]) + cv;
-                        const float yp = (__builtin_fabsf(sv) + sv) * 0.5f;
-                        *wp = __builtin_fmaf(bn, yp - tr.y[i], yp);
-                        tr.y[i] = yp;
-                        if (use_tol) {
-                            tr.u[i] = __builtin_fmaf(omt, tr.u[i], th * cv);
-                            if (chk && tr.act && 16 * (T - 1) + 4 * (lane >> 5) + i < m) {
-                                const float tt = cv + tr.pd[i];
-                                tvh = fmaxf(tvh, tt);
-                                tmh = fmaxf(tmh, __builtin_fabsf(cv) + __builtin_fabsf(tr.pd[i]));
-                                twm = fminf(twm, wv);
-                                tgap -= (double)wv * (double)tt;
-                                tvz = fmaxf(tvz, tr.u[i] + tr.pd[i]);
-                            }
-                        }
-                    }
-                    if (chk) {  // the two row groups (lanes l, l ^ 32) of each column
-                        tvz = bfly<32>(tvz, OpMax{});
-                        tvh = bfly<32>(tvh, OpMax{});
-                        tmh = bfly<32>(tmh, OpMax{});
-                        twm = bfly<32>(twm, OpMin{});
-                        tgap = bfly<32>(tgap, OpAdd{});
-                        if (lane < 32) {
-                            PanelSlot2& S = L.slots[(lane >> 4) & 1][T - 1];
-                            S.f[lane & 15] = make_float4(tvz, tvh, tmh, twm);
-                            S.gap[lane & 15] = tgap;
-                        }
-                    }
-                }
             }
             if constexpr (NU > 0) {
                 f32x4 acc[2];
@@ -1294,16 +1071,6 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                             L.Zh[p0 + q][slot] = make_float4(z[q][0], z[q][1], z[q][2], z[q][3]);
                         }
                     }
-                    if constexpr (OWN) {
-                        const bool outB = tr.act && ((m2 >> (16 * ((lane >> 4) & 1) + (lane & 15))) & 1u);
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            float* zp = tail_slot<T>(L.Zh[0], lane, i);
-                            const int row = 16 * (T - 1) + 4 * (lane >> 5) + i;
-                            if (outB && row < n) a.z[(size_t)tr.inst * n + row] = *zp;
-                            *zp = tr.z[i];
-                        }
-                    }
                     __syncthreads();
                     if constexpr (NU > 0) {
                         f32x4 cz[2];
@@ -1327,22 +1094,6 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                             if (j == 0)  // the stage-1 reads of every wave precede the barrier above
                                 L.slots[p0 + q][t].f[c] = make_float4(vc, vc, mc, INFINITY);
                         }
-                    }
-                    if constexpr (OWN) {  // G_L z of the tail rows, on the owner alone
-                        const f32x4 cz = tail_full<T, KQ>(L, 1, L.Zh[0], lane);
-                        const bool nom = tr.act && ((mA >> (16 * ((lane >> 4) & 1) + (lane & 15))) & 1u);
-                        float vc = -INFINITY, mc = 0.0f;
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            if (nom && 16 * (T - 1) + 4 * (lane >> 5) + i < m) {
-                                tr.u[i] = cz[i];
-                                vc = fmaxf(vc, cz[i] + tr.pd[i]);
-                                mc = fmaxf(mc, __builtin_fabsf(cz[i]) + __builtin_fabsf(tr.pd[i]));
-                            }
-                        }
-                        vc = bfly<32>(vc, OpMax{});
-                        mc = bfly<32>(mc, OpMax{});
-                        if (lane < 32) L.slots[(lane >> 4) & 1][T - 1].f[lane & 15] = make_float4(vc, vc, mc, INFINITY);
                     }
                     __syncthreads();
                     bool ver = false;
@@ -1379,21 +1130,6 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                     }
                 }
             }
-            if constexpr (OWN) {  // the tail rows of finished columns
-                const int bit = 16 * ((lane >> 4) & 1) + (lane & 15);
-                const int cdq = ((m1 >> bit) & 1u) ? 1 : (((m2 >> bit) & 1u) ? 2 : 0);
-                if (tr.act && (cdq != 0 || v >= N)) {
-                    const size_t b = (size_t)tr.inst;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int row = 16 * (T - 1) + 4 * (lane >> 5) + i;
-                        if (row < n && (cdq != 2 || zh_out))
-                            a.z[b * n + row] = cdq == 2 ? *tail_slot<T>(L.Zh[0], lane, i) : tr.z[i];
-                        if (row < m) a.y[b * m + row] = tr.y[i];
-                    }
-                    tr.act = false;
-                }
-            }
             live &= ~(m1 | m2);
             if (v >= N) live = 0u;
             if (v >= a.v_end || live == 0u) break;
@@ -1424,21 +1160,6 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 }
             }
         }
-        if constexpr (OWN) {
-            if (carry && tr.act && v >= a.v_end) {  // park the tail rows
-                const size_t b = (size_t)tr.inst;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int row = 16 * (T - 1) + 4 * (lane >> 5) + i;
-                    if (row < n) a.z[b * n + row] = tr.z[i];
-                    if (row < m) {
-                        a.y[b * m + row] = tr.y[i];
-                        a.wc[b * m + row] = *tail_slot<T>(L.Wl[0], lane, i);
-                        if (use_tol) a.uc[b * m + row] = tr.u[i];
-                    }
-                }
-            }
-        }
         __syncthreads();
     }
     if (a.gmax_part) {  // this wave's max |g| -> L.gred (reduced by the kernel at exit)
@@ -1452,12 +1173,9 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
 // (6.16 vs 5.98 us per iteration at 4 panels, profiles/r03_single_mode_ab.txt).  DROP: the
 // test-only fault-injection instantiation (GPAD_OPT_DEBUG_DROP_HANDOFF), launched instead of the
 // product kernel only while that option is set, so the product kernel carries no trace of it.
-// TL: the TailPair layout for the pair phases (T = 13, KQ <= 2: 192 < n, m <= 200); one-panel phases
-// run the relay layout as without it.
-template <int T, int KQ, bool DROP = false, bool TL = false>
+template <int T, int KQ, bool DROP = false>
 __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
     static_assert(T > 8 && T <= 16, "panel pairs need 8 < T <= 16");
-    static_assert(!TL || (T == 13 && KQ > 0 && KQ <= 2 && !DROP), "tail layout shape");
     constexpr int D = 2 * T - 16;  // double waves
     __shared__ Panel2Lds<T> L;
     const int count = a.count_in ? __builtin_amdgcn_readfirstlane(*a.count_in) : a.batch;
@@ -1485,36 +1203,8 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
         L.hdrop = DROP && blockIdx.x == 0;  // tests: workgroup 0 drops one post
     }
     if (threadIdx.x < 16) L.gred[threadIdx.x] = 0.0f;
-    if constexpr (TL) {  // the tail rows' A operands: row 16 (T-1) + r sits in fragment lane 16 j + pi16(r)
-        if (pair) {
-            const float4* F = static_cast<const float4*>(a.frag);
-            for (int e = threadIdx.x; e < 2 * 8 * 4 * T; e += blockDim.x) {
-                const int g = e / (8 * 4 * T), r = (e / (4 * T)) % 8, j = (e / T) % 4, kb = e % T;
-                L.TA[g][r][j][kb] = F[(size_t)g * T * T * 64 + ((size_t)kb * T + (T - 1)) * 64 + 16 * j + pi16(r)];
-            }
-        }
-    }
     __syncthreads();
-    if constexpr (TL) {
-        if (pair) {  // waves 0..3 (the oldest of each SIMD): the tail relay pieces, no sixteen-row chain;
-            // 4..15: doubles of tiles 0..T-2 (24 chains, 6 per SIMD; TailPair)
-            switch (w0) {
-                case 0: panel2_run<T, 0, 0, 0, 0, false, KQ, false, 0>(a, L, 0, 0, true, items, count); break;
-                case 1: panel2_run<T, 0, 0, 0, 0, false, KQ, false, 1>(a, L, 0, 0, true, items, count); break;
-                case 2: panel2_run<T, 0, 0, 0, 0, false, KQ, false, 2>(a, L, 0, 0, true, items, count); break;
-                case 3: panel2_run<T, 0, 0, 0, 0, false, KQ, false, 3>(a, L, 0, 0, true, items, count); break;
-                default: panel2_run<T, 2, 0, 0, 0, false, KQ>(a, L, w0 - 4, 0, true, items, count);
-            }
-        } else {  // one panel: the relay layout of tile T-1 (as the hand-off branch below)
-            using H = Handoff<T>;
-            if (ho && w == T - 1) panel2_run<T, 1, 2, H::R2, 0, true, 0>(a, L, w, 0, false, items, count, HoSlots{1, -1});
-            else if (ho && w == T) panel2_run<T, 0, 3, 0, H::R1, true, 0>(a, L, T - 1, 0, false, items, count, HoSlots{-1, 0});
-            else if (ho && w == T + 1)
-                panel2_run<T, 0, 3, H::R1, H::R2, true, 0>(a, L, T - 1, 0, false, items, count, HoSlots{0, 1});
-            else if (w < T) panel2_run<T, 1, 0, 0, 0, false, 0>(a, L, w, 0, false, items, count);
-            else panel2_run<T, 0, 0, 0, 0, false, 0>(a, L, 0, 0, false, items, count);
-        }
-    } else if constexpr (Handoff<T>::on) {
+    if constexpr (Handoff<T>::on) {
         using H = Handoff<T>;
         if (pair) {  // waves 12, 13 (SIMDs 0, 1; tile T-2) receive from 14, 15 (SIMDs 2, 3; tile T-1)
             if (w < D) panel2_run<T, 2, 0, 0, 0, false, KQ, DROP>(a, L, w, 0, true, items, count);
@@ -1904,10 +1594,6 @@ static void launch_panel_kernel(const SolveArgs<float>& a, int grid, hipStream_t
                 else hipLaunchKernelGGL((gpad_panel2_kernel<T, 0, true>), dim3(grid), dim3(1024), 0, s, a);
                 return;
             }
-            // 192 < n, m <= 200: the pair phases on the TailPair layout (GPAD_OPT_PAIR_TAIL, default on)
-            const bool tl = full && kq1 <= 2 && (!a.tune || a.tune->pair_tail);
-            if (tl && kq1 == 1) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 1, false, true>), dim3(grid), dim3(1024), 0, s, a); return; }
-            if (tl && kq1 == 2) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 2, false, true>), dim3(grid), dim3(1024), 0, s, a); return; }
             if (full && kq1 == 1) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 1>), dim3(grid), dim3(1024), 0, s, a); return; }
             if (full && kq1 == 2) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 2>), dim3(grid), dim3(1024), 0, s, a); return; }
             if (full && kq1 == 3) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 3>), dim3(grid), dim3(1024), 0, s, a); return; }

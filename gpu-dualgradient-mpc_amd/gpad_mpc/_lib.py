@@ -48,7 +48,6 @@ OPT_PHASE_LEN, OPT_FINISH_THRESH, OPT_PLAN, OPT_PHASED, OPT_LPT = 1, 2, 3, 4, 6
 OPT_PANEL_MAX_GRID, OPT_DUO_MAX_GRID, OPT_FLAT_PANEL_MIN, OPT_FLAT_PANELS = 7, 8, 9, 10
 OPT_FLAT_WAVES, OPT_FLAT_A_LDS = 11, 12
 OPT_DEBUG_DROP_HANDOFF = 16  # test-only fault injection
-OPT_PAIR_TAIL = 17  # 192 < n, m <= 200 pairs with the 4x4x1 tail chain (default 1)
 OPT_RETIRED = (5, 13, 14, 15)  # finisher kind, solo finisher workgroups, plan finisher cost (0.3);
 # condensed panels (0.4, with the condensed operator)
 OPTIONS = {"phase_len": OPT_PHASE_LEN, "finish_thresh": OPT_FINISH_THRESH, "plan": OPT_PLAN,
@@ -56,7 +55,7 @@ OPTIONS = {"phase_len": OPT_PHASE_LEN, "finish_thresh": OPT_FINISH_THRESH, "plan
            "panel_max_grid": OPT_PANEL_MAX_GRID, "duo_max_grid": OPT_DUO_MAX_GRID,
            "flat_panel_min": OPT_FLAT_PANEL_MIN, "flat_panels": OPT_FLAT_PANELS,
            "flat_waves": OPT_FLAT_WAVES, "flat_a_lds": OPT_FLAT_A_LDS,
-           "debug_drop_handoff": OPT_DEBUG_DROP_HANDOFF, "pair_tail": OPT_PAIR_TAIL}
+           "debug_drop_handoff": OPT_DEBUG_DROP_HANDOFF}
 
 FILE_ROWMAJOR, FILE_FLIPPED, FILE_FLAT = 0, 1, 2
 

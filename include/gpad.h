@@ -379,9 +379,6 @@ int gpad_schedule(int N, int kind, double* theta, double* beta);
 #define GPAD_OPT_FLAT_PANELS 10    /* panels per flat-panel workgroup, 1..4 (0 = auto, default)    */
 #define GPAD_OPT_FLAT_WAVES 11     /* flat-panel workgroup waves: 0 auto (default), 8 or 16         */
 #define GPAD_OPT_FLAT_A_LDS 12     /* 1: flat fragment image staged in LDS when it fits (default)  */
-#define GPAD_OPT_PAIR_TAIL 17        /* 1 (default): panel pairs of 192 < n, m <= 200 run the last 8 rows
-                                      * of both panels as one 4x4x1 MFMA chain (no padded tile rows);
-                                      * 0: sixteen-row tiles throughout                               */
 #define GPAD_OPT_DEBUG_DROP_HANDOFF 16 /* test only (fault injection): 1 = every panel solve that
                                     * uses the chain hand-off withholds its first post, so the
                                     * receiver's bounded wait expires and the run ends in

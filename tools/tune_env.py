@@ -19,7 +19,6 @@ _MAP = {  # env name -> (option, value transform)
     "GPAD_NO_LPT": ("lpt", lambda v: 0),
     "GPAD_PANEL_MAX_GRID": ("panel_max_grid", int),
     "GPAD_DUO_MAX_GRID": ("duo_max_grid", int),
-    "GPAD_PAIR_TAIL": ("pair_tail", int),
     "GPAD_FLAT_PANEL_MIN": ("flat_panel_min", int),
     "GPAD_FLAT_PANELS": ("flat_panels", int),
     "GPAD_FLAT_WAVES": ("flat_waves", int),
