@@ -12,6 +12,10 @@ per slot on MFMA, a slot's last column on DPP.  The current C4 plan is phase 2 o
 (260 -> 290, 6.9 us per iteration) then the duo.  Prints the tail length (us) per scheme; the
 measured duo is ~10-20 % above the model (its step overhead is larger than OV), the measured quad
 far above (profiles/r03_quad_finisher.txt: 1.1-3.5k cycles of step overhead, not 850).
+Round 4 (profiles/r04_duo_solo.txt): two live slots 2.27 us per slot-iteration, one live slot (solo
+mode) 1.63, the resident kernel 1.31-1.33 in tol mode; a per-CU simulation with those speeds gives
+solo mode -8 to -10 us over the old one-slot speed (1.80) and migrating a busy CU's second slot to an
+idle CU once the queue drains -3 to -27 us (seeds 0, 1).
 """
 import heapq
 import os
