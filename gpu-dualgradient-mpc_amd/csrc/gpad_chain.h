@@ -274,6 +274,7 @@ __device__ __forceinline__ float chain_regs(const float (&r)[K], const float* v)
 }
 
 constexpr int kResidentMaxThreads = 512;
+static_assert(kResidentMaxThreads / 64 <= 8, "check_stage1 / check_verify reduce one slot per lane over lanes 0..7");
 constexpr int kResidentMaxRow = 208;
 
 // chain-length buckets (multiples of 32 up to 192, then 200 and the 208 cap)

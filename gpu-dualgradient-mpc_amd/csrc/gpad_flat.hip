@@ -32,6 +32,7 @@
 namespace gpad {
 
 constexpr int kFlatBlock = 256;
+static_assert(kFlatBlock / 64 <= 8, "test slots: one per lane over lanes 0..7 (gpad_chain.h check_stage1)");
 constexpr size_t kFlatStageMax = 64 * 1024;  // bytes of flat matrices staged in LDS
 
 

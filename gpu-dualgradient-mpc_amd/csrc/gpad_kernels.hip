@@ -38,6 +38,7 @@ namespace gpad {
 // gpad_stream_kernel
 // =========================================================================================
 constexpr int kStreamBlock = 256;
+static_assert(kStreamBlock / 64 <= 8, "test slots: one per lane over lanes 0..7 (gpad_chain.h check_stage1)");
 constexpr int kUnrollK = 8;
 
 template <typename T>
