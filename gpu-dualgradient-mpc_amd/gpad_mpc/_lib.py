@@ -48,8 +48,9 @@ OPT_PHASE_LEN, OPT_FINISH_THRESH, OPT_PLAN, OPT_PHASED, OPT_LPT = 1, 2, 3, 4, 6
 OPT_PANEL_MAX_GRID, OPT_DUO_MAX_GRID, OPT_FLAT_PANEL_MIN, OPT_FLAT_PANELS = 7, 8, 9, 10
 OPT_FLAT_WAVES, OPT_FLAT_A_LDS = 11, 12
 OPT_DEBUG_DROP_HANDOFF = 16  # test-only fault injection
-OPT_RETIRED = (5, 13, 14, 15)  # finisher kind, solo finisher workgroups, plan finisher cost (0.3);
-# condensed panels (0.4, with the condensed operator)
+OPT_RETIRED = (5, 13, 14, 15, 17)  # finisher kind, solo finisher workgroups, plan finisher cost (0.3);
+# condensed panels (0.4, with the condensed operator); 17: the opt-in pair layouts measured in round 4
+# and left out of the product (W32, TailPair)
 OPTIONS = {"phase_len": OPT_PHASE_LEN, "finish_thresh": OPT_FINISH_THRESH, "plan": OPT_PLAN,
            "phased": OPT_PHASED, "lpt": OPT_LPT,
            "panel_max_grid": OPT_PANEL_MAX_GRID, "duo_max_grid": OPT_DUO_MAX_GRID,

@@ -371,7 +371,8 @@ int gpad_schedule(int N, int kind, double* theta, double* beta);
                                     * panels: from 4 panels per CU), 2: always, 0: one launch       */
 /* 5 (finisher kind), 13 (solo finisher workgroups), 15 (plan finisher cost): retired in 0.3 after
  * measuring no gain; 14 (condensed panels): removed with the condensed operator in
- * 0.4; setting them returns GPAD_ERR_INVALID                                                    */
+ * 0.4; 17: the round-4 pair layouts (W32, TailPair) measured slower and left out of 0.4; setting
+ * them returns GPAD_ERR_INVALID                                                                  */
 #define GPAD_OPT_LPT 6             /* 1: longest-predicted-first finisher queue (default)          */
 #define GPAD_OPT_PANEL_MAX_GRID 7  /* cap on the panel grid, workgroups (0 = none, default)        */
 #define GPAD_OPT_DUO_MAX_GRID 8    /* cap on the finisher grid (0 = none, default)                 */
