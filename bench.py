@@ -619,6 +619,87 @@ def closed_loop_leg(dev, batch=8192, steps=20, N=100, cpu=True, flat=False):
     return out
 
 
+def sharded_leg(dev, ndev, n=200, m=200, batch=65536, steps=6, warmup=2, max_iters=5000, tol=1e-4, devices=None):
+    """BASELINE config C4 through the library's own multi-device entry (include/gpad.h
+    gpad_group_*, the path gpad_solve_sharded caches): the 65536-instance batch resident on device
+    0, scattered to devices 0..ndev-1 by the group's RCCL clique (ncclBroadcast of the shared
+    matrices at setup, grouped ncclSend/Recv of M, g, z0, y0 per run), one shard solved per device,
+    (z*, y*) gathered back -- FRESH q/b every run, each run synchronous (wall clock around it).
+    The same inputs then go through ONE handle on device 0 (device-event time per solve): the
+    ratio is the strong-scaling speedup of the global batch, and the last run's iteration counts,
+    z* and y* must be bit-identical between the two (the shards are independent instances).
+    Run on rank 0 after every rank's timed region; skipped with fewer than 2 distinct devices
+    (``devices`` overrides the list: tests run it over [0, 0] on the peer-copy transport).
+    The reference solves one problem per process (Code/CUDA/FinalProject/main.cu:106-108)."""
+    import torch
+
+    import gpad_mpc
+    ML, G, L, _, _ = make_shard(n, m, 1, 0)
+    L32 = float(np.float32(L))
+    f32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)  # noqa: E731
+    fresh = [(f32(a), f32(b)) for a, b in make_stream(n, m, batch, warmup + steps, 99)]
+    dML, dG = f32(ML), f32(G)
+    z = torch.zeros(batch, n, device=dev)
+    y = torch.zeros(batch, m, device=dev)
+    devices = list(devices) if devices is not None else list(range(ndev))
+    it_g = np.zeros(batch, np.int32)
+    torch.cuda.synchronize(dev)
+    with gpad_mpc.GpadGroup(devices) as grp:
+        transport = grp.transport
+        grp.setup(dML, dG, L32, n=n, m=m, batch=batch, shared=True, check_every=10)
+        t = []
+        for k in range(warmup + steps):
+            z.zero_()
+            y.zero_()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            st = grp.run(z, y, *fresh[k], max_iters, tol, iters=it_g)
+            t.append(time.perf_counter() - t0)
+        zg, yg = z.clone(), y.clone()
+    group_s = sum(t[warmup:])
+    it_1 = np.zeros(batch, np.int32)
+    stream = torch.cuda.current_stream(dev)
+    with gpad_mpc.GpadSolver(dev.index or 0, stream=stream.cuda_stream) as s:
+        s.setup(dML, dG, L32, n=n, m=m, batch=batch, shared=True, check_every=10)
+        for k in range(warmup):
+            s.run(z.zero_(), y.zero_(), *fresh[k], max_iters, tol, stats=False)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for k in range(warmup, warmup + steps):
+            st1 = s.run(z.zero_(), y.zero_(), *fresh[k], max_iters, tol, iters=it_1)
+        one_s = time.perf_counter() - t0
+    same = bool(np.array_equal(it_g, it_1) and torch.equal(zg, z) and torch.equal(yg, y))
+    total = int(it_g.sum())
+    return {"config": f"C4 global batch: {batch} instances sharing ML/G, n={n}, m={m}, eps={tol}, resident on "
+                      f"device 0, gpad_group over devices {devices} ({transport}), fresh q/b every run "
+                      f"({steps} timed after {warmup})",
+            "n_devices": len(devices), "transport": transport, "kernel": st["kernel"],
+            "ms_per_solve": group_s / steps * 1e3, "qp_solves_per_s": batch * steps / group_s,
+            "last_run_iters_per_s": total / t[-1], "converged_last": st["converged"],
+            "one_gpu_ms_per_solve": one_s / steps * 1e3, "strong_scaling_speedup": one_s / group_s,
+            "bitexact_vs_one_handle": same,
+            "note": "ms_per_solve includes the scatter of M, g, z0, y0 and the gather of (z*, y*) over the "
+                    "group's transport; one_gpu_ms_per_solve is the same batches on one handle (host clock, "
+                    "stats copied each run); bitexact_vs_one_handle compares the last run's counts, z*, y*"}
+
+
+def launch_ranks(gpus, argv):
+    """``python bench.py --gpus N`` without a launcher: start the N ranks as ONE child process
+    (torch.distributed.run, one rank per GPU, rendezvous on 127.0.0.1) and return its exit status.
+    Runs before this process imports torch or touches the GPU; rank 0's JSON line reaches stdout
+    through the inherited file descriptors.  The parent never execs itself."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    sys.stdout.flush()
+    return subprocess.call(cmd)
+
+
 def make_stream(n, m, batch, count, rank, seed=0):
     """``count`` independent draws of this rank's shard for the timed steps: every step solves
     NEW problems (q, b of the SURVEY §8d generator, fresh per instance and per step), so the
@@ -655,9 +736,20 @@ def main():
     ap.add_argument("--repeat-inputs", action="store_true",
                     help="headline on the SAME inputs every step (the planner then sees its own future); "
                          "default: fresh inputs per step, the repeated-input rate reported beside it")
+    ap.add_argument("--no-sharded", action="store_true",
+                    help="N > 1: skip rank 0's gpad_group leg over devices 0..N-1 after the timed region")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) for real runs; gloo to rehearse ranks sharing one GPU")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:  # no launcher: start the ranks ourselves
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}: the launcher started a different "
+              "number of ranks than the run was asked for", file=sys.stderr)
+        sys.exit(2)
 
     import torch
     import torch.distributed as dist
@@ -678,6 +770,9 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+    # a host-side group for the end-of-run barrier: the other ranks wait off the GPU while rank 0
+    # runs its post-timing legs (the sharded leg drives every rank's device)
+    host_pg = dist.new_group(backend="gloo") if world > 1 else None
     comm_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
     stream = torch.cuda.current_stream(dev)
 
@@ -818,6 +913,15 @@ def main():
                     "gather_ms: one blocking gather of a step's (z*, y*) measured alone after the timed "
                     "regions (max over ranks)"}
 
+    # the C-ABI multi-device path on rank 0 (every rank's timed region is over, the barrier above;
+    # the other ranks wait on host_pg): the global batch over devices 0..N-1 through gpad_group
+    ndist = min(world, ndev)
+    if multi is not None:
+        multi["sharded_c4_global"] = (sharded_leg(dev, ndist, n, m) if rank == 0 and ndist >= 2 and
+                                      not args.no_sharded else
+                                      {"skipped": f"{ndist} distinct device(s) visible" if ndist < 2 else
+                                       "--no-sharded"})
+
     # CPU reference on rank 0 (all ranks' timed regions are over: the barrier above)
     ref = None
     if rank == 0 and not args.no_cpu:
@@ -945,6 +1049,7 @@ def main():
         print(json.dumps(out))
     solver.close()
     if world > 1:
+        dist.barrier(group=host_pg)
         dist.destroy_process_group()
 
 

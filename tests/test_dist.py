@@ -82,3 +82,18 @@ def test_sharded_solve_gloo_matches_single_process(tmp_path, oracle, world, tota
                                        qp.g[b].astype(np.float32), 3000, L, 1e-4)
         assert np.array_equal(res["Z"][b], z) and np.array_equal(res["Y"][b], y)
         assert res["it"][b] == it
+
+
+@pytest.mark.parametrize("gpus,world", [(2, "3"), (1, "2"), (8, "1")])
+def test_bench_rejects_gpus_world_size_mismatch(gpus, world):
+    """bench.py --gpus N under a launcher that started a different number of ranks exits non-zero
+    before touching torch or the GPU (the driver's scaling run must not silently measure fewer)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE=world, RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(gpus), "--no-cpu"],
+                       capture_output=True, text=True, timeout=60, env=env, cwd=root)
+    assert r.returncode == 2
+    assert f"--gpus {gpus} but WORLD_SIZE={world}" in r.stderr
+    assert not r.stdout.strip()

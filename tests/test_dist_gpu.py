@@ -5,8 +5,9 @@ driver's 8-GPU SCALE run uses one GPU per rank over RCCL with the same code.
 * parallel.solve_sharded + parallel.gpu_solve_fn (libgpad on each rank, C4-generator shards
   of 1100 instances each, phased panel solves to eps = 1e-4) gathered to rank 0: every
   instance bit-exact vs the oracle, iteration counts included.
-* bench.py under torch.distributed.run with 2 ranks: the JSON line's n_gpus, global batch and
-  converged count are consistent.
+* bench.py under torch.distributed.run with 2 ranks, and plain ``python bench.py --gpus 2`` (the
+  bench starts its own ranks): the JSON line's n_gpus, global batch and converged count are
+  consistent; with one device the rank-0 gpad_group leg over devices 0..N-1 reports skipped.
 """
 from __future__ import annotations
 
@@ -85,13 +86,17 @@ def test_sharded_libgpad_two_ranks_bitexact(gpu, oracle, tmp_path):
     np.testing.assert_array_equal(res["Y"], Y)
 
 
-def test_bench_two_ranks_rehearsal(gpu):
-    """bench.py as the driver launches it for N = 2 (gloo, both ranks on cuda:0)."""
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--dist-backend", "gloo", "--no-extra", "--no-cpu", "--steps", "3", "--warmup", "2",
-           "--batch", "2048"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+@pytest.mark.parametrize("launcher", ["torchrun", "self"])
+def test_bench_two_ranks_rehearsal(gpu, launcher):
+    """bench.py for N = 2 (gloo, both ranks on cuda:0): as the driver launches it under
+    torch.distributed.run, and as plain ``python bench.py --gpus 2`` (bench.py starts the ranks)."""
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--no-extra", "--no-cpu",
+            "--steps", "3", "--warmup", "2", "--batch", "2048"]
+    pre = (["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+            "--master-port", str(free_port())] if launcher == "torchrun" else [])
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, *pre, *args], capture_output=True, text=True, timeout=300, cwd=ROOT,
+                       env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
     d = json.loads(line)
@@ -105,3 +110,19 @@ def test_bench_two_ranks_rehearsal(gpu):
     assert mg["gather_ms"] > 0 and mg["drain_ms_max"] >= 0
     assert mg["gather_bytes_per_rank"] == 2048 * 400 * 4
     assert d["config"]["parallelism"] == "instance-sharded x2, gloo gather"
+    import torch
+    if torch.cuda.device_count() < 2:
+        assert "skipped" in mg["sharded_c4_global"]
+
+
+def test_bench_sharded_leg_runs_bitexact(gpu):
+    """bench.sharded_leg -- the rank-0 gpad_group leg of an N > 1 run -- over devices [0, 0] (the
+    peer-copy transport of one GPU; distinct devices use the RCCL clique): it runs, converges, and
+    the group's counts, z*, y* equal one handle's on the same fresh batches."""
+    sys.path.insert(0, ROOT)
+    import bench
+    r = bench.sharded_leg(gpu, 2, batch=4096, steps=2, warmup=1, devices=[0, 0])
+    assert r["transport"] == "peer" and r["n_devices"] == 2
+    assert r["bitexact_vs_one_handle"] is True
+    assert r["converged_last"] == 4096 and r["kernel"] == "panel"
+    assert r["ms_per_solve"] > 0 and r["one_gpu_ms_per_solve"] > 0
