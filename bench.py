@@ -936,6 +936,7 @@ def main():
         iters_per_launch = total_iters / args.steps
         F = flops_per_iter(n, m)
         achieved_tf = iters_per_launch * F / avg_kernel_s / 1e12
+        hbm_alg_gbs = bytes_per_iter_shared(n, m, B) * (iters_per_launch / B) / (ms_per_step / 1e3) / 1e9
         mean_iters = iters_per_launch / B
         util = phase_util(head["iters_host"], args.max_iters, 10, head["plan"])
         T = (max(n, m) + 15) // 16
@@ -1033,6 +1034,10 @@ def main():
             "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved_tf / FP32_PEAK_TFLOPS,
                          "traffic": traffic, "traffic_source": traffic_src,
+                         "hbm_algorithmic_gbs": hbm_alg_gbs, "hbm_algorithmic_frac": hbm_alg_gbs / HBM_PEAK_GBS,
+                         "hbm_note": "SURVEY.md §8d algorithmic bytes, 4 (2nm + B (4m + 3n)) per batch-iteration x "
+                                     "mean iterations to eps, per GPU per step time, / 8 TB/s; the shared "
+                                     "matrices are L2-resident, so HBM sees far less (traffic)",
                          "kernel_ms": avg_kernel_s * 1e3, "launches_per_solve": launches,
                          "note": "fp32 matrix-core bound (shared matrices stay in L2, traffic = "
                                  "per-instance vectors); achieved = useful flops (F = 4nm+5m+4n "

@@ -146,9 +146,15 @@ int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* dims, int n_u, const flo
  * dims.dtype / dims.memory of the bound problem; symmetric positive definite) and so enable the
  * value-function branches of Algorithm 1 (acceldualgrad.m:30-33,73,76) in later gpad_run /
  * gpad_run_state calls with tol > 0.  The QP is then min 1/2 z'Hz + f'z, G z <= g with f = H M
- * (M = H^-1 f is the vector gpad_run takes).  Those solves run on the stream kernel family (f32 or
- * f64; the latency and panel kernels do not evaluate the value functions: forcing them returns
- * GPAD_ERR_UNSUPPORTED).  H = NULL unbinds.  gpad_setup / gpad_setup_scaled unbind as well.
+ * (M = H^-1 f is the vector gpad_run takes).  Which kernel evaluates the value functions:
+ *   f64, shared matrices, n, m <= 256: the f64 MFMA panels (gpad_panel64.hip) when forced
+ *     (GPAD_KERNEL_PANEL) or under AUTO from 16 instances per CU on (gpad_host.cpp, the f64
+ *     panel branch of gpad_run); bit-identical to the f64 stream kernel, codes 3 / 4 included;
+ *   otherwise (f32, f64 below that batch, distinct matrices, larger n or m): the stream kernel.
+ * The f32 panel and the latency (resident / duo / flat) kernels do not evaluate the value
+ * functions: with H bound, forcing GPAD_KERNEL_RESIDENT, or GPAD_KERNEL_PANEL where the f64
+ * panels do not apply (f32, distinct matrices, n or m > 256), returns GPAD_ERR_UNSUPPORTED.
+ * H = NULL unbinds.  gpad_setup / gpad_setup_scaled unbind as well.
  * Replaces acceldualgrad.m's own H (the MATLAB function receives H, :1). */
 int gpad_setup_hessian(gpad_handle_t h, const void* H);
 
