@@ -9,7 +9,7 @@ Sources of truth:
   * our oracle (oracle/liboracle.so) for the Algorithm-1 (tol) runs, which the reference lacks.
 
 Inputs are stored in float64; the fp32 path receives ``x.astype(np.float32)`` of them.
-Usage:  python tests/golden/make_golden.py
+Usage:  python tests/golden/make_golden.py [--o3-only]
 """
 from __future__ import annotations
 
@@ -177,7 +177,56 @@ def make_closed_loop():
     print(f"closed_loop_battery_3x4: steps={steps}")
 
 
+def make_o3(O):
+    """End states from the reference's OTHER build, _ref/libref_seq_o3.so (seq_functions.cpp at
+    -O3 -march=x86-64-v3: GCC vectorises the products, vmulps + in-order vaddss, no FMA; the build
+    bench.py times as cpu_baseline).  The parity pin is the FMA build (libref_seq.so); these
+    fixtures state how far the HIP path is from the unfused one (tests/test_o3_parity.py):
+      * the golden sets at K = 100 (main.cu:87's N_v) and K = 1000, from zero;
+      * 16 C4-generator instances (bench.make_shard, n = m = 200) at K = 265 (the C4 mean to eps)
+        and K = 450 (its longest solves), their fp32 inputs stored with them."""
+    R3 = pyoracle.RefSeq(pyoracle.REF_O3)
+    R = pyoracle.RefSeq()
+    f32 = lambda a: np.asarray(a, np.float64).astype(np.float32)  # noqa: E731
+    out = {}
+    for name, qp in problem_set().items():
+        n, m = qp.n, qp.m
+        ML, M, G, g, L = f32(qp.ML), f32(qp.M), f32(qp.G), f32(qp.g), np.float32(qp.L)
+        MGneg, GL, pD = O.scale(ML, G, g, L)
+        th, be = O.schedule_f32(1000)
+        for K in (100, 1000):
+            z, y = R3.solve(np.zeros(n, np.float32), np.zeros(m, np.float32), MGneg, M, GL, pD, th, be, K)
+            out[f"{name}_z_{K}"], out[f"{name}_y_{K}"] = z, y
+            zf, yf = R.solve(np.zeros(n, np.float32), np.zeros(m, np.float32), MGneg, M, GL, pD, th, be, K)
+            print(f"{name} K={K}: |dz|/|z| {np.linalg.norm(z - zf) / np.linalg.norm(zf):.3g} "
+                  f"|dy|/|y| {np.linalg.norm(y - yf) / np.linalg.norm(yf):.3g} (O3 vs FMA build)")
+    sys.path.insert(0, ROOT)
+    import bench
+    ML, G, L, M, g = bench.make_shard(200, 200, 16, 0)
+    ML, G, M, g, L = f32(ML), f32(G), f32(M), f32(g), np.float32(L)
+    out.update(c4_ML=ML, c4_G=G, c4_M=M, c4_g=g, c4_L=L)
+    MGneg, GL, _ = O.scale(ML, G, g[0], L)
+    PD = O.scale_vec(g, L)
+    th, be = O.schedule_f32(450)
+    for K in (265, 450):
+        Z = np.zeros((16, 200), np.float32)
+        Y = np.zeros((16, 200), np.float32)
+        Zf, Yf = Z.copy(), Y.copy()
+        for i in range(16):
+            Z[i], Y[i] = R3.solve(Z[i], Y[i], MGneg, M[i], GL, PD[i], th, be, K)
+            Zf[i], Yf[i] = R.solve(Zf[i], Yf[i], MGneg, M[i], GL, PD[i], th, be, K)
+        out[f"c4_z_{K}"], out[f"c4_y_{K}"] = Z, Y
+        rz = np.linalg.norm(Z - Zf, axis=1) / np.linalg.norm(Zf, axis=1)
+        ry = np.linalg.norm(Y - Yf, axis=1) / np.linalg.norm(Yf, axis=1)
+        print(f"c4 K={K}: max |dz|/|z| {rz.max():.3g} max |dy|/|y| {ry.max():.3g} (O3 vs FMA build)")
+    np.savez_compressed(os.path.join(HERE, "ref_o3.npz"), **out)
+
+
 def main():
+    if "--o3-only" in sys.argv:
+        pyoracle.build(ref=True)
+        make_o3(pyoracle.Oracle())
+        return
     pyoracle.build(ref=True)
     O = pyoracle.Oracle()
     R = pyoracle.RefSeq()
@@ -185,6 +234,7 @@ def main():
         make(name, qp, O, R)
     make_datafile(O, R)
     make_closed_loop()
+    make_o3(O)
     make_flat("battery_flat_4x10", 4, 10, 0, O, R)
     d = make_flat("battery_flat_3x4", 3, 4, 5, O, R)
     write_flat_datafile(os.path.join(HERE, "datafile_battery_flat_3x4.txt"), d, 3, 4)
