@@ -168,6 +168,9 @@ struct gpad_handle_s {
     int num_cus = 256;
     bool timed = false;
     gpad::Tuning tune;                  // gpad_set_option
+    bool failed_run = false;            // the last run's device error was reported (fetch_status
+                                        // clears the device word): later stats calls for that
+                                        // run keep returning GPAD_ERR_DEVICE until the next run
 };
 
 
@@ -180,6 +183,7 @@ static int reset_status(gpad_handle_t h, double tol, double floor_scale) {
                                 sizeof(RunStatus) - offsetof(RunStatus, part), h->stream));
     h->last_tol = tol;
     h->last_floor_scale = floor_scale;
+    h->failed_run = false;
     return GPAD_OK;
 }
 
@@ -204,8 +208,12 @@ static double status_gmax(gpad_handle_t h, const RunStatus& rs) {
     return g;
 }
 
-static int status_error(const RunStatus& rs) {
-    if (rs.err == 0) return GPAD_OK;
+static int status_error(gpad_handle_t h, const RunStatus& rs) {
+    if (rs.err == 0 && !h->failed_run) return GPAD_OK;
+    if (rs.err == 0)
+        return fail(GPAD_ERR_DEVICE, "the run failed on the device (reported by an earlier call; its results "
+                                     "are invalid)");
+    h->failed_run = true;
     return fail(GPAD_ERR_DEVICE, std::string("device error bits 0x") + std::to_string(rs.err) +
                                      ((rs.err & gpad::kDevErrHandoff) ? ": a chain hand-off wait expired "
                                                                         "(the run's results are invalid)"
@@ -341,7 +349,7 @@ int gpad_sync(gpad_handle_t h) {
     int rc = fetch_status(h, &rs);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(h->stream));
-    return status_error(rs);
+    return status_error(h, rs);
 }
 
 int gpad_schedule(int N, int kind, double* theta, double* beta) {
@@ -658,7 +666,7 @@ static int collect_stats(gpad_handle_t h, gpad_stats_t* st) {
     st->flags = (h->last_tol > 0.0 && h->last_tol < st->tol_floor) ? GPAD_FLAG_TOL_FLOOR : 0;
     if (h->last_tol > 0.0 && !std::isfinite(st->tol_floor))  // NaN / inf in g: nothing certifies
         st->flags |= GPAD_FLAG_TOL_FLOOR | GPAD_FLAG_NONFINITE_G;
-    return status_error(rs);
+    return status_error(h, rs);
 }
 
 int gpad_accumulate_iterations(gpad_handle_t h, long long* acc) {

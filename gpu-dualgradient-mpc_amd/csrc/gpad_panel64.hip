@@ -399,6 +399,10 @@ hipError_t launch_pack_panel64(const double* src, int rows, int cols, double sca
 hipError_t launch_panel64(const SolveArgs<double>& a, hipStream_t s) {
     const int T = p64_tiles(a.n, a.m);
     if (!T || !a.frag || a.frag_tiles != T || a.strideA || a.strideB) return hipErrorInvalidValue;
+    // fresh, whole solves only: the kernel starts every instance at v = 0 from (z_{-1}, y_0) and runs
+    // no phases -- a phased caller's window, work list or carried w / u would be silently ignored
+    if (a.v_begin != 0 || a.v_end != 0 || a.pwork || a.idx_in || a.count_in || a.wc || a.uc)
+        return hipErrorInvalidValue;
     const int panels = (a.batch + 15) / 16;
     const int grid = panels < a.num_cus ? panels : a.num_cus;
     switch (T) {

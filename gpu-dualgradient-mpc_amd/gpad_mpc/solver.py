@@ -21,6 +21,14 @@ def _is_torch(x) -> bool:
     return type(x).__module__.startswith("torch")
 
 
+def _count_array(arr, field: str, entries: int):
+    """A caller's host iters / codes array for gpad_stats_t: int32, C-contiguous, >= entries."""
+    if not isinstance(arr, np.ndarray) or arr.dtype != np.int32 or not arr.flags["C_CONTIGUOUS"] \
+            or arr.size < entries:
+        raise ValueError(f"{field} must be a C-contiguous host int32 array with >= {entries} entries")
+    return arr.ctypes.data_as(C.POINTER(C.c_int))
+
+
 def _dtype_code(x) -> int:
     if _is_torch(x):
         import torch
@@ -137,12 +145,11 @@ class GpadSolver:
         """Run GPAD in place on z [batch][n] / y [batch][m].  Returns a dict of stats, or None
         when ``stats`` is False and the inputs are device tensors (asynchronous launch)."""
         st = Stats()
-        it_arr = None
+        nb = max(1, self.dims.batch if self.dims else 1)
         if iters is not None:
-            it_arr = iters
-            st.iters = it_arr.ctypes.data_as(C.POINTER(C.c_int))
+            st.iters = _count_array(iters, "iters", nb)
         if codes is not None:  # per-instance termination codes 0..4 (host int32 [batch])
-            st.codes = codes.ctypes.data_as(C.POINTER(C.c_int))
+            st.codes = _count_array(codes, "codes", nb)
         want = stats or not _is_torch(z)
         for tab in (theta, beta):  # host tables whatever the memory kind (include/gpad.h)
             if tab is not None and (_is_torch(tab) or not isinstance(tab, np.ndarray)):
@@ -163,7 +170,7 @@ class GpadSolver:
     def last_stats(self, iters=None) -> dict:
         st = Stats()
         if iters is not None:
-            st.iters = iters.ctypes.data_as(C.POINTER(C.c_int))
+            st.iters = _count_array(iters, "iters", max(1, self.dims.batch if self.dims else 1))
         check(self.lib.gpad_last_stats(self.h, C.byref(st)), "gpad_last_stats")
         return self._stats_dict(st)
 
@@ -285,9 +292,7 @@ class GpadSolver:
         st = Stats()
         for arr, field in ((iters, "iters"), (codes, "codes")):
             if arr is not None:
-                if arr.dtype != np.int32 or arr.size < steps * max(1, self.dims.batch if self.dims else 1):
-                    raise ValueError(f"{field} must be host int32 with steps * batch entries")
-                setattr(st, field, arr.ctypes.data_as(C.POINTER(C.c_int)))
+                setattr(st, field, _count_array(arr, field, steps * max(1, self.dims.batch if self.dims else 1)))
         want = stats or iters is not None or codes is not None or not _is_torch(z)
         opt = lambda a: _ptr(a) if a is not None else None  # noqa: E731
         check(self.lib.gpad_closed_loop(self.h, _ptr(x), _ptr(z), _ptr(y), int(steps), int(N),
@@ -373,10 +378,11 @@ class GpadGroup:
 
     def run(self, z, y, M, g, N: int, tol: float = 0.0, *, iters=None, codes=None) -> dict:
         st = Stats()
+        nb = max(1, self.dims.batch if self.dims else 1)
         if iters is not None:
-            st.iters = iters.ctypes.data_as(C.POINTER(C.c_int))
+            st.iters = _count_array(iters, "iters", nb)
         if codes is not None:  # per-instance termination codes, [batch] in global order
-            st.codes = codes.ctypes.data_as(C.POINTER(C.c_int))
+            st.codes = _count_array(codes, "codes", nb)
         check(self.lib.gpad_group_run(self.g, _ptr(z), _ptr(y), _ptr(M), _ptr(g), int(N), float(tol),
                                       C.byref(st)), "gpad_group_run")
         return GpadSolver._stats_dict(st)

@@ -46,7 +46,8 @@ extern "C" {
                                     * gpad_sync, host-memory runs) -- never GPAD_OK; the error
                                     * is kept on the device until one of those reports it, so
                                     * asynchronous runs queued behind a failed one do not
-                                    * hide it                                                  */
+                                    * hide it, and once reported every later sync / stats call
+                                    * on the handle returns it again until the next run starts */
 
 /* theta/beta schedule (acceldualgrad.m:18,27,55-56 vs paper eq. 8e) */
 #define GPAD_SCHEDULE_MATLAB 0 /* beta lagged one iteration, as the reference's MATLAB  */

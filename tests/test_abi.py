@@ -174,3 +174,14 @@ def test_phase_planner_host_only():
     from gpad_mpc import _lib
     with pytest.raises(_lib.GpadError):
         GpadSolver.plan_phases(it[:0], 200, 200, 5000)
+
+
+@pytest.mark.parametrize("arr", [np.zeros(8, np.int64), np.zeros(7, np.int32), np.zeros(16, np.int32)[::2],
+                                 [0] * 8])
+def test_count_arrays_are_checked(arr):
+    """iters / codes handed to the C stats collection must be host int32, contiguous and
+    large enough -- an int64 or short array would be written out of bounds."""
+    from gpad_mpc.solver import _count_array
+    with pytest.raises(ValueError):
+        _count_array(arr, "iters", 8)
+    assert _count_array(np.zeros(8, np.int32), "iters", 8) is not None

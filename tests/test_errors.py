@@ -63,8 +63,9 @@ def test_dropped_handoff_fails_the_run(gpu, oracle, batch):
 
 def test_device_error_is_sticky_across_async_runs(gpu):
     """a faulty asynchronous run followed by a clean one, then one gpad_sync: the sync
-    reports the first run's GPAD_ERR_DEVICE (the second run's status reset must not wipe it), and
-    the error is reported once -- the next sync is clean."""
+    reports the first run's GPAD_ERR_DEVICE (the second run's status reset must not wipe it); every
+    later sync / stats call keeps reporting it (gpad_last_stats after the failing sync
+    must not return GPAD_OK) until the next run starts."""
     import torch
 
     import gpad_mpc
@@ -84,7 +85,10 @@ def test_device_error_is_sticky_across_async_runs(gpu):
         with pytest.raises(_lib.GpadError) as ei:
             s.sync()
         assert ei.value.code == _lib.ERR_DEVICE
-        s.sync()  # reported once
+        for call in (s.sync, s.last_stats):  # still failed: the results are invalid
+            with pytest.raises(_lib.GpadError) as ei:
+                call()
+            assert ei.value.code == _lib.ERR_DEVICE
         st = s.run(z.zero_(), y.zero_(), dM, dg, 20, 0.0)
         assert st["kernel"] == "panel"
 
