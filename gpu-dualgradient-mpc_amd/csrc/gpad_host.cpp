@@ -338,6 +338,12 @@ int gpad_set_option(gpad_handle_t h, int option, int value) {
             return set(t.flat_waves, 0, 16, def.flat_waves);
         case GPAD_OPT_FLAT_A_LDS: return set(t.flat_a_lds, 0, 1, def.flat_a_lds);
         case GPAD_OPT_DEBUG_DROP_HANDOFF: return set(t.debug_drop_handoff, 0, 1, def.debug_drop_handoff);
+        case GPAD_OPT_P64_RELAY: {
+            int on = 1 - t.p64_no_relay;
+            const int rc = set(on, 0, 1, 1);
+            t.p64_no_relay = 1 - on;
+            return rc;
+        }
         default: return fail(GPAD_ERR_INVALID, "gpad_set_option: unknown option");
     }
 }

@@ -101,6 +101,48 @@ __device__ __forceinline__ f64x4 gemm64(__amdgpu_buffer_rsrc_t PA, const f64x4* 
     return acc;
 }
 
+// blocks [KB0, KB1) of the chain of the tile at voff, continued from acc (a relay piece, or the
+// owner's last piece): the same MFMA sequence as gemm64's, so the cut is bit-invisible
+template <int T, int KB0, int KB1>
+__device__ __forceinline__ void chain64(__amdgpu_buffer_rsrc_t PA, const f64x4* __restrict__ Bl, int voff, int lane,
+                                        f64x4& acc) {
+    f64x4 a[2], b[2];
+    a[0] = ld_a(PA, voff, KB0 * T * 2048);
+    b[0] = Bl[KB0 * 64 + lane];
+#pragma unroll
+    for (int kb = KB0; kb < KB1; ++kb) {
+        const int cur = (kb - KB0) & 1, nxt = cur ^ 1;
+        if (kb + 1 < KB1) {
+            a[nxt] = ld_a(PA, voff, (kb + 1) * T * 2048);
+            b[nxt] = Bl[(kb + 1) * 64 + lane];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[cur][0], b[cur][0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[cur][1], b[cur][1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[cur][2], b[cur][2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[cur][3], b[cur][3], acc, 0, 0, 0);
+        asm volatile("" ::: "memory");
+    }
+}
+
+// The relay layout (round 5).  One panel per 13-wave workgroup put 4,3,3,3 chains on the SIMDs
+// (the f64 pipe is saturated by ONE dependent chain per SIMD -- 74 cycles per step alone, 64 at
+// full rate, profiles/r04_mfma_f64.txt -- so the busiest SIMD's chain count is the iteration time).
+// With 16 waves, tile T-1's chain is cut into four pieces: k-blocks [0, C1) on relay wave 0,
+// [C1, C2) on relay wave 1, [C2, C3) on relay wave 2 -- one on each SIMD that lacks tile T-1 --
+// and [C3, T) plus the epilogue on the tile's owner; each piece continues from the accumulator the
+// previous one parked in LDS (bit-identical: the same ascending-k MFMA sequence).  T = 13: SIMD
+// loads 52,39,39,39 k-blocks -> 43,42,42,42.  Roles are dealt from the last wave down (the SIMD
+// issues MFMAs oldest wave first), so the sequential relay runs on the oldest waves, at raised
+// priority, as in the f32 one-panel relay (gpad_panel.hip Handoff).  Relay waves own a phantom
+// tile T (no rows) everywhere else, so they follow the workgroup's control flow and barriers
+// without touching the real tiles' state.
+template <int T>
+struct P64Relay {
+    static constexpr bool on = T == 9 || T == 13;  // T % 4 == 1: SIMD 0 carries the extra tile
+    static constexpr int C1 = T / 4, C2 = 2 * T / 4, C3 = 3 * T / 4;
+};
+
 struct P64Slot {  // per tile and column: the test partials / the value-function sums
     double violz[16], violh[16], wmin[16], gap[16], magh[16];
 };
@@ -121,17 +163,103 @@ __device__ __forceinline__ double col_sum(double v) {
 
 }  // namespace
 
-template <int T>
-__global__ __launch_bounds__(64 * T) void gpad_panel64_kernel(SolveArgs<double> a) {
-    __shared__ f64x4 Wl[T * 64];  // w    (B of GEMM 1), fragment order
-    __shared__ f64x4 Zh[T * 64];  // zhat (B of GEMM 2)
-    __shared__ f64x4 Xv[T * 64];  // z for the (A) verification; the value branches' operands
-    __shared__ f64x4 Gp[T * 64];  // g_P of this lane's rows (in LDS: registers are the limit)
-    __shared__ P64Slot slots[T];
-    __shared__ double vsum[2][T][16];  // value branches: per tile and column, V / dual sums
+// LDS of the kernel: w (B of GEMM 1, fragment order), zhat (B of GEMM 2), Xv (z for the (A)
+// verification; the value branches' operands), g_P of the lanes' rows (registers are the limit),
+// the test slots and the value sums, per tile -- plus the relay waves' phantom tile -- and:
+template <int T, bool RELAY>
+struct P64Lds {
+    static constexpr int TL = RELAY ? T + 1 : T;
+};
+template <bool RELAY>
+struct P64Hand {
+    f64x4 hand[RELAY ? 3 : 1][64];  // relay: parked accumulators
+    int hflag[3];                   // relay: hand-off generation per slot
+    int herr;                       // relay: a wait expired (reported at exit, GPAD_ERR_DEVICE)
+};
+
+// bounded wait for a parked accumulator (as gpad_panel.hip handoff_wait: an expired wait is
+// recorded and fails the run rather than hanging the GPU or returning stale results)
+template <class Lds>
+__device__ __forceinline__ f64x4 p64_wait(Lds& L, int slot, int gen, int lane) {
+    for (int s = 0;; ++s) {
+        if (__hip_atomic_load(&L.hflag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == gen) break;
+        if (s == (1 << 20)) {
+            L.herr = 1;
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    asm volatile("" ::: "memory");
+    return L.hand[slot][lane];
+}
+
+template <class Lds>
+__device__ __forceinline__ void p64_post(Lds& L, int slot, int gen, int lane, const f64x4& h) {
+    L.hand[slot][lane] = h;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the accumulator lands before the flag
+    __hip_atomic_store(&L.hflag[slot], gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// a main GEMM of tile t (gemm64), or -- relay layout -- this wave's piece of tile T-1's chain
+template <int T, bool RELAY, class Lds>
+__device__ __forceinline__ f64x4 p64_gemm(Lds& L, __amdgpu_buffer_rsrc_t PA, const f64x4* __restrict__ Bl, int voff,
+                                          int lane, int nkb, bool on, int rrole, int gen) {
+    using R = P64Relay<T>;
+    if constexpr (RELAY) {
+        const int vo = (T - 1) * 2048 + lane * 32;
+        f64x4 h = {0.0, 0.0, 0.0, 0.0};
+        if (rrole == 0) {
+            __builtin_amdgcn_s_setprio(3);
+            chain64<T, 0, R::C1>(PA, Bl, vo, lane, h);
+            p64_post(L, 0, gen, lane, h);
+            __builtin_amdgcn_s_setprio(0);
+            return f64x4{0.0, 0.0, 0.0, 0.0};
+        }
+        if (rrole == 1 || rrole == 2) {
+            h = p64_wait(L, rrole - 1, gen, lane);
+            __builtin_amdgcn_s_setprio(3);
+            if (rrole == 1) chain64<T, R::C1, R::C2>(PA, Bl, vo, lane, h);
+            else chain64<T, R::C2, R::C3>(PA, Bl, vo, lane, h);
+            p64_post(L, rrole, gen, lane, h);
+            __builtin_amdgcn_s_setprio(0);
+            return f64x4{0.0, 0.0, 0.0, 0.0};
+        }
+        if (rrole == 3) {  // the owner of tile T-1: the last piece
+            h = p64_wait(L, 2, gen, lane);
+            __builtin_amdgcn_s_setprio(2);
+            chain64<T, R::C3, T>(PA, Bl, vo, lane, h);
+            __builtin_amdgcn_s_setprio(0);
+            return h;
+        }
+        if (rrole > 3) return f64x4{0.0, 0.0, 0.0, 0.0};  // idle (T = 9: waves past the relay)
+    }
+    return on ? gemm64<T>(PA, Bl, voff, lane, nkb) : f64x4{0.0, 0.0, 0.0, 0.0};
+}
+
+template <int T, bool RELAY>
+__global__ __launch_bounds__(RELAY ? 1024 : 64 * T) void gpad_panel64_kernel(SolveArgs<double> a) {
+    constexpr int TL = P64Lds<T, RELAY>::TL;
+    __shared__ f64x4 Wl[TL * 64];
+    __shared__ f64x4 Zh[TL * 64];
+    __shared__ f64x4 Xv[TL * 64];
+    __shared__ f64x4 Gp[TL * 64];
+    __shared__ P64Slot slots[TL];
+    __shared__ double vsum[2][TL][16];
+    __shared__ P64Hand<RELAY> L;
 
     const int lane = threadIdx.x & 63;
-    const int t = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // role: tile index (relay layout: dealt from the last wave down; roles >= T are relay waves
+    // on the phantom tile T); rrole: 0..2 relay pieces, 3 the owner of tile T-1, -1 none
+    const int w0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int role = RELAY ? 15 - w0 : w0;
+    const int t = role < T ? role : T;
+    const int rrole = !RELAY ? -1 : (role == T - 1 ? 3 : (role >= T ? (role - T < 3 ? role - T : 4) : -1));
+    if (RELAY) {
+        if (threadIdx.x < 3) L.hflag[threadIdx.x] = 0;
+        if (threadIdx.x == 0) L.herr = 0;
+        __syncthreads();
+    }
+    int hgen = 0;
     const int j = lane >> 4, c = lane & 15;
     const int n = a.n, m = a.m, N = a.N, K = a.check_every;
     const int nkb1 = (m + 15) / 16, nkb2 = (n + 15) / 16;  // k-blocks of GEMM 1 (K = m), GEMM 2 / H (K = n)
@@ -187,7 +315,7 @@ __global__ __launch_bounds__(64 * T) void gpad_panel64_kernel(SolveArgs<double> 
             const double omt = 1.0 - th;
             // ---- GEMM 1 + epilogue: zhat = -ML w - g_P (8b), z = (1-th) z + th zhat (8c) ----
             {
-                const f64x4 acc = on1 ? gemm64<T>(PA1, Wl, voff, lane, nkb1) : f64x4{0.0, 0.0, 0.0, 0.0};
+                const f64x4 acc = p64_gemm<T, RELAY>(L, PA1, Wl, voff, lane, nkb1, on1, rrole, ++hgen);
                 const f64x4 gp = Gp[slot];
                 f64x4 zh;
 #pragma unroll
@@ -202,7 +330,7 @@ __global__ __launch_bounds__(64 * T) void gpad_panel64_kernel(SolveArgs<double> 
             // ---- GEMM 2 + epilogue: y+ = [w + G_L zhat + p_D]+ (8d), next w (8a), test partials ----
             double violz = -INFINITY, violh = -INFINITY, wmin = INFINITY, magh = 0.0, gap = 0.0;
             {
-                const f64x4 acc = on2 ? gemm64<T>(PA2, Zh, voff, lane, nkb2) : f64x4{0.0, 0.0, 0.0, 0.0};
+                const f64x4 acc = p64_gemm<T, RELAY>(L, PA2, Zh, voff, lane, nkb2, on2, rrole, ++hgen);
                 const f64x4 wv = Wl[slot];
                 f64x4 wn;
 #pragma unroll
@@ -380,6 +508,7 @@ __global__ __launch_bounds__(64 * T) void gpad_panel64_kernel(SolveArgs<double> 
         }
         __syncthreads();  // the next panel reuses the LDS tiles
     }
+    if (RELAY && threadIdx.x == 0 && L.herr) atomicOr(a.err, kDevErrHandoff);  // (the last barrier above)
 }
 
 bool panel64_supported(int n, int m) { return p64_tiles(n, m) > 0; }
@@ -396,6 +525,32 @@ hipError_t launch_pack_panel64(const double* src, int rows, int cols, double sca
     return hipGetLastError();
 }
 
+// Workgroups per CU the kernel's registers and LDS allow (hipOccupancy..., cached per
+// instantiation): a persistent grid of num_cus x that, so small tile counts fill the CU with
+// several panels (num_cus workgroups of T waves left T <= 4 at 1-4 waves per CU).
+template <int T, bool RELAY>
+int p64_per_cu() {
+    static int occ = 0;
+    if (!occ) {
+        int o = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, gpad_panel64_kernel<T, RELAY>, RELAY ? 1024 : 64 * T, 0) !=
+                hipSuccess ||
+            o < 1)
+            o = 1;
+        occ = o;
+    }
+    return occ;
+}
+
+template <int T, bool RELAY>
+hipError_t launch_p64(const SolveArgs<double>& a, hipStream_t s) {
+    const int panels = (a.batch + 15) / 16;
+    const int cap = a.num_cus * p64_per_cu<T, RELAY>();
+    const int grid = panels < cap ? panels : cap;
+    hipLaunchKernelGGL((gpad_panel64_kernel<T, RELAY>), dim3(grid), dim3(RELAY ? 1024 : 64 * T), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_panel64(const SolveArgs<double>& a, hipStream_t s) {
     const int T = p64_tiles(a.n, a.m);
     if (!T || !a.frag || a.frag_tiles != T || a.strideA || a.strideB) return hipErrorInvalidValue;
@@ -403,17 +558,19 @@ hipError_t launch_panel64(const SolveArgs<double>& a, hipStream_t s) {
     // no phases -- a phased caller's window, work list or carried w / u would be silently ignored
     if (a.v_begin != 0 || a.v_end != 0 || a.pwork || a.idx_in || a.count_in || a.wc || a.uc)
         return hipErrorInvalidValue;
-    const int panels = (a.batch + 15) / 16;
-    const int grid = panels < a.num_cus ? panels : a.num_cus;
+    // the relay layout needs full-length chains in both GEMMs (tile T-1 has rows in both)
+    const bool relay = (a.n + 15) / 16 == T && (a.m + 15) / 16 == T && !(a.tune && a.tune->p64_no_relay);
     switch (T) {
 #define GPAD_P64(TT) \
-    case TT: hipLaunchKernelGGL((gpad_panel64_kernel<TT>), dim3(grid), dim3(64 * TT), 0, s, a); break;
+    case TT: return launch_p64<TT, false>(a, s);
+#define GPAD_P64R(TT) \
+    case TT: return relay ? launch_p64<TT, true>(a, s) : launch_p64<TT, false>(a, s);
         GPAD_P64(1) GPAD_P64(2) GPAD_P64(3) GPAD_P64(4) GPAD_P64(5) GPAD_P64(6) GPAD_P64(7) GPAD_P64(8)
-        GPAD_P64(9) GPAD_P64(10) GPAD_P64(11) GPAD_P64(12) GPAD_P64(13) GPAD_P64(14) GPAD_P64(15) GPAD_P64(16)
+        GPAD_P64R(9) GPAD_P64(10) GPAD_P64(11) GPAD_P64(12) GPAD_P64R(13) GPAD_P64(14) GPAD_P64(15) GPAD_P64(16)
 #undef GPAD_P64
+#undef GPAD_P64R
         default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
 }
 
 }  // namespace gpad

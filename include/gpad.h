@@ -393,6 +393,8 @@ int gpad_schedule(int N, int kind, double* theta, double* beta);
                                     * GPAD_ERR_DEVICE; 0 (default) = off.  Honoured by the
                                     * 193..208-row shapes (the C3/C4 tiling, T = 13), which run
                                     * a separate test-only kernel instantiation while it is set */
+#define GPAD_OPT_P64_RELAY 18      /* 1: f64 panels at T = 9, 13 (n, m in (128, 144], (192, 208]) run
+                                    * the 16-wave relay layout (default); 0: one wave per tile */
 int gpad_set_option(gpad_handle_t h, int option, int value);
 
 /* Synchronise the handle's stream (for callers using device memory + async runs). */

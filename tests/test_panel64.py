@@ -20,7 +20,7 @@ from test_value import value_problem
 pytestmark = pytest.mark.gpu
 
 
-def _run(ML, G, L, M, g, N, tol, *, kernel, H=None, tol_gap=0.0, K=10, dev=True):
+def _run(ML, G, L, M, g, N, tol, *, kernel, H=None, tol_gap=0.0, K=10, dev=True, opts=None):
     import torch
 
     import gpad_mpc
@@ -37,6 +37,7 @@ def _run(ML, G, L, M, g, N, tol, *, kernel, H=None, tol_gap=0.0, K=10, dev=True)
         s.setup(t(ML), t(G), float(L), n=n, m=m, batch=B, check_every=K, kernel=kern, tol_gap=tol_gap)
         if H is not None:
             s.setup_hessian(t(H))
+        s.set_options(**(opts or {}))
         st = s.run(z, y, t(M), t(g), N, tol, iters=it, codes=codes)
     return z.cpu().numpy(), y.cpu().numpy(), it, codes, st
 
@@ -73,14 +74,17 @@ class TestCodes:
         assert {3, 4} & self.seen, self.seen
 
 
-def test_panel64_reference_tolerance_c4_shape(gpu, oracle):
+@pytest.mark.parametrize("relay", [1, 0])
+def test_panel64_reference_tolerance_c4_shape(gpu, oracle, relay):
     """C4 shape (n = m = 200, T = 13), the reference's e_g = e_V = 1e-6 with H bound, 512 instances
     (value problems: constraints active at an optimum with a positive objective): bit-exact with the
     f64 stream kernel on every instance, and a spread sample equal to the fp64 oracle (counts,
-    codes, z to 1e-12); every instance converged (codes 2 / 3)."""
+    codes, z to 1e-12); every instance converged (codes 2 / 3).  relay = 1: the 16-wave layout
+    (tile 12's chain cut over four waves, round 5), 0: one wave per tile."""
     B, tol = 512, 1e-6
     H, ML, M, G, g, L = (np.asarray(a) for a in value_problem(200, 200, 7, 1.0, batch=B)[:6])
-    zp, yp, itp, cp, stp = _run(ML, G, L, M, g, 20000, tol, kernel="panel", H=H, tol_gap=tol)
+    zp, yp, itp, cp, stp = _run(ML, G, L, M, g, 20000, tol, kernel="panel", H=H, tol_gap=tol,
+                                opts={"p64_relay": relay})
     zs, ys, its, cs, _ = _run(ML, G, L, M, g, 20000, tol, kernel="stream", H=H, tol_gap=tol)
     assert stp["kernel"] == "panel" and stp["converged"] == B
     np.testing.assert_array_equal(itp, its)
@@ -95,17 +99,23 @@ def test_panel64_reference_tolerance_c4_shape(gpu, oracle):
         np.testing.assert_allclose(zp[b], zo, rtol=1e-12, atol=1e-14)
 
 
-@pytest.mark.parametrize("n,m", [(37, 53), (200, 180), (256, 256), (5, 129), (160, 200)])
-def test_panel64_fixed_n_ragged(gpu, n, m):
+@pytest.mark.parametrize("n,m,B", [(37, 53, 40), (200, 180, 40), (256, 256, 40), (5, 129, 40), (160, 200, 40),
+                                   (144, 144, 40), (130, 137, 40), (200, 193, 40), (40, 53, 4100), (16, 16, 5000)])
+def test_panel64_fixed_n_ragged(gpu, n, m, B):
     """Fixed N = 60 (no test) and eps = 1e-6 without H on ragged shapes: bit-exact with the f64
-    stream kernel (zero-padded k-steps and skipped tiles)."""
+    stream kernel (zero-padded k-steps and skipped tiles).  (144, 144), (130, 137), (200, 193): the
+    relay layout at T = 9 / 13; (40, 53) and (16, 16) at thousands of instances: several small
+    workgroups per CU (the occupancy-sized grid)."""
     from gpad_mpc import problems
-    B = 40
     qp = problems.synthetic_qp(n, m, batch=B, seed=n + m)
     ML, G = np.asarray(qp.ML), np.asarray(qp.G)
     M, g = np.asarray(qp.M).reshape(B, n), np.asarray(qp.g).reshape(B, m)
     for N, tol in ((60, 0.0), (3000, 1e-6)):
         a = _run(ML, G, qp.L, M, g, N, tol, kernel="panel")
+        if n > 128:  # the relay and the one-wave-per-tile layout agree bit for bit too
+            c = _run(ML, G, qp.L, M, g, N, tol, kernel="panel", opts={"p64_relay": 0})
+            for x, y_ in zip(a[:4], c[:4]):
+                np.testing.assert_array_equal(x, y_)
         b = _run(ML, G, qp.L, M, g, N, tol, kernel="stream")
         assert a[4]["kernel"] == "panel"
         for x, y_ in zip(a[:4], b[:4]):
@@ -131,3 +141,19 @@ def test_panel64_auto_c4_batch_certified(gpu, oracle):
         zo, yo, ito, co = oracle.solve_f64(np.zeros(n), np.zeros(m), ML, M[b], G, g[b], 20000, L, tol, tol_gap=tol)
         assert it[b] == ito and co and codes[b] in (1, 2), b
         np.testing.assert_allclose(z[b], zo, rtol=1e-12, atol=1e-14)
+
+
+@pytest.mark.parametrize("shift,tol,tol_gap,K", [(1.0, 1e-5, 1e-5, 10), (3.0, 1e-3, 1e-2, 1)])
+def test_panel64_value_branches_relay_t9(gpu, shift, tol, tol_gap, K):
+    """n = m = 140 (T = 9): the relay layout with the value branches (H bound) equals the f64 stream
+    kernel bit for bit -- counts and codes included -- and the one-wave-per-tile layout."""
+    B = 256
+    H, ML, M, G, g, L = (np.asarray(a) for a in value_problem(140, 140, 5, shift, batch=B)[:6])
+    a = _run(ML, G, L, M, g, 20000, tol, kernel="panel", H=H, tol_gap=tol_gap, K=K)
+    b = _run(ML, G, L, M, g, 20000, tol, kernel="stream", H=H, tol_gap=tol_gap, K=K)
+    c = _run(ML, G, L, M, g, 20000, tol, kernel="panel", H=H, tol_gap=tol_gap, K=K, opts={"p64_relay": 0})
+    assert a[4]["kernel"] == "panel" and a[4]["converged"] == B
+    for x, y_, w in zip(a[:4], b[:4], c[:4]):
+        np.testing.assert_array_equal(x, y_)
+        np.testing.assert_array_equal(x, w)
+    assert set(a[3].tolist()) & {3, 4}
