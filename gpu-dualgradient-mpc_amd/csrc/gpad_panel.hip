@@ -686,15 +686,30 @@ struct Panel2Lds {
 #ifdef GPAD_STAMP
 constexpr int kStampV0 = 101, kStampIts = 4, kStampPts = 6;
 __device__ unsigned long long g_stamps[16][kStampIts][kStampPts];
-#define GPAD_STAMP_AT(P)                                                                          \
-    do {                                                                                          \
-        if (blockIdx.x == 0 && v >= kStampV0 && v < kStampV0 + kStampIts && lane == 0)            \
-            g_stamps[threadIdx.x >> 6][v - kStampV0][P] = __builtin_amdgcn_s_memtime();           \
+// s_memtime into SGPRs at each point (pinned by scheduling barriers), stored once per iteration after
+// the closing barrier: the store's lgkmcnt wait then sits where no LDS or scalar load is in flight,
+// instead of behind each stamp (where it made every stamp wait for the LDS operands and the
+// schedule's scalar loads, r03_stamp_*.txt)
+#define GPAD_STAMP_AT(P)                                      \
+    do {                                                      \
+        __builtin_amdgcn_sched_barrier(0);                    \
+        stv[P] = __builtin_amdgcn_s_memtime();                \
+        __builtin_amdgcn_sched_barrier(0);                    \
     } while (0)
+#define GPAD_STAMP_FLUSH()                                                                  \
+    do {                                                                                    \
+        if (blockIdx.x == 0 && v >= kStampV0 && v < kStampV0 + kStampIts && lane == 0)      \
+            for (int q_ = 0; q_ < kStampPts; ++q_) g_stamps[threadIdx.x >> 6][v - kStampV0][q_] = stv[q_]; \
+    } while (0)
+#define GPAD_STAMP_DECL unsigned long long stv[kStampPts] = {0, 0, 0, 0, 0, 0};
 #else
 #define GPAD_STAMP_AT(P) \
     do {                 \
     } while (0)
+#define GPAD_STAMP_FLUSH() \
+    do {                   \
+    } while (0)
+#define GPAD_STAMP_DECL
 #endif
 
 struct HoSlots {
@@ -881,6 +896,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
         };
         prefetch(PA1);
         int v = a.v_begin;
+        GPAD_STAMP_DECL
         int kc = K - v % K;  // iterations to the next test: chk <=> v % K == 0 (a countdown, no division)
         float th = a.theta[v], bn = a.beta[v + 1];
         while (true) {
@@ -1035,6 +1051,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             bn = bn_next;
             GPAD_STAMP_AT(5);
             __syncthreads();
+            GPAD_STAMP_FLUSH();
             if (!chk && v < a.v_end) continue;
 
             // ---- Algorithm 1 test per column: every wave reduces the tile partials of all the

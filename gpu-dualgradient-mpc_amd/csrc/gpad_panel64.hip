@@ -75,12 +75,14 @@ __device__ __forceinline__ f64x4 ld_a(__amdgpu_buffer_rsrc_t PA, int voff, int s
 
 // acc = A[tile t] x B over k-blocks [0, nkb) (ascending k: the fma chain), A streamed from L2 one
 // block ahead, B (fragment order) from LDS one block ahead.  Zero-padded k-steps add +0 only.
+// gemm64p: block 0's A operand a0 given (loaded before the barrier that precedes the GEMM, so the
+// chain does not start with an L2 round trip)
 template <int T>
-__device__ __forceinline__ f64x4 gemm64(__amdgpu_buffer_rsrc_t PA, const f64x4* __restrict__ Bl, int voff, int lane,
-                                        int nkb) {
+__device__ __forceinline__ f64x4 gemm64p(__amdgpu_buffer_rsrc_t PA, const f64x4* __restrict__ Bl, int voff, int lane,
+                                         int nkb, const f64x4& a0) {
     f64x4 acc = {0.0, 0.0, 0.0, 0.0};
     f64x4 a[2], b[2];
-    a[0] = ld_a(PA, voff, 0);
+    a[0] = a0;
     b[0] = Bl[lane];
 #pragma unroll
     for (int kb = 0; kb < T; ++kb) {
@@ -101,13 +103,19 @@ __device__ __forceinline__ f64x4 gemm64(__amdgpu_buffer_rsrc_t PA, const f64x4* 
     return acc;
 }
 
+template <int T>
+__device__ __forceinline__ f64x4 gemm64(__amdgpu_buffer_rsrc_t PA, const f64x4* __restrict__ Bl, int voff, int lane,
+                                        int nkb) {
+    return gemm64p<T>(PA, Bl, voff, lane, nkb, ld_a(PA, voff, 0));
+}
+
 // blocks [KB0, KB1) of the chain of the tile at voff, continued from acc (a relay piece, or the
 // owner's last piece): the same MFMA sequence as gemm64's, so the cut is bit-invisible
 template <int T, int KB0, int KB1>
 __device__ __forceinline__ void chain64(__amdgpu_buffer_rsrc_t PA, const f64x4* __restrict__ Bl, int voff, int lane,
-                                        f64x4& acc) {
+                                        f64x4& acc, const f64x4& a0) {
     f64x4 a[2], b[2];
-    a[0] = ld_a(PA, voff, KB0 * T * 2048);
+    a[0] = a0;  // block KB0, loaded ahead
     b[0] = Bl[KB0 * 64 + lane];
 #pragma unroll
     for (int kb = KB0; kb < KB1; ++kb) {
@@ -201,16 +209,30 @@ __device__ __forceinline__ void p64_post(Lds& L, int slot, int gen, int lane, co
 }
 
 // a main GEMM of tile t (gemm64), or -- relay layout -- this wave's piece of tile T-1's chain
+// the first A block this wave's part of a main GEMM needs (issued before the preceding barrier)
+template <int T, bool RELAY>
+__device__ __forceinline__ f64x4 p64_first_a(__amdgpu_buffer_rsrc_t PA, int voff, int lane, bool on, int rrole) {
+    using R = P64Relay<T>;
+    if constexpr (RELAY) {
+        if (rrole >= 0 && rrole <= 3) {
+            const int kb = rrole == 0 ? 0 : (rrole == 1 ? R::C1 : (rrole == 2 ? R::C2 : R::C3));
+            return ld_a(PA, (T - 1) * 2048 + lane * 32, kb * T * 2048);
+        }
+        if (rrole > 3) return f64x4{0.0, 0.0, 0.0, 0.0};
+    }
+    return on ? ld_a(PA, voff, 0) : f64x4{0.0, 0.0, 0.0, 0.0};
+}
+
 template <int T, bool RELAY, class Lds>
 __device__ __forceinline__ f64x4 p64_gemm(Lds& L, __amdgpu_buffer_rsrc_t PA, const f64x4* __restrict__ Bl, int voff,
-                                          int lane, int nkb, bool on, int rrole, int gen) {
+                                          int lane, int nkb, bool on, int rrole, int gen, const f64x4& a0) {
     using R = P64Relay<T>;
     if constexpr (RELAY) {
         const int vo = (T - 1) * 2048 + lane * 32;
         f64x4 h = {0.0, 0.0, 0.0, 0.0};
         if (rrole == 0) {
             __builtin_amdgcn_s_setprio(3);
-            chain64<T, 0, R::C1>(PA, Bl, vo, lane, h);
+            chain64<T, 0, R::C1>(PA, Bl, vo, lane, h, a0);
             p64_post(L, 0, gen, lane, h);
             __builtin_amdgcn_s_setprio(0);
             return f64x4{0.0, 0.0, 0.0, 0.0};
@@ -218,8 +240,8 @@ __device__ __forceinline__ f64x4 p64_gemm(Lds& L, __amdgpu_buffer_rsrc_t PA, con
         if (rrole == 1 || rrole == 2) {
             h = p64_wait(L, rrole - 1, gen, lane);
             __builtin_amdgcn_s_setprio(3);
-            if (rrole == 1) chain64<T, R::C1, R::C2>(PA, Bl, vo, lane, h);
-            else chain64<T, R::C2, R::C3>(PA, Bl, vo, lane, h);
+            if (rrole == 1) chain64<T, R::C1, R::C2>(PA, Bl, vo, lane, h, a0);
+            else chain64<T, R::C2, R::C3>(PA, Bl, vo, lane, h, a0);
             p64_post(L, rrole, gen, lane, h);
             __builtin_amdgcn_s_setprio(0);
             return f64x4{0.0, 0.0, 0.0, 0.0};
@@ -227,13 +249,13 @@ __device__ __forceinline__ f64x4 p64_gemm(Lds& L, __amdgpu_buffer_rsrc_t PA, con
         if (rrole == 3) {  // the owner of tile T-1: the last piece
             h = p64_wait(L, 2, gen, lane);
             __builtin_amdgcn_s_setprio(2);
-            chain64<T, R::C3, T>(PA, Bl, vo, lane, h);
+            chain64<T, R::C3, T>(PA, Bl, vo, lane, h, a0);
             __builtin_amdgcn_s_setprio(0);
             return h;
         }
         if (rrole > 3) return f64x4{0.0, 0.0, 0.0, 0.0};  // idle (T = 9: waves past the relay)
     }
-    return on ? gemm64<T>(PA, Bl, voff, lane, nkb) : f64x4{0.0, 0.0, 0.0, 0.0};
+    return on ? gemm64p<T>(PA, Bl, voff, lane, nkb, a0) : f64x4{0.0, 0.0, 0.0, 0.0};
 }
 
 template <int T, bool RELAY>
@@ -308,6 +330,7 @@ __global__ __launch_bounds__(RELAY ? 1024 : 64 * T) void gpad_panel64_kernel(Sol
         __syncthreads();
 
         int v = 0;
+        f64x4 apre = p64_first_a<T, RELAY>(PA1, voff, lane, on1, rrole);  // GEMM 1's first A block
         while (true) {
             const double th = a.theta[v], bn = a.beta[v + 1];
             ++v;
@@ -315,7 +338,8 @@ __global__ __launch_bounds__(RELAY ? 1024 : 64 * T) void gpad_panel64_kernel(Sol
             const double omt = 1.0 - th;
             // ---- GEMM 1 + epilogue: zhat = -ML w - g_P (8b), z = (1-th) z + th zhat (8c) ----
             {
-                const f64x4 acc = p64_gemm<T, RELAY>(L, PA1, Wl, voff, lane, nkb1, on1, rrole, ++hgen);
+                const f64x4 acc = p64_gemm<T, RELAY>(L, PA1, Wl, voff, lane, nkb1, on1, rrole, ++hgen, apre);
+                apre = p64_first_a<T, RELAY>(PA2, voff, lane, on2, rrole);  // GEMM 2's, across the barrier
                 const f64x4 gp = Gp[slot];
                 f64x4 zh;
 #pragma unroll
@@ -330,7 +354,8 @@ __global__ __launch_bounds__(RELAY ? 1024 : 64 * T) void gpad_panel64_kernel(Sol
             // ---- GEMM 2 + epilogue: y+ = [w + G_L zhat + p_D]+ (8d), next w (8a), test partials ----
             double violz = -INFINITY, violh = -INFINITY, wmin = INFINITY, magh = 0.0, gap = 0.0;
             {
-                const f64x4 acc = p64_gemm<T, RELAY>(L, PA2, Zh, voff, lane, nkb2, on2, rrole, ++hgen);
+                const f64x4 acc = p64_gemm<T, RELAY>(L, PA2, Zh, voff, lane, nkb2, on2, rrole, ++hgen, apre);
+                apre = p64_first_a<T, RELAY>(PA1, voff, lane, on1, rrole);  // the next GEMM 1's
                 const f64x4 wv = Wl[slot];
                 f64x4 wn;
 #pragma unroll
