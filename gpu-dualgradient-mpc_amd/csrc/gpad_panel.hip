@@ -408,6 +408,33 @@ __global__ __launch_bounds__(64 * T) void gpad_panel_kernel(SolveArgs<float> a) 
     }
 }
 
+// Prelude priority (r05).  The SIMD issues oldest wave first, VALU and MFMA from one port: while
+// an older wave has an MFMA ready (a double wave always has), a younger wave cannot issue even the
+// VALU ops between the barrier and its first MFMA (uniform-branch compares, spilled-SGPR
+// v_readlanes, LDS addresses), so it does not even read its first B fragment until the older
+// chains are done, and each hand-over between the waves of a SIMD costs the younger wave's whole
+// prelude plus the LDS latency of its B reads (~600 cycles, profiles/r05_stamp_*.txt: the loop tops
+// of a SIMD's waves fall 1.3k, 5k, 7.6k cycles after the barrier).  So every wave raises its
+// priority before the barriers of the solve loop and drops it right before its first MFMA of the
+// next GEMM: all waves get through their preludes and issue their first B reads right after the
+// barrier, and the chains then run oldest-first with their operands already in registers.
+#ifndef GPAD_NO_PRELUDE_PRIO
+#define GPAD_PRELUDE_HI() __builtin_amdgcn_s_setprio(2)
+#define GPAD_PRELUDE_LO()                  \
+    do {                                   \
+        __builtin_amdgcn_sched_barrier(0); \
+        __builtin_amdgcn_s_setprio(0);     \
+        __builtin_amdgcn_sched_barrier(0); \
+    } while (0)
+#else
+#define GPAD_PRELUDE_HI() \
+    do {                  \
+    } while (0)
+#define GPAD_PRELUDE_LO() \
+    do {                  \
+    } while (0)
+#endif
+
 // ---------------------------------------------------------------------------------------
 // Panel pairs (8 < T <= 16): a 16-wave workgroup owns TWO panels, balanced over the SIMDs.
 // A 13-wave single-panel workgroup puts 4,3,3,3 waves (tile chains) on the CU's SIMDs, and a
@@ -429,6 +456,7 @@ __device__ __forceinline__ void panel_gemm2(__amdgpu_buffer_rsrc_t PA, const flo
     a[0] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, 0, 0));
     b0[0] = B0[lane];
     if constexpr (DUAL) b1[0] = B1[lane];
+    GPAD_PRELUDE_LO();
 #pragma unroll
     for (int kb = 0; kb < T; ++kb) {
         const int cur = kb & 1, nxt = cur ^ 1;
@@ -477,13 +505,66 @@ __device__ __forceinline__ void panel_gemm3(__amdgpu_buffer_rsrc_t PA, const flo
     for (int p = 0; p < PD; ++p) a[p] = ap[p];
     b0[0] = B0[lane];
     if constexpr (DUAL) b1[0] = B1[lane];
+    b0[1] = B0[64 + lane];  // (block 1 too, so the whole prelude precedes the priority drop)
+    if constexpr (DUAL) b1[1] = B1[64 + lane];
+    GPAD_PRELUDE_LO();
+#ifdef GPAD_ROLLED_GEMM
+    // experiment (r05): the T-1 full blocks as a loop unrolled by U (kb % R and kb & 1 static in
+    // every copy), loads clamped to the last block, then the last block -- a fraction of the
+    // fully unrolled code, to test the instruction-fetch cost of the 94 KB kernel
+    constexpr int U = R == 2 ? 2 : 6;
+#pragma unroll U
+    for (int kb = 0; kb < T - 1; ++kb) {
+        const int cur = kb & 1;
+        const float4 ak = a[kb % R];
+        a[(kb + PD) % R] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(
+            PA, voff, (kb + PD < T ? kb + PD : T - 1) * T * 1024, 0));
+        __builtin_amdgcn_sched_barrier(0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, b0[cur].x, acc0, 0, 0, 0);
+        if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, b1[cur].x, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, b0[cur].y, acc0, 0, 0, 0);
+        if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, b1[cur].y, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, b0[cur].z, acc0, 0, 0, 0);
+        if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, b1[cur].z, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, b0[cur].w, acc0, 0, 0, 0);
+        if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, b1[cur].w, acc1, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        const int kn = kb + 2 < T ? kb + 2 : T - 1;
+        b0[cur] = B0[kn * 64 + lane];
+        if constexpr (DUAL) b1[cur] = B1[kn * 64 + lane];
+        if constexpr (DUAL) asm volatile("" : "+v"(acc0), "+v"(acc1)::"memory");
+        else asm volatile("" : "+v"(acc0)::"memory");
+    }
+    {
+        constexpr int kb = T - 1, cur = kb & 1;
+        const float4 ak = a[kb % R];
+        __builtin_amdgcn_sched_barrier(0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, b0[cur].x, acc0, 0, 0, 0);
+        if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, b1[cur].x, acc1, 0, 0, 0);
+        if (kq > 1) {
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, b0[cur].y, acc0, 0, 0, 0);
+            if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, b1[cur].y, acc1, 0, 0, 0);
+        }
+        if (kq > 2) {
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, b0[cur].z, acc0, 0, 0, 0);
+            if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, b1[cur].z, acc1, 0, 0, 0);
+        }
+        if (kq > 3) {
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, b0[cur].w, acc0, 0, 0, 0);
+            if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, b1[cur].w, acc1, 0, 0, 0);
+        }
+        if constexpr (DUAL) asm volatile("" : "+v"(acc0), "+v"(acc1)::"memory");
+        else asm volatile("" : "+v"(acc0)::"memory");
+    }
+    return;
+#endif
 #pragma unroll
     for (int kb = 0; kb < T; ++kb) {
         const int cur = kb & 1, nxt = cur ^ 1;
         const float4 ak = a[kb % R];
         if (kb + PD < T)
             a[(kb + PD) % R] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb + PD) * T * 1024, 0));
-        if (kb + 1 < T) {
+        if (kb >= 1 && kb + 1 < T) {  // (blocks 0 and 1 were read before the loop)
             b0[nxt] = B0[(kb + 1) * 64 + lane];
             if constexpr (DUAL) b1[nxt] = B1[(kb + 1) * 64 + lane];
         }
@@ -544,6 +625,7 @@ __device__ __forceinline__ void panel_gemm_rt(__amdgpu_buffer_rsrc_t PA, const f
     };
     float4 a0 = ap[0], a1 = PD == 2 ? ap[PD - 1] : ap[0];
     float4 e0 = B0[lane], f0 = DUAL ? B1[lane] : e0, e1, f1;
+    GPAD_PRELUDE_LO();
     for (int kb = 0;; kb += 2) {
         const int k1 = kb + 1 < last ? kb + 1 : last, k2 = kb + 2 < last ? kb + 2 : last;
         if constexpr (PD == 1) a1 = lda(kb + 1);
@@ -565,7 +647,7 @@ __device__ __forceinline__ void panel_gemm_rt(__amdgpu_buffer_rsrc_t PA, const f
 
 // k-blocks [KB0, KB1) of one chain, continuing acc (not reset): the A ring PD blocks deep is
 // seeded with blocks KB0.. by panel_a_prefetch_from; the last matrix block issues kq steps.
-template <int T, int PD, int KB0, int KB1>
+template <int T, int PD, int KB0, int KB1, bool LO = true>
 __device__ __forceinline__ void panel_chain(__amdgpu_buffer_rsrc_t PA, const float4* B0, int voff, int lane,
                                             f32x4& acc, const float4 (&ap)[PD], int kq) {
     constexpr int R = PD + 1;
@@ -573,6 +655,7 @@ __device__ __forceinline__ void panel_chain(__amdgpu_buffer_rsrc_t PA, const flo
 #pragma unroll
     for (int p = 0; p < PD; ++p) a[p] = ap[p];
     b[0] = B0[KB0 * 64 + lane];
+    if constexpr (LO) GPAD_PRELUDE_LO();  // (LO = false: a relay piece that runs at its own priority)
 #pragma unroll
     for (int kb = KB0; kb < KB1; ++kb) {
         const int i = kb - KB0, cur = i & 1, nxt = cur ^ 1;
@@ -684,7 +767,7 @@ struct Panel2Lds {
 // at six points per iteration -- loop top, GEMM-1 issued, before its barrier, after it, GEMM-2
 // issued, before the closing barrier -- read back with gpad_debug_stamps (tools/stamp_panel.py).
 #ifdef GPAD_STAMP
-constexpr int kStampV0 = 101, kStampIts = 4, kStampPts = 6;
+constexpr int kStampV0 = 101, kStampIts = 4, kStampPts = 8;  // 6, 7: GEMM 1 / 2 hand-off wait returned
 __device__ unsigned long long g_stamps[16][kStampIts][kStampPts];
 // s_memtime into SGPRs at each point (pinned by scheduling barriers), stored once per iteration after
 // the closing barrier: the store's lgkmcnt wait then sits where no LDS or scalar load is in flight,
@@ -701,7 +784,19 @@ __device__ unsigned long long g_stamps[16][kStampIts][kStampPts];
         if (blockIdx.x == 0 && v >= kStampV0 && v < kStampV0 + kStampIts && lane == 0)      \
             for (int q_ = 0; q_ < kStampPts; ++q_) g_stamps[threadIdx.x >> 6][v - kStampV0][q_] = stv[q_]; \
     } while (0)
-#define GPAD_STAMP_DECL unsigned long long stv[kStampPts] = {0, 0, 0, 0, 0, 0};
+#define GPAD_STAMP_DECL unsigned long long stv[kStampPts] = {0, 0, 0, 0, 0, 0, 0, 0};
+// phase anatomy of workgroup 0 in the phase that starts at kStampPhaseV: entry, state loaded, after
+// the load barrier, loop exit, survivors parked, after the closing barrier
+constexpr int kStampPhaseV = 100, kStampPhasePts = 6;
+__device__ unsigned long long g_pstamps[16][kStampPhasePts];
+#define GPAD_PSTAMP(P)                                                                              \
+    do {                                                                                            \
+        __builtin_amdgcn_sched_barrier(0);                                                          \
+        if (blockIdx.x == 0 && a.v_begin == kStampPhaseV && (threadIdx.x & 63) == 0)               \
+            g_pstamps[threadIdx.x >> 6][P] = __builtin_amdgcn_s_memtime();                          \
+        __builtin_amdgcn_sched_barrier(0);                                                          \
+    } while (0)
+#define GPAD_STAMP_PTR(P) (&stv[P])
 #else
 #define GPAD_STAMP_AT(P) \
     do {                 \
@@ -710,6 +805,10 @@ __device__ unsigned long long g_stamps[16][kStampIts][kStampPts];
     do {                   \
     } while (0)
 #define GPAD_STAMP_DECL
+#define GPAD_STAMP_PTR(P) nullptr
+#define GPAD_PSTAMP(P) \
+    do {               \
+    } while (0)
 #endif
 
 struct HoSlots {
@@ -750,11 +849,13 @@ __device__ __forceinline__ void handoff_post(Panel2Lds<T>& L, int slot, int gen,
 // first hand-off withholds its post, so its receiver's wait expires
 template <int T, int PD, int KB0, int KB1, bool PRIO, bool DROP>
 __device__ __forceinline__ void handoff_piece(Panel2Lds<T>& L, __amdgpu_buffer_rsrc_t PA, const float4* B0, int voff,
-                                              int lane, const float4 (&aph)[PD], HoSlots hs, int gen) {
+                                              int lane, const float4 (&aph)[PD], HoSlots hs, int gen,
+                                              unsigned long long* ts = nullptr) {
     f32x4 h = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     if (hs.in >= 0) h = handoff_wait(L, hs.in, gen, lane);
+    if (ts) *ts = __builtin_amdgcn_s_memtime();  // (stamped builds only)
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
-    panel_chain<T, PD, KB0, KB1>(PA, B0, voff, lane, h, aph, 4);
+    panel_chain<T, PD, KB0, KB1, !PRIO>(PA, B0, voff, lane, h, aph, 4);
     if (!(DROP && gen == 1 && hs.in < 0 && L.hdrop)) handoff_post(L, hs.out, gen, lane, h);
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
 }
@@ -763,10 +864,11 @@ __device__ __forceinline__ void handoff_piece(Panel2Lds<T>& L, __amdgpu_buffer_r
 template <int T, int PD, int KB0, bool PRIO>
 __device__ __forceinline__ void handoff_take(Panel2Lds<T>& L, __amdgpu_buffer_rsrc_t PA, const float4* B0, int voff,
                                              int lane, const float4 (&ap)[PD], HoSlots hs, int gen, int kq,
-                                             f32x4& acc) {
+                                             f32x4& acc, unsigned long long* ts = nullptr) {
     acc = handoff_wait(L, hs.in, gen, lane);
+    if (ts) *ts = __builtin_amdgcn_s_memtime();  // (stamped builds only)
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(2);
-    panel_chain<T, PD, KB0, T>(PA, B0, voff, lane, acc, ap, kq);
+    panel_chain<T, PD, KB0, T, !PRIO>(PA, B0, voff, lane, acc, ap, kq);
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
@@ -808,6 +910,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
     float gmx = 0.0f;                // max |g| over the rows this lane loads (gmax_part)
 
     for (int it = blockIdx.x; it < items; it += gridDim.x) {
+        GPAD_PSTAMP(0);
         // columns still running, bit 16 pp + c for panel pp of this item: the same word in every
         // wave (derived from uniform values and LDS), so the test needs no vote barrier
         unsigned live = 0u;
@@ -821,40 +924,73 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
         bool act[Q];
         int inst[Q];
         float z[Q][4], y[Q][4], u[Q][4];
+        // The columns' state, so that the loads are in flight together (r05): the instance of each
+        // column (one load), then per panel every operand load unconditionally at clamped addresses
+        // (an inactive column reads instance 0, a padding row the last real row), then the selects.  Loading under per-row / per-column conditions made the compiler branch around
+        // every load and drain vmcnt at the joins -- 8-18 dependent round trips to memory per wave,
+        // 10-23 us per phase start (profiles/r05_phase_*.txt).
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             act[q] = false;
             inst[q] = 0;
             if constexpr (NU == 0) continue;
-            const int pq = p0 + q;
-            const int k = 16 * (pair ? 2 * it + pq : it) + c;
+            const int k = 16 * (pair ? 2 * it + p0 + q : it) + c;
             act[q] = k < count;
-            inst[q] = act[q] ? (a.idx_in ? a.idx_in[k] : k) : 0;
-            float gp[4], pd[4], wv[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int i = 16 * t + 4 * r + j;
-                const bool okn = act[q] && i < n, okm = act[q] && i < m;
-                const size_t b = (size_t)inst[q];
-                z[q][r] = okn ? a.z[b * n + i] : 0.0f;
-                gp[r] = okn ? a.gP[b * a.ld_gP + i] : 0.0f;
-                y[q][r] = okm ? a.y[b * m + i] : 0.0f;
-                const float gr = okm ? a.g[b * a.ld_g + i] : 0.0f;
-                pd[r] = (float)(a.gscale * (double)gr);
-                gmx = absmax_nan(gmx, gr);
-                if (fresh) {  // w_0 = y_0 + beta_0 (y_0 - y_{-1}), y_{-1} = y_0
-                    wv[r] = __builtin_fmaf(a.beta[0], y[q][r] - y[q][r], y[q][r]);
-                    u[q][r] = 0.0f;
-                } else {
-                    wv[r] = okm ? a.wc[b * m + i] : 0.0f;
-                    u[q][r] = okm && use_tol ? a.uc[b * m + i] : 0.0f;
-                }
-            }
-            L.Gp[pq][slot] = make_float4(gp[0], gp[1], gp[2], gp[3]);
-            L.Pd[pq][slot] = make_float4(pd[0], pd[1], pd[2], pd[3]);
-            L.Wl[pq][slot] = make_float4(wv[0], wv[1], wv[2], wv[3]);
-            if (fresh && use_tol) L.Zh[pq][slot] = make_float4(z[q][0], z[q][1], z[q][2], z[q][3]);
+            inst[q] = a.idx_in ? a.idx_in[act[q] ? k : 0] : (act[q] ? k : 0);
         }
+        if constexpr (NU > 0) {
+            const float beta0 = a.beta[0];
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {  // one round trip per panel (a double wave: two)
+                float zl[4], gpl[4], yl[4], gl[4], wl[4], ul[4];
+                const size_t b = (size_t)inst[q];
+                const float* zb = a.z + b * n;
+                const float* gpb = a.gP + b * a.ld_gP;
+                const float* yb = a.y + b * m;
+                const float* gb = a.g + b * a.ld_g;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 16 * t + 4 * r + j;
+                    const int in = i < n ? i : n - 1, im = i < m ? i : m - 1;
+                    zl[r] = zb[in];
+                    gpl[r] = gpb[in];
+                    yl[r] = yb[im];
+                    gl[r] = gb[im];
+                    if (!fresh) {
+                        wl[r] = a.wc[b * m + im];
+                        ul[r] = use_tol ? a.uc[b * m + im] : 0.0f;
+                    }
+                }
+                const int pq = p0 + q;
+                float gp[4], pd[4], wv[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 16 * t + 4 * r + j;
+                    const bool okn = act[q] && i < n, okm = act[q] && i < m;
+                    z[q][r] = okn ? zl[r] : 0.0f;
+                    gp[r] = okn ? gpl[r] : 0.0f;
+                    y[q][r] = okm ? yl[r] : 0.0f;
+                    const float gr = okm ? gl[r] : 0.0f;
+                    pd[r] = (float)(a.gscale * (double)gr);
+                    gmx = absmax_nan(gmx, gr);
+                    if (fresh) {  // w_0 = y_0 + beta_0 (y_0 - y_{-1}), y_{-1} = y_0
+                        wv[r] = __builtin_fmaf(beta0, y[q][r] - y[q][r], y[q][r]);
+                        u[q][r] = 0.0f;
+                    } else {
+                        wv[r] = okm ? wl[r] : 0.0f;
+                        u[q][r] = okm ? ul[r] : 0.0f;
+                    }
+                }
+                L.Gp[pq][slot] = make_float4(gp[0], gp[1], gp[2], gp[3]);
+                L.Pd[pq][slot] = make_float4(pd[0], pd[1], pd[2], pd[3]);
+                L.Wl[pq][slot] = make_float4(wv[0], wv[1], wv[2], wv[3]);
+                if (fresh && use_tol) L.Zh[pq][slot] = make_float4(z[q][0], z[q][1], z[q][2], z[q][3]);
+            }
+        }
+#ifdef GPAD_STAMP
+        if constexpr (NU > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's state is in
+#endif
+        GPAD_PSTAMP(1);
         if (fresh && use_tol) {  // u = G_L z_{-1} -- zero, and no GEMM, when every z_{-1} is zero
             // (a cold start: every chain step fma(G_L, 0, +0) gives +0, so u = +0 exactly)
             bool nz = false;
@@ -894,26 +1030,29 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             if constexpr (ROLE == 1) panel_a_prefetch<T, PD>(PA, voff_r, aph);
             if constexpr (ROLE == 3) panel_a_prefetch_from<T, PD>(PA, voff, aph, KB0);
         };
+        GPAD_PSTAMP(2);
         prefetch(PA1);
         int v = a.v_begin;
         GPAD_STAMP_DECL
         int kc = K - v % K;  // iterations to the next test: chk <=> v % K == 0 (a countdown, no division)
         float th = a.theta[v], bn = a.beta[v + 1];
         while (true) {
+            GPAD_STAMP_AT(0);  // (before the schedule's scalar loads, which a later s_memtime queues behind)
             const float th_next = a.theta[v + 1], bn_next = a.beta[v + 2];
             ++v;
             const bool chk = use_tol && --kc == 0;
             if (kc == 0) kc = K;
             const float omt = 1.0f - th;
-            GPAD_STAMP_AT(0);
             // ---- GEMM 1 + epilogue: zhat = -ML w - g_P (8b), z = (1-th) z + th zhat (8c) ----
             if constexpr (NU > 0) {
                 f32x4 acc[2];
                 ++hgen;
                 if constexpr (ROLE == 1)
-                    handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA1, L.Wl[p0], voff_r, lane, aph, hs, hgen);
+                    handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA1, L.Wl[p0], voff_r, lane, aph, hs, hgen,
+                                                               GPAD_STAMP_PTR(6));
                 if constexpr (ROLE == 2)
-                    handoff_take<T, PD, KB0, PRIO>(L, PA1, L.Wl[p0], voff, lane, ap, hs, hgen, kq1, acc[0]);
+                    handoff_take<T, PD, KB0, PRIO>(L, PA1, L.Wl[p0], voff, lane, ap, hs, hgen, kq1, acc[0],
+                                                   GPAD_STAMP_PTR(6));
                 else if (on1 && nkb1 == T)
                     panel_gemm3<T, NU == 2, PD>(PA1, L.Wl[p0], L.Wl[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1],
                                                 ap, kq1);
@@ -943,10 +1082,12 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 }
             } else if constexpr (ROLE == 3) {
                 ++hgen;
-                handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA1, L.Wl[p0], voff, lane, aph, hs, hgen);
+                handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA1, L.Wl[p0], voff, lane, aph, hs, hgen,
+                                                           GPAD_STAMP_PTR(6));
                 prefetch(PA2);
             }
             GPAD_STAMP_AT(2);
+            GPAD_PRELUDE_HI();
             __syncthreads();
             GPAD_STAMP_AT(3);
             // ---- GEMM 2 + epilogue: y+ = [w + G_L zhat + p_D]+ (8d), next w (8a) ----------
@@ -963,9 +1104,11 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 f32x4 acc[2];
                 ++hgen;
                 if constexpr (ROLE == 1)
-                    handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA2, L.Zh[p0], voff_r, lane, aph, hs, hgen);
+                    handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA2, L.Zh[p0], voff_r, lane, aph, hs, hgen,
+                                                               GPAD_STAMP_PTR(7));
                 if constexpr (ROLE == 2)
-                    handoff_take<T, PD, KB0, PRIO>(L, PA2, L.Zh[p0], voff, lane, ap, hs, hgen, kq2, acc[0]);
+                    handoff_take<T, PD, KB0, PRIO>(L, PA2, L.Zh[p0], voff, lane, ap, hs, hgen, kq2, acc[0],
+                                                   GPAD_STAMP_PTR(7));
                 else if (on2 && nkb2 == T)
                     panel_gemm3<T, NU == 2, PD>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1],
                                                 ap, kq2);
@@ -1044,12 +1187,14 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 }
             } else if constexpr (ROLE == 3) {
                 ++hgen;
-                handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA2, L.Zh[p0], voff, lane, aph, hs, hgen);
+                handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA2, L.Zh[p0], voff, lane, aph, hs, hgen,
+                                                           GPAD_STAMP_PTR(7));
                 prefetch(PA1);
             }
             th = th_next;
             bn = bn_next;
             GPAD_STAMP_AT(5);
+            GPAD_PRELUDE_HI();
             __syncthreads();
             GPAD_STAMP_FLUSH();
             if (!chk && v < a.v_end) continue;
@@ -1125,23 +1270,40 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             }
             // ---- finished columns: results out ---------------------------------------------
             if constexpr (NU > 0) {
+                // values and row pointers first, the stores after (see the phase-end park below)
+                bool out[Q];
+                int cd[Q];
+                float zo[Q][4];
+                float *zr[Q], *yr[Q];
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
                     const int bit = 16 * (p0 + q) + c;
-                    const int cdq = ((m1 >> bit) & 1u) ? 1 : (((m2 >> bit) & 1u) ? 2 : 0);
-                    if (act[q] && (cdq != 0 || v >= N)) {
-                        const float4 h4 = L.Zh[p0 + q][slot];
-                        const float zh[4] = {h4.x, h4.y, h4.z, h4.w};
-                        const size_t b = (size_t)inst[q];
+                    cd[q] = ((m1 >> bit) & 1u) ? 1 : (((m2 >> bit) & 1u) ? 2 : 0);
+                    out[q] = act[q] && (cd[q] != 0 || v >= N);
+                    const float4 h4 = L.Zh[p0 + q][slot];
+                    const bool use_zh = cd[q] == 2;
+                    zo[q][0] = use_zh ? h4.x : z[q][0];
+                    zo[q][1] = use_zh ? h4.y : z[q][1];
+                    zo[q][2] = use_zh ? h4.z : z[q][2];
+                    zo[q][3] = use_zh ? h4.w : z[q][3];
+                    const size_t b = (size_t)inst[q];
+                    zr[q] = a.z + b * n + 16 * t + j;
+                    yr[q] = a.y + b * m + 16 * t + j;
+                }
+                const bool fn = 16 * t + 16 <= n, fm = 16 * t + 16 <= m;
+#pragma unroll
+                for (int q = 0; q < Q; ++q) {
+                    if (out[q]) {
+                        const bool zw = cd[q] != 2 || zh_out;  // (B)'s zhat already out before (A)'s GEMM
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             const int i = 16 * t + 4 * r + j;
-                            if (i < n && (cdq != 2 || zh_out)) a.z[b * n + i] = cdq == 2 ? zh[r] : z[q][r];
-                            if (i < m) a.y[b * m + i] = y[q][r];
+                            if ((fn || i < n) && zw) zr[q][4 * r] = zo[q][r];
+                            if (fm || i < m) yr[q][4 * r] = y[q][r];
                         }
                         if (t == 0 && j == 0) {
-                            a.iters[b] = v;
-                            a.conv[b] = cdq;
+                            a.iters[inst[q]] = v;
+                            a.conv[inst[q]] = cd[q];
                         }
                         act[q] = false;
                     }
@@ -1152,32 +1314,54 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             if (v >= a.v_end || live == 0u) break;
         }
         // ---- phase end: park the survivors -----------------------------------------------
+        GPAD_PSTAMP(3);
         if constexpr (NU > 0) {
             if (carry) {
+                // values and row pointers first, then every store (r05): vmcnt counts stores on
+                // gfx9, so a spill reload between stores waits for all the stores before it -- the
+                // interleaved form took 7-17 us per phase end (profiles/r05_phase_*.txt)
+                bool pk[Q];
+                float wv[Q][4];
+                float *zr[Q], *yr[Q], *wr[Q], *ur[Q];
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
-                    const bool park = act[q] && v >= a.v_end;
-                    if (park) {
-                        const float4 w4 = L.Wl[p0 + q][slot];
-                        const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
-                        const size_t b = (size_t)inst[q];
+                    pk[q] = act[q] && v >= a.v_end;
+                    const float4 w4 = L.Wl[p0 + q][slot];
+                    wv[q][0] = w4.x;
+                    wv[q][1] = w4.y;
+                    wv[q][2] = w4.z;
+                    wv[q][3] = w4.w;
+                    const size_t b = (size_t)inst[q];
+                    zr[q] = a.z + b * n + 16 * t + j;
+                    yr[q] = a.y + b * m + 16 * t + j;
+                    wr[q] = a.wc + b * m + 16 * t + j;
+                    ur[q] = a.uc + b * m + 16 * t + j;
+                }
+                const bool fn = 16 * t + 16 <= n, fm = 16 * t + 16 <= m;  // full tiles: no row checks
+#pragma unroll
+                for (int q = 0; q < Q; ++q) {
+                    if (pk[q]) {
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             const int i = 16 * t + 4 * r + j;
-                            if (i < n) a.z[b * n + i] = z[q][r];
-                            if (i < m) {
-                                a.y[b * m + i] = y[q][r];
-                                a.wc[b * m + i] = wv[r];
-                                if (use_tol) a.uc[b * m + i] = u[q][r];
+                            if (fn || i < n) zr[q][4 * r] = z[q][r];
+                            if (fm || i < m) {
+                                yr[q][4 * r] = y[q][r];
+                                wr[q][4 * r] = wv[q][r];
+                                if (use_tol) ur[q][4 * r] = u[q][r];
                             }
                         }
                     }
-                    if (t == 0)  // the tile-0 owner of panel p0+q lists its survivors
-                        list_survivors(a, pair ? 2 * it + p0 + q : it, park, inst[q], lane, j);
+                }
+                if (t == 0) {  // the tile-0 owner of each panel lists its survivors
+#pragma unroll
+                    for (int q = 0; q < Q; ++q) list_survivors(a, pair ? 2 * it + p0 + q : it, pk[q], inst[q], lane, j);
                 }
             }
         }
+        GPAD_PSTAMP(4);
         __syncthreads();
+        GPAD_PSTAMP(5);
     }
     if (a.gmax_part) {  // this wave's max |g| -> L.gred (reduced by the kernel at exit)
         for (int o = 32; o > 0; o >>= 1) gmx = absmax_nan(gmx, __shfl_xor(gmx, o, 64));
@@ -1701,8 +1885,13 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
 
 #ifdef GPAD_STAMP
 hipError_t read_stamps(unsigned long long* out, size_t bytes) {
-    if (bytes > sizeof(g_stamps)) bytes = sizeof(g_stamps);
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), bytes, 0, hipMemcpyDeviceToHost);
+    // g_stamps, then (when the buffer has room) g_pstamps
+    size_t b0 = bytes > sizeof(g_stamps) ? sizeof(g_stamps) : bytes;
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), b0, 0, hipMemcpyDeviceToHost);
+    if (e != hipSuccess || bytes <= sizeof(g_stamps)) return e;
+    size_t b1 = bytes - sizeof(g_stamps);
+    if (b1 > sizeof(g_pstamps)) b1 = sizeof(g_pstamps);
+    return hipMemcpyFromSymbol(out + sizeof(g_stamps) / 8, HIP_SYMBOL(g_pstamps), b1, 0, hipMemcpyDeviceToHost);
 }
 #endif
 

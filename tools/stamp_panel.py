@@ -27,45 +27,36 @@ def main():
     r = microbench.case("panel", 200, 200, args.batch, args.N, reps=1)
     from gpad_mpc import _lib
     L = _lib.load()
-    ITS, PTS = 4, 6
+    ITS, PTS = 4, 8
     buf = (C.c_ulonglong * (16 * ITS * PTS))()
     f = L._lib.gpad_debug_stamps if hasattr(L, "_lib") else L.gpad_debug_stamps
     f.argtypes = [C.c_void_p, C.c_size_t]
     assert f(buf, C.sizeof(buf)) == 0
-    st = np.array(buf, dtype=np.int64).reshape(16, ITS, PTS)
-    names = ["gemm1", "epi1", "bar1", "gemm2", "epi2", "bar2"]
+    st = np.array(buf, dtype=np.int64).reshape(16, ITS, PTS).astype(np.float64)
+    st[st == 0] = np.nan
     print(f"batch {args.batch}: {r['us_per_iter']} us/iteration (stamped build)")
     pair = (args.batch + 15) // 16 > 256
-    per_iter = []
+    # times relative to each iteration's loop-top release (min over waves of stamp 0), averaged
+    # over the stamped iterations; columns in program order
+    cols = [(0, "top"), (6, "wait1"), (1, "gemm1"), (2, "prebar1"), (3, "bar1"), (7, "wait2"), (4, "gemm2"),
+            (5, "prebar2")]
+    ref = np.nanmin(st[:, :, 0], axis=0)  # [ITS]
+    nxt = np.nanmin(st[:, 1:, 0], axis=0)  # next iteration's release
+    print("cycles after the iteration's loop-top release (min over waves of stamp 0); '-' = no stamp:")
+    print("wave SIMD role " + " ".join(f"{n:>8s}" for _, n in cols))
     for w in range(16):
-        # the role this wave plays (gpad_panel2_kernel: one panel -> 15 - w; pairs -> the receiver swap)
         role = ((w + 4) if (w >> 1) == 4 else ((w - 4) if (w >> 1) == 6 else w)) if pair else 15 - w
-        d = np.zeros(PTS)
-        ok = np.ones(PTS, bool)
-        for i in range(ITS - 1):
-            s_ = st[w, i]
-            nxt = st[w, i + 1, 0]
-            pts = list(s_) + [nxt]
-            for k in range(PTS):
-                if pts[k] == 0 or pts[k + 1] == 0:
-                    ok[k] = False
-                else:
-                    d[k] += pts[k + 1] - pts[k]
-        d /= ITS - 1
-        it = (st[w, ITS - 1, 0] - st[w, 0, 0]) / (ITS - 1)
-        per_iter.append(it)
-        # relay waves (no GEMM-issue stamps): merge the issue and epilogue segments
-        if not ok[1] or not ok[0]:
-            seg = f"piece1+epi1 {int(st[w, :ITS - 1, 2].astype(float).mean() - st[w, :ITS - 1, 0].astype(float).mean()):6d}"
-        else:
-            seg = f"{names[0]} {int(d[0]):6d}  {names[1]} {int(d[1]):6d}"
-        rest = "  ".join(f"{n} {int(x):6d}" if ok[k] else f"{n}      -" for k, (n, x) in enumerate(zip(names, d)) if k >= 2)
-        print(f"wave {w:2d} SIMD {w % 4} role {role:2d}: {seg}  {rest}  | iter {int(it)}")
-    t0 = st[:, :, 0]
-    print("loop-top skew across waves (cycles):", int(t0[:, 1].max() - t0[:, 1].min()))
-    cyc = float(np.mean(per_iter))
-    print(f"cycles per iteration {cyc:.0f}; implied clock {cyc / r['us_per_iter'] / 1e3:.2f} GHz "
-          f"(stamps from a stamped build, whose iteration may differ from the product's)")
+        vals = []
+        for k, _ in cols:
+            x = st[w, :, k] - ref
+            m = np.nanmean(x[:ITS - 1]) if np.isfinite(x[:ITS - 1]).any() else np.nan
+            vals.append("       -" if np.isnan(m) else f"{int(m):8d}")
+        print(f"{w:4d} {w % 4:4d} {role:4d} " + " ".join(vals))
+    it = float(np.nanmean(nxt - ref[:ITS - 1]))
+    print(f"iteration (release to release): {it:.0f} cycles; implied clock {it / r['us_per_iter'] / 1e3:.2f} GHz "
+          f"(stamped build)")
+    bar1 = np.nanmin(st[:, :, 3] - ref, axis=0)[:ITS - 1].mean()
+    print(f"barrier-1 release at {bar1:.0f}; GEMM-2 phase {it - bar1:.0f}")
 
 
 if __name__ == "__main__":
