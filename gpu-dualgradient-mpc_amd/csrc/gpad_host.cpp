@@ -129,6 +129,7 @@ struct gpad_handle_s {
     bool frag64_ok = false;
     int frag64_tiles = 0;
     DevBuf hfrag64;      // ... and H's, bound by gpad_setup_hessian (value branches on the f64 panels)
+    DevBuf q64;          // f64 panels: the refill queue counter (one int, zeroed per launch)
     bool hfrag64_ok = false;
     int frag_tiles = 0;
     DevBuf theta, beta;
@@ -282,6 +283,7 @@ int gpad_destroy(gpad_handle_t h) {
     h->Hq.release();
     h->frag64.release();
     h->hfrag64.release();
+    h->q64.release();
     h->frag.release();
     h->stage.release();
     h->theta.release();
@@ -338,6 +340,12 @@ int gpad_set_option(gpad_handle_t h, int option, int value) {
             return set(t.flat_waves, 0, 16, def.flat_waves);
         case GPAD_OPT_FLAT_A_LDS: return set(t.flat_a_lds, 0, 1, def.flat_a_lds);
         case GPAD_OPT_DEBUG_DROP_HANDOFF: return set(t.debug_drop_handoff, 0, 1, def.debug_drop_handoff);
+        case GPAD_OPT_P64_REFILL: {
+            int on = 1 - t.p64_no_refill;
+            const int rc = set(on, 0, 1, 1);
+            t.p64_no_refill = 1 - on;
+            return rc;
+        }
         case GPAD_OPT_P64_RELAY: {
             int on = 1 - t.p64_no_relay;
             const int rc = set(on, 0, 1, 1);
@@ -826,6 +834,8 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
         if (h->frag64_ok && (kernel == GPAD_KERNEL_PANEL || (kernel == GPAD_KERNEL_AUTO && batch >= 16 * h->num_cus))) {
             a.frag = h->frag64.p;
             a.frag_tiles = h->frag64_tiles;
+            if (int rq = h->q64.ensure(sizeof(int))) return rq;
+            a.qctr = static_cast<int*>(h->q64.p);
             a.hfrag64 = (a.Hq && h->hfrag64_ok) ? h->hfrag64.p : nullptr;
             a.Hq = nullptr;
             e = gpad::launch_panel64(a, h->stream);

@@ -29,6 +29,7 @@ struct Tuning {
     int flat_a_lds = 1;       // GPAD_OPT_FLAT_A_LDS: flat fragment image in LDS when it fits
     int debug_drop_handoff = 0;  // GPAD_OPT_DEBUG_DROP_HANDOFF: test-only fault injection
     int p64_no_relay = 0;     // GPAD_OPT_P64_RELAY = 0: f64 panels without the relay layout
+    int p64_no_refill = 0;    // GPAD_OPT_P64_REFILL = 0: f64 panels without column refills
 };
 
 // Device error word of a run (SolveArgs::err): kernels OR these bits in with a vector atomic;

@@ -258,7 +258,15 @@ __device__ __forceinline__ f64x4 p64_gemm(Lds& L, __amdgpu_buffer_rsrc_t PA, con
     return on ? gemm64p<T>(PA, Bl, voff, lane, nkb, a0) : f64x4{0.0, 0.0, 0.0, 0.0};
 }
 
-template <int T, bool RELAY>
+// REFILL (round 5, tol > 0 with N a multiple of the test period and more panels than workgroups):
+// a finished column takes the next instance of the batch from a device counter (a.qctr) at the
+// test event that finished it, instead of idling until its panel's slowest column is done.  Each
+// column keeps its own iteration count vc (theta_vc, beta_vc+1 per lane); columns start only at
+// test events, so every column's vc stays congruent to the workgroup's step count modulo K and the
+// test events stay uniform.  Every column's arithmetic is the one-panel-at-a-time kernel's (the
+// MFMA output column depends on its B column only), so z, y, counts and codes are bit-identical.
+// 8192 value problems on 256 CUs (two per column on average): profiles/r05_p64_refill_ab.txt.
+template <int T, bool RELAY, bool REFILL>
 __global__ __launch_bounds__(RELAY ? 1024 : 64 * T) void gpad_panel64_kernel(SolveArgs<double> a) {
     constexpr int TL = P64Lds<T, RELAY>::TL;
     __shared__ f64x4 Wl[TL * 64];
@@ -268,6 +276,7 @@ __global__ __launch_bounds__(RELAY ? 1024 : 64 * T) void gpad_panel64_kernel(Sol
     __shared__ P64Slot slots[TL];
     __shared__ double vsum[2][TL][16];
     __shared__ P64Hand<RELAY> L;
+    __shared__ int newinst[16];  // REFILL: the instance each column takes next (-1 none, -2 keeps its own)
 
     const int lane = threadIdx.x & 63;
     // role: tile index (relay layout: dealt from the last wave down; roles >= T are relay waves
@@ -299,28 +308,40 @@ __global__ __launch_bounds__(RELAY ? 1024 : 64 * T) void gpad_panel64_kernel(Sol
     const double eV = a.tol_gap;
     const int panels = (a.batch + 15) / 16;
 
-    for (int p = blockIdx.x; p < panels; p += gridDim.x) {
-        const int inst = 16 * p + c;
+    // (REFILL: one pass -- the panels past the first grid are dealt column by column through the queue)
+    for (int p = blockIdx.x; p < panels && (!REFILL || p == (int)blockIdx.x); p += gridDim.x) {
+        int inst = 16 * p + c;
         bool active = inst < a.batch;
         // register r <-> row 16t + 4r + j of the column's instance
         double z[4], y[4], u[4], pd[4];
-        {
+        // a column's starting state (every column at a panel's start; REFILL: the refilled ones)
+        auto load_col = [&](bool mine) {
             f64x4 w, gp;
+            const f64x4 w_old = Wl[slot], gp_old = Gp[slot];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int i = 16 * t + 4 * r + j;
                 const bool okn = active && i < n, okm = active && i < m;
-                z[r] = okn ? a.z[(size_t)inst * n + i] : 0.0;
+                const double zr = okn ? a.z[(size_t)inst * n + i] : 0.0;
                 gp[r] = okn ? a.gP[(size_t)inst * a.ld_gP + i] : 0.0;
-                y[r] = okm ? a.y[(size_t)inst * m + i] : 0.0;
-                pd[r] = okm ? a.gscale * a.g[(size_t)inst * a.ld_g + i] : 0.0;
-                w[r] = __builtin_fma(a.beta[0], y[r] - y[r], y[r]);  // 8a with y_0 = y_{-1}
-                u[r] = 0.0;
+                const double yr = okm ? a.y[(size_t)inst * m + i] : 0.0;
+                const double pr = okm ? a.gscale * a.g[(size_t)inst * a.ld_g + i] : 0.0;
+                w[r] = __builtin_fma(a.beta[0], yr - yr, yr);  // 8a with y_0 = y_{-1}
+                if (mine) {
+                    z[r] = zr;
+                    y[r] = yr;
+                    pd[r] = pr;
+                    u[r] = 0.0;
+                } else {
+                    w[r] = w_old[r];
+                    gp[r] = gp_old[r];
+                }
             }
             Wl[slot] = w;
             Gp[slot] = gp;
             Xv[slot] = f64x4{z[0], z[1], z[2], z[3]};
-        }
+        };
+        load_col(true);
         __syncthreads();
         if (use_tol && on2) {  // u = G_L z_{-1}, then the 8c recursion
             const f64x4 cz = gemm64<T>(PA2, Xv, voff, lane, nkb2);
@@ -329,11 +350,14 @@ __global__ __launch_bounds__(RELAY ? 1024 : 64 * T) void gpad_panel64_kernel(Sol
         }
         __syncthreads();
 
-        int v = 0;
+        int v = 0;   // workgroup steps (= every column's iteration count without REFILL)
+        int vc = 0;  // REFILL: this column's iteration count
         f64x4 apre = p64_first_a<T, RELAY>(PA1, voff, lane, on1, rrole);  // GEMM 1's first A block
         while (true) {
-            const double th = a.theta[v], bn = a.beta[v + 1];
+            const int vi = REFILL ? vc : v;
+            const double th = a.theta[vi], bn = a.beta[vi + 1];
             ++v;
+            if (REFILL && active) ++vc;
             const bool chk = use_tol && (v % K) == 0;
             const double omt = 1.0 - th;
             // ---- GEMM 1 + epilogue: zhat = -ML w - g_P (8b), z = (1-th) z + th zhat (8c) ----
@@ -395,7 +419,8 @@ __global__ __launch_bounds__(RELAY ? 1024 : 64 * T) void gpad_panel64_kernel(Sol
                 }
             }
             __syncthreads();
-            if (!chk && v < N) continue;
+            if (REFILL ? !chk : (!chk && v < N)) continue;  // (REFILL: N % K == 0, a column reaches N at a test)
+            const int vd = REFILL ? vc : v;  // this column's iteration count
 
             // ---- Algorithm 1, per column (lane c's column; every wave reads every tile) ----------
             int code = 0;
@@ -515,7 +540,7 @@ __global__ __launch_bounds__(RELAY ? 1024 : 64 * T) void gpad_panel64_kernel(Sol
                 }
             }
             // ---- finished columns: results out (tests (B), (B'), (B'') certify zhat) -----------
-            if (active && (code != 0 || v >= N)) {
+            if (active && (code != 0 || vd >= N)) {
                 const f64x4 zk = Zh[slot];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -524,10 +549,46 @@ __global__ __launch_bounds__(RELAY ? 1024 : 64 * T) void gpad_panel64_kernel(Sol
                     if (i < m) a.y[(size_t)inst * m + i] = y[r];
                 }
                 if (t == 0 && j == 0) {
-                    a.iters[inst] = v;
+                    a.iters[inst] = vd;
                     a.conv[inst] = code;
                 }
                 active = false;
+            }
+            if constexpr (REFILL) {
+                // finished columns take the next instances (wave 0 claims for the workgroup; the
+                // instances past the first grid x 16 are dealt in claim order)
+                if (w0 == 0 && lane < 16) {
+                    const unsigned long long needm = __ballot(!active);
+                    const int cnt = (int)__popcll(needm & 0xffffull);
+                    int base = 0;
+                    if (lane == 0 && cnt) base = atomicAdd(a.qctr, cnt);
+                    base = __shfl(base, 0, 64);
+                    const int rank = (int)__popcll(needm & ((1ull << lane) - 1ull));
+                    const int k = 16 * (int)gridDim.x + base + rank;
+                    newinst[lane] = active ? -2 : (k < a.batch ? k : -1);
+                }
+                __syncthreads();
+                const int nk = newinst[c];
+                const bool fresh_col = nk >= 0;
+                if (fresh_col) {
+                    inst = nk;
+                    active = true;
+                    vc = 0;
+                }
+                if (__syncthreads_or(fresh_col ? 1 : 0)) {
+                    load_col(fresh_col);
+                    bool znz = false;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) znz = znz || (fresh_col && z[r] != 0.0);
+                    if (__syncthreads_or(znz ? 1 : 0)) {  // u = G_L z_{-1} for the new columns (Xv = z)
+                        const f64x4 cz = on2 ? gemm64<T>(PA2, Xv, voff, lane, nkb2) : f64x4{0.0, 0.0, 0.0, 0.0};
+                        if (fresh_col) {
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) u[r] = cz[r];
+                        }
+                        __syncthreads();
+                    }
+                }
             }
             if (!__syncthreads_or(active ? 1 : 0)) break;
         }
@@ -558,8 +619,8 @@ int p64_per_cu() {
     static int occ = 0;
     if (!occ) {
         int o = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, gpad_panel64_kernel<T, RELAY>, RELAY ? 1024 : 64 * T, 0) !=
-                hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, gpad_panel64_kernel<T, RELAY, true>, RELAY ? 1024 : 64 * T,
+                                                         0) != hipSuccess ||
             o < 1)
             o = 1;
         occ = o;
@@ -572,7 +633,16 @@ hipError_t launch_p64(const SolveArgs<double>& a, hipStream_t s) {
     const int panels = (a.batch + 15) / 16;
     const int cap = a.num_cus * p64_per_cu<T, RELAY>();
     const int grid = panels < cap ? panels : cap;
-    hipLaunchKernelGGL((gpad_panel64_kernel<T, RELAY>), dim3(grid), dim3(RELAY ? 1024 : 64 * T), 0, s, a);
+    const int K = a.check_every > 0 ? a.check_every : 1;
+    // refills need a counter, a tolerance, N on a test event, and more panels than workgroups
+    const bool refill = a.qctr && a.tol > 0.0 && a.N % K == 0 && panels > grid && !(a.tune && a.tune->p64_no_refill);
+    if (refill) {
+        hipError_t e = hipMemsetAsync(a.qctr, 0, sizeof(int), s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((gpad_panel64_kernel<T, RELAY, true>), dim3(grid), dim3(RELAY ? 1024 : 64 * T), 0, s, a);
+    } else {
+        hipLaunchKernelGGL((gpad_panel64_kernel<T, RELAY, false>), dim3(grid), dim3(RELAY ? 1024 : 64 * T), 0, s, a);
+    }
     return hipGetLastError();
 }
 

@@ -395,6 +395,9 @@ int gpad_schedule(int N, int kind, double* theta, double* beta);
                                     * a separate test-only kernel instantiation while it is set */
 #define GPAD_OPT_P64_RELAY 18      /* 1: f64 panels at T = 9, 13 (n, m in (128, 144], (192, 208]) run
                                     * the 16-wave relay layout (default); 0: one wave per tile */
+#define GPAD_OPT_P64_REFILL 19     /* 1: f64 panel solves with tol > 0, N a multiple of check_every and
+                                    * more panels than workgroups refill a finished column with the
+                                    * next instance (default); 0: each panel runs to its slowest column */
 int gpad_set_option(gpad_handle_t h, int option, int value);
 
 /* Synchronise the handle's stream (for callers using device memory + async runs). */

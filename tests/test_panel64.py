@@ -157,3 +157,36 @@ def test_panel64_value_branches_relay_t9(gpu, shift, tol, tol_gap, K):
         np.testing.assert_array_equal(x, y_)
         np.testing.assert_array_equal(x, w)
     assert set(a[3].tolist()) & {3, 4}
+
+
+@pytest.mark.parametrize("K", [10, 1])
+def test_panel64_refill_bitexact(gpu, K):
+    """More panels than workgroups at the C4 shape (4608 value problems, n = m = 200: 288 panels on
+    at most 256 one-panel workgroups) with e_g = e_V = 1e-6 and H bound: finished columns take the
+    next instances (column refills, round 5).  Bit-identical to the run without refills and to the
+    f64 stream kernel -- z, y, counts and codes."""
+    B, tol = 4608, 1e-6
+    H, ML, M, G, g, L = (np.asarray(a) for a in value_problem(200, 200, 7, 1.0, batch=B)[:6])
+    N = 20000 if K == 10 else 19999  # K = 1: every N is a test event
+    a = _run(ML, G, L, M, g, N, tol, kernel="panel", H=H, tol_gap=tol, K=K)
+    b = _run(ML, G, L, M, g, N, tol, kernel="panel", H=H, tol_gap=tol, K=K, opts={"p64_refill": 0})
+    c = _run(ML, G, L, M, g, N, tol, kernel="stream", H=H, tol_gap=tol, K=K)
+    assert a[4]["kernel"] == "panel" and a[4]["converged"] == B
+    for x, y_, w in zip(a[:4], b[:4], c[:4]):
+        np.testing.assert_array_equal(x, y_)
+        np.testing.assert_array_equal(x, w)
+
+
+def test_panel64_refill_max_iterations(gpu):
+    """Refills with columns that stop at N (N a multiple of the test period, tolerance out of reach
+    for some): the counts and codes (0 = ran to N) equal the run without refills."""
+    from gpad_mpc import problems
+    B, n, m = 4200, 200, 200
+    qp = problems.synthetic_qp(n, m, batch=B, seed=5)
+    ML, G = np.asarray(qp.ML), np.asarray(qp.G)
+    M, g = np.asarray(qp.M).reshape(B, n), np.asarray(qp.g).reshape(B, m)
+    a = _run(ML, G, qp.L, M, g, 120, 1e-12, kernel="panel")
+    b = _run(ML, G, qp.L, M, g, 120, 1e-12, kernel="panel", opts={"p64_refill": 0})
+    for x, y_ in zip(a[:4], b[:4]):
+        np.testing.assert_array_equal(x, y_)
+    assert (a[3] == 0).any() and (a[2] <= 120).all()

@@ -37,7 +37,8 @@ def main():
     dH, dML, dG, dM, dg = f64(H), f64(ML), f64(G), f64(M), f64(g)
     z = torch.zeros(B, n, dtype=torch.float64, device=dev)
     y = torch.zeros(B, m, dtype=torch.float64, device=dev)
-    variants = {"relay": {"p64_relay": 1}, "tiles": {"p64_relay": 0}}
+    variants = {"relay+refill": {"p64_relay": 1, "p64_refill": 1}, "relay": {"p64_relay": 1, "p64_refill": 0},
+                "tiles": {"p64_relay": 0, "p64_refill": 0}}
     solvers = {}
     for name, opts in variants.items():
         s = gpad_mpc.GpadSolver(0)
