@@ -1492,7 +1492,16 @@ struct PlanModel {
     int T, n, m, num_cus, grid;
     bool handoff;  // gpad_panel2_kernel's hand-off shapes (Handoff)
     bool relay;    // ... and its one-panel relay (T = 9, 13)
-    double t_chain, t_res, t_launch = 5.0;
+#ifndef GPAD_PLAN_TLAUNCH
+#define GPAD_PLAN_TLAUNCH 5.0
+#endif
+#ifndef GPAD_PLAN_TLAT
+#define GPAD_PLAN_TLAT 1.4
+#endif
+#ifndef GPAD_PLAN_CARRY_BW
+#define GPAD_PLAN_CARRY_BW 5e6
+#endif
+    double t_chain, t_res, t_launch = GPAD_PLAN_TLAUNCH;
     double iter_time(long long panels) const {
         if (panels <= 0) return 0.0;
         double chains;
@@ -1519,10 +1528,10 @@ struct PlanModel {
     }
     double phase(int v0, int v1, long long s0) const {
         const double it = iter_time((s0 + 15) / 16);
-        return 2 * t_launch + (v1 - v0 + 1) * it + (double)s0 * 16.0 * (n + m) / 5e6;
+        return 2 * t_launch + (v1 - v0 + 1) * it + (double)s0 * 16.0 * (n + m) / GPAD_PLAN_CARRY_BW;
     }
     double finisher(int longest, long long work) const {
-        const double lat = longest * 1.4 * t_res;
+        const double lat = longest * GPAD_PLAN_TLAT * t_res;
         const double thr = (double)work * 1.1 * t_res / num_cus;
         return 2 * t_launch + (lat > thr ? lat : thr);
     }
