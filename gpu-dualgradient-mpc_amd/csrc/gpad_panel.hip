@@ -815,12 +815,66 @@ struct HoSlots {
     int in, out;  // LDS hand-off slots taken / given (-1: none)
 };
 
+// This lane's four rows 16t + 4r + j (r = 0..3) of one instance's vector (r05).  vec: one 16-B load
+// of rows 16t + 4j .. +3 per lane (the 16 columns x 64 contiguous bytes of a wave's tile, a quarter
+// of the requests of four 4-B loads per lane), transposed through 1 KiB of LDS the wave owns (its
+// (panel, tile) block of Zh, free until the first GEMM's epilogue): column c's 16 floats with the
+// 16-B chunks XOR-swizzled by c >> 2, so the four reads are conflict-free.  The tile's rows past
+// `rows` read the last four rows (the caller zeroes them).  Else four 4-B loads at clamped rows.
+__device__ __forceinline__ void rows4(const float* base, int t, int rows, bool vec, float* st, int lane,
+                                      float (&out)[4]) {
+    const int j = lane >> 4, c = lane & 15, sw = (c >> 2) & 3;
+    if (vec) {
+        const int r0 = 16 * t + 4 * j;
+        const int rr = r0 + 3 < rows ? r0 : rows - 4;
+        const float4 v = *reinterpret_cast<const float4*>(base + rr);
+        *reinterpret_cast<float4*>(st + 16 * c + 4 * (j ^ sw)) = v;
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[r] = st[16 * c + 4 * (r ^ sw) + j];
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the next use of the block writes it)
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = 16 * t + 4 * r + j;
+            out[r] = base[i < rows ? i : rows - 1];
+        }
+    }
+}
+
 // The waves of a workgroup are co-resident, so a post always arrives unless the layout logic is
 // broken; the wait is still bounded (2^20 sleeps, ~30 ms) so that such a bug cannot hang the GPU,
 // and an expired wait is recorded (L.herr) and ORed into the run's error word when the workgroup
 // exits (gpad_panel2_kernel): the host then fails the run with GPAD_ERR_DEVICE instead of
 // returning the stale accumulator's results as GPAD_OK.  Nothing of this sits on the hand-off's
 // own path: the record is made only after the bound expired.
+// The reverse of rows4: this lane's rows 16t + 4r + j to an instance's vector, on lanes whose `on`
+// holds (uniform over a column's four lanes); vec: through the same LDS block into one 16-B store per
+// lane of rows 16t + 4j .. +3 (every lane takes part in the transpose; rows past `rows` not stored).
+__device__ __forceinline__ void rows4_store(float* base, int t, int rows, bool vec, float* st, int lane,
+                                            const float (&v)[4], bool on) {
+    const int j = lane >> 4, c = lane & 15, sw = (c >> 2) & 3;
+    if (vec) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st[16 * c + 4 * (r ^ sw) + j] = v[r];
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const float4 o = *reinterpret_cast<const float4*>(st + 16 * c + 4 * (j ^ sw));
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const int r0 = 16 * t + 4 * j;
+        if (on && r0 < rows) *reinterpret_cast<float4*>(base + r0) = o;
+    } else if (on) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = 16 * t + 4 * r + j;
+            if (i < rows) base[i] = v[r];
+        }
+    }
+}
+
 template <int T>
 __device__ __forceinline__ f32x4 handoff_wait(Panel2Lds<T>& L, int slot, int gen, int lane) {
     for (int s = 0;; ++s) {
@@ -908,6 +962,11 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
     const int voff_r = voff - 1024;  // helper: the receiver's tile t - 1 (Handoff)
     int hgen = 0;                    // hand-off generation, counted alike by helper and receiver
     float gmx = 0.0f;                // max |g| over the rows this lane loads (gmax_part)
+    // 16-B vector state I/O (rows4 / rows4_store) when every row start is 16-B aligned (uniform)
+    const bool vec_io = ((n | m | (int)a.ld_gP | (int)a.ld_g) & 3) == 0 && n >= 4 && m >= 4 &&
+                        ((reinterpret_cast<size_t>(a.z) | reinterpret_cast<size_t>(a.gP) |
+                          reinterpret_cast<size_t>(a.y) | reinterpret_cast<size_t>(a.g) |
+                          reinterpret_cast<size_t>(a.wc) | reinterpret_cast<size_t>(a.uc)) & 15) == 0;
 
     for (int it = blockIdx.x; it < items; it += gridDim.x) {
         GPAD_PSTAMP(0);
@@ -940,26 +999,20 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
         }
         if constexpr (NU > 0) {
             const float beta0 = a.beta[0];
+            const bool vec = vec_io;
 #pragma unroll
             for (int q = 0; q < Q; ++q) {  // one round trip per panel (a double wave: two)
                 float zl[4], gpl[4], yl[4], gl[4], wl[4], ul[4];
                 const size_t b = (size_t)inst[q];
-                const float* zb = a.z + b * n;
-                const float* gpb = a.gP + b * a.ld_gP;
-                const float* yb = a.y + b * m;
-                const float* gb = a.g + b * a.ld_g;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int i = 16 * t + 4 * r + j;
-                    const int in = i < n ? i : n - 1, im = i < m ? i : m - 1;
-                    zl[r] = zb[in];
-                    gpl[r] = gpb[in];
-                    yl[r] = yb[im];
-                    gl[r] = gb[im];
-                    if (!fresh) {
-                        wl[r] = a.wc[b * m + im];
-                        ul[r] = use_tol ? a.uc[b * m + im] : 0.0f;
-                    }
+                float* const st = reinterpret_cast<float*>(&L.Zh[p0 + q][64 * t]);
+                rows4(a.z + b * n, t, n, vec, st, lane, zl);
+                rows4(a.gP + b * a.ld_gP, t, n, vec, st, lane, gpl);
+                rows4(a.y + b * m, t, m, vec, st, lane, yl);
+                rows4(a.g + b * a.ld_g, t, m, vec, st, lane, gl);
+                if (!fresh) {
+                    rows4(a.wc + b * m, t, m, vec, st, lane, wl);
+                    if (use_tol) rows4(a.uc + b * m, t, m, vec, st, lane, ul);
+                    else ul[0] = ul[1] = ul[2] = ul[3] = 0.0f;
                 }
                 const int pq = p0 + q;
                 float gp[4], pd[4], wv[4];
@@ -1274,7 +1327,6 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 bool out[Q];
                 int cd[Q];
                 float zo[Q][4];
-                float *zr[Q], *yr[Q];
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
                     const int bit = 16 * (p0 + q) + c;
@@ -1286,21 +1338,15 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                     zo[q][1] = use_zh ? h4.y : z[q][1];
                     zo[q][2] = use_zh ? h4.z : z[q][2];
                     zo[q][3] = use_zh ? h4.w : z[q][3];
-                    const size_t b = (size_t)inst[q];
-                    zr[q] = a.z + b * n + 16 * t + j;
-                    yr[q] = a.y + b * m + 16 * t + j;
                 }
-                const bool fn = 16 * t + 16 <= n, fm = 16 * t + 16 <= m;
 #pragma unroll
-                for (int q = 0; q < Q; ++q) {
+                for (int q = 0; q < Q; ++q) {  // (Zh's block is free again: the rows4 transpose)
+                    const size_t b = (size_t)inst[q];
+                    float* const st = reinterpret_cast<float*>(&L.Zh[p0 + q][64 * t]);
+                    const bool zw = cd[q] != 2 || zh_out;  // (B)'s zhat already out before (A)'s GEMM
+                    rows4_store(a.z + b * n, t, n, vec_io, st, lane, zo[q], out[q] && zw);
+                    rows4_store(a.y + b * m, t, m, vec_io, st, lane, y[q], out[q]);
                     if (out[q]) {
-                        const bool zw = cd[q] != 2 || zh_out;  // (B)'s zhat already out before (A)'s GEMM
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const int i = 16 * t + 4 * r + j;
-                            if ((fn || i < n) && zw) zr[q][4 * r] = zo[q][r];
-                            if (fm || i < m) yr[q][4 * r] = y[q][r];
-                        }
                         if (t == 0 && j == 0) {
                             a.iters[inst[q]] = v;
                             a.conv[inst[q]] = cd[q];
@@ -1317,12 +1363,10 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
         GPAD_PSTAMP(3);
         if constexpr (NU > 0) {
             if (carry) {
-                // values and row pointers first, then every store (r05): vmcnt counts stores on
-                // gfx9, so a spill reload between stores waits for all the stores before it -- the
-                // interleaved form took 7-17 us per phase end (profiles/r05_phase_*.txt)
+                // the stores after every value they take (r05): vmcnt counts stores on gfx9, so a
+                // spill reload between stores would wait for all the stores before it
                 bool pk[Q];
                 float wv[Q][4];
-                float *zr[Q], *yr[Q], *wr[Q], *ur[Q];
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
                     pk[q] = act[q] && v >= a.v_end;
@@ -1331,27 +1375,15 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                     wv[q][1] = w4.y;
                     wv[q][2] = w4.z;
                     wv[q][3] = w4.w;
-                    const size_t b = (size_t)inst[q];
-                    zr[q] = a.z + b * n + 16 * t + j;
-                    yr[q] = a.y + b * m + 16 * t + j;
-                    wr[q] = a.wc + b * m + 16 * t + j;
-                    ur[q] = a.uc + b * m + 16 * t + j;
                 }
-                const bool fn = 16 * t + 16 <= n, fm = 16 * t + 16 <= m;  // full tiles: no row checks
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
-                    if (pk[q]) {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const int i = 16 * t + 4 * r + j;
-                            if (fn || i < n) zr[q][4 * r] = z[q][r];
-                            if (fm || i < m) {
-                                yr[q][4 * r] = y[q][r];
-                                wr[q][4 * r] = wv[q][r];
-                                if (use_tol) ur[q][4 * r] = u[q][r];
-                            }
-                        }
-                    }
+                    const size_t b = (size_t)inst[q];
+                    float* const st = reinterpret_cast<float*>(&L.Zh[p0 + q][64 * t]);
+                    rows4_store(a.z + b * n, t, n, vec_io, st, lane, z[q], pk[q]);
+                    rows4_store(a.y + b * m, t, m, vec_io, st, lane, y[q], pk[q]);
+                    rows4_store(a.wc + b * m, t, m, vec_io, st, lane, wv[q], pk[q]);
+                    if (use_tol) rows4_store(a.uc + b * m, t, m, vec_io, st, lane, u[q], pk[q]);
                 }
                 if (t == 0) {  // the tile-0 owner of each panel lists its survivors
 #pragma unroll
