@@ -352,6 +352,7 @@ int gpad_set_option(gpad_handle_t h, int option, int value) {
             t.p64_no_relay = 1 - on;
             return rc;
         }
+        case GPAD_OPT_PANEL_DATAFLOW: return set(t.panel_dataflow, 0, 7, def.panel_dataflow);
         default: return fail(GPAD_ERR_INVALID, "gpad_set_option: unknown option");
     }
 }

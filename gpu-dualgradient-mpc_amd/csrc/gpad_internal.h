@@ -30,6 +30,7 @@ struct Tuning {
     int debug_drop_handoff = 0;  // GPAD_OPT_DEBUG_DROP_HANDOFF: test-only fault injection
     int p64_no_relay = 0;     // GPAD_OPT_P64_RELAY = 0: f64 panels without the relay layout
     int p64_no_refill = 0;    // GPAD_OPT_P64_REFILL = 0: f64 panels without column refills
+    int panel_dataflow = 0;   // GPAD_OPT_PANEL_DATAFLOW: bits 1 one-panel, 2 pairs, 4 one-panel tile order
 };
 
 // Device error word of a run (SolveArgs::err): kernels OR these bits in with a vector atomic;
@@ -117,6 +118,7 @@ struct SolveArgs {
                            // branches)
     int* err;              // device error word (kDevErr* bits), never null on a solve launch
     int debug;             // kDebug* fault-injection bits (tests only)
+    int dflow;             // gpad_panel2_kernel: dataflow GEMM boundaries (Tuning::panel_dataflow bits)
 };
 
 // launchers (return hipError_t of the launch)

@@ -435,6 +435,55 @@ __global__ __launch_bounds__(64 * T) void gpad_panel_kernel(SolveArgs<float> a) 
     } while (0)
 #endif
 
+// Dataflow across the GEMM boundaries (r05, SolveArgs::dflow).  Block kb of a chain reads row tile
+// kb of the other GEMM's output and nothing else of it, so a chain need not wait for the barrier
+// that closes the other GEMM: each (panel, row tile) of Zh / Wl carries the generation of the GEMM
+// that last wrote it (Panel2Lds::zf / wf, posted by the tile's owner after its epilogue's LDS writes
+// complete), and a chain polls the flags only when it reaches a block past the prefix it has seen
+// written.  Overwriting a tile is safe without a barrier: the owner's next chain needs every tile
+// of the other GEMM, and each of those was written after its own chain had read every tile of this
+// one.  The SIMDs then keep issuing while the last chains of a GEMM drain -- the barrier's cost in
+// the phase anatomy (profiles/r05_c3_anatomy.txt).  The ascending-k MFMA sequence of every chain
+// is unchanged, so results are bit-identical.  Barriers remain where the whole panel is read at
+// once: the test iterations, the phase ends, the seed and verification GEMMs.
+struct NoWait {
+    __device__ __forceinline__ void operator()(int) const {}
+};
+struct DfWait {
+    const int* f0;  // flags of the chain's panel (lanes 0..31 poll f0) and of a double wave's
+    const int* f1;  // second panel (lanes 32..63 poll f1; = f0 for one panel)
+    int nt;         // row tiles
+    int need;       // generation of the producing GEMM
+    int rdy;        // tiles [0, rdy) seen written (64 without dataflow: never polls)
+    int* err;       // an expired wait (bounded like handoff_wait) fails the run
+    __device__ __forceinline__ void operator()(int kb) {
+        if (kb < rdy) return;
+        const int lane = __lane_id(), l = lane & 31;
+        const int* f = lane < 32 ? f0 : f1;
+        for (int s = 0;; ++s) {
+            const int v = l < nt ? __hip_atomic_load(f + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : need;
+            const unsigned long long nr = __ballot(v - need < 0);
+            const unsigned lo = (unsigned)nr, hi = (unsigned)(nr >> 32);
+            const int p0 = lo ? __builtin_ctz(lo) : 32, p1 = hi ? __builtin_ctz(hi) : 32;
+            rdy = __builtin_amdgcn_readfirstlane(p0 < p1 ? p0 : p1);
+            if (kb < rdy) break;
+            if (s == (1 << 20)) {
+                *err = 1;
+                rdy = 64;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        asm volatile("" ::: "memory");  // the tile's reads stay after the flag that covers them
+    }
+};
+// the owner's post of its row tile(s) after the epilogue's LDS writes
+__device__ __forceinline__ void df_post(int* f, int stride, int cnt, int gen, int lane) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0)
+        for (int q = 0; q < cnt; ++q) __hip_atomic_store(f + q * stride, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // ---------------------------------------------------------------------------------------
 // Panel pairs (8 < T <= 16): a 16-wave workgroup owns TWO panels, balanced over the SIMDs.
 // A 13-wave single-panel workgroup puts 4,3,3,3 waves (tile chains) on the CU's SIMDs, and a
@@ -493,18 +542,20 @@ __device__ __forceinline__ void panel_a_prefetch(__amdgpu_buffer_rsrc_t PA, int 
 // panel_gemm2 with an A ring PD blocks deep, seeded by panel_a_prefetch.  The last k-block
 // issues only its first kq MFMA steps: k-steps past the matrix are zero in both operands, so
 // skipping them is exact (an accumulator started at +0 never holds -0).  kq is wave-uniform.
-template <int T, bool DUAL, int PD>
+template <int T, bool DUAL, int PD, class W = NoWait>
 __device__ __forceinline__ void panel_gemm3(__amdgpu_buffer_rsrc_t PA, const float4* B0, const float4* B1,
                                             int voff, int lane, f32x4& acc0, f32x4& acc1,
-                                            const float4 (&ap)[PD], int kq) {
+                                            const float4 (&ap)[PD], int kq, W&& wt = W{}) {
     acc0 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     acc1 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     constexpr int R = PD + 1;
     float4 a[R], b0[2], b1[2];
 #pragma unroll
     for (int p = 0; p < PD; ++p) a[p] = ap[p];
+    wt(0);
     b0[0] = B0[lane];
     if constexpr (DUAL) b1[0] = B1[lane];
+    wt(1);
     b0[1] = B0[64 + lane];  // (block 1 too, so the whole prelude precedes the priority drop)
     if constexpr (DUAL) b1[1] = B1[64 + lane];
     GPAD_PRELUDE_LO();
@@ -565,6 +616,7 @@ __device__ __forceinline__ void panel_gemm3(__amdgpu_buffer_rsrc_t PA, const flo
         if (kb + PD < T)
             a[(kb + PD) % R] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb + PD) * T * 1024, 0));
         if (kb >= 1 && kb + 1 < T) {  // (blocks 0 and 1 were read before the loop)
+            wt(kb + 1);
             b0[nxt] = B0[(kb + 1) * 64 + lane];
             if constexpr (DUAL) b1[nxt] = B1[(kb + 1) * 64 + lane];
         }
@@ -594,10 +646,10 @@ __device__ __forceinline__ void panel_gemm3(__amdgpu_buffer_rsrc_t PA, const flo
 // clamped to the last block), so each block's waitcnt counts only the loads issued after its
 // operands -- a rotated ring with conditional loads made the compiler drain both counters at
 // every block.  A is PD (1 or 2) blocks ahead, B one block ahead; soffset in an SGPR.
-template <int T, bool DUAL, int PD>
+template <int T, bool DUAL, int PD, class W = NoWait>
 __device__ __forceinline__ void panel_gemm_rt(__amdgpu_buffer_rsrc_t PA, const float4* B0, const float4* B1,
                                               int voff, int lane, f32x4& acc0, f32x4& acc1,
-                                              const float4 (&ap)[PD], int nkb, int kq) {
+                                              const float4 (&ap)[PD], int nkb, int kq, W&& wt = W{}) {
     static_assert(PD == 1 || PD == 2, "A ring depth 1 or 2");
     acc0 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     acc1 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -624,17 +676,20 @@ __device__ __forceinline__ void panel_gemm_rt(__amdgpu_buffer_rsrc_t PA, const f
         __builtin_amdgcn_sched_barrier(0);
     };
     float4 a0 = ap[0], a1 = PD == 2 ? ap[PD - 1] : ap[0];
+    wt(0);
     float4 e0 = B0[lane], f0 = DUAL ? B1[lane] : e0, e1, f1;
     GPAD_PRELUDE_LO();
     for (int kb = 0;; kb += 2) {
         const int k1 = kb + 1 < last ? kb + 1 : last, k2 = kb + 2 < last ? kb + 2 : last;
         if constexpr (PD == 1) a1 = lda(kb + 1);
+        wt(k1);
         e1 = B0[k1 * 64 + lane];
         if constexpr (DUAL) f1 = B1[k1 * 64 + lane];
         blk(a0, e0, f0, kb < last ? 4 : kq);
         if constexpr (PD == 2) a0 = lda(kb + 2);
         if (kb + 1 > last) break;
         if constexpr (PD == 1) a0 = lda(kb + 2);
+        wt(k2);
         e0 = B0[k2 * 64 + lane];
         if constexpr (DUAL) f0 = B1[k2 * 64 + lane];
         blk(a1, e1, f1, kb + 1 < last ? 4 : kq);
@@ -647,13 +702,14 @@ __device__ __forceinline__ void panel_gemm_rt(__amdgpu_buffer_rsrc_t PA, const f
 
 // k-blocks [KB0, KB1) of one chain, continuing acc (not reset): the A ring PD blocks deep is
 // seeded with blocks KB0.. by panel_a_prefetch_from; the last matrix block issues kq steps.
-template <int T, int PD, int KB0, int KB1, bool LO = true>
+template <int T, int PD, int KB0, int KB1, bool LO = true, class W = NoWait>
 __device__ __forceinline__ void panel_chain(__amdgpu_buffer_rsrc_t PA, const float4* B0, int voff, int lane,
-                                            f32x4& acc, const float4 (&ap)[PD], int kq) {
+                                            f32x4& acc, const float4 (&ap)[PD], int kq, W&& wt = W{}) {
     constexpr int R = PD + 1;
     float4 a[R], b[2];
 #pragma unroll
     for (int p = 0; p < PD; ++p) a[p] = ap[p];
+    wt(KB0);
     b[0] = B0[KB0 * 64 + lane];
     if constexpr (LO) GPAD_PRELUDE_LO();  // (LO = false: a relay piece that runs at its own priority)
 #pragma unroll
@@ -662,7 +718,10 @@ __device__ __forceinline__ void panel_chain(__amdgpu_buffer_rsrc_t PA, const flo
         const float4 ak = a[i % R];
         if (kb + PD < KB1)
             a[(i + PD) % R] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb + PD) * T * 1024, 0));
-        if (kb + 1 < KB1) b[nxt] = B0[(kb + 1) * 64 + lane];
+        if (kb + 1 < KB1) {
+            wt(kb + 1);
+            b[nxt] = B0[(kb + 1) * 64 + lane];
+        }
         __builtin_amdgcn_sched_barrier(0);
         acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, b[cur].x, acc, 0, 0, 0);
         if (kb + 1 < T || kq > 1) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, b[cur].y, acc, 0, 0, 0);
@@ -754,8 +813,10 @@ struct Panel2Lds {
     float4 Gp[2][T * 64];  //                            g_P rows
     float4 Pd[2][T * 64];  //                            p_D rows
     PanelSlot2 slots[2][T];
-    float4 hand[3][64];    // hand-off accumulators
-    int hflag[3];          // hand-off generation per slot
+    float4 hand[6][64];    // hand-off accumulators: slot s of generation g at s + 3 (g & 1)
+    int hflag[6];          // hand-off generation per slot
+    int zf[2][16];         // dataflow (SolveArgs::dflow): generation of the GEMM that last wrote
+    int wf[2][16];         // Zh / Wl row tile t of panel p (zf: GEMM 1, wf: GEMM 2)
     int herr;              // a wait expired (handoff_wait): reported to the run's error word at exit
     int hdrop;             // fault injection (kDebugDropHandoff) for this workgroup
     int znz[16];           // per wave: a non-zero z_{-1} among its rows (fresh seed GEMM needed)
@@ -877,6 +938,7 @@ __device__ __forceinline__ void rows4_store(float* base, int t, int rows, bool v
 
 template <int T>
 __device__ __forceinline__ f32x4 handoff_wait(Panel2Lds<T>& L, int slot, int gen, int lane) {
+    slot += 3 * (gen & 1);
     for (int s = 0;; ++s) {
         if (__hip_atomic_load(&L.hflag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == gen) break;
         if (s == (1 << 20)) {
@@ -892,6 +954,7 @@ __device__ __forceinline__ f32x4 handoff_wait(Panel2Lds<T>& L, int slot, int gen
 
 template <int T>
 __device__ __forceinline__ void handoff_post(Panel2Lds<T>& L, int slot, int gen, int lane, const f32x4& h) {
+    slot += 3 * (gen & 1);  // (dataflow: a piece of the next GEMM may post before this one is taken)
     L.hand[slot][lane] = make_float4(h[0], h[1], h[2], h[3]);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the accumulator lands before the flag
     __hip_atomic_store(&L.hflag[slot], gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -903,13 +966,13 @@ __device__ __forceinline__ void handoff_post(Panel2Lds<T>& L, int slot, int gen,
 // first hand-off withholds its post, so its receiver's wait expires
 template <int T, int PD, int KB0, int KB1, bool PRIO, bool DROP>
 __device__ __forceinline__ void handoff_piece(Panel2Lds<T>& L, __amdgpu_buffer_rsrc_t PA, const float4* B0, int voff,
-                                              int lane, const float4 (&aph)[PD], HoSlots hs, int gen,
+                                              int lane, const float4 (&aph)[PD], HoSlots hs, int gen, DfWait& wt,
                                               unsigned long long* ts = nullptr) {
     f32x4 h = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     if (hs.in >= 0) h = handoff_wait(L, hs.in, gen, lane);
     if (ts) *ts = __builtin_amdgcn_s_memtime();  // (stamped builds only)
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
-    panel_chain<T, PD, KB0, KB1, !PRIO>(PA, B0, voff, lane, h, aph, 4);
+    panel_chain<T, PD, KB0, KB1, !PRIO>(PA, B0, voff, lane, h, aph, 4, wt);
     if (!(DROP && gen == 1 && hs.in < 0 && L.hdrop)) handoff_post(L, hs.out, gen, lane, h);
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
 }
@@ -918,11 +981,11 @@ __device__ __forceinline__ void handoff_piece(Panel2Lds<T>& L, __amdgpu_buffer_r
 template <int T, int PD, int KB0, bool PRIO>
 __device__ __forceinline__ void handoff_take(Panel2Lds<T>& L, __amdgpu_buffer_rsrc_t PA, const float4* B0, int voff,
                                              int lane, const float4 (&ap)[PD], HoSlots hs, int gen, int kq,
-                                             f32x4& acc, unsigned long long* ts = nullptr) {
+                                             f32x4& acc, DfWait& wt, unsigned long long* ts = nullptr) {
     acc = handoff_wait(L, hs.in, gen, lane);
     if (ts) *ts = __builtin_amdgcn_s_memtime();  // (stamped builds only)
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(2);
-    panel_chain<T, PD, KB0, T, !PRIO>(PA, B0, voff, lane, acc, ap, kq);
+    panel_chain<T, PD, KB0, T, !PRIO>(PA, B0, voff, lane, acc, ap, kq, wt);
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
@@ -961,6 +1024,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
     const bool on1 = FULL || 16 * t < n, on2 = FULL || 16 * t < m;
     const int voff_r = voff - 1024;  // helper: the receiver's tile t - 1 (Handoff)
     int hgen = 0;                    // hand-off generation, counted alike by helper and receiver
+    const bool df = (a.dflow & (pair ? 2 : 1)) != 0;  // dataflow GEMM boundaries (DfWait)
     float gmx = 0.0f;                // max |g| over the rows this lane loads (gmax_part)
     // 16-B vector state I/O (rows4 / rows4_store) when every row start is 16-B aligned (uniform)
     const bool vec_io = ((n | m | (int)a.ld_gP | (int)a.ld_g) & 3) == 0 && n >= 4 && m >= 4 &&
@@ -1100,18 +1164,19 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             if constexpr (NU > 0) {
                 f32x4 acc[2];
                 ++hgen;
+                DfWait wt{L.wf[p0], L.wf[NU == 2 ? 1 : p0], T, hgen - 1, df ? 0 : 64, &L.herr};
                 if constexpr (ROLE == 1)
-                    handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA1, L.Wl[p0], voff_r, lane, aph, hs, hgen,
+                    handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA1, L.Wl[p0], voff_r, lane, aph, hs, hgen, wt,
                                                                GPAD_STAMP_PTR(6));
                 if constexpr (ROLE == 2)
-                    handoff_take<T, PD, KB0, PRIO>(L, PA1, L.Wl[p0], voff, lane, ap, hs, hgen, kq1, acc[0],
+                    handoff_take<T, PD, KB0, PRIO>(L, PA1, L.Wl[p0], voff, lane, ap, hs, hgen, kq1, acc[0], wt,
                                                    GPAD_STAMP_PTR(6));
                 else if (on1 && nkb1 == T)
                     panel_gemm3<T, NU == 2, PD>(PA1, L.Wl[p0], L.Wl[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1],
-                                                ap, kq1);
+                                                ap, kq1, wt);
                 else if (on1)
                     panel_gemm_rt<T, NU == 2, PD>(PA1, L.Wl[p0], L.Wl[NU == 2 ? 1 : p0], voff, lane, acc[0],
-                                                   acc[1], ap, nkb1, kq1);
+                                                   acc[1], ap, nkb1, kq1, wt);
                 else
                     acc[0] = acc[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
                 GPAD_STAMP_AT(1);
@@ -1133,15 +1198,17 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                     z[q][2] = z1.x;
                     z[q][3] = z1.y;
                 }
+                if (df) df_post(&L.zf[p0][t], 16, Q, hgen, lane);
             } else if constexpr (ROLE == 3) {
                 ++hgen;
-                handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA1, L.Wl[p0], voff, lane, aph, hs, hgen,
+                DfWait wt{L.wf[p0], L.wf[p0], T, hgen - 1, df ? 0 : 64, &L.herr};
+                handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA1, L.Wl[p0], voff, lane, aph, hs, hgen, wt,
                                                            GPAD_STAMP_PTR(6));
                 prefetch(PA2);
             }
             GPAD_STAMP_AT(2);
             GPAD_PRELUDE_HI();
-            __syncthreads();
+            if (!df) __syncthreads();
             GPAD_STAMP_AT(3);
             // ---- GEMM 2 + epilogue: y+ = [w + G_L zhat + p_D]+ (8d), next w (8a) ----------
             float violz[Q], violh[Q], wmin[Q], magh[Q];
@@ -1156,18 +1223,19 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             if constexpr (NU > 0) {
                 f32x4 acc[2];
                 ++hgen;
+                DfWait wt{L.zf[p0], L.zf[NU == 2 ? 1 : p0], T, hgen - 1, df ? 0 : 64, &L.herr};
                 if constexpr (ROLE == 1)
-                    handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA2, L.Zh[p0], voff_r, lane, aph, hs, hgen,
+                    handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA2, L.Zh[p0], voff_r, lane, aph, hs, hgen, wt,
                                                                GPAD_STAMP_PTR(7));
                 if constexpr (ROLE == 2)
-                    handoff_take<T, PD, KB0, PRIO>(L, PA2, L.Zh[p0], voff, lane, ap, hs, hgen, kq2, acc[0],
+                    handoff_take<T, PD, KB0, PRIO>(L, PA2, L.Zh[p0], voff, lane, ap, hs, hgen, kq2, acc[0], wt,
                                                    GPAD_STAMP_PTR(7));
                 else if (on2 && nkb2 == T)
                     panel_gemm3<T, NU == 2, PD>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1],
-                                                ap, kq2);
+                                                ap, kq2, wt);
                 else if (on2)
                     panel_gemm_rt<T, NU == 2, PD>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, acc[0],
-                                                   acc[1], ap, nkb2, kq2);
+                                                   acc[1], ap, nkb2, kq2, wt);
                 else
                     acc[0] = acc[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
                 GPAD_STAMP_AT(4);
@@ -1238,9 +1306,11 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                         }
                     }
                 }
+                if (df) df_post(&L.wf[p0][t], 16, Q, hgen, lane);
             } else if constexpr (ROLE == 3) {
                 ++hgen;
-                handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA2, L.Zh[p0], voff, lane, aph, hs, hgen,
+                DfWait wt{L.zf[p0], L.zf[p0], T, hgen - 1, df ? 0 : 64, &L.herr};
+                handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA2, L.Zh[p0], voff, lane, aph, hs, hgen, wt,
                                                            GPAD_STAMP_PTR(7));
                 prefetch(PA1);
             }
@@ -1248,7 +1318,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             bn = bn_next;
             GPAD_STAMP_AT(5);
             GPAD_PRELUDE_HI();
-            __syncthreads();
+            if (!df || chk || v >= a.v_end) __syncthreads();
             GPAD_STAMP_FLUSH();
             if (!chk && v < a.v_end) continue;
 
@@ -1430,7 +1500,11 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
     // hand-off (Handoff): both GEMMs run full-length chains on tiles T-2 and T-1
     const bool ho = Handoff<T>::on && (KQ > 0 || (16 * (T - 1) < a.n && 16 * (T - 1) < a.m &&
                                                   (a.m + 15) / 16 == T && (a.n + 15) / 16 == T));
-    if (threadIdx.x < 3) L.hflag[threadIdx.x] = 0;
+    if (threadIdx.x < 6) L.hflag[threadIdx.x] = 0;
+    if (threadIdx.x < 32) {
+        (&L.zf[0][0])[threadIdx.x] = 0;
+        (&L.wf[0][0])[threadIdx.x] = 0;
+    }
     if (threadIdx.x == 0) {
         L.herr = 0;
         L.hdrop = DROP && blockIdx.x == 0;  // tests: workgroup 0 drops one post
@@ -1455,7 +1529,8 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
                 panel2_run<T, 0, 3, 0, H::R1, true, 0, DROP>(a, L, T - 1, 0, false, items, count, HoSlots{-1, 0});
             else if (ho && w == T + 1)
                 panel2_run<T, 0, 3, H::R1, H::R2, true, 0, DROP>(a, L, T - 1, 0, false, items, count, HoSlots{0, 1});
-            else if (w < T) panel2_run<T, 1, 0, 0, 0, false, 0, DROP>(a, L, w, 0, false, items, count);
+            else if (w < T)  // (dflow bit 4: tiles 0..T-2 dealt oldest wave first, so they are written in order)
+                panel2_run<T, 1, 0, 0, 0, false, 0, DROP>(a, L, (a.dflow & 4) ? T - 2 - w : w, 0, false, items, count);
             else panel2_run<T, 0, 0, 0, 0, false, 0, DROP>(a, L, 0, 0, false, items, count);
         }
     } else if (pair) {
@@ -1465,10 +1540,10 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
         if (w < T) panel2_run<T, 1, 0, 0, 0, false, 0, DROP>(a, L, w, 0, false, items, count);
         else panel2_run<T, 0, 0, 0, 0, false, 0, DROP>(a, L, 0, 0, false, items, count);
     }
-    if (Handoff<T>::on || a.gmax_part) {
+    if (Handoff<T>::on || a.gmax_part || a.dflow) {
         __syncthreads();
-        // an expired hand-off wait fails the run (GPAD_ERR_DEVICE)
-        if (Handoff<T>::on && threadIdx.x == 0 && L.herr) atomicOr(a.err, kDevErrHandoff);
+        // an expired hand-off or dataflow wait fails the run (GPAD_ERR_DEVICE)
+        if ((Handoff<T>::on || a.dflow) && threadIdx.x == 0 && L.herr) atomicOr(a.err, kDevErrHandoff);
         if (a.gmax_part && threadIdx.x == 0) {  // the run's max |g|: this workgroup's slot
             float g = 0.0f;
             for (int i = 0; i < 16; ++i) g = absmax_nan(g, L.gred[i]);
@@ -1856,6 +1931,7 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     int grid = panels < resident ? panels : resident;
     const Tuning tn = a.tune ? *a.tune : Tuning{};
     if (tn.panel_max_grid > 0 && tn.panel_max_grid < grid) grid = tn.panel_max_grid;  // grid-stride panels
+    a.dflow = T > 8 ? tn.panel_dataflow : 0;
     const bool phased = a.tol > 0.0 && a.pwork != nullptr && tn.phased;
     a.fin_thresh = phased ? panel_fin_thresh(a.n, a.m, a.num_cus, &tn) : 0;
     if (!phased) {  // fixed N (or no workspace): one phase, nothing carried

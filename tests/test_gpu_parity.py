@@ -204,6 +204,58 @@ def test_panel_phased_compaction_bitexact(gpu, oracle, grid, phase, fin, tol, N,
         assert_bitexact(y[b], yo, f"instance {b} y")
 
 
+@pytest.mark.parametrize("dflow", [3, 7])
+@pytest.mark.parametrize("grid,phase,fin", [(3, 20, 24), (0, 10, 0), (1, 0, None)])
+@pytest.mark.parametrize("tol,N", [(1e-4, 3000), (0.0, 57)])
+@pytest.mark.parametrize("nm,B", [((150, 130), 40), ((131, 256), 37), ((200, 200), 120), ((193, 207), 101),
+                                  ((207, 194), 70), ((140, 135), 90), ((170, 176), 80)])
+def test_panel_dataflow_bitexact(gpu, oracle, dflow, grid, phase, fin, tol, N, nm, B):
+    """GPAD_OPT_PANEL_DATAFLOW (gpad_panel.hip DfWait): the chains of both layouts start on the
+    other GEMM's row tiles as their owners post them, without the barrier between the GEMMs
+    (bit 4: the one-panel tiles dealt oldest wave first).  Pairs (grid 3), one panel per workgroup
+    (grid 0 at these batches), the hand-off and relay shapes (T = 9, 11, 13), T = 10 and 16, phased
+    compaction with warm starts: every instance equals its own oracle solve, count included."""
+    from gpad_mpc import problems
+    opts = dict(panel_max_grid=grid, phase_len=phase, finish_thresh=-1 if fin is None else fin,
+                panel_dataflow=dflow)
+    n, m = nm
+    qp = problems.synthetic_qp(n, m, batch=B, seed=8)
+    ML, G = qp.ML.astype(np.float32), qp.G.astype(np.float32)
+    M, g = qp.M.astype(np.float32), qp.g.astype(np.float32)
+    L = np.float32(qp.L)
+    rng = np.random.default_rng(1)
+    z0 = (0.1 * rng.normal(size=(B, n))).astype(np.float32)
+    z, y, st, iters = run_gpu(ML, M, G, g, L, N, tol=tol, kernel="panel", z0=z0, opts=opts)
+    assert st["kernel"] == "panel"
+    for b in range(B):
+        zo, yo, it, _ = oracle.solve_f32(z0[b], np.zeros(m), ML, M[b], G, g[b], N, L, tol)
+        assert iters[b] == it, b
+        assert_bitexact(z[b], zo, f"instance {b} z")
+        assert_bitexact(y[b], yo, f"instance {b} y")
+
+
+@pytest.mark.parametrize("B", [4096, 8192])
+def test_panel_dataflow_c3_c4_batches(gpu, oracle, B):
+    """The C3 (4096: one panel per CU) and C4-shard (8192: pairs) batches to eps with dataflow on
+    equal the barrier schedule bit for bit (z, y, every count); instances spot-checked against
+    the oracle."""
+    import bench
+    n = m = 200
+    ML, G, L, M, g = bench.make_shard(n, m, B, 0)
+    f = lambda a: np.ascontiguousarray(np.asarray(a, np.float32))  # noqa: E731
+    ML, G, M, g, L = f(ML), f(G), f(M), f(g), np.float32(L)
+    z0, y0, st0, it0 = run_gpu(ML, M, G, g, L, 5000, tol=1e-4, kernel="panel", opts=dict(panel_dataflow=0))
+    z1, y1, st1, it1 = run_gpu(ML, M, G, g, L, 5000, tol=1e-4, kernel="panel", opts=dict(panel_dataflow=7))
+    assert np.array_equal(it0, it1)
+    assert_bitexact(z1, z0, "z")
+    assert_bitexact(y1, y0, "y")
+    for b in (0, 1, B // 2 + 3, B - 1):
+        zo, yo, it, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), ML, M[b], G, g[b], 5000, L, 1e-4)
+        assert it1[b] == it, b
+        assert_bitexact(z1[b], zo, f"instance {b} z")
+        assert_bitexact(y1[b], yo, f"instance {b} y")
+
+
 @pytest.mark.parametrize("tol,N", [(1e-4, 2000), (0.0, 37)])
 @pytest.mark.parametrize("nm,B", [((200, 900), 40), ((300, 300), 20), ((257, 130), 33), ((520, 600), 17), ((1000, 300), 9)])
 @pytest.mark.parametrize("grid,phase", [(0, 0), (2, 20)])
