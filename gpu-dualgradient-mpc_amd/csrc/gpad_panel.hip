@@ -29,6 +29,7 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 #include <string>
 #include <vector>
 
@@ -447,9 +448,13 @@ __global__ __launch_bounds__(64 * T) void gpad_panel_kernel(SolveArgs<float> a) 
 // is unchanged, so results are bit-identical.  Barriers remain where the whole panel is read at
 // once: the test iterations, the phase ends, the seed and verification GEMMs.
 struct NoWait {
+    template <class... A>
+    __device__ __forceinline__ NoWait(A&&...) {}
     __device__ __forceinline__ void operator()(int) const {}
 };
 struct DfWait {
+    __device__ __forceinline__ DfWait(const int* a, const int* b, int t, int nd, int r, int* e)
+        : f0(a), f1(b), nt(t), need(nd), rdy(r), err(e) {}
     const int* f0;  // flags of the chain's panel (lanes 0..31 poll f0) and of a double wave's
     const int* f1;  // second panel (lanes 32..63 poll f1; = f0 for one panel)
     int nt;         // row tiles
@@ -938,7 +943,6 @@ __device__ __forceinline__ void rows4_store(float* base, int t, int rows, bool v
 
 template <int T>
 __device__ __forceinline__ f32x4 handoff_wait(Panel2Lds<T>& L, int slot, int gen, int lane) {
-    slot += 3 * (gen & 1);
     for (int s = 0;; ++s) {
         if (__hip_atomic_load(&L.hflag[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == gen) break;
         if (s == (1 << 20)) {
@@ -954,7 +958,6 @@ __device__ __forceinline__ f32x4 handoff_wait(Panel2Lds<T>& L, int slot, int gen
 
 template <int T>
 __device__ __forceinline__ void handoff_post(Panel2Lds<T>& L, int slot, int gen, int lane, const f32x4& h) {
-    slot += 3 * (gen & 1);  // (dataflow: a piece of the next GEMM may post before this one is taken)
     L.hand[slot][lane] = make_float4(h[0], h[1], h[2], h[3]);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the accumulator lands before the flag
     __hip_atomic_store(&L.hflag[slot], gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -964,11 +967,17 @@ __device__ __forceinline__ void handoff_post(Panel2Lds<T>& L, int slot, int gen,
 // from slot hs.in (or from zero), parked in slot hs.out; PRIO raises the wave's issue priority
 // fault injection (DROP, the kernel's test-only instantiation; L.hdrop): the first piece of the
 // first hand-off withholds its post, so its receiver's wait expires
-template <int T, int PD, int KB0, int KB1, bool PRIO, bool DROP>
+// DF (dataflow): slot s of generation g is s + 3 (g & 1) -- a piece of the next GEMM may post
+// before this one is taken
+template <int T, int PD, int KB0, int KB1, bool PRIO, bool DROP, bool DF = false, class W>
 __device__ __forceinline__ void handoff_piece(Panel2Lds<T>& L, __amdgpu_buffer_rsrc_t PA, const float4* B0, int voff,
-                                              int lane, const float4 (&aph)[PD], HoSlots hs, int gen, DfWait& wt,
+                                              int lane, const float4 (&aph)[PD], HoSlots hs, int gen, W& wt,
                                               unsigned long long* ts = nullptr) {
     f32x4 h = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    if constexpr (DF) {
+        hs.in += hs.in >= 0 ? 3 * (gen & 1) : 0;
+        hs.out += 3 * (gen & 1);
+    }
     if (hs.in >= 0) h = handoff_wait(L, hs.in, gen, lane);
     if (ts) *ts = __builtin_amdgcn_s_memtime();  // (stamped builds only)
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
@@ -978,11 +987,11 @@ __device__ __forceinline__ void handoff_piece(Panel2Lds<T>& L, __amdgpu_buffer_r
 }
 
 // the chain's last piece on its owner: blocks [KB0, T) from slot hs.in
-template <int T, int PD, int KB0, bool PRIO>
+template <int T, int PD, int KB0, bool PRIO, bool DF = false, class W>
 __device__ __forceinline__ void handoff_take(Panel2Lds<T>& L, __amdgpu_buffer_rsrc_t PA, const float4* B0, int voff,
                                              int lane, const float4 (&ap)[PD], HoSlots hs, int gen, int kq,
-                                             f32x4& acc, DfWait& wt, unsigned long long* ts = nullptr) {
-    acc = handoff_wait(L, hs.in, gen, lane);
+                                             f32x4& acc, W& wt, unsigned long long* ts = nullptr) {
+    acc = handoff_wait(L, hs.in + (DF ? 3 * (gen & 1) : 0), gen, lane);
     if (ts) *ts = __builtin_amdgcn_s_memtime();  // (stamped builds only)
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(2);
     panel_chain<T, PD, KB0, T, !PRIO>(PA, B0, voff, lane, acc, ap, kq, wt);
@@ -997,7 +1006,8 @@ __device__ __forceinline__ void handoff_take(Panel2Lds<T>& L, __amdgpu_buffer_rs
 // GEMMs (16 (T-1) < n, m <= 16 T) whose last k-block issues KQ steps in both: no runtime kq tests
 // (scalar branches whose conditions the compiler spilled to VGPR lanes) and no short-chain paths.
 // DROP: the fault-injection instantiation (handoff_piece).
-template <int T, int NU, int ROLE = 0, int KB0 = 0, int KB1 = 0, bool PRIO = false, int KQ = 0, bool DROP = false>
+template <int T, int NU, int ROLE = 0, int KB0 = 0, int KB1 = 0, bool PRIO = false, int KQ = 0, bool DROP = false,
+          bool DF = false>
 __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<T>& L, int t, int p0,
                                            bool pair, int items, int count, HoSlots hs = HoSlots{-1, -1}) {
     static_assert(ROLE == 0 || (Handoff<T>::on && (ROLE == 3 ? NU == 0 : NU == 1)), "hand-off roles");
@@ -1024,7 +1034,8 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
     const bool on1 = FULL || 16 * t < n, on2 = FULL || 16 * t < m;
     const int voff_r = voff - 1024;  // helper: the receiver's tile t - 1 (Handoff)
     int hgen = 0;                    // hand-off generation, counted alike by helper and receiver
-    const bool df = (a.dflow & (pair ? 2 : 1)) != 0;  // dataflow GEMM boundaries (DfWait)
+    const bool df = DF && (a.dflow & (pair ? 2 : 1)) != 0;  // dataflow GEMM boundaries (DfWait)
+    using Wt = std::conditional_t<DF, DfWait, NoWait>;
     float gmx = 0.0f;                // max |g| over the rows this lane loads (gmax_part)
     // 16-B vector state I/O (rows4 / rows4_store) when every row start is 16-B aligned (uniform)
     const bool vec_io = ((n | m | (int)a.ld_gP | (int)a.ld_g) & 3) == 0 && n >= 4 && m >= 4 &&
@@ -1164,12 +1175,12 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             if constexpr (NU > 0) {
                 f32x4 acc[2];
                 ++hgen;
-                DfWait wt{L.wf[p0], L.wf[NU == 2 ? 1 : p0], T, hgen - 1, df ? 0 : 64, &L.herr};
+                Wt wt(L.wf[p0], L.wf[NU == 2 ? 1 : p0], T, hgen - 1, df ? 0 : 64, &L.herr);
                 if constexpr (ROLE == 1)
-                    handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA1, L.Wl[p0], voff_r, lane, aph, hs, hgen, wt,
+                    handoff_piece<T, PD, KB0, KB1, PRIO, DROP, DF>(L, PA1, L.Wl[p0], voff_r, lane, aph, hs, hgen, wt,
                                                                GPAD_STAMP_PTR(6));
                 if constexpr (ROLE == 2)
-                    handoff_take<T, PD, KB0, PRIO>(L, PA1, L.Wl[p0], voff, lane, ap, hs, hgen, kq1, acc[0], wt,
+                    handoff_take<T, PD, KB0, PRIO, DF>(L, PA1, L.Wl[p0], voff, lane, ap, hs, hgen, kq1, acc[0], wt,
                                                    GPAD_STAMP_PTR(6));
                 else if (on1 && nkb1 == T)
                     panel_gemm3<T, NU == 2, PD>(PA1, L.Wl[p0], L.Wl[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1],
@@ -1201,8 +1212,8 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 if (df) df_post(&L.zf[p0][t], 16, Q, hgen, lane);
             } else if constexpr (ROLE == 3) {
                 ++hgen;
-                DfWait wt{L.wf[p0], L.wf[p0], T, hgen - 1, df ? 0 : 64, &L.herr};
-                handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA1, L.Wl[p0], voff, lane, aph, hs, hgen, wt,
+                Wt wt(L.wf[p0], L.wf[p0], T, hgen - 1, df ? 0 : 64, &L.herr);
+                handoff_piece<T, PD, KB0, KB1, PRIO, DROP, DF>(L, PA1, L.Wl[p0], voff, lane, aph, hs, hgen, wt,
                                                            GPAD_STAMP_PTR(6));
                 prefetch(PA2);
             }
@@ -1223,12 +1234,12 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             if constexpr (NU > 0) {
                 f32x4 acc[2];
                 ++hgen;
-                DfWait wt{L.zf[p0], L.zf[NU == 2 ? 1 : p0], T, hgen - 1, df ? 0 : 64, &L.herr};
+                Wt wt(L.zf[p0], L.zf[NU == 2 ? 1 : p0], T, hgen - 1, df ? 0 : 64, &L.herr);
                 if constexpr (ROLE == 1)
-                    handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA2, L.Zh[p0], voff_r, lane, aph, hs, hgen, wt,
+                    handoff_piece<T, PD, KB0, KB1, PRIO, DROP, DF>(L, PA2, L.Zh[p0], voff_r, lane, aph, hs, hgen, wt,
                                                                GPAD_STAMP_PTR(7));
                 if constexpr (ROLE == 2)
-                    handoff_take<T, PD, KB0, PRIO>(L, PA2, L.Zh[p0], voff, lane, ap, hs, hgen, kq2, acc[0], wt,
+                    handoff_take<T, PD, KB0, PRIO, DF>(L, PA2, L.Zh[p0], voff, lane, ap, hs, hgen, kq2, acc[0], wt,
                                                    GPAD_STAMP_PTR(7));
                 else if (on2 && nkb2 == T)
                     panel_gemm3<T, NU == 2, PD>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1],
@@ -1309,8 +1320,8 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 if (df) df_post(&L.wf[p0][t], 16, Q, hgen, lane);
             } else if constexpr (ROLE == 3) {
                 ++hgen;
-                DfWait wt{L.zf[p0], L.zf[p0], T, hgen - 1, df ? 0 : 64, &L.herr};
-                handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA2, L.Zh[p0], voff, lane, aph, hs, hgen, wt,
+                Wt wt(L.zf[p0], L.zf[p0], T, hgen - 1, df ? 0 : 64, &L.herr);
+                handoff_piece<T, PD, KB0, KB1, PRIO, DROP, DF>(L, PA2, L.Zh[p0], voff, lane, aph, hs, hgen, wt,
                                                            GPAD_STAMP_PTR(7));
                 prefetch(PA1);
             }
@@ -1476,7 +1487,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
 // (6.16 vs 5.98 us per iteration at 4 panels, profiles/r03_single_mode_ab.txt).  DROP: the
 // test-only fault-injection instantiation (GPAD_OPT_DEBUG_DROP_HANDOFF), launched instead of the
 // product kernel only while that option is set, so the product kernel carries no trace of it.
-template <int T, int KQ, bool DROP = false>
+template <int T, int KQ, bool DROP = false, bool DF = false>
 __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
     static_assert(T > 8 && T <= 16, "panel pairs need 8 < T <= 16");
     constexpr int D = 2 * T - 16;  // double waves
@@ -1514,36 +1525,36 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
     if constexpr (Handoff<T>::on) {
         using H = Handoff<T>;
         if (pair) {  // waves 12, 13 (SIMDs 0, 1; tile T-2) receive from 14, 15 (SIMDs 2, 3; tile T-1)
-            if (w < D) panel2_run<T, 2, 0, 0, 0, false, KQ, DROP>(a, L, w, 0, true, items, count);
+            if (w < D) panel2_run<T, 2, 0, 0, 0, false, KQ, DROP, DF>(a, L, w, 0, true, items, count);
             else if (ho && w >= 14)
-                panel2_run<T, 1, 1, 0, H::S, false, KQ, DROP>(a, L, T - 1, w & 1, true, items, count, HoSlots{-1, w & 1});
+                panel2_run<T, 1, 1, 0, H::S, false, KQ, DROP, DF>(a, L, T - 1, w & 1, true, items, count, HoSlots{-1, w & 1});
             else if (ho && w >= 12)
-                panel2_run<T, 1, 2, H::S, 0, false, KQ, DROP>(a, L, T - 2, w & 1, true, items, count, HoSlots{w & 1, -1});
-            else panel2_run<T, 1, 0, 0, 0, false, KQ, DROP>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
+                panel2_run<T, 1, 2, H::S, 0, false, KQ, DROP, DF>(a, L, T - 2, w & 1, true, items, count, HoSlots{w & 1, -1});
+            else panel2_run<T, 1, 0, 0, 0, false, KQ, DROP, DF>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
         } else {  // tile T-1 as a relay: waves T -> T+1 -> T-1
             if constexpr (!H::relay) {
-                if (w < T) panel2_run<T, 1, 0, 0, 0, false, 0, DROP>(a, L, w, 0, false, items, count);
-                else panel2_run<T, 0, 0, 0, 0, false, 0, DROP>(a, L, 0, 0, false, items, count);
-            } else if (ho && w == T - 1) panel2_run<T, 1, 2, H::R2, 0, true, 0, DROP>(a, L, w, 0, false, items, count, HoSlots{1, -1});
+                if (w < T) panel2_run<T, 1, 0, 0, 0, false, 0, DROP, DF>(a, L, w, 0, false, items, count);
+                else panel2_run<T, 0, 0, 0, 0, false, 0, DROP, DF>(a, L, 0, 0, false, items, count);
+            } else if (ho && w == T - 1) panel2_run<T, 1, 2, H::R2, 0, true, 0, DROP, DF>(a, L, w, 0, false, items, count, HoSlots{1, -1});
             else if (ho && w == T)
-                panel2_run<T, 0, 3, 0, H::R1, true, 0, DROP>(a, L, T - 1, 0, false, items, count, HoSlots{-1, 0});
+                panel2_run<T, 0, 3, 0, H::R1, true, 0, DROP, DF>(a, L, T - 1, 0, false, items, count, HoSlots{-1, 0});
             else if (ho && w == T + 1)
-                panel2_run<T, 0, 3, H::R1, H::R2, true, 0, DROP>(a, L, T - 1, 0, false, items, count, HoSlots{0, 1});
+                panel2_run<T, 0, 3, H::R1, H::R2, true, 0, DROP, DF>(a, L, T - 1, 0, false, items, count, HoSlots{0, 1});
             else if (w < T)  // (dflow bit 4: tiles 0..T-2 dealt oldest wave first, so they are written in order)
-                panel2_run<T, 1, 0, 0, 0, false, 0, DROP>(a, L, (a.dflow & 4) ? T - 2 - w : w, 0, false, items, count);
-            else panel2_run<T, 0, 0, 0, 0, false, 0, DROP>(a, L, 0, 0, false, items, count);
+                panel2_run<T, 1, 0, 0, 0, false, 0, DROP, DF>(a, L, (DF && (a.dflow & 4)) ? T - 2 - w : w, 0, false, items, count);
+            else panel2_run<T, 0, 0, 0, 0, false, 0, DROP, DF>(a, L, 0, 0, false, items, count);
         }
     } else if (pair) {
-        if (w < D) panel2_run<T, 2, 0, 0, 0, false, KQ, DROP>(a, L, w, 0, true, items, count);
-        else panel2_run<T, 1, 0, 0, 0, false, KQ, DROP>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
+        if (w < D) panel2_run<T, 2, 0, 0, 0, false, KQ, DROP, DF>(a, L, w, 0, true, items, count);
+        else panel2_run<T, 1, 0, 0, 0, false, KQ, DROP, DF>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
     } else {
-        if (w < T) panel2_run<T, 1, 0, 0, 0, false, 0, DROP>(a, L, w, 0, false, items, count);
-        else panel2_run<T, 0, 0, 0, 0, false, 0, DROP>(a, L, 0, 0, false, items, count);
+        if (w < T) panel2_run<T, 1, 0, 0, 0, false, 0, DROP, DF>(a, L, w, 0, false, items, count);
+        else panel2_run<T, 0, 0, 0, 0, false, 0, DROP, DF>(a, L, 0, 0, false, items, count);
     }
-    if (Handoff<T>::on || a.gmax_part || a.dflow) {
+    if (Handoff<T>::on || a.gmax_part || DF) {
         __syncthreads();
         // an expired hand-off or dataflow wait fails the run (GPAD_ERR_DEVICE)
-        if ((Handoff<T>::on || a.dflow) && threadIdx.x == 0 && L.herr) atomicOr(a.err, kDevErrHandoff);
+        if ((Handoff<T>::on || DF) && threadIdx.x == 0 && L.herr) atomicOr(a.err, kDevErrHandoff);
         if (a.gmax_part && threadIdx.x == 0) {  // the run's max |g|: this workgroup's slot
             float g = 0.0f;
             for (int i = 0; i < 16; ++i) g = absmax_nan(g, L.gred[i]);
@@ -1911,6 +1922,10 @@ static void launch_panel_kernel(const SolveArgs<float>& a, int grid, hipStream_t
                 else hipLaunchKernelGGL((gpad_panel2_kernel<T, 0, true>), dim3(grid), dim3(1024), 0, s, a);
                 return;
             }
+            if (a.dflow) {  // the opt-in dataflow boundaries (runtime chain shape)
+                hipLaunchKernelGGL((gpad_panel2_kernel<T, 0, false, true>), dim3(grid), dim3(1024), 0, s, a);
+                return;
+            }
             if (full && kq1 == 1) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 1>), dim3(grid), dim3(1024), 0, s, a); return; }
             if (full && kq1 == 2) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 2>), dim3(grid), dim3(1024), 0, s, a); return; }
             if (full && kq1 == 3) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 3>), dim3(grid), dim3(1024), 0, s, a); return; }
@@ -1931,7 +1946,7 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     int grid = panels < resident ? panels : resident;
     const Tuning tn = a.tune ? *a.tune : Tuning{};
     if (tn.panel_max_grid > 0 && tn.panel_max_grid < grid) grid = tn.panel_max_grid;  // grid-stride panels
-    a.dflow = T > 8 ? tn.panel_dataflow : 0;
+    a.dflow = T == 13 ? tn.panel_dataflow : 0;  // (instantiated for the C3 / C4 tiling only)
     const bool phased = a.tol > 0.0 && a.pwork != nullptr && tn.phased;
     a.fin_thresh = phased ? panel_fin_thresh(a.n, a.m, a.num_cus, &tn) : 0;
     if (!phased) {  // fixed N (or no workspace): one phase, nothing carried

@@ -398,7 +398,7 @@ int gpad_schedule(int N, int kind, double* theta, double* beta);
 #define GPAD_OPT_P64_REFILL 19     /* 1: f64 panel solves with tol > 0, N a multiple of check_every and
                                     * more panels than workgroups refill a finished column with the
                                     * next instance (default); 0: each panel runs to its slowest column */
-#define GPAD_OPT_PANEL_DATAFLOW 20 /* f32 panels (n, m in (128, 256]): bits 1 / 2 let the one-panel /
+#define GPAD_OPT_PANEL_DATAFLOW 20 /* f32 panels, n, m in (192, 208]: bits 1 / 2 let the one-panel /
                                     * pair layout's chains start on the other GEMM's row tiles as they
                                     * are written instead of after a barrier (bit-identical results);
                                     * bit 4: one-panel row tiles dealt oldest wave first */

@@ -210,10 +210,11 @@ def test_panel_phased_compaction_bitexact(gpu, oracle, grid, phase, fin, tol, N,
 @pytest.mark.parametrize("nm,B", [((150, 130), 40), ((131, 256), 37), ((200, 200), 120), ((193, 207), 101),
                                   ((207, 194), 70), ((140, 135), 90), ((170, 176), 80)])
 def test_panel_dataflow_bitexact(gpu, oracle, dflow, grid, phase, fin, tol, N, nm, B):
-    """GPAD_OPT_PANEL_DATAFLOW (gpad_panel.hip DfWait): the chains of both layouts start on the
-    other GEMM's row tiles as their owners post them, without the barrier between the GEMMs
-    (bit 4: the one-panel tiles dealt oldest wave first).  Pairs (grid 3), one panel per workgroup
-    (grid 0 at these batches), the hand-off and relay shapes (T = 9, 11, 13), T = 10 and 16, phased
+    """GPAD_OPT_PANEL_DATAFLOW (gpad_panel.hip DfWait, instantiated for T = 13: (200, 200),
+    (193, 207), (207, 194); the other shapes check that the option leaves them alone): the chains
+    of both layouts start on the other GEMM's row tiles as their owners post them, without the
+    barrier between the GEMMs (bit 4: the one-panel tiles dealt oldest wave first).  Pairs (grid
+    3), one panel per workgroup (grid 0 at these batches), the relay and hand-off, phased
     compaction with warm starts: every instance equals its own oracle solve, count included."""
     from gpad_mpc import problems
     opts = dict(panel_max_grid=grid, phase_len=phase, finish_thresh=-1 if fin is None else fin,
