@@ -706,6 +706,26 @@ def sharded_leg(dev, ndev, n=200, m=200, batch=65536, steps=6, warmup=2, max_ite
                     "stats copied each run); bitexact_vs_one_handle compares the last run's counts, z*, y*"}
 
 
+def guarded(fn, timeout_s, what):
+    """Run fn() in a daemon thread; past timeout_s return a "skipped" record instead of its result,
+    so a hung multi-device leg cannot take the bench's JSON line with it (rank 0 then prints the
+    line and leaves with os._exit, the other ranks' final barrier fails and they exit cleanly)."""
+    import threading
+    box = {}
+
+    def run():
+        try:
+            box["r"] = fn()
+        except Exception as e:  # reported in the line, not raised: the timed results stand
+            box["r"] = {"skipped": f"{what} failed: {type(e).__name__}: {e}"}
+    th = threading.Thread(target=run, daemon=True)
+    th.start()
+    th.join(timeout_s)
+    if th.is_alive():
+        return {"skipped": f"{what} did not finish in {timeout_s} s"}, True
+    return box["r"], False
+
+
 def launch_ranks(gpus, argv):
     """``python bench.py --gpus N`` without a launcher: start the N ranks as ONE child process
     (torch.distributed.run, one rank per GPU, rendezvous on 127.0.0.1) and return its exit status.
@@ -939,11 +959,14 @@ def main():
     # the C-ABI multi-device path on rank 0 (every rank's timed region is over, the barrier above;
     # the other ranks wait on host_pg): the global batch over devices 0..N-1 through gpad_group
     ndist = min(world, ndev)
+    hung = False
     if multi is not None:
-        multi["sharded_c4_global"] = (sharded_leg(dev, ndist, n, m) if rank == 0 and ndist >= 2 and
-                                      not args.no_sharded else
-                                      {"skipped": f"{ndist} distinct device(s) visible" if ndist < 2 else
-                                       "--no-sharded"})
+        if rank == 0 and ndist >= 2 and not args.no_sharded:
+            multi["sharded_c4_global"], hung = guarded(lambda: sharded_leg(dev, ndist, n, m), 240,
+                                                       "sharded_leg")
+        else:
+            multi["sharded_c4_global"] = {"skipped": f"{ndist} distinct device(s) visible" if ndist < 2 else
+                                          "--no-sharded"}
 
     # CPU reference on rank 0 (all ranks' timed regions are over: the barrier above)
     ref = None
@@ -1074,11 +1097,17 @@ def main():
             "cpu_baseline": cpu,
             "legs": extra,
         }
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
+    if hung:  # a multi-device call never returned: leave without joining it (guarded)
+        sys.stderr.flush()
+        os._exit(0)
     solver.close()
     if world > 1:
-        dist.barrier(group=host_pg)
-        dist.destroy_process_group()
+        try:
+            dist.barrier(group=host_pg)
+            dist.destroy_process_group()
+        except Exception as e:  # rank 0 left early (guarded): the results are already printed
+            print(f"bench.py rank {rank}: final barrier: {type(e).__name__}: {e}", file=sys.stderr)
 
 
 if __name__ == "__main__":

@@ -97,3 +97,19 @@ def test_bench_rejects_gpus_world_size_mismatch(gpus, world):
     assert r.returncode == 2
     assert f"--gpus {gpus} but WORLD_SIZE={world}" in r.stderr
     assert not r.stdout.strip()
+
+
+def test_bench_guarded_leg_times_out_and_reports_errors():
+    """bench.guarded: a multi-device leg that never returns (or raises) becomes a "skipped" record,
+    so rank 0 still prints the JSON line."""
+    import threading
+
+    import bench
+    done = threading.Event()
+    r, hung = bench.guarded(lambda: done.wait(30) and {"ok": 1}, 0.2, "leg")
+    assert hung and "did not finish" in r["skipped"]
+    done.set()
+    r, hung = bench.guarded(lambda: 1 / 0, 5, "leg")
+    assert not hung and "ZeroDivisionError" in r["skipped"]
+    r, hung = bench.guarded(lambda: {"ms": 1.0}, 5, "leg")
+    assert not hung and r == {"ms": 1.0}
