@@ -655,7 +655,7 @@ template <int T, bool DUAL, int PD, class W = NoWait>
 __device__ __forceinline__ void panel_gemm_rt(__amdgpu_buffer_rsrc_t PA, const float4* B0, const float4* B1,
                                               int voff, int lane, f32x4& acc0, f32x4& acc1,
                                               const float4 (&ap)[PD], int nkb, int kq, W&& wt = W{}) {
-    static_assert(PD == 1 || PD == 2, "A ring depth 1 or 2");
+    constexpr int PR = PD > 2 ? 2 : PD;  // (deeper rings seed only their first two blocks here)
     acc0 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     acc1 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     const int last = nkb - 1;
@@ -680,25 +680,25 @@ __device__ __forceinline__ void panel_gemm_rt(__amdgpu_buffer_rsrc_t PA, const f
         }
         __builtin_amdgcn_sched_barrier(0);
     };
-    float4 a0 = ap[0], a1 = PD == 2 ? ap[PD - 1] : ap[0];
+    float4 a0 = ap[0], a1 = PR == 2 ? ap[1] : ap[0];
     wt(0);
     float4 e0 = B0[lane], f0 = DUAL ? B1[lane] : e0, e1, f1;
     GPAD_PRELUDE_LO();
     for (int kb = 0;; kb += 2) {
         const int k1 = kb + 1 < last ? kb + 1 : last, k2 = kb + 2 < last ? kb + 2 : last;
-        if constexpr (PD == 1) a1 = lda(kb + 1);
+        if constexpr (PR == 1) a1 = lda(kb + 1);
         wt(k1);
         e1 = B0[k1 * 64 + lane];
         if constexpr (DUAL) f1 = B1[k1 * 64 + lane];
         blk(a0, e0, f0, kb < last ? 4 : kq);
-        if constexpr (PD == 2) a0 = lda(kb + 2);
+        if constexpr (PR == 2) a0 = lda(kb + 2);
         if (kb + 1 > last) break;
-        if constexpr (PD == 1) a0 = lda(kb + 2);
+        if constexpr (PR == 1) a0 = lda(kb + 2);
         wt(k2);
         e0 = B0[k2 * 64 + lane];
         if constexpr (DUAL) f0 = B1[k2 * 64 + lane];
         blk(a1, e1, f1, kb + 1 < last ? 4 : kq);
-        if constexpr (PD == 2) a1 = lda(kb + 3);
+        if constexpr (PR == 2) a1 = lda(kb + 3);
         if (kb + 2 > last) break;
     }
     if constexpr (DUAL) asm volatile("" : "+v"(acc0), "+v"(acc1)::"memory");
@@ -1149,7 +1149,13 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
         }
         __syncthreads();
 
-        constexpr int PD = NU == 2 ? 1 : (ROLE == 3 ? Handoff<T>::R1 : 2);
+#ifndef GPAD_PD_SINGLE
+#define GPAD_PD_SINGLE 2  // (experiment knob: A ring depth of single-chain waves)
+#endif
+#ifndef GPAD_PD_DOUBLE
+#define GPAD_PD_DOUBLE 1
+#endif
+        constexpr int PD = NU == 2 ? GPAD_PD_DOUBLE : (ROLE == 3 ? Handoff<T>::R1 : GPAD_PD_SINGLE);
         float4 ap[PD];  // A blocks of the next GEMM, in flight across the barrier before it
         float4 aph[PD];  // helper / relay: the piece's first blocks
         auto prefetch = [&](__amdgpu_buffer_rsrc_t PA) {
