@@ -833,7 +833,13 @@ struct Panel2Lds {
 // at six points per iteration -- loop top, GEMM-1 issued, before its barrier, after it, GEMM-2
 // issued, before the closing barrier -- read back with gpad_debug_stamps (tools/stamp_panel.py).
 #ifdef GPAD_STAMP
-constexpr int kStampV0 = 101, kStampIts = 4, kStampPts = 8;  // 6, 7: GEMM 1 / 2 hand-off wait returned
+#ifndef GPAD_STAMP_V0
+#define GPAD_STAMP_V0 101
+#endif
+#ifndef GPAD_STAMP_PHASE_V
+#define GPAD_STAMP_PHASE_V 100
+#endif
+constexpr int kStampV0 = GPAD_STAMP_V0, kStampIts = 4, kStampPts = 8;  // 6, 7: GEMM 1 / 2 hand-off wait returned
 __device__ unsigned long long g_stamps[16][kStampIts][kStampPts];
 // s_memtime into SGPRs at each point (pinned by scheduling barriers), stored once per iteration after
 // the closing barrier: the store's lgkmcnt wait then sits where no LDS or scalar load is in flight,
@@ -853,7 +859,7 @@ __device__ unsigned long long g_stamps[16][kStampIts][kStampPts];
 #define GPAD_STAMP_DECL unsigned long long stv[kStampPts] = {0, 0, 0, 0, 0, 0, 0, 0};
 // phase anatomy of workgroup 0 in the phase that starts at kStampPhaseV: entry, state loaded, after
 // the load barrier, loop exit, survivors parked, after the closing barrier
-constexpr int kStampPhaseV = 100, kStampPhasePts = 6;
+constexpr int kStampPhaseV = GPAD_STAMP_PHASE_V, kStampPhasePts = 10;  // 6..9: the phase's last test (below)
 __device__ unsigned long long g_pstamps[16][kStampPhasePts];
 #define GPAD_PSTAMP(P)                                                                              \
     do {                                                                                            \
@@ -863,7 +869,15 @@ __device__ unsigned long long g_pstamps[16][kStampPhasePts];
         __builtin_amdgcn_sched_barrier(0);                                                          \
     } while (0)
 #define GPAD_STAMP_PTR(P) (&stv[P])
+// the test at the phase's last iteration: entry, decisions voted, verification done, results out
+#define GPAD_PSTAMP_END(P)                  \
+    do {                                    \
+        if (v >= a.v_end) GPAD_PSTAMP(P);   \
+    } while (0)
 #else
+#define GPAD_PSTAMP_END(P) \
+    do {                   \
+    } while (0)
 #define GPAD_STAMP_AT(P) \
     do {                 \
     } while (0)
@@ -1342,6 +1356,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             // ---- Algorithm 1 test per column: every wave reduces the tile partials of all the
             // item's columns (lane 16 pp + cc <-> panel pp, column cc) and votes by ballot, so the
             // outcome is uniform across the workgroup without a second barrier ---------------------
+            GPAD_PSTAMP_END(6);
             unsigned m1 = 0u, m2 = 0u;
             bool zh_out = true;  // this iteration's zhat still in L.Zh (no verification GEMM ran)
             if (chk) {
@@ -1355,6 +1370,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                             (red.w >= 0.0f) && (gq * a.L <= a.tol_gap)) ? 2 : 0);
                 const unsigned mA = (unsigned)__ballot(st1 & 1);
                 m2 = (unsigned)__ballot(st1 & 2);
+                GPAD_PSTAMP_END(7);
                 if (mA) {  // (A) nominated for some column of the item: G_L z of both panels
                     zh_out = false;
                     if constexpr (NU > 0) {
@@ -1407,6 +1423,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                     m1 = (unsigned)__ballot(ver);
                     m2 &= ~m1;
                 }
+                GPAD_PSTAMP_END(8);
             }
             // ---- finished columns: results out ---------------------------------------------
             if constexpr (NU > 0) {
@@ -1442,6 +1459,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                     }
                 }
             }
+            GPAD_PSTAMP_END(9);
             live &= ~(m1 | m2);
             if (v >= N) live = 0u;
             if (v >= a.v_end || live == 0u) break;
