@@ -69,16 +69,18 @@ __device__ __forceinline__ void row_st(void* base, size_t b, int ld, int off4, f
 
 // slot s takes list position p (empty if p >= count); uniform, contains barriers
 // gp_l / pd_l: this slot's per-row constants (g_P of the -ML rows, p_D of the G/L rows)
+// vs0 >= 0: an instance adopted through the mailbox, vs0 iterations done (its state carried)
 template <int KB, int K>
 __device__ __forceinline__ void duo_refill(const SolveArgs<float>& a, const DuoCtx& c, DuoSlot& s, int p,
                                            float* w_l, float* gp_l, float* pd_l, float* z_l,
-                                           const float (&r)[K]) {
+                                           const float (&r)[K], int vs0 = -1) {
     s.pos = __builtin_amdgcn_readfirstlane(p);  // (uniform: scalar bookkeeping, see duo_step)
-    s.vs = c.v0;
-    s.kc = c.kc0;
+    const int v = vs0 >= 0 ? vs0 : c.v0;
+    s.vs = v;
+    s.kc = vs0 >= 0 ? c.Kc - v % c.Kc : c.kc0;
     s.need8d = false;
-    s.th = sched(a.theta, c.v0);
-    s.bn = sched(a.beta, c.v0 + 1);
+    s.th = sched(a.theta, v);
+    s.bn = sched(a.beta, v + 1);
     s.x0 = s.x1 = s.x2 = 0.0f;
     const bool has = p < c.count;
     if (has) {
@@ -322,6 +324,22 @@ __device__ __forceinline__ void duo_solo(const SolveArgs<float>& a, const DuoCtx
     }
 }
 
+// Slot hand-off mailbox (Tuning::duo_mailbox; a.mbox).  Once the queue is drained, a workgroup
+// whose two slots are still live runs both at the two-slot speed (2.27 us per slot-iteration)
+// while workgroups whose slots have finished idle; a workgroup with nothing left takes a ticket
+// (head[0]), and a two-slot workgroup that sees an unserved ticket hands over the slot that sits at
+// its iteration boundary: it writes the instance's state (z, y, w, u -- the phased solve's carry
+// arrays) and posts (list position, iterations done) in entry head[1]++; the taker continues the
+// instance in solo mode (1.63 us) from exactly that state, so every instance runs the same
+// arithmetic and results stay bit-identical.  head[2] counts the workgroups that can no longer give
+// (at most one live slot with the queue drained): a taker leaves once every workgroup is counted
+// there and no entry is due for its ticket.  Entries carry the launch's tag (a.mgen; -mgen:
+// cancelled, when two givers raced for one ticket), so only the 4-int header needs zeroing.  Every
+// wait is bounded (an expired wait fails the run, GPAD_ERR_DEVICE).
+__device__ __forceinline__ int mb_load(const int* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int KA, int KB>
 __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs<float> a) {
     constexpr int K = KA > KB ? KA : KB;
@@ -334,6 +352,7 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs
     __shared__ CheckSlot slots[2][kResidentMaxThreads / 64];
     __shared__ CheckSlot vslots[kResidentMaxThreads / 64];  // verification of a nominated test (A)
     __shared__ int claim_l[2];
+    __shared__ int mb_l[3];  // mailbox decision / adopted position / iterations, broadcast by thread 0
 
     DuoCtx c;
     c.tid = threadIdx.x;
@@ -343,6 +362,8 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs
     c.count = a.count_in ? __builtin_amdgcn_readfirstlane(*a.count_in) : a.batch;
     if (a.count_in && c.count > a.fin_thresh) return;  // the panel phase has them
     c.G = gridDim.x;
+    // (mailbox) only when some workgroup starts with two instances, i.e. every workgroup with one
+    int* const mb = c.count > c.G ? a.mbox : nullptr;
     if ((int)blockIdx.x >= c.count) return;
     c.v0 = a.v_begin;
     c.fresh = c.v0 == 0;
@@ -390,7 +411,14 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs
     s1.nextp = __builtin_amdgcn_readfirstlane(claim_l[1]);
     duo_refill<KB, K>(a, c, s0, blockIdx.x, w_l[0], gp_l[0], pd_l[0], z_l, r);
     duo_refill<KB, K>(a, c, s1, blockIdx.x + c.G, w_l[1], gp_l[1], pd_l[1], z_l, r);
+    bool retired = false;  // (mailbox) counted in head[2]: this workgroup gives no more
+    auto retire = [&]() {
+        if (c.tid == 0) atomicAdd(&mb[2], 1);
+        retired = true;
+    };
+    int pairs = 0;
     while (s0.pos < c.count || s1.pos < c.count) {
+        if (mb && !retired && (s0.pos >= c.count || s1.pos >= c.count)) retire();
         if (s0.pos >= c.count) {
             duo_solo<KA, KB, K>(a, c, s1, w_l[1], zh_l[1], gp_l[1], pd_l[1], slots[1], vslots, &claim_l[1], z_l, r);
             break;
@@ -403,6 +431,82 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs
                             vslots, &claim_l[1], z_l, r);
         duo_step<KA, KB, K>(a, c, s1, s0, w_l[1], zh_l[1], gp_l[1], w_l[0], zh_l[0], gp_l[0], pd_l[0], slots[0],
                             vslots, &claim_l[0], z_l, r);
+        // (mailbox) slot 0 sits at its iteration boundary here; every fourth pair, once the queue is
+        // drained for both slots, give it to an unserved ticket
+        if (mb && s0.pos < c.count && s1.pos < c.count && s0.nextp >= c.count && s1.nextp >= c.count &&
+            (++pairs & 3) == 0) {
+            if (c.tid == 0) {
+                int d = 0;
+                if (mb_load(&mb[0]) > mb_load(&mb[1])) {
+                    const int j = atomicAdd(&mb[1], 1);
+                    d = (j < mb_load(&mb[0]) && j < kMboxSlots) ? j + 1 : -(j + 1);
+                }
+                mb_l[0] = d;
+            }
+            __syncthreads();
+            const int d = __builtin_amdgcn_readfirstlane(mb_l[0]);
+            if (d > 0) {
+                const size_t b = (size_t)__builtin_amdgcn_readfirstlane(a.idx_in ? a.idx_in[s0.pos] : s0.pos);
+                if (c.live) {
+                    if (c.isA) {
+                        row_st(a.z, b, c.n, 4 * c.row, s0.x0);
+                    } else {
+                        row_st(a.y, b, c.m, 4 * c.row, s0.x0);
+                        row_st(a.wc, b, c.m, 4 * c.row, s0.x1);
+                        row_st(a.uc, b, c.m, 4 * c.row, s0.x2);
+                    }
+                }
+                __syncthreads();  // (every wave's stores complete)
+                if (c.tid == 0) {
+                    int* const e = mb + 4 + 4 * (d - 1);
+                    e[0] = s0.pos;
+                    e[1] = s0.vs;
+                    __threadfence();  // the state and the entry before its tag
+                    __hip_atomic_store(&e[2], a.mgen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                s0.pos = c.count;  // slot 0 empty: slot 1 goes on alone (duo_solo, from its 8d half)
+                s0.nextp = c.count;
+            } else if (d < 0 && c.tid == 0 && -d <= kMboxSlots) {
+                __hip_atomic_store(&mb[4 + 4 * (-d - 1) + 2], -a.mgen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+    if (!mb) return;
+    // (mailbox) nothing left here: take tickets until every workgroup has stopped giving
+    if (!retired) retire();
+    for (;;) {
+        if (c.tid == 0) {
+            int k = atomicAdd(&mb[0], 1), res = 0;
+            for (int sp = 0;; ++sp) {
+                const int tag = k < kMboxSlots ? __hip_atomic_load(&mb[4 + 4 * k + 2], __ATOMIC_ACQUIRE,
+                                                                   __HIP_MEMORY_SCOPE_AGENT) : 0;
+                if (tag == a.mgen) {
+                    res = k + 1;
+                    mb_l[1] = mb[4 + 4 * k];
+                    mb_l[2] = mb[4 + 4 * k + 1];
+                    break;
+                }
+                if (tag == -a.mgen) {  // its giver lost a race: a new ticket
+                    k = atomicAdd(&mb[0], 1);
+                    continue;
+                }
+                if (mb_load(&mb[2]) >= c.G && mb_load(&mb[1]) <= k) break;  // none due
+                if (sp == (1 << 20)) {
+                    atomicOr(a.err, kDevErrHandoff);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            mb_l[0] = res;
+        }
+        __syncthreads();
+        if (__builtin_amdgcn_readfirstlane(mb_l[0]) == 0) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the giver's rows
+        const int p = __builtin_amdgcn_readfirstlane(mb_l[1]), vs = __builtin_amdgcn_readfirstlane(mb_l[2]);
+        duo_refill<KB, K>(a, c, s0, p, w_l[0], gp_l[0], pd_l[0], z_l, r, vs);
+        s0.nextp = c.count;
+        duo_solo<KA, KB, K>(a, c, s0, w_l[0], zh_l[0], gp_l[0], pd_l[0], slots[0], vslots, &claim_l[0], z_l, r);
+        __syncthreads();  // (mb_l reused)
     }
 }
 

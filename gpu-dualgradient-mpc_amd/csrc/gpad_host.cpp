@@ -353,6 +353,7 @@ int gpad_set_option(gpad_handle_t h, int option, int value) {
             return rc;
         }
         case GPAD_OPT_PANEL_DATAFLOW: return set(t.panel_dataflow, 0, 7, def.panel_dataflow);
+        case GPAD_OPT_DUO_MAILBOX: return set(t.duo_mailbox, 0, 1, def.duo_mailbox);
         default: return fail(GPAD_ERR_INVALID, "gpad_set_option: unknown option");
     }
 }

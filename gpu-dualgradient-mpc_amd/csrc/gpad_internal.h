@@ -31,11 +31,13 @@ struct Tuning {
     int p64_no_relay = 0;     // GPAD_OPT_P64_RELAY = 0: f64 panels without the relay layout
     int p64_no_refill = 0;    // GPAD_OPT_P64_REFILL = 0: f64 panels without column refills
     int panel_dataflow = 0;   // GPAD_OPT_PANEL_DATAFLOW: bits 1 one-panel, 2 pairs, 4 one-panel tile order
+    int duo_mailbox = 0;      // GPAD_OPT_DUO_MAILBOX: drained finisher workgroups hand a slot to idle ones
 };
 
 // Device error word of a run (SolveArgs::err): kernels OR these bits in with a vector atomic;
 // the host turns a non-zero word into GPAD_ERR_DEVICE when it collects or syncs the run.
 constexpr int kDevErrHandoff = 1;  // a chain hand-off wait expired (gpad_panel.hip handoff_wait)
+constexpr int kMboxSlots = 1024;  // duo mailbox entries (one per donation; at most one per workgroup)
 // SolveArgs::debug bits (fault injection for tests; 0 in production)
 constexpr int kDebugDropHandoff = 1;  // the first hand-off helper skips its first post
 
@@ -119,6 +121,8 @@ struct SolveArgs {
     int* err;              // device error word (kDevErr* bits), never null on a solve launch
     int debug;             // kDebug* fault-injection bits (tests only)
     int dflow;             // gpad_panel2_kernel: dataflow GEMM boundaries (Tuning::panel_dataflow bits)
+    int* mbox;             // duo kernel: slot hand-off mailbox (gpad_duo.hip), or null; header zeroed
+    int mgen;              // ... this launch's tag of its mailbox entries (never 0, unique per launch)
 };
 
 // launchers (return hipError_t of the launch)

@@ -27,6 +27,7 @@
 // one float4 per lane per (block, tile): 1 KiB per wave-instruction, fully coalesced.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <type_traits>
@@ -1784,9 +1785,11 @@ int panel_plan(const int* iters, int batch, int n, int m, int N, int check_every
 
 size_t panel_work_bytes(int m, int batch) {
     // idx ping-pong [2][batch] | phase counts [kPanelMaxPhases] | finisher queue counters
-    // [kPanelMaxPhases] | carried w, u [batch][m] each | per-panel survivor lists: seg_idx
-    // [batch + 32], seg_cnt [batch / 16 + 2] (list_survivors)
-    return sizeof(int) * (2 * (size_t)batch + 2 * kPanelMaxPhases) + 2 * sizeof(float) * (size_t)batch * m +
+    // [kPanelMaxPhases] | duo mailbox: header [4], entries [kMboxSlots][4] | carried w, u
+    // [batch][m] each | per-panel survivor lists: seg_idx [batch + 32], seg_cnt [batch / 16 + 2]
+    // (list_survivors)
+    return sizeof(int) * (2 * (size_t)batch + 2 * kPanelMaxPhases + 4 + 4 * (size_t)kMboxSlots) +
+           2 * sizeof(float) * (size_t)batch * m +
            sizeof(int) * ((size_t)batch + 32 + (size_t)batch / 16 + 2);
 }
 
@@ -1985,7 +1988,8 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     int* idx1 = idx0 + a.batch;
     int* counts = idx1 + a.batch;
     int* qctrs = counts + kPanelMaxPhases;
-    float* wc = reinterpret_cast<float*>(qctrs + kPanelMaxPhases);
+    int* mbox = qctrs + kPanelMaxPhases;  // (header zeroed with the counters; entries tagged by mgen)
+    float* wc = reinterpret_cast<float*>(mbox + 4 + 4 * kMboxSlots);
     a.wc = wc;
     a.uc = wc + (size_t)a.batch * a.m;
     // survivors listed per panel, densified at each boundary by phase_compact_kernel (one idx
@@ -1994,8 +1998,15 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     a.seg_cnt = a.seg_idx + a.batch + 32;
     a.idx_out = nullptr;
     a.count_out = nullptr;
-    hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * 2 * kPanelMaxPhases, s);
+    hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * (2 * kPanelMaxPhases + 4), s);
     if (e != hipSuccess) return e;
+    if (tn.duo_mailbox) {
+        static std::atomic<int> gen{0};
+        int g;
+        while ((g = ++gen) <= 0) gen = 0;  // (positive, so -g marks a cancelled entry)
+        a.mbox = mbox;
+        a.mgen = g;
+    }
     // phase length: a multiple of the test period (phases end right after a test); default
     // four tests, doubling after 10 phases so a long tail costs O(log N) launches (a phase with
     // no survivors left costs one empty launch, ~5 us)

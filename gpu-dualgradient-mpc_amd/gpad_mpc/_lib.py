@@ -51,6 +51,7 @@ OPT_DEBUG_DROP_HANDOFF = 16  # test-only fault injection
 OPT_P64_RELAY = 18  # f64 panels: 16-wave relay layout at T = 9, 13 (default 1)
 OPT_P64_REFILL = 19  # f64 panels: refill finished columns from the batch (default 1)
 OPT_PANEL_DATAFLOW = 20  # f32 panels: dataflow GEMM boundaries, bits 1 one-panel, 2 pairs, 4 tile order
+OPT_DUO_MAILBOX = 21  # finisher: drained workgroups hand a live instance to idle ones
 OPT_RETIRED = (5, 13, 14, 15, 17)  # finisher kind, solo finisher workgroups, plan finisher cost (0.3);
 # condensed panels (0.4, with the condensed operator); 17: the opt-in pair layouts measured in round 4
 # and left out of the product (W32, TailPair)
@@ -60,7 +61,8 @@ OPTIONS = {"phase_len": OPT_PHASE_LEN, "finish_thresh": OPT_FINISH_THRESH, "plan
            "flat_panel_min": OPT_FLAT_PANEL_MIN, "flat_panels": OPT_FLAT_PANELS,
            "flat_waves": OPT_FLAT_WAVES, "flat_a_lds": OPT_FLAT_A_LDS,
            "debug_drop_handoff": OPT_DEBUG_DROP_HANDOFF, "p64_relay": OPT_P64_RELAY,
-           "p64_refill": OPT_P64_REFILL, "panel_dataflow": OPT_PANEL_DATAFLOW}
+           "p64_refill": OPT_P64_REFILL, "panel_dataflow": OPT_PANEL_DATAFLOW,
+           "duo_mailbox": OPT_DUO_MAILBOX}
 
 FILE_ROWMAJOR, FILE_FLIPPED, FILE_FLAT = 0, 1, 2
 

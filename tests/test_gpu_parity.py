@@ -257,6 +257,28 @@ def test_panel_dataflow_c3_c4_batches(gpu, oracle, B):
         assert_bitexact(y1[b], yo, f"instance {b} y")
 
 
+@pytest.mark.parametrize("B", [4096, 8192])
+def test_duo_mailbox_c3_c4_batches(gpu, oracle, B):
+    """GPAD_OPT_DUO_MAILBOX on the C3 / C4-shard batches to eps (the planned phases, the duo finisher
+    from ~270-290 with hundreds of workgroups): z, y and every count equal the solve without it;
+    instances spot-checked against the oracle."""
+    import bench
+    n = m = 200
+    ML, G, L, M, g = bench.make_shard(n, m, B, 0)
+    f = lambda a: np.ascontiguousarray(np.asarray(a, np.float32))  # noqa: E731
+    ML, G, M, g, L = f(ML), f(G), f(M), f(g), np.float32(L)
+    z0, y0, _, it0 = run_gpu(ML, M, G, g, L, 5000, tol=1e-4, kernel="panel", opts=dict(duo_mailbox=0))
+    z1, y1, _, it1 = run_gpu(ML, M, G, g, L, 5000, tol=1e-4, kernel="panel", opts=dict(duo_mailbox=1))
+    assert np.array_equal(it0, it1)
+    assert_bitexact(z1, z0, "z")
+    assert_bitexact(y1, y0, "y")
+    for b in (0, int(np.argmax(it1)), B - 1):
+        zo, yo, it, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), ML, M[b], G, g[b], 5000, L, 1e-4)
+        assert it1[b] == it, b
+        assert_bitexact(z1[b], zo, f"instance {b} z")
+        assert_bitexact(y1[b], yo, f"instance {b} y")
+
+
 @pytest.mark.parametrize("tol,N", [(1e-4, 2000), (0.0, 37)])
 @pytest.mark.parametrize("nm,B", [((200, 900), 40), ((300, 300), 20), ((257, 130), 33), ((520, 600), 17), ((1000, 300), 9)])
 @pytest.mark.parametrize("grid,phase", [(0, 0), (2, 20)])
@@ -282,16 +304,18 @@ def test_bigpanel_bitexact(gpu, oracle, tol, N, nm, B, grid, phase):
         assert_bitexact(y[b], yo, f"instance {b} y")
 
 
+@pytest.mark.parametrize("mailbox", [0, 1])
 @pytest.mark.parametrize("grid", [1, 3, 5, 0])
 @pytest.mark.parametrize("nm,B,z0s", [((200, 200), 120, 0.0), ((40, 180), 200, 0.1), ((131, 64), 97, 0.1)])
-def test_finisher_queue_bitexact(gpu, oracle, grid, nm, B, z0s):
+def test_finisher_queue_bitexact(gpu, oracle, grid, nm, B, z0s, mailbox):
     """The tail of a phased panel solve on the duo finisher (two instances per workgroup in
     ping-pong, slots refilled from the survivor list through a device counter; grid capped to 1, 3
     or 5 workgroups to force many claims).  The finisher takes over after the first 10-iteration
     phase, so nearly the whole solve runs there; every instance must match its own oracle solve,
-    iteration count included."""
+    iteration count included.  mailbox = 1 (GPAD_OPT_DUO_MAILBOX): once the queue is drained, a
+    workgroup with two live slots hands one to a workgroup with none (grids 3 and 5)."""
     from gpad_mpc import problems
-    opts = dict(phase_len=10, finish_thresh=100000, duo_max_grid=grid)
+    opts = dict(phase_len=10, finish_thresh=100000, duo_max_grid=grid, duo_mailbox=mailbox)
     n, m = nm
     qp = problems.synthetic_qp(n, m, batch=B, seed=12)
     ML, G = qp.ML.astype(np.float32), qp.G.astype(np.float32)
