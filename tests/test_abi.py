@@ -185,3 +185,15 @@ def test_count_arrays_are_checked(arr):
     with pytest.raises(ValueError):
         _count_array(arr, "iters", 8)
     assert _count_array(np.zeros(8, np.int32), "iters", 8) is not None
+
+
+def test_python_option_names_match_the_header():
+    """Every gpad_set_option name of the Python mirror (gpad_mpc._lib.OPTIONS) is the number the
+    header defines for it, and every live option of the header has a Python name."""
+    from gpad_mpc import _lib
+    hdr = {k.lower(): int(v) for k, v in re.findall(r"#define GPAD_OPT_(\w+)\s+(\d+)", open(HEADER).read())}
+    hdr.pop("default", None)
+    for name, num in _lib.OPTIONS.items():
+        assert hdr.get(name) == num, name
+    live = {k: v for k, v in hdr.items() if v not in _lib.OPT_RETIRED}
+    assert set(live) <= set(_lib.OPTIONS), set(live) - set(_lib.OPTIONS)
