@@ -889,8 +889,11 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
         const int panel_min = gpad::resident_supported(n, m) ? 4 * h->num_cus : 64;
         if (kernel == GPAD_KERNEL_PANEL || (kernel == GPAD_KERNEL_AUTO && d.shared && batch > panel_min)) {
             if (tol > 0.0 && h->frag_ok) {  // phased compaction workspace (gpad_panel.hip)
+                void* const before = h->pwork.p;
                 int rc = h->pwork.ensure(gpad::panel_work_bytes(m, batch));
                 if (rc) return rc;
+                if (h->pwork.p != before)  // a new buffer: no stale words that a finisher mailbox
+                    HIP_TRY(hipMemsetAsync(h->pwork.p, 0, h->pwork.bytes, h->stream));  // entry could read as tagged
                 a.pwork = h->pwork.p;
                 a.plan = &h->plan;
                 // the previous phased solve's counts are still in `iters` for every instance this

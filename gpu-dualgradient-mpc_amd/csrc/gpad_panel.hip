@@ -1998,14 +1998,15 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     a.seg_cnt = a.seg_idx + a.batch + 32;
     a.idx_out = nullptr;
     a.count_out = nullptr;
-    hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * (2 * kPanelMaxPhases + 4), s);
+    // the phase counters and queue counters; with the mailbox its header and entries too (one memset)
+    hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * (2 * kPanelMaxPhases + 4 + (tn.duo_mailbox ? 4 * kMboxSlots : 0)), s);
     if (e != hipSuccess) return e;
     if (tn.duo_mailbox) {
-        static std::atomic<int> gen{0};
-        int g;
-        while ((g = ++gen) <= 0) gen = 0;  // (positive, so -g marks a cancelled entry)
+        // entries zeroed with the counters above; the tag (a quiet-NaN bit pattern, per launch) and
+        // -tag (a cancelled entry) are never 0
+        static std::atomic<unsigned> gen{0};
         a.mbox = mbox;
-        a.mgen = g;
+        a.mgen = (int)(0x7FC00001u + gen.fetch_add(1) % 0x3FFFFEu);
     }
     // phase length: a multiple of the test period (phases end right after a test); default
     // four tests, doubling after 10 phases so a long tail costs O(log N) launches (a phase with
