@@ -333,9 +333,12 @@ __device__ __forceinline__ void duo_solo(const SolveArgs<float>& a, const DuoCtx
 // instance in solo mode (1.63 us) from exactly that state, so every instance runs the same
 // arithmetic and results stay bit-identical.  head[2] counts the workgroups that can no longer give
 // (at most one live slot with the queue drained): a taker leaves once every workgroup is counted
-// there and no entry is due for its ticket.  Entries carry the launch's tag (a.mgen; -mgen:
-// cancelled, when two givers raced for one ticket), so only the 4-int header needs zeroing.  Every
-// wait is bounded (an expired wait fails the run, GPAD_ERR_DEVICE).
+// there and no entry is due for its ticket.  Entries (zeroed with the solve's counters) carry the
+// launch's tag (a.mgen; -mgen: cancelled, when two givers raced for one ticket), written by
+// compare-and-swap, and a taker whose wait grows long (a giver with thousands of iterations left)
+// gives its ticket up by the same swap, so no instance is ever handed to nobody and no wait is
+// unbounded.
+constexpr int kMboxAbandoned = 1;  // an entry whose taker gave up (tags are >= 0x7FC00001 or negative)
 __device__ __forceinline__ int mb_load(const int* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -462,12 +465,22 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs
                     e[0] = s0.pos;
                     e[1] = s0.vs;
                     __threadfence();  // the state and the entry before its tag
-                    __hip_atomic_store(&e[2], a.mgen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    // the tag by compare-and-swap: a taker that gave up (kMboxAbandoned) keeps the
+                    // instance here (the rows written are then simply not read)
+                    int expect = 0;
+                    mb_l[0] = __hip_atomic_compare_exchange_strong(&e[2], &expect, a.mgen, __ATOMIC_RELEASE,
+                                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                  ? 1 : 0;
                 }
-                s0.pos = c.count;  // slot 0 empty: slot 1 goes on alone (duo_solo, from its 8d half)
-                s0.nextp = c.count;
+                __syncthreads();
+                if (__builtin_amdgcn_readfirstlane(mb_l[0])) {
+                    s0.pos = c.count;  // slot 0 given: slot 1 goes on alone (duo_solo, from its 8d half)
+                    s0.nextp = c.count;
+                }
             } else if (d < 0 && c.tid == 0 && -d <= kMboxSlots) {
-                __hip_atomic_store(&mb[4 + 4 * (-d - 1) + 2], -a.mgen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                int expect = 0;
+                (void)__hip_atomic_compare_exchange_strong(&mb[4 + 4 * (-d - 1) + 2], &expect, -a.mgen, __ATOMIC_RELEASE,
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     }
@@ -478,8 +491,8 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs
         if (c.tid == 0) {
             int k = atomicAdd(&mb[0], 1), res = 0;
             for (int sp = 0;; ++sp) {
-                const int tag = k < kMboxSlots ? __hip_atomic_load(&mb[4 + 4 * k + 2], __ATOMIC_ACQUIRE,
-                                                                   __HIP_MEMORY_SCOPE_AGENT) : 0;
+                if (k >= kMboxSlots) break;  // (no entry: its giver cancels, keeps the instance)
+                const int tag = __hip_atomic_load(&mb[4 + 4 * k + 2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
                 if (tag == a.mgen) {
                     res = k + 1;
                     mb_l[1] = mb[4 + 4 * k];
@@ -491,9 +504,13 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs
                     continue;
                 }
                 if (mb_load(&mb[2]) >= c.G && mb_load(&mb[1]) <= k) break;  // none due
-                if (sp == (1 << 20)) {
-                    atomicOr(a.err, kDevErrHandoff);
-                    break;
+                if (sp >= (1 << 20)) {  // a long wait (givers with long solves): give the ticket up;
+                    int expect = 0;     // a giver that claims it later keeps its instance
+                    if (__hip_atomic_compare_exchange_strong(&mb[4 + 4 * k + 2], &expect, kMboxAbandoned,
+                                                             __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT))
+                        break;
+                    continue;  // (tagged meanwhile: handled above)
                 }
                 __builtin_amdgcn_s_sleep(2);
             }
