@@ -343,7 +343,9 @@ __device__ __forceinline__ int mb_load(const int* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int KA, int KB>
+// MB: the instantiation with the mailbox (launch_duo, a.mbox set; C3 / C4 rows only); the other runs
+// the plain loop, so the mailbox costs it nothing
+template <int KA, int KB, bool MB = false>
 __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs<float> a) {
     constexpr int K = KA > KB ? KA : KB;
     constexpr int PA = (KA + 63) / 64 * 64, PB = (KB + 63) / 64 * 64;
@@ -366,7 +368,7 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs
     if (a.count_in && c.count > a.fin_thresh) return;  // the panel phase has them
     c.G = gridDim.x;
     // (mailbox) only when some workgroup starts with two instances, i.e. every workgroup with one
-    int* const mb = c.count > c.G ? a.mbox : nullptr;
+    int* const mb = MB && c.count > c.G ? a.mbox : nullptr;
     if ((int)blockIdx.x >= c.count) return;
     c.v0 = a.v_begin;
     c.fresh = c.v0 == 0;
@@ -414,12 +416,38 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs
     s1.nextp = __builtin_amdgcn_readfirstlane(claim_l[1]);
     duo_refill<KB, K>(a, c, s0, blockIdx.x, w_l[0], gp_l[0], pd_l[0], z_l, r);
     duo_refill<KB, K>(a, c, s1, blockIdx.x + c.G, w_l[1], gp_l[1], pd_l[1], z_l, r);
+    if constexpr (!MB) {
+        while (s0.pos < c.count || s1.pos < c.count) {
+            if (s0.pos >= c.count) {
+                duo_solo<KA, KB, K>(a, c, s1, w_l[1], zh_l[1], gp_l[1], pd_l[1], slots[1], vslots, &claim_l[1], z_l,
+                                    r);
+                break;
+            }
+            if (s1.pos >= c.count) {
+                duo_solo<KA, KB, K>(a, c, s0, w_l[0], zh_l[0], gp_l[0], pd_l[0], slots[0], vslots, &claim_l[0], z_l,
+                                    r);
+                break;
+            }
+            duo_step<KA, KB, K>(a, c, s0, s1, w_l[0], zh_l[0], gp_l[0], w_l[1], zh_l[1], gp_l[1], pd_l[1], slots[1],
+                                vslots, &claim_l[1], z_l, r);
+            duo_step<KA, KB, K>(a, c, s1, s0, w_l[1], zh_l[1], gp_l[1], w_l[0], zh_l[0], gp_l[0], pd_l[0], slots[0],
+                                vslots, &claim_l[0], z_l, r);
+        }
+        return;
+    }
     bool retired = false;  // (mailbox) counted in head[2]: this workgroup gives no more
     auto retire = [&]() {
         if (c.tid == 0) atomicAdd(&mb[2], 1);
         retired = true;
     };
-    int pairs = 0;
+    int pairs = 0, tk = 0, po = 0;  // (mailbox) check counter; ticket / post counts of the last check
+    // two live slots while the queue still feeds one of them: the plain ping-pong (no mailbox work)
+    while (s0.pos < c.count && s1.pos < c.count && (s0.nextp < c.count || s1.nextp < c.count)) {
+        duo_step<KA, KB, K>(a, c, s0, s1, w_l[0], zh_l[0], gp_l[0], w_l[1], zh_l[1], gp_l[1], pd_l[1], slots[1],
+                            vslots, &claim_l[1], z_l, r);
+        duo_step<KA, KB, K>(a, c, s1, s0, w_l[1], zh_l[1], gp_l[1], w_l[0], zh_l[0], gp_l[0], pd_l[0], slots[0],
+                            vslots, &claim_l[0], z_l, r);
+    }
     while (s0.pos < c.count || s1.pos < c.count) {
         if (mb && !retired && (s0.pos >= c.count || s1.pos >= c.count)) retire();
         if (s0.pos >= c.count) {
@@ -430,24 +458,29 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs
             duo_solo<KA, KB, K>(a, c, s0, w_l[0], zh_l[0], gp_l[0], pd_l[0], slots[0], vslots, &claim_l[0], z_l, r);
             break;
         }
+        // (mailbox) every fourth pair once the queue is drained for both slots: thread 0 decides
+        // between the pair's two steps on the ticket and post counts it read at the previous check
+        // (four pairs back, so their latency -- coherent loads past the L2 -- never stalls a step;
+        // the claim itself re-reads), and the steps' own barriers publish the decision; slot 0
+        // sits at its iteration boundary after the pair
+        const bool mbchk = mb && s0.nextp >= c.count && s1.nextp >= c.count && (++pairs & 3) == 0;
         duo_step<KA, KB, K>(a, c, s0, s1, w_l[0], zh_l[0], gp_l[0], w_l[1], zh_l[1], gp_l[1], pd_l[1], slots[1],
                             vslots, &claim_l[1], z_l, r);
+        if (mbchk && c.tid == 0) {
+            int d = 0;
+            if (tk > po) {
+                const int j = atomicAdd(&mb[1], 1);
+                d = (j < mb_load(&mb[0]) && j < kMboxSlots) ? j + 1 : -(j + 1);
+            }
+            mb_l[0] = d;
+            tk = mb_load(&mb[0]);  // (for the next check)
+            po = mb_load(&mb[1]);
+        }
         duo_step<KA, KB, K>(a, c, s1, s0, w_l[1], zh_l[1], gp_l[1], w_l[0], zh_l[0], gp_l[0], pd_l[0], slots[0],
                             vslots, &claim_l[0], z_l, r);
-        // (mailbox) slot 0 sits at its iteration boundary here; every fourth pair, once the queue is
-        // drained for both slots, give it to an unserved ticket
-        if (mb && s0.pos < c.count && s1.pos < c.count && s0.nextp >= c.count && s1.nextp >= c.count &&
-            (++pairs & 3) == 0) {
-            if (c.tid == 0) {
-                int d = 0;
-                if (mb_load(&mb[0]) > mb_load(&mb[1])) {
-                    const int j = atomicAdd(&mb[1], 1);
-                    d = (j < mb_load(&mb[0]) && j < kMboxSlots) ? j + 1 : -(j + 1);
-                }
-                mb_l[0] = d;
-            }
-            __syncthreads();
-            const int d = __builtin_amdgcn_readfirstlane(mb_l[0]);
+        if (mbchk) {
+            int d = __builtin_amdgcn_readfirstlane(mb_l[0]);
+            if (d > 0 && (s0.pos >= c.count || s1.pos >= c.count)) d = -d;  // a slot finished meanwhile
             if (d > 0) {
                 const size_t b = (size_t)__builtin_amdgcn_readfirstlane(a.idx_in ? a.idx_in[s0.pos] : s0.pos);
                 if (c.live) {
@@ -547,6 +580,10 @@ hipError_t launch_duo(const SolveArgs<float>& a, int grid, hipStream_t st) {
     const int threads = 64 * (((a.n + 63) >> 6) + ((a.m + 63) >> 6));
     const dim3 g(grid), bl(threads);
     const int ka = res_bucket(a.m), kb = res_bucket(a.n);
+    if (a.mbox && ka == 200 && kb == 200) {  // the mailbox instantiation (GPAD_OPT_DUO_MAILBOX): C3 / C4 rows
+        hipLaunchKernelGGL((gpad_duo_kernel<200, 200, true>), g, bl, 0, st, a);
+        return hipGetLastError();
+    }
     switch (ka) {
         case 32: launch_duo_b<32>(kb, g, bl, st, a); break;
         case 64: launch_duo_b<64>(kb, g, bl, st, a); break;

@@ -31,7 +31,7 @@ struct Tuning {
     int p64_no_relay = 0;     // GPAD_OPT_P64_RELAY = 0: f64 panels without the relay layout
     int p64_no_refill = 0;    // GPAD_OPT_P64_REFILL = 0: f64 panels without column refills
     int panel_dataflow = 0;   // GPAD_OPT_PANEL_DATAFLOW: bits 1 one-panel, 2 pairs, 4 one-panel tile order
-    int duo_mailbox = 1;      // GPAD_OPT_DUO_MAILBOX: drained finisher workgroups hand a slot to idle ones
+    int duo_mailbox = 0;      // GPAD_OPT_DUO_MAILBOX: drained finisher workgroups hand a slot to idle ones
 };
 
 // Device error word of a run (SolveArgs::err): kernels OR these bits in with a vector atomic;

@@ -51,7 +51,7 @@ OPT_DEBUG_DROP_HANDOFF = 16  # test-only fault injection
 OPT_P64_RELAY = 18  # f64 panels: 16-wave relay layout at T = 9, 13 (default 1)
 OPT_P64_REFILL = 19  # f64 panels: refill finished columns from the batch (default 1)
 OPT_PANEL_DATAFLOW = 20  # f32 panels: dataflow GEMM boundaries, bits 1 one-panel, 2 pairs, 4 tile order
-OPT_DUO_MAILBOX = 21  # finisher: drained workgroups hand a live instance to idle ones (default 1)
+OPT_DUO_MAILBOX = 21  # finisher: drained workgroups hand a live instance to idle ones (default 0)
 OPT_RETIRED = (5, 13, 14, 15, 17)  # finisher kind, solo finisher workgroups, plan finisher cost (0.3);
 # condensed panels (0.4, with the condensed operator); 17: the opt-in pair layouts measured in round 4
 # and left out of the product (W32, TailPair)

@@ -402,9 +402,10 @@ int gpad_schedule(int N, int kind, double* theta, double* beta);
                                     * pair layout's chains start on the other GEMM's row tiles as they
                                     * are written instead of after a barrier (bit-identical results);
                                     * bit 4: one-panel row tiles dealt oldest wave first */
-#define GPAD_OPT_DUO_MAILBOX 21    /* 1 (default): once its queue is drained, a finisher workgroup with
-                                    * two live instances hands one, at its iteration boundary, to a
-                                    * workgroup with none (bit-identical results); 0: never */
+#define GPAD_OPT_DUO_MAILBOX 21    /* 1: once its queue is drained, a finisher workgroup with two live
+                                    * instances hands one, at its iteration boundary, to a workgroup
+                                    * with none (bit-identical results; n, m in (192, 200], the C3 / C4
+                                    * rows); 0 (default): never */
 int gpad_set_option(gpad_handle_t h, int option, int value);
 
 /* Synchronise the handle's stream (for callers using device memory + async runs). */

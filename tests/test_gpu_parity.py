@@ -312,8 +312,9 @@ def test_finisher_queue_bitexact(gpu, oracle, grid, nm, B, z0s, mailbox):
     ping-pong, slots refilled from the survivor list through a device counter; grid capped to 1, 3
     or 5 workgroups to force many claims).  The finisher takes over after the first 10-iteration
     phase, so nearly the whole solve runs there; every instance must match its own oracle solve,
-    iteration count included.  mailbox = 1 (GPAD_OPT_DUO_MAILBOX): once the queue is drained, a
-    workgroup with two live slots hands one to a workgroup with none (grids 3 and 5)."""
+    iteration count included.  mailbox = 1 (GPAD_OPT_DUO_MAILBOX, instantiated for the 200 x 200
+    rows): once the queue is drained, a workgroup with two live slots hands one to a workgroup with
+    none (grids 3 and 5)."""
     from gpad_mpc import problems
     opts = dict(phase_len=10, finish_thresh=100000, duo_max_grid=grid, duo_mailbox=mailbox)
     n, m = nm
