@@ -231,6 +231,40 @@ def traffic_from_profile(kernel_name):
     return sum(tot) / solves, os.path.relpath(path, ROOT)
 
 
+def kernel_ms_from_profile(kernel_prefix):
+    """Device time per C4 solve of one kernel family from the committed kernel trace of this same
+    bench command (the newest profiles/rNN_bench_summary.json, `kernels` = rocprofv3 --stats): the
+    total of every instantiation whose name starts with ``kernel_prefix`` / the profiled run's
+    solves (2 x (--warmup + --steps), as traffic_from_profile).  (None, None) when absent."""
+    import glob
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_bench_summary.json")))
+    if not found:
+        return None, None
+    try:
+        d = json.load(open(found[-1]))
+        args = d.get("bench_args", "").split()
+        solves = 2 * (int(args[args.index("--steps") + 1]) + int(args[args.index("--warmup") + 1]))
+    except (OSError, ValueError, IndexError):
+        return None, None
+    tot = sum(v["total_ns"] for k, v in d.get("kernels", {}).items() if k.startswith(kernel_prefix))
+    if not tot or solves <= 0:
+        return None, None
+    return tot / solves / 1e6, os.path.relpath(found[-1], ROOT)
+
+
+def panel_share(iters, phases):
+    """Instance-iterations of one phased solve that ran on the panels: everything up to the
+    finisher's takeover (gpad_last_phases: the first phase whose input the duo took), the rest on
+    the finisher."""
+    it = np.asarray(iters, np.int64)
+    take = phases.get("takeover") if phases else None
+    if not take:
+        return int(it.sum()), 0, None
+    v = int(take["iteration"])
+    pan = int(np.minimum(it, v).sum())
+    return pan, int(it.sum()) - pan, v
+
+
 def hbm_leg(dev, batch=1024, n=800, m=800, N=20, ref=None):
     """C5: long horizon (N = 200 -> n = 800), m = 800, 1024 instances with DISTINCT matrices:
     the matrices cannot stay on chip, so every iteration streams 5.1 MB per instance from HBM
@@ -918,7 +952,13 @@ def main():
             per_rank = [[float(v) for v in t.cpu()] for t in allr]
         return dict(dt=dt_all, iters_all=iters_all, converged_all=conv_all, total_iters=total_iters,
                     kern_ms=kern_ms, st=st, iters_host=iters_host, plan=solver.phase_plan(),
-                    drain_ms=drain_ms, per_rank=per_rank)
+                    phases=last_phases(), drain_ms=drain_ms, per_rank=per_rank)
+
+    def last_phases():
+        try:
+            return solver.last_phases()
+        except gpad_mpc.GpadError:  # (an A/B build older than gpad_last_phases, GPAD_LIB_TOLERANT)
+            return None
 
     def gather_ms(reps=3):
         """One step's gather of (z*, y*) to rank 0 on its own: barrier, blocking gather, device
@@ -990,6 +1030,12 @@ def main():
             if st["kernel"] == "panel" else f"gpad::gpad_{st['kernel']}_kernel"
         traffic, traffic_src = traffic_from_profile(kname)
         launches = util["launches_per_solve"] if st["kernel"] == "panel" else 1
+        # the dominant kernel alone: useful flops the panels did in the last
+        # fresh-input solve (its counts up to the finisher's takeover) / the panel kernel's rocprof
+        # time per solve from the committed profile of this bench command
+        pan_iters, fin_iters, v_take = panel_share(head["iters_host"], head["phases"])
+        pan_ms, pan_src = kernel_ms_from_profile(kname[:-1] + ", " if kname.endswith(">") else kname)
+        kernel_frac = (pan_iters * F / (pan_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS) if pan_ms else None
         # single instances (configs C1 and C2): latency kernels, fixed iteration counts
         singles = {}
         from gpad_mpc import problems
@@ -1085,6 +1131,15 @@ def main():
                                      "mean iterations to eps, per GPU per step time, / 8 TB/s; the shared "
                                      "matrices are L2-resident, so HBM sees far less (traffic)",
                          "kernel_ms": avg_kernel_s * 1e3, "launches_per_solve": launches,
+                         "kernel_frac": kernel_frac,
+                         "kernel_frac_detail": {
+                             "kernel": kname, "panel_instance_iterations": pan_iters,
+                             "finisher_instance_iterations": fin_iters, "finisher_takeover": v_take,
+                             "panel_ms_per_solve": pan_ms, "source": pan_src,
+                             "note": "useful flops on the panel kernel (F per instance-iteration up to the "
+                                     "finisher takeover of the last fresh-input solve) / the panel kernel's "
+                                     "rocprof time per solve in the committed profile of this command, / "
+                                     "the fp32 matrix peak; frac above is the whole step"},
                          "note": "fp32 matrix-core bound (shared matrices stay in L2, traffic = "
                                  "per-instance vectors); achieved = useful flops (F = 4nm+5m+4n "
                                  "per executed instance-iteration) of one solve / its device time "

@@ -3,7 +3,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
-#include <utility>
 
 #include "gpad_chain.h"
 #include "gpad_internal.h"
@@ -69,15 +68,14 @@ __device__ __forceinline__ void row_st(void* base, size_t b, int ld, int off4, f
 
 // slot s takes list position p (empty if p >= count); uniform, contains barriers
 // gp_l / pd_l: this slot's per-row constants (g_P of the -ML rows, p_D of the G/L rows)
-// vs0 >= 0: an instance adopted through the mailbox, vs0 iterations done (its state carried)
 template <int KB, int K>
 __device__ __forceinline__ void duo_refill(const SolveArgs<float>& a, const DuoCtx& c, DuoSlot& s, int p,
                                            float* w_l, float* gp_l, float* pd_l, float* z_l,
-                                           const float (&r)[K], int vs0 = -1) {
+                                           const float (&r)[K]) {
     s.pos = __builtin_amdgcn_readfirstlane(p);  // (uniform: scalar bookkeeping, see duo_step)
-    const int v = vs0 >= 0 ? vs0 : c.v0;
+    const int v = c.v0;
     s.vs = v;
-    s.kc = vs0 >= 0 ? c.Kc - v % c.Kc : c.kc0;
+    s.kc = c.kc0;
     s.need8d = false;
     s.th = sched(a.theta, v);
     s.bn = sched(a.beta, v + 1);
@@ -324,28 +322,7 @@ __device__ __forceinline__ void duo_solo(const SolveArgs<float>& a, const DuoCtx
     }
 }
 
-// Slot hand-off mailbox (Tuning::duo_mailbox; a.mbox).  Once the queue is drained, a workgroup
-// whose two slots are still live runs both at the two-slot speed (2.27 us per slot-iteration)
-// while workgroups whose slots have finished idle; a workgroup with nothing left takes a ticket
-// (head[0]), and a two-slot workgroup that sees an unserved ticket hands over the slot that sits at
-// its iteration boundary: it writes the instance's state (z, y, w, u -- the phased solve's carry
-// arrays) and posts (list position, iterations done) in entry head[1]++; the taker continues the
-// instance in solo mode (1.63 us) from exactly that state, so every instance runs the same
-// arithmetic and results stay bit-identical.  head[2] counts the workgroups that can no longer give
-// (at most one live slot with the queue drained): a taker leaves once every workgroup is counted
-// there and no entry is due for its ticket.  Entries (zeroed with the solve's counters) carry the
-// launch's tag (a.mgen; -mgen: cancelled, when two givers raced for one ticket), written by
-// compare-and-swap, and a taker whose wait grows long (a giver with thousands of iterations left)
-// gives its ticket up by the same swap, so no instance is ever handed to nobody and no wait is
-// unbounded.
-constexpr int kMboxAbandoned = 1;  // an entry whose taker gave up (tags are >= 0x7FC00001 or negative)
-__device__ __forceinline__ int mb_load(const int* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// MB: the instantiation with the mailbox (launch_duo, a.mbox set; C3 / C4 rows only); the other runs
-// the plain loop, so the mailbox costs it nothing
-template <int KA, int KB, bool MB = false>
+template <int KA, int KB>
 __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs<float> a) {
     constexpr int K = KA > KB ? KA : KB;
     constexpr int PA = (KA + 63) / 64 * 64, PB = (KB + 63) / 64 * 64;
@@ -357,7 +334,6 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs
     __shared__ CheckSlot slots[2][kResidentMaxThreads / 64];
     __shared__ CheckSlot vslots[kResidentMaxThreads / 64];  // verification of a nominated test (A)
     __shared__ int claim_l[2];
-    __shared__ int mb_l[3];  // mailbox decision / adopted position / iterations, broadcast by thread 0
 
     DuoCtx c;
     c.tid = threadIdx.x;
@@ -367,8 +343,6 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs
     c.count = a.count_in ? __builtin_amdgcn_readfirstlane(*a.count_in) : a.batch;
     if (a.count_in && c.count > a.fin_thresh) return;  // the panel phase has them
     c.G = gridDim.x;
-    // (mailbox) only when some workgroup starts with two instances, i.e. every workgroup with one
-    int* const mb = MB && c.count > c.G ? a.mbox : nullptr;
     if ((int)blockIdx.x >= c.count) return;
     c.v0 = a.v_begin;
     c.fresh = c.v0 == 0;
@@ -416,40 +390,7 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs
     s1.nextp = __builtin_amdgcn_readfirstlane(claim_l[1]);
     duo_refill<KB, K>(a, c, s0, blockIdx.x, w_l[0], gp_l[0], pd_l[0], z_l, r);
     duo_refill<KB, K>(a, c, s1, blockIdx.x + c.G, w_l[1], gp_l[1], pd_l[1], z_l, r);
-    if constexpr (!MB) {
-        while (s0.pos < c.count || s1.pos < c.count) {
-            if (s0.pos >= c.count) {
-                duo_solo<KA, KB, K>(a, c, s1, w_l[1], zh_l[1], gp_l[1], pd_l[1], slots[1], vslots, &claim_l[1], z_l,
-                                    r);
-                break;
-            }
-            if (s1.pos >= c.count) {
-                duo_solo<KA, KB, K>(a, c, s0, w_l[0], zh_l[0], gp_l[0], pd_l[0], slots[0], vslots, &claim_l[0], z_l,
-                                    r);
-                break;
-            }
-            duo_step<KA, KB, K>(a, c, s0, s1, w_l[0], zh_l[0], gp_l[0], w_l[1], zh_l[1], gp_l[1], pd_l[1], slots[1],
-                                vslots, &claim_l[1], z_l, r);
-            duo_step<KA, KB, K>(a, c, s1, s0, w_l[1], zh_l[1], gp_l[1], w_l[0], zh_l[0], gp_l[0], pd_l[0], slots[0],
-                                vslots, &claim_l[0], z_l, r);
-        }
-        return;
-    }
-    bool retired = false;  // (mailbox) counted in head[2]: this workgroup gives no more
-    auto retire = [&]() {
-        if (c.tid == 0) atomicAdd(&mb[2], 1);
-        retired = true;
-    };
-    int pairs = 0, tk = 0, po = 0;  // (mailbox) check counter; ticket / post counts of the last check
-    // two live slots while the queue still feeds one of them: the plain ping-pong (no mailbox work)
-    while (s0.pos < c.count && s1.pos < c.count && (s0.nextp < c.count || s1.nextp < c.count)) {
-        duo_step<KA, KB, K>(a, c, s0, s1, w_l[0], zh_l[0], gp_l[0], w_l[1], zh_l[1], gp_l[1], pd_l[1], slots[1],
-                            vslots, &claim_l[1], z_l, r);
-        duo_step<KA, KB, K>(a, c, s1, s0, w_l[1], zh_l[1], gp_l[1], w_l[0], zh_l[0], gp_l[0], pd_l[0], slots[0],
-                            vslots, &claim_l[0], z_l, r);
-    }
     while (s0.pos < c.count || s1.pos < c.count) {
-        if (mb && !retired && (s0.pos >= c.count || s1.pos >= c.count)) retire();
         if (s0.pos >= c.count) {
             duo_solo<KA, KB, K>(a, c, s1, w_l[1], zh_l[1], gp_l[1], pd_l[1], slots[1], vslots, &claim_l[1], z_l, r);
             break;
@@ -458,105 +399,10 @@ __global__ __launch_bounds__(kResidentMaxThreads) void gpad_duo_kernel(SolveArgs
             duo_solo<KA, KB, K>(a, c, s0, w_l[0], zh_l[0], gp_l[0], pd_l[0], slots[0], vslots, &claim_l[0], z_l, r);
             break;
         }
-        // (mailbox) every fourth pair once the queue is drained for both slots: thread 0 decides
-        // between the pair's two steps on the ticket and post counts it read at the previous check
-        // (four pairs back, so their latency -- coherent loads past the L2 -- never stalls a step;
-        // the claim itself re-reads), and the steps' own barriers publish the decision; slot 0
-        // sits at its iteration boundary after the pair
-        const bool mbchk = mb && s0.nextp >= c.count && s1.nextp >= c.count && (++pairs & 3) == 0;
         duo_step<KA, KB, K>(a, c, s0, s1, w_l[0], zh_l[0], gp_l[0], w_l[1], zh_l[1], gp_l[1], pd_l[1], slots[1],
                             vslots, &claim_l[1], z_l, r);
-        if (mbchk && c.tid == 0) {
-            int d = 0;
-            if (tk > po) {
-                const int j = atomicAdd(&mb[1], 1);
-                d = (j < mb_load(&mb[0]) && j < kMboxSlots) ? j + 1 : -(j + 1);
-            }
-            mb_l[0] = d;
-            tk = mb_load(&mb[0]);  // (for the next check)
-            po = mb_load(&mb[1]);
-        }
         duo_step<KA, KB, K>(a, c, s1, s0, w_l[1], zh_l[1], gp_l[1], w_l[0], zh_l[0], gp_l[0], pd_l[0], slots[0],
                             vslots, &claim_l[0], z_l, r);
-        if (mbchk) {
-            int d = __builtin_amdgcn_readfirstlane(mb_l[0]);
-            if (d > 0 && (s0.pos >= c.count || s1.pos >= c.count)) d = -d;  // a slot finished meanwhile
-            if (d > 0) {
-                const size_t b = (size_t)__builtin_amdgcn_readfirstlane(a.idx_in ? a.idx_in[s0.pos] : s0.pos);
-                if (c.live) {
-                    if (c.isA) {
-                        row_st(a.z, b, c.n, 4 * c.row, s0.x0);
-                    } else {
-                        row_st(a.y, b, c.m, 4 * c.row, s0.x0);
-                        row_st(a.wc, b, c.m, 4 * c.row, s0.x1);
-                        row_st(a.uc, b, c.m, 4 * c.row, s0.x2);
-                    }
-                }
-                __syncthreads();  // (every wave's stores complete)
-                if (c.tid == 0) {
-                    int* const e = mb + 4 + 4 * (d - 1);
-                    e[0] = s0.pos;
-                    e[1] = s0.vs;
-                    __threadfence();  // the state and the entry before its tag
-                    // the tag by compare-and-swap: a taker that gave up (kMboxAbandoned) keeps the
-                    // instance here (the rows written are then simply not read)
-                    int expect = 0;
-                    mb_l[0] = __hip_atomic_compare_exchange_strong(&e[2], &expect, a.mgen, __ATOMIC_RELEASE,
-                                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                  ? 1 : 0;
-                }
-                __syncthreads();
-                if (__builtin_amdgcn_readfirstlane(mb_l[0])) {
-                    s0.pos = c.count;  // slot 0 given: slot 1 goes on alone (duo_solo, from its 8d half)
-                    s0.nextp = c.count;
-                }
-            } else if (d < 0 && c.tid == 0 && -d <= kMboxSlots) {
-                int expect = 0;
-                (void)__hip_atomic_compare_exchange_strong(&mb[4 + 4 * (-d - 1) + 2], &expect, -a.mgen, __ATOMIC_RELEASE,
-                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-    }
-    if (!mb) return;
-    // (mailbox) nothing left here: take tickets until every workgroup has stopped giving
-    if (!retired) retire();
-    for (;;) {
-        if (c.tid == 0) {
-            int k = atomicAdd(&mb[0], 1), res = 0;
-            for (int sp = 0;; ++sp) {
-                if (k >= kMboxSlots) break;  // (no entry: its giver cancels, keeps the instance)
-                const int tag = __hip_atomic_load(&mb[4 + 4 * k + 2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                if (tag == a.mgen) {
-                    res = k + 1;
-                    mb_l[1] = mb[4 + 4 * k];
-                    mb_l[2] = mb[4 + 4 * k + 1];
-                    break;
-                }
-                if (tag == -a.mgen) {  // its giver lost a race: a new ticket
-                    k = atomicAdd(&mb[0], 1);
-                    continue;
-                }
-                if (mb_load(&mb[2]) >= c.G && mb_load(&mb[1]) <= k) break;  // none due
-                if (sp >= (1 << 20)) {  // a long wait (givers with long solves): give the ticket up;
-                    int expect = 0;     // a giver that claims it later keeps its instance
-                    if (__hip_atomic_compare_exchange_strong(&mb[4 + 4 * k + 2], &expect, kMboxAbandoned,
-                                                             __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_AGENT))
-                        break;
-                    continue;  // (tagged meanwhile: handled above)
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-            mb_l[0] = res;
-        }
-        __syncthreads();
-        if (__builtin_amdgcn_readfirstlane(mb_l[0]) == 0) return;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the giver's rows
-        const int p = __builtin_amdgcn_readfirstlane(mb_l[1]), vs = __builtin_amdgcn_readfirstlane(mb_l[2]);
-        duo_refill<KB, K>(a, c, s0, p, w_l[0], gp_l[0], pd_l[0], z_l, r, vs);
-        s0.nextp = c.count;
-        duo_solo<KA, KB, K>(a, c, s0, w_l[0], zh_l[0], gp_l[0], pd_l[0], slots[0], vslots, &claim_l[0], z_l, r);
-        __syncthreads();  // (mb_l reused)
     }
 }
 
@@ -580,10 +426,6 @@ hipError_t launch_duo(const SolveArgs<float>& a, int grid, hipStream_t st) {
     const int threads = 64 * (((a.n + 63) >> 6) + ((a.m + 63) >> 6));
     const dim3 g(grid), bl(threads);
     const int ka = res_bucket(a.m), kb = res_bucket(a.n);
-    if (a.mbox && ka == 200 && kb == 200) {  // the mailbox instantiation (GPAD_OPT_DUO_MAILBOX): C3 / C4 rows
-        hipLaunchKernelGGL((gpad_duo_kernel<200, 200, true>), g, bl, 0, st, a);
-        return hipGetLastError();
-    }
     switch (ka) {
         case 32: launch_duo_b<32>(kb, g, bl, st, a); break;
         case 64: launch_duo_b<64>(kb, g, bl, st, a); break;

@@ -18,10 +18,11 @@
 // (hipMemcpyPeerAsync), ordered by events exactly where the RCCL calls are.
 #include <hip/hip_runtime.h>
 #include <dlfcn.h>
-#include <rccl/rccl.h>  // types only: librccl is loaded on first use (rccl() below), not linked
+#include <rccl/rccl.h>  // types only: librccl is loaded on first use (current_rccl() below), not linked
 
 #include <algorithm>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -43,8 +44,13 @@ int gfail(int code, const std::string& msg) { return gpad::set_last_error(code, 
 // RCCL entry points, resolved from librccl on the first group over distinct devices, so that
 // single-GPU users of libgpad (gpad_solve, the handle API) never need RCCL installed.  Without it a
 // group falls back to the peer-copy transport (gpad_group_transport reports which).
+// gpad_group_rccl_library swaps the library (tests: a stub that moves the same bytes with HIP copies
+// and accepts a repeated device, so the RCCL branch runs with several ranks on a one-GPU box); a
+// group keeps the entry points it was created with.
 struct Rccl {
     bool ok = false;
+    bool force = false;  // RCCL transport even for a repeated device (gpad_group_rccl_library)
+    std::string path;    // (empty: the default librccl)
     ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
     ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
     ncclResult_t (*GroupStart)() = nullptr;
@@ -55,31 +61,45 @@ struct Rccl {
     const char* (*GetErrorString)(ncclResult_t) = nullptr;
 };
 
-const Rccl& rccl() {
-    static Rccl r;
-    static std::once_flag once;
-    std::call_once(once, [] {
-        void* lib = nullptr;
+std::shared_ptr<const Rccl> load_rccl(const std::string& path, bool force) {
+    auto r = std::make_shared<Rccl>();
+    r->path = path;
+    void* lib = nullptr;
+    if (!path.empty()) {
+        lib = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+    } else {
         for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
             if ((lib = dlopen(name, RTLD_NOW | RTLD_LOCAL))) break;
-        if (!lib) return;
-        auto sym = [&](auto& fn, const char* name) {
-            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(lib, name));
-            return fn != nullptr;
-        };
-        r.ok = sym(r.CommInitAll, "ncclCommInitAll") && sym(r.CommDestroy, "ncclCommDestroy") &&
-               sym(r.GroupStart, "ncclGroupStart") && sym(r.GroupEnd, "ncclGroupEnd") && sym(r.Send, "ncclSend") &&
-               sym(r.Recv, "ncclRecv") && sym(r.Broadcast, "ncclBroadcast") &&
-               sym(r.GetErrorString, "ncclGetErrorString");
-    });
+    }
+    if (!lib) return r;  // (never dlclose'd: groups created from it may outlive a swap)
+    auto sym = [&](auto& fn, const char* name) {
+        fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(lib, name));
+        return fn != nullptr;
+    };
+    r->ok = sym(r->CommInitAll, "ncclCommInitAll") && sym(r->CommDestroy, "ncclCommDestroy") &&
+            sym(r->GroupStart, "ncclGroupStart") && sym(r->GroupEnd, "ncclGroupEnd") && sym(r->Send, "ncclSend") &&
+            sym(r->Recv, "ncclRecv") && sym(r->Broadcast, "ncclBroadcast") &&
+            sym(r->GetErrorString, "ncclGetErrorString");
+    r->force = r->ok && force;
     return r;
+}
+
+std::mutex g_rccl_mu;
+std::shared_ptr<const Rccl> g_rccl;  // loaded on first use (default librccl), or set by gpad_group_rccl_library
+unsigned g_rccl_gen = 0;             // bumped by every gpad_group_rccl_library (the sharded cache re-creates)
+
+std::shared_ptr<const Rccl> current_rccl(unsigned* gen = nullptr) {
+    std::lock_guard<std::mutex> lk(g_rccl_mu);
+    if (!g_rccl) g_rccl = load_rccl(std::string(), false);
+    if (gen) *gen = g_rccl_gen;
+    return g_rccl;
 }
 
 #define G_NCCL(expr)                                                                                  \
     do {                                                                                              \
-        ncclResult_t _r = rccl().expr;                                                                \
+        ncclResult_t _r = g->r->expr;                                                                 \
         if (_r != ncclSuccess)                                                                        \
-            return gfail(GPAD_ERR_HIP, std::string("nccl" #expr) + ": " + rccl().GetErrorString(_r));  \
+            return gfail(GPAD_ERR_HIP, std::string("nccl" #expr) + ": " + g->r->GetErrorString(_r));   \
     } while (0)
 
 size_t esz(int dtype) { return dtype == GPAD_DTYPE_F64 ? sizeof(double) : sizeof(float); }
@@ -93,6 +113,7 @@ struct gpad_group_s {
     std::vector<hipStream_t> st;
     std::vector<hipEvent_t> ev;      // one per device: ordering of the peer-copy transport
     std::vector<ncclComm_t> comm;    // empty: peer-copy transport (a device listed twice)
+    std::shared_ptr<const Rccl> r;   // the RCCL entry points the clique was created with
     gpad_dims_t dims{};              // the whole batch
     double L = 0.0;
     bool ready = false;
@@ -122,7 +143,7 @@ int release(gpad_group_s* g) {
         (void)hipSetDevice(g->dev[0]);
         (void)hipEventDestroy(g->caller_ev);
     }
-    for (ncclComm_t c : g->comm) (void)rccl().CommDestroy(c);
+    for (ncclComm_t c : g->comm) (void)g->r->CommDestroy(c);
     delete g;
     return GPAD_OK;
 }
@@ -258,13 +279,14 @@ int gpad_group_create(gpad_group_t* out, int ndev, const int* devices) {
     std::vector<int> sorted(g->dev);
     std::sort(sorted.begin(), sorted.end());
     const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
-    if (distinct && rccl().ok) {  // one RCCL clique, rank d on devices[d]
+    g->r = current_rccl();
+    if ((distinct || g->r->force) && g->r->ok) {  // one RCCL clique, rank d on devices[d]
         g->comm.assign(ndev, nullptr);
-        const ncclResult_t r = rccl().CommInitAll(g->comm.data(), ndev, g->dev.data());
+        const ncclResult_t r = g->r->CommInitAll(g->comm.data(), ndev, g->dev.data());
         if (r != ncclSuccess) {
             g->comm.clear();
             release(g);
-            return gfail(GPAD_ERR_HIP, std::string("ncclCommInitAll: ") + rccl().GetErrorString(r));
+            return gfail(GPAD_ERR_HIP, std::string("ncclCommInitAll: ") + g->r->GetErrorString(r));
         }
     }
     *out = g;
@@ -274,6 +296,19 @@ int gpad_group_create(gpad_group_t* out, int ndev, const int* devices) {
 int gpad_group_destroy(gpad_group_t g) {
     if (!g) return GPAD_OK;
     return release(g);
+}
+
+int gpad_group_rccl_library(const char* path, int force_rccl) {
+    auto r = load_rccl(path ? std::string(path) : std::string(), force_rccl != 0);
+    {
+        std::lock_guard<std::mutex> lk(g_rccl_mu);
+        g_rccl = r;
+        ++g_rccl_gen;
+    }
+    if (!r->ok)
+        return gfail(GPAD_ERR_UNSUPPORTED, std::string("gpad_group_rccl_library: cannot load the RCCL entry points from ") +
+                                               (path ? path : "librccl") + " (groups use peer copies)");
+    return GPAD_OK;
 }
 
 int gpad_group_transport(gpad_group_t g) {
@@ -454,6 +489,7 @@ namespace {
 struct ShardCache {
     gpad_group_t grp = nullptr;
     std::vector<int> devs;
+    unsigned rccl_gen = 0;  // the RCCL configuration the group was created under
 };
 thread_local ShardCache t_shard_cache;
 }  // namespace
@@ -472,12 +508,15 @@ int gpad_solve_sharded(int ndev, const int* devices, void* z0, void* y0, const v
     ShardCache& cache = t_shard_cache;
     if (ndev <= 0 || !devices) return gfail(GPAD_ERR_INVALID, "gpad_solve_sharded: bad device list");
     std::vector<int> want(devices, devices + ndev);
-    if (!cache.grp || cache.devs != want) {
+    unsigned gen = 0;
+    (void)current_rccl(&gen);
+    if (!cache.grp || cache.devs != want || cache.rccl_gen != gen) {
         if (cache.grp) gpad_group_destroy(cache.grp);
         cache.grp = nullptr;
         int rc = gpad_group_create(&cache.grp, ndev, devices);
         if (rc) return rc;
         cache.devs = want;
+        cache.rccl_gen = gen;
     }
     int rc = gpad_group_setup(cache.grp, dims, ML, G, L);
     if (rc) return rc;

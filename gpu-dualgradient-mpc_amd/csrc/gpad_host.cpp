@@ -12,8 +12,11 @@
 #include <cstdio>
 #include <cstddef>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "../../include/gpad.h"
@@ -150,6 +153,9 @@ struct gpad_handle_s {
     int last_N = 0;
     gpad::PanelPlan plan;
     unsigned long long plan_key = 0;    // fingerprint of the counts the plan was built from
+    gpad::PanelPlan prior;              // a handle without its own plan: the shape's last plan (plan_prior)
+    bool last_prior = false;            // the last run followed `prior`
+    gpad::PanelPlan last_phases;        // the phases the last phased panel solve launched (gpad_last_phases)
     int flat_vpred = 0;                 // flat panels: last iteration of the previous phased solve
     // asynchronous runs (no stats): the counts of each phased solve are copied to pinned host
     // memory behind it; the next run re-plans from them once that copy has landed, so a pipeline
@@ -223,7 +229,7 @@ static int status_error(gpad_handle_t h, const RunStatus& rs) {
 
 extern "C" {
 
-const char* gpad_version(void) { return "gpad-mi355x 0.4 (gfx950)"; }
+const char* gpad_version(void) { return "gpad-mi355x 0.5 (gfx950)"; }
 
 int gpad_device_count(void) {
     int count = 0;
@@ -352,8 +358,6 @@ int gpad_set_option(gpad_handle_t h, int option, int value) {
             t.p64_no_relay = 1 - on;
             return rc;
         }
-        case GPAD_OPT_PANEL_DATAFLOW: return set(t.panel_dataflow, 0, 7, def.panel_dataflow);
-        case GPAD_OPT_DUO_MAILBOX: return set(t.duo_mailbox, 0, 1, def.duo_mailbox);
         default: return fail(GPAD_ERR_INVALID, "gpad_set_option: unknown option");
     }
 }
@@ -627,6 +631,42 @@ static int ensure_schedule(gpad_handle_t h, int N, const void* theta_in, const v
     return GPAD_OK;
 }
 
+// Shape-keyed plan prior.  A handle plans a phased solve from its OWN previous
+// solve's counts, so its first solve ran the default schedule -- ~15 % slower on fresh C4 inputs
+// (3.86 vs 3.3-3.4 ms, a second handle's first solve in a warm process), which every new
+// gpad_solve caller thread paid once.  The last plan any handle of the process made is kept per
+// (n, m, batch, check_every, N, CUs, finisher threshold option), and a handle with no plan of its
+// own follows it.  A plan only moves launch boundaries and the finisher takeover (results are
+// bit-identical under any plan), so a stale prior costs time, never correctness.
+using PlanShape = std::tuple<int, int, int, int, int, int, int>;
+static std::mutex g_prior_mu;
+static std::map<PlanShape, gpad::PanelPlan>& prior_plans() {
+    static std::map<PlanShape, gpad::PanelPlan> m;
+    return m;
+}
+static PlanShape plan_shape(gpad_handle_t h, int batch, int N) {
+    return PlanShape{h->dims.n, h->dims.m, batch, h->dims.check_every, N, h->num_cus, h->tune.finish_thresh};
+}
+static void plan_prior_store(gpad_handle_t h, int batch, int N) {
+    if (h->plan.nph <= 0) return;
+    std::lock_guard<std::mutex> lk(g_prior_mu);
+    auto& m = prior_plans();
+    if (m.size() >= 64 && !m.count(plan_shape(h, batch, N))) m.clear();  // (bounded: a handful of shapes)
+    m[plan_shape(h, batch, N)] = h->plan;
+}
+// the plan a phased solve of this handle follows: its own, else the shape's prior (or none)
+static const gpad::PanelPlan* plan_for(gpad_handle_t h, int batch, int N) {
+    h->last_prior = false;
+    if (!h->tune.plan) return nullptr;
+    if (h->plan.nph > 0 && h->plan.N == N) return &h->plan;
+    std::lock_guard<std::mutex> lk(g_prior_mu);
+    auto it = prior_plans().find(plan_shape(h, batch, N));
+    if (it == prior_plans().end()) return nullptr;
+    h->prior = it->second;
+    h->last_prior = true;
+    return &h->prior;
+}
+
 // The phase plan is a pure function of the per-instance counts (and the shape): rebuild it only
 // when they changed (repeated solves of one batch skip the DP).
 static void update_plan(gpad_handle_t h, const int* counts, int batch, int N) {
@@ -642,6 +682,7 @@ static void update_plan(gpad_handle_t h, const int* counts, int batch, int N) {
         gpad::panel_plan(counts, batch, h->dims.n, h->dims.m, N, h->dims.check_every, h->num_cus, &h->tune,
                          &h->plan);
         h->plan_key = key;
+        plan_prior_store(h, batch, N);
     }
 }
 
@@ -712,6 +753,24 @@ int gpad_phase_plan(gpad_handle_t h, int* ends, int* fins, int cap, double* cost
     }
     if (cost_us) *cost_us = h->plan.cost_us;
     return n;
+}
+
+int gpad_last_phases(gpad_handle_t h, int* ends, int* fins, int* counts, int cap, int* prior) {
+    if (!h || cap < 0) return fail(GPAD_ERR_INVALID, "gpad_last_phases: bad argument");
+    if (prior) *prior = h->last_prior ? 1 : 0;
+    if (!h->last_phased || !h->pwork.p || h->flat) return 0;
+    const int k = std::min(cap, h->last_phases.nph);
+    for (int i = 0; i < k; ++i) {
+        if (ends) ends[i] = h->last_phases.ends[i];
+        if (fins) fins[i] = h->last_phases.fins[i];
+    }
+    if (counts && k > 0) {
+        HIP_TRY(hipSetDevice(h->device));
+        const int* dev = reinterpret_cast<const int*>(h->pwork.p) + 2 * (size_t)h->last_batch;  // panel_work_bytes
+        HIP_TRY(hipMemcpyAsync(counts, dev, sizeof(int) * (size_t)k, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+    }
+    return k;
 }
 
 int gpad_phase_counts(gpad_handle_t h, int* counts, int cap) {
@@ -889,13 +948,11 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
         const int panel_min = gpad::resident_supported(n, m) ? 4 * h->num_cus : 64;
         if (kernel == GPAD_KERNEL_PANEL || (kernel == GPAD_KERNEL_AUTO && d.shared && batch > panel_min)) {
             if (tol > 0.0 && h->frag_ok) {  // phased compaction workspace (gpad_panel.hip)
-                void* const before = h->pwork.p;
                 int rc = h->pwork.ensure(gpad::panel_work_bytes(m, batch));
                 if (rc) return rc;
-                if (h->pwork.p != before)  // a new buffer: no stale words that a finisher mailbox
-                    HIP_TRY(hipMemsetAsync(h->pwork.p, 0, h->pwork.bytes, h->stream));  // entry could read as tagged
                 a.pwork = h->pwork.p;
-                a.plan = &h->plan;
+                a.plan = plan_for(h, batch, N);
+                a.used = &h->last_phases;
                 // the previous phased solve's counts are still in `iters` for every instance this
                 // solve has not finished yet: the finisher orders its queue by them
                 if (prev_phased && h->last_batch == batch && h->last_steps == 1) a.pred = iters;

@@ -30,14 +30,11 @@ struct Tuning {
     int debug_drop_handoff = 0;  // GPAD_OPT_DEBUG_DROP_HANDOFF: test-only fault injection
     int p64_no_relay = 0;     // GPAD_OPT_P64_RELAY = 0: f64 panels without the relay layout
     int p64_no_refill = 0;    // GPAD_OPT_P64_REFILL = 0: f64 panels without column refills
-    int panel_dataflow = 0;   // GPAD_OPT_PANEL_DATAFLOW: bits 1 one-panel, 2 pairs, 4 one-panel tile order
-    int duo_mailbox = 0;      // GPAD_OPT_DUO_MAILBOX: drained finisher workgroups hand a slot to idle ones
 };
 
 // Device error word of a run (SolveArgs::err): kernels OR these bits in with a vector atomic;
 // the host turns a non-zero word into GPAD_ERR_DEVICE when it collects or syncs the run.
 constexpr int kDevErrHandoff = 1;  // a chain hand-off wait expired (gpad_panel.hip handoff_wait)
-constexpr int kMboxSlots = 1024;  // duo mailbox entries (one per donation; at most one per workgroup)
 // SolveArgs::debug bits (fault injection for tests; 0 in production)
 constexpr int kDebugDropHandoff = 1;  // the first hand-off helper skips its first post
 
@@ -112,6 +109,7 @@ struct SolveArgs {
     int n_u;               // flat battery path: cells (n = n_u * horizon), see gpad_flat.hip
     int flat_staged;       // flat path: matrices staged in LDS (set by launch_flat)
     const struct PanelPlan* plan;  // panel phases: host-side plan from the previous solve (or null)
+    struct PanelPlan* used;        // panel phases: host-side record of the phases launched (or null)
     const Tuning* tune;    // host-side tuning options (never null on a launch from gpad_host.cpp)
     const T* Hq;           // QP Hessian H, k-major [n][ldn] (gpad_setup_hessian), or null: enables the
                            // value-function branches of the test (stream kernel only)
@@ -120,9 +118,6 @@ struct SolveArgs {
                            // branches)
     int* err;              // device error word (kDevErr* bits), never null on a solve launch
     int debug;             // kDebug* fault-injection bits (tests only)
-    int dflow;             // gpad_panel2_kernel: dataflow GEMM boundaries (Tuning::panel_dataflow bits)
-    int* mbox;             // duo kernel: slot hand-off mailbox (gpad_duo.hip), or null; header zeroed
-    int mgen;              // ... this launch's tag of its mailbox entries (never 0, unique per launch)
 };
 
 // launchers (return hipError_t of the launch)

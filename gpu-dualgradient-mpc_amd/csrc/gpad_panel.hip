@@ -27,7 +27,6 @@
 // one float4 per lane per (block, tile): 1 KiB per wave-instruction, fully coalesced.
 #include <hip/hip_runtime.h>
 
-#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <type_traits>
@@ -420,7 +419,9 @@ __global__ __launch_bounds__(64 * T) void gpad_panel_kernel(SolveArgs<float> a) 
 // priority before the barriers of the solve loop and drops it right before its first MFMA of the
 // next GEMM: all waves get through their preludes and issue their first B reads right after the
 // barrier, and the chains then run oldest-first with their operands already in registers.
-#ifndef GPAD_NO_PRELUDE_PRIO
+// Invariant: a wave holds priority 2 only between a loop barrier and its next chain (or the point
+// where it learns it has none); every path out of that window -- a GEMM helper's prelude, the
+// no-GEMM branches of the tiles past the output rows, the loop exit -- drops it to 0.
 #define GPAD_PRELUDE_HI() __builtin_amdgcn_s_setprio(2)
 #define GPAD_PRELUDE_LO()                  \
     do {                                   \
@@ -428,67 +429,6 @@ __global__ __launch_bounds__(64 * T) void gpad_panel_kernel(SolveArgs<float> a) 
         __builtin_amdgcn_s_setprio(0);     \
         __builtin_amdgcn_sched_barrier(0); \
     } while (0)
-#else
-#define GPAD_PRELUDE_HI() \
-    do {                  \
-    } while (0)
-#define GPAD_PRELUDE_LO() \
-    do {                  \
-    } while (0)
-#endif
-
-// Dataflow across the GEMM boundaries (r05, SolveArgs::dflow).  Block kb of a chain reads row tile
-// kb of the other GEMM's output and nothing else of it, so a chain need not wait for the barrier
-// that closes the other GEMM: each (panel, row tile) of Zh / Wl carries the generation of the GEMM
-// that last wrote it (Panel2Lds::zf / wf, posted by the tile's owner after its epilogue's LDS writes
-// complete), and a chain polls the flags only when it reaches a block past the prefix it has seen
-// written.  Overwriting a tile is safe without a barrier: the owner's next chain needs every tile
-// of the other GEMM, and each of those was written after its own chain had read every tile of this
-// one.  The SIMDs then keep issuing while the last chains of a GEMM drain -- the barrier's cost in
-// the phase anatomy (profiles/r05_c3_anatomy.txt).  The ascending-k MFMA sequence of every chain
-// is unchanged, so results are bit-identical.  Barriers remain where the whole panel is read at
-// once: the test iterations, the phase ends, the seed and verification GEMMs.
-struct NoWait {
-    template <class... A>
-    __device__ __forceinline__ NoWait(A&&...) {}
-    __device__ __forceinline__ void operator()(int) const {}
-};
-struct DfWait {
-    __device__ __forceinline__ DfWait(const int* a, const int* b, int t, int nd, int r, int* e)
-        : f0(a), f1(b), nt(t), need(nd), rdy(r), err(e) {}
-    const int* f0;  // flags of the chain's panel (lanes 0..31 poll f0) and of a double wave's
-    const int* f1;  // second panel (lanes 32..63 poll f1; = f0 for one panel)
-    int nt;         // row tiles
-    int need;       // generation of the producing GEMM
-    int rdy;        // tiles [0, rdy) seen written (64 without dataflow: never polls)
-    int* err;       // an expired wait (bounded like handoff_wait) fails the run
-    __device__ __forceinline__ void operator()(int kb) {
-        if (kb < rdy) return;
-        const int lane = __lane_id(), l = lane & 31;
-        const int* f = lane < 32 ? f0 : f1;
-        for (int s = 0;; ++s) {
-            const int v = l < nt ? __hip_atomic_load(f + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : need;
-            const unsigned long long nr = __ballot(v - need < 0);
-            const unsigned lo = (unsigned)nr, hi = (unsigned)(nr >> 32);
-            const int p0 = lo ? __builtin_ctz(lo) : 32, p1 = hi ? __builtin_ctz(hi) : 32;
-            rdy = __builtin_amdgcn_readfirstlane(p0 < p1 ? p0 : p1);
-            if (kb < rdy) break;
-            if (s == (1 << 20)) {
-                *err = 1;
-                rdy = 64;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        asm volatile("" ::: "memory");  // the tile's reads stay after the flag that covers them
-    }
-};
-// the owner's post of its row tile(s) after the epilogue's LDS writes
-__device__ __forceinline__ void df_post(int* f, int stride, int cnt, int gen, int lane) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0)
-        for (int q = 0; q < cnt; ++q) __hip_atomic_store(f + q * stride, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 
 // ---------------------------------------------------------------------------------------
 // Panel pairs (8 < T <= 16): a 16-wave workgroup owns TWO panels, balanced over the SIMDs.
@@ -548,73 +488,21 @@ __device__ __forceinline__ void panel_a_prefetch(__amdgpu_buffer_rsrc_t PA, int 
 // panel_gemm2 with an A ring PD blocks deep, seeded by panel_a_prefetch.  The last k-block
 // issues only its first kq MFMA steps: k-steps past the matrix are zero in both operands, so
 // skipping them is exact (an accumulator started at +0 never holds -0).  kq is wave-uniform.
-template <int T, bool DUAL, int PD, class W = NoWait>
+template <int T, bool DUAL, int PD>
 __device__ __forceinline__ void panel_gemm3(__amdgpu_buffer_rsrc_t PA, const float4* B0, const float4* B1,
                                             int voff, int lane, f32x4& acc0, f32x4& acc1,
-                                            const float4 (&ap)[PD], int kq, W&& wt = W{}) {
+                                            const float4 (&ap)[PD], int kq) {
     acc0 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     acc1 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     constexpr int R = PD + 1;
     float4 a[R], b0[2], b1[2];
 #pragma unroll
     for (int p = 0; p < PD; ++p) a[p] = ap[p];
-    wt(0);
     b0[0] = B0[lane];
     if constexpr (DUAL) b1[0] = B1[lane];
-    wt(1);
     b0[1] = B0[64 + lane];  // (block 1 too, so the whole prelude precedes the priority drop)
     if constexpr (DUAL) b1[1] = B1[64 + lane];
     GPAD_PRELUDE_LO();
-#ifdef GPAD_ROLLED_GEMM
-    // experiment (r05): the T-1 full blocks as a loop unrolled by U (kb % R and kb & 1 static in
-    // every copy), loads clamped to the last block, then the last block -- a fraction of the
-    // fully unrolled code, to test the instruction-fetch cost of the 94 KB kernel
-    constexpr int U = R == 2 ? 2 : 6;
-#pragma unroll U
-    for (int kb = 0; kb < T - 1; ++kb) {
-        const int cur = kb & 1;
-        const float4 ak = a[kb % R];
-        a[(kb + PD) % R] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(
-            PA, voff, (kb + PD < T ? kb + PD : T - 1) * T * 1024, 0));
-        __builtin_amdgcn_sched_barrier(0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, b0[cur].x, acc0, 0, 0, 0);
-        if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, b1[cur].x, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, b0[cur].y, acc0, 0, 0, 0);
-        if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, b1[cur].y, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, b0[cur].z, acc0, 0, 0, 0);
-        if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, b1[cur].z, acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, b0[cur].w, acc0, 0, 0, 0);
-        if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, b1[cur].w, acc1, 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        const int kn = kb + 2 < T ? kb + 2 : T - 1;
-        b0[cur] = B0[kn * 64 + lane];
-        if constexpr (DUAL) b1[cur] = B1[kn * 64 + lane];
-        if constexpr (DUAL) asm volatile("" : "+v"(acc0), "+v"(acc1)::"memory");
-        else asm volatile("" : "+v"(acc0)::"memory");
-    }
-    {
-        constexpr int kb = T - 1, cur = kb & 1;
-        const float4 ak = a[kb % R];
-        __builtin_amdgcn_sched_barrier(0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, b0[cur].x, acc0, 0, 0, 0);
-        if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, b1[cur].x, acc1, 0, 0, 0);
-        if (kq > 1) {
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, b0[cur].y, acc0, 0, 0, 0);
-            if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, b1[cur].y, acc1, 0, 0, 0);
-        }
-        if (kq > 2) {
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, b0[cur].z, acc0, 0, 0, 0);
-            if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.z, b1[cur].z, acc1, 0, 0, 0);
-        }
-        if (kq > 3) {
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, b0[cur].w, acc0, 0, 0, 0);
-            if constexpr (DUAL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.w, b1[cur].w, acc1, 0, 0, 0);
-        }
-        if constexpr (DUAL) asm volatile("" : "+v"(acc0), "+v"(acc1)::"memory");
-        else asm volatile("" : "+v"(acc0)::"memory");
-    }
-    return;
-#endif
 #pragma unroll
     for (int kb = 0; kb < T; ++kb) {
         const int cur = kb & 1, nxt = cur ^ 1;
@@ -622,7 +510,6 @@ __device__ __forceinline__ void panel_gemm3(__amdgpu_buffer_rsrc_t PA, const flo
         if (kb + PD < T)
             a[(kb + PD) % R] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb + PD) * T * 1024, 0));
         if (kb >= 1 && kb + 1 < T) {  // (blocks 0 and 1 were read before the loop)
-            wt(kb + 1);
             b0[nxt] = B0[(kb + 1) * 64 + lane];
             if constexpr (DUAL) b1[nxt] = B1[(kb + 1) * 64 + lane];
         }
@@ -652,10 +539,10 @@ __device__ __forceinline__ void panel_gemm3(__amdgpu_buffer_rsrc_t PA, const flo
 // clamped to the last block), so each block's waitcnt counts only the loads issued after its
 // operands -- a rotated ring with conditional loads made the compiler drain both counters at
 // every block.  A is PD (1 or 2) blocks ahead, B one block ahead; soffset in an SGPR.
-template <int T, bool DUAL, int PD, class W = NoWait>
+template <int T, bool DUAL, int PD>
 __device__ __forceinline__ void panel_gemm_rt(__amdgpu_buffer_rsrc_t PA, const float4* B0, const float4* B1,
                                               int voff, int lane, f32x4& acc0, f32x4& acc1,
-                                              const float4 (&ap)[PD], int nkb, int kq, W&& wt = W{}) {
+                                              const float4 (&ap)[PD], int nkb, int kq) {
     constexpr int PR = PD > 2 ? 2 : PD;  // (deeper rings seed only their first two blocks here)
     acc0 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     acc1 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -682,20 +569,17 @@ __device__ __forceinline__ void panel_gemm_rt(__amdgpu_buffer_rsrc_t PA, const f
         __builtin_amdgcn_sched_barrier(0);
     };
     float4 a0 = ap[0], a1 = PR == 2 ? ap[1] : ap[0];
-    wt(0);
     float4 e0 = B0[lane], f0 = DUAL ? B1[lane] : e0, e1, f1;
     GPAD_PRELUDE_LO();
     for (int kb = 0;; kb += 2) {
         const int k1 = kb + 1 < last ? kb + 1 : last, k2 = kb + 2 < last ? kb + 2 : last;
         if constexpr (PR == 1) a1 = lda(kb + 1);
-        wt(k1);
         e1 = B0[k1 * 64 + lane];
         if constexpr (DUAL) f1 = B1[k1 * 64 + lane];
         blk(a0, e0, f0, kb < last ? 4 : kq);
         if constexpr (PR == 2) a0 = lda(kb + 2);
         if (kb + 1 > last) break;
         if constexpr (PR == 1) a0 = lda(kb + 2);
-        wt(k2);
         e0 = B0[k2 * 64 + lane];
         if constexpr (DUAL) f0 = B1[k2 * 64 + lane];
         blk(a1, e1, f1, kb + 1 < last ? 4 : kq);
@@ -708,14 +592,13 @@ __device__ __forceinline__ void panel_gemm_rt(__amdgpu_buffer_rsrc_t PA, const f
 
 // k-blocks [KB0, KB1) of one chain, continuing acc (not reset): the A ring PD blocks deep is
 // seeded with blocks KB0.. by panel_a_prefetch_from; the last matrix block issues kq steps.
-template <int T, int PD, int KB0, int KB1, bool LO = true, class W = NoWait>
+template <int T, int PD, int KB0, int KB1, bool LO = true>
 __device__ __forceinline__ void panel_chain(__amdgpu_buffer_rsrc_t PA, const float4* B0, int voff, int lane,
-                                            f32x4& acc, const float4 (&ap)[PD], int kq, W&& wt = W{}) {
+                                            f32x4& acc, const float4 (&ap)[PD], int kq) {
     constexpr int R = PD + 1;
     float4 a[R], b[2];
 #pragma unroll
     for (int p = 0; p < PD; ++p) a[p] = ap[p];
-    wt(KB0);
     b[0] = B0[KB0 * 64 + lane];
     if constexpr (LO) GPAD_PRELUDE_LO();  // (LO = false: a relay piece that runs at its own priority)
 #pragma unroll
@@ -724,10 +607,7 @@ __device__ __forceinline__ void panel_chain(__amdgpu_buffer_rsrc_t PA, const flo
         const float4 ak = a[i % R];
         if (kb + PD < KB1)
             a[(i + PD) % R] = as_float4(__builtin_amdgcn_raw_buffer_load_b128(PA, voff, (kb + PD) * T * 1024, 0));
-        if (kb + 1 < KB1) {
-            wt(kb + 1);
-            b[nxt] = B0[(kb + 1) * 64 + lane];
-        }
+        if (kb + 1 < KB1) b[nxt] = B0[(kb + 1) * 64 + lane];
         __builtin_amdgcn_sched_barrier(0);
         acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.x, b[cur].x, acc, 0, 0, 0);
         if (kb + 1 < T || kq > 1) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ak.y, b[cur].y, acc, 0, 0, 0);
@@ -819,10 +699,8 @@ struct Panel2Lds {
     float4 Gp[2][T * 64];  //                            g_P rows
     float4 Pd[2][T * 64];  //                            p_D rows
     PanelSlot2 slots[2][T];
-    float4 hand[6][64];    // hand-off accumulators: slot s of generation g at s + 3 (g & 1)
-    int hflag[6];          // hand-off generation per slot
-    int zf[2][16];         // dataflow (SolveArgs::dflow): generation of the GEMM that last wrote
-    int wf[2][16];         // Zh / Wl row tile t of panel p (zf: GEMM 1, wf: GEMM 2)
+    float4 hand[2][64];    // hand-off accumulators (the pair helpers' / the relay's slots)
+    int hflag[2];          // hand-off generation per slot
     int herr;              // a wait expired (handoff_wait): reported to the run's error word at exit
     int hdrop;             // fault injection (kDebugDropHandoff) for this workgroup
     int znz[16];           // per wave: a non-zero z_{-1} among its rows (fresh seed GEMM needed)
@@ -982,34 +860,28 @@ __device__ __forceinline__ void handoff_post(Panel2Lds<T>& L, int slot, int gen,
 // from slot hs.in (or from zero), parked in slot hs.out; PRIO raises the wave's issue priority
 // fault injection (DROP, the kernel's test-only instantiation; L.hdrop): the first piece of the
 // first hand-off withholds its post, so its receiver's wait expires
-// DF (dataflow): slot s of generation g is s + 3 (g & 1) -- a piece of the next GEMM may post
-// before this one is taken
-template <int T, int PD, int KB0, int KB1, bool PRIO, bool DROP, bool DF = false, class W>
+template <int T, int PD, int KB0, int KB1, bool PRIO, bool DROP>
 __device__ __forceinline__ void handoff_piece(Panel2Lds<T>& L, __amdgpu_buffer_rsrc_t PA, const float4* B0, int voff,
-                                              int lane, const float4 (&aph)[PD], HoSlots hs, int gen, W& wt,
+                                              int lane, const float4 (&aph)[PD], HoSlots hs, int gen,
                                               unsigned long long* ts = nullptr) {
     f32x4 h = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    if constexpr (DF) {
-        hs.in += hs.in >= 0 ? 3 * (gen & 1) : 0;
-        hs.out += 3 * (gen & 1);
-    }
     if (hs.in >= 0) h = handoff_wait(L, hs.in, gen, lane);
     if (ts) *ts = __builtin_amdgcn_s_memtime();  // (stamped builds only)
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
-    panel_chain<T, PD, KB0, KB1, !PRIO>(PA, B0, voff, lane, h, aph, 4, wt);
+    panel_chain<T, PD, KB0, KB1, !PRIO>(PA, B0, voff, lane, h, aph, 4);
     if (!(DROP && gen == 1 && hs.in < 0 && L.hdrop)) handoff_post(L, hs.out, gen, lane, h);
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
 // the chain's last piece on its owner: blocks [KB0, T) from slot hs.in
-template <int T, int PD, int KB0, bool PRIO, bool DF = false, class W>
+template <int T, int PD, int KB0, bool PRIO>
 __device__ __forceinline__ void handoff_take(Panel2Lds<T>& L, __amdgpu_buffer_rsrc_t PA, const float4* B0, int voff,
                                              int lane, const float4 (&ap)[PD], HoSlots hs, int gen, int kq,
-                                             f32x4& acc, W& wt, unsigned long long* ts = nullptr) {
-    acc = handoff_wait(L, hs.in + (DF ? 3 * (gen & 1) : 0), gen, lane);
+                                             f32x4& acc, unsigned long long* ts = nullptr) {
+    acc = handoff_wait(L, hs.in, gen, lane);
     if (ts) *ts = __builtin_amdgcn_s_memtime();  // (stamped builds only)
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(2);
-    panel_chain<T, PD, KB0, T, !PRIO>(PA, B0, voff, lane, acc, ap, kq, wt);
+    panel_chain<T, PD, KB0, T, !PRIO>(PA, B0, voff, lane, acc, ap, kq);
     if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
@@ -1021,8 +893,7 @@ __device__ __forceinline__ void handoff_take(Panel2Lds<T>& L, __amdgpu_buffer_rs
 // GEMMs (16 (T-1) < n, m <= 16 T) whose last k-block issues KQ steps in both: no runtime kq tests
 // (scalar branches whose conditions the compiler spilled to VGPR lanes) and no short-chain paths.
 // DROP: the fault-injection instantiation (handoff_piece).
-template <int T, int NU, int ROLE = 0, int KB0 = 0, int KB1 = 0, bool PRIO = false, int KQ = 0, bool DROP = false,
-          bool DF = false>
+template <int T, int NU, int ROLE = 0, int KB0 = 0, int KB1 = 0, bool PRIO = false, int KQ = 0, bool DROP = false>
 __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<T>& L, int t, int p0,
                                            bool pair, int items, int count, HoSlots hs = HoSlots{-1, -1}) {
     static_assert(ROLE == 0 || (Handoff<T>::on && (ROLE == 3 ? NU == 0 : NU == 1)), "hand-off roles");
@@ -1049,8 +920,6 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
     const bool on1 = FULL || 16 * t < n, on2 = FULL || 16 * t < m;
     const int voff_r = voff - 1024;  // helper: the receiver's tile t - 1 (Handoff)
     int hgen = 0;                    // hand-off generation, counted alike by helper and receiver
-    const bool df = DF && (a.dflow & (pair ? 2 : 1)) != 0;  // dataflow GEMM boundaries (DfWait)
-    using Wt = std::conditional_t<DF, DfWait, NoWait>;
     float gmx = 0.0f;                // max |g| over the rows this lane loads (gmax_part)
     // 16-B vector state I/O (rows4 / rows4_store) when every row start is 16-B aligned (uniform)
     const bool vec_io = ((n | m | (int)a.ld_gP | (int)a.ld_g) & 3) == 0 && n >= 4 && m >= 4 &&
@@ -1164,13 +1033,9 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
         }
         __syncthreads();
 
-#ifndef GPAD_PD_SINGLE
-#define GPAD_PD_SINGLE 2  // (experiment knob: A ring depth of single-chain waves)
-#endif
-#ifndef GPAD_PD_DOUBLE
-#define GPAD_PD_DOUBLE 1
-#endif
-        constexpr int PD = NU == 2 ? GPAD_PD_DOUBLE : (ROLE == 3 ? Handoff<T>::R1 : GPAD_PD_SINGLE);
+        // A ring depth: doubles 1 block ahead, singles 2 (deeper rings measured within noise,
+        // profiles/r05_a_ring_depth_ab.txt); a relay piece prefetches its whole first piece
+        constexpr int PD = NU == 2 ? 1 : (ROLE == 3 ? Handoff<T>::R1 : 2);
         float4 ap[PD];  // A blocks of the next GEMM, in flight across the barrier before it
         float4 aph[PD];  // helper / relay: the piece's first blocks
         auto prefetch = [&](__amdgpu_buffer_rsrc_t PA) {
@@ -1196,21 +1061,22 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             if constexpr (NU > 0) {
                 f32x4 acc[2];
                 ++hgen;
-                Wt wt(L.wf[p0], L.wf[NU == 2 ? 1 : p0], T, hgen - 1, df ? 0 : 64, &L.herr);
                 if constexpr (ROLE == 1)
-                    handoff_piece<T, PD, KB0, KB1, PRIO, DROP, DF>(L, PA1, L.Wl[p0], voff_r, lane, aph, hs, hgen, wt,
+                    handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA1, L.Wl[p0], voff_r, lane, aph, hs, hgen,
                                                                GPAD_STAMP_PTR(6));
                 if constexpr (ROLE == 2)
-                    handoff_take<T, PD, KB0, PRIO, DF>(L, PA1, L.Wl[p0], voff, lane, ap, hs, hgen, kq1, acc[0], wt,
+                    handoff_take<T, PD, KB0, PRIO>(L, PA1, L.Wl[p0], voff, lane, ap, hs, hgen, kq1, acc[0],
                                                    GPAD_STAMP_PTR(6));
                 else if (on1 && nkb1 == T)
                     panel_gemm3<T, NU == 2, PD>(PA1, L.Wl[p0], L.Wl[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1],
-                                                ap, kq1, wt);
+                                                ap, kq1);
                 else if (on1)
                     panel_gemm_rt<T, NU == 2, PD>(PA1, L.Wl[p0], L.Wl[NU == 2 ? 1 : p0], voff, lane, acc[0],
-                                                   acc[1], ap, nkb1, kq1, wt);
-                else
+                                                   acc[1], ap, nkb1, kq1);
+                else {
+                    GPAD_PRELUDE_LO();
                     acc[0] = acc[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+                }
                 GPAD_STAMP_AT(1);
                 prefetch(PA2);
                 float4 g4[Q];
@@ -1230,17 +1096,17 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                     z[q][2] = z1.x;
                     z[q][3] = z1.y;
                 }
-                if (df) df_post(&L.zf[p0][t], 16, Q, hgen, lane);
             } else if constexpr (ROLE == 3) {
                 ++hgen;
-                Wt wt(L.wf[p0], L.wf[p0], T, hgen - 1, df ? 0 : 64, &L.herr);
-                handoff_piece<T, PD, KB0, KB1, PRIO, DROP, DF>(L, PA1, L.Wl[p0], voff, lane, aph, hs, hgen, wt,
+                handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA1, L.Wl[p0], voff, lane, aph, hs, hgen,
                                                            GPAD_STAMP_PTR(6));
                 prefetch(PA2);
+            } else {
+                GPAD_PRELUDE_LO();  // (a wave with no chain: the window of the invariant ends here)
             }
             GPAD_STAMP_AT(2);
             GPAD_PRELUDE_HI();
-            if (!df) __syncthreads();
+            __syncthreads();
             GPAD_STAMP_AT(3);
             // ---- GEMM 2 + epilogue: y+ = [w + G_L zhat + p_D]+ (8d), next w (8a) ----------
             float violz[Q], violh[Q], wmin[Q], magh[Q];
@@ -1255,21 +1121,22 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             if constexpr (NU > 0) {
                 f32x4 acc[2];
                 ++hgen;
-                Wt wt(L.zf[p0], L.zf[NU == 2 ? 1 : p0], T, hgen - 1, df ? 0 : 64, &L.herr);
                 if constexpr (ROLE == 1)
-                    handoff_piece<T, PD, KB0, KB1, PRIO, DROP, DF>(L, PA2, L.Zh[p0], voff_r, lane, aph, hs, hgen, wt,
+                    handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA2, L.Zh[p0], voff_r, lane, aph, hs, hgen,
                                                                GPAD_STAMP_PTR(7));
                 if constexpr (ROLE == 2)
-                    handoff_take<T, PD, KB0, PRIO, DF>(L, PA2, L.Zh[p0], voff, lane, ap, hs, hgen, kq2, acc[0], wt,
+                    handoff_take<T, PD, KB0, PRIO>(L, PA2, L.Zh[p0], voff, lane, ap, hs, hgen, kq2, acc[0],
                                                    GPAD_STAMP_PTR(7));
                 else if (on2 && nkb2 == T)
                     panel_gemm3<T, NU == 2, PD>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, acc[0], acc[1],
-                                                ap, kq2, wt);
+                                                ap, kq2);
                 else if (on2)
                     panel_gemm_rt<T, NU == 2, PD>(PA2, L.Zh[p0], L.Zh[NU == 2 ? 1 : p0], voff, lane, acc[0],
-                                                   acc[1], ap, nkb2, kq2, wt);
-                else
+                                                   acc[1], ap, nkb2, kq2);
+                else {
+                    GPAD_PRELUDE_LO();
                     acc[0] = acc[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+                }
                 GPAD_STAMP_AT(4);
                 prefetch(PA1);
                 // (reading these LDS operands before the GEMM measured no faster: profiles/r02_epilogue_ab.txt)
@@ -1338,19 +1205,19 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                         }
                     }
                 }
-                if (df) df_post(&L.wf[p0][t], 16, Q, hgen, lane);
             } else if constexpr (ROLE == 3) {
                 ++hgen;
-                Wt wt(L.zf[p0], L.zf[p0], T, hgen - 1, df ? 0 : 64, &L.herr);
-                handoff_piece<T, PD, KB0, KB1, PRIO, DROP, DF>(L, PA2, L.Zh[p0], voff, lane, aph, hs, hgen, wt,
+                handoff_piece<T, PD, KB0, KB1, PRIO, DROP>(L, PA2, L.Zh[p0], voff, lane, aph, hs, hgen,
                                                            GPAD_STAMP_PTR(7));
                 prefetch(PA1);
+            } else {
+                GPAD_PRELUDE_LO();
             }
             th = th_next;
             bn = bn_next;
             GPAD_STAMP_AT(5);
             GPAD_PRELUDE_HI();
-            if (!df || chk || v >= a.v_end) __syncthreads();
+            __syncthreads();
             GPAD_STAMP_FLUSH();
             if (!chk && v < a.v_end) continue;
 
@@ -1465,6 +1332,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             if (v >= N) live = 0u;
             if (v >= a.v_end || live == 0u) break;
         }
+        GPAD_PRELUDE_LO();  // (the loop's last barrier left every wave at priority 2)
         // ---- phase end: park the survivors -----------------------------------------------
         GPAD_PSTAMP(3);
         if constexpr (NU > 0) {
@@ -1512,7 +1380,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
 // (6.16 vs 5.98 us per iteration at 4 panels, profiles/r03_single_mode_ab.txt).  DROP: the
 // test-only fault-injection instantiation (GPAD_OPT_DEBUG_DROP_HANDOFF), launched instead of the
 // product kernel only while that option is set, so the product kernel carries no trace of it.
-template <int T, int KQ, bool DROP = false, bool DF = false>
+template <int T, int KQ, bool DROP = false>
 __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
     static_assert(T > 8 && T <= 16, "panel pairs need 8 < T <= 16");
     constexpr int D = 2 * T - 16;  // double waves
@@ -1537,10 +1405,6 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
     const bool ho = Handoff<T>::on && (KQ > 0 || (16 * (T - 1) < a.n && 16 * (T - 1) < a.m &&
                                                   (a.m + 15) / 16 == T && (a.n + 15) / 16 == T));
     if (threadIdx.x < 6) L.hflag[threadIdx.x] = 0;
-    if (threadIdx.x < 32) {
-        (&L.zf[0][0])[threadIdx.x] = 0;
-        (&L.wf[0][0])[threadIdx.x] = 0;
-    }
     if (threadIdx.x == 0) {
         L.herr = 0;
         L.hdrop = DROP && blockIdx.x == 0;  // tests: workgroup 0 drops one post
@@ -1550,36 +1414,36 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
     if constexpr (Handoff<T>::on) {
         using H = Handoff<T>;
         if (pair) {  // waves 12, 13 (SIMDs 0, 1; tile T-2) receive from 14, 15 (SIMDs 2, 3; tile T-1)
-            if (w < D) panel2_run<T, 2, 0, 0, 0, false, KQ, DROP, DF>(a, L, w, 0, true, items, count);
+            if (w < D) panel2_run<T, 2, 0, 0, 0, false, KQ, DROP>(a, L, w, 0, true, items, count);
             else if (ho && w >= 14)
-                panel2_run<T, 1, 1, 0, H::S, false, KQ, DROP, DF>(a, L, T - 1, w & 1, true, items, count, HoSlots{-1, w & 1});
+                panel2_run<T, 1, 1, 0, H::S, false, KQ, DROP>(a, L, T - 1, w & 1, true, items, count, HoSlots{-1, w & 1});
             else if (ho && w >= 12)
-                panel2_run<T, 1, 2, H::S, 0, false, KQ, DROP, DF>(a, L, T - 2, w & 1, true, items, count, HoSlots{w & 1, -1});
-            else panel2_run<T, 1, 0, 0, 0, false, KQ, DROP, DF>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
+                panel2_run<T, 1, 2, H::S, 0, false, KQ, DROP>(a, L, T - 2, w & 1, true, items, count, HoSlots{w & 1, -1});
+            else panel2_run<T, 1, 0, 0, 0, false, KQ, DROP>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
         } else {  // tile T-1 as a relay: waves T -> T+1 -> T-1
             if constexpr (!H::relay) {
-                if (w < T) panel2_run<T, 1, 0, 0, 0, false, 0, DROP, DF>(a, L, w, 0, false, items, count);
-                else panel2_run<T, 0, 0, 0, 0, false, 0, DROP, DF>(a, L, 0, 0, false, items, count);
-            } else if (ho && w == T - 1) panel2_run<T, 1, 2, H::R2, 0, true, 0, DROP, DF>(a, L, w, 0, false, items, count, HoSlots{1, -1});
+                if (w < T) panel2_run<T, 1, 0, 0, 0, false, 0, DROP>(a, L, w, 0, false, items, count);
+                else panel2_run<T, 0, 0, 0, 0, false, 0, DROP>(a, L, 0, 0, false, items, count);
+            } else if (ho && w == T - 1) panel2_run<T, 1, 2, H::R2, 0, true, 0, DROP>(a, L, w, 0, false, items, count, HoSlots{1, -1});
             else if (ho && w == T)
-                panel2_run<T, 0, 3, 0, H::R1, true, 0, DROP, DF>(a, L, T - 1, 0, false, items, count, HoSlots{-1, 0});
+                panel2_run<T, 0, 3, 0, H::R1, true, 0, DROP>(a, L, T - 1, 0, false, items, count, HoSlots{-1, 0});
             else if (ho && w == T + 1)
-                panel2_run<T, 0, 3, H::R1, H::R2, true, 0, DROP, DF>(a, L, T - 1, 0, false, items, count, HoSlots{0, 1});
-            else if (w < T)  // (dflow bit 4: tiles 0..T-2 dealt oldest wave first, so they are written in order)
-                panel2_run<T, 1, 0, 0, 0, false, 0, DROP, DF>(a, L, (DF && (a.dflow & 4)) ? T - 2 - w : w, 0, false, items, count);
-            else panel2_run<T, 0, 0, 0, 0, false, 0, DROP, DF>(a, L, 0, 0, false, items, count);
+                panel2_run<T, 0, 3, H::R1, H::R2, true, 0, DROP>(a, L, T - 1, 0, false, items, count, HoSlots{0, 1});
+            else if (w < T)
+                panel2_run<T, 1, 0, 0, 0, false, 0, DROP>(a, L, w, 0, false, items, count);
+            else panel2_run<T, 0, 0, 0, 0, false, 0, DROP>(a, L, 0, 0, false, items, count);
         }
     } else if (pair) {
-        if (w < D) panel2_run<T, 2, 0, 0, 0, false, KQ, DROP, DF>(a, L, w, 0, true, items, count);
-        else panel2_run<T, 1, 0, 0, 0, false, KQ, DROP, DF>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
+        if (w < D) panel2_run<T, 2, 0, 0, 0, false, KQ, DROP>(a, L, w, 0, true, items, count);
+        else panel2_run<T, 1, 0, 0, 0, false, KQ, DROP>(a, L, D + ((w - D) >> 1), (w - D) & 1, true, items, count);
     } else {
-        if (w < T) panel2_run<T, 1, 0, 0, 0, false, 0, DROP, DF>(a, L, w, 0, false, items, count);
-        else panel2_run<T, 0, 0, 0, 0, false, 0, DROP, DF>(a, L, 0, 0, false, items, count);
+        if (w < T) panel2_run<T, 1, 0, 0, 0, false, 0, DROP>(a, L, w, 0, false, items, count);
+        else panel2_run<T, 0, 0, 0, 0, false, 0, DROP>(a, L, 0, 0, false, items, count);
     }
-    if (Handoff<T>::on || a.gmax_part || DF) {
+    if (Handoff<T>::on || a.gmax_part) {
         __syncthreads();
         // an expired hand-off or dataflow wait fails the run (GPAD_ERR_DEVICE)
-        if ((Handoff<T>::on || DF) && threadIdx.x == 0 && L.herr) atomicOr(a.err, kDevErrHandoff);
+        if (Handoff<T>::on && threadIdx.x == 0 && L.herr) atomicOr(a.err, kDevErrHandoff);
         if (a.gmax_part && threadIdx.x == 0) {  // the run's max |g|: this workgroup's slot
             float g = 0.0f;
             for (int i = 0; i < 16; ++i) g = absmax_nan(g, L.gred[i]);
@@ -1635,16 +1499,9 @@ struct PlanModel {
     int T, n, m, num_cus, grid;
     bool handoff;  // gpad_panel2_kernel's hand-off shapes (Handoff)
     bool relay;    // ... and its one-panel relay (T = 9, 13)
-#ifndef GPAD_PLAN_TLAUNCH
-#define GPAD_PLAN_TLAUNCH 5.0
-#endif
-#ifndef GPAD_PLAN_TLAT
-#define GPAD_PLAN_TLAT 1.4
-#endif
-#ifndef GPAD_PLAN_CARRY_BW
-#define GPAD_PLAN_CARRY_BW 5e6
-#endif
-    double t_chain, t_res, t_launch = GPAD_PLAN_TLAUNCH;
+    static constexpr double kTLat = 1.4;        // finisher latency factor over t_res (two per CU)
+    static constexpr double kCarryBw = 5e6;     // carried state, bytes per us
+    double t_chain, t_res, t_launch = 5.0;
     double iter_time(long long panels) const {
         if (panels <= 0) return 0.0;
         double chains;
@@ -1671,10 +1528,10 @@ struct PlanModel {
     }
     double phase(int v0, int v1, long long s0) const {
         const double it = iter_time((s0 + 15) / 16);
-        return 2 * t_launch + (v1 - v0 + 1) * it + (double)s0 * 16.0 * (n + m) / GPAD_PLAN_CARRY_BW;
+        return 2 * t_launch + (v1 - v0 + 1) * it + (double)s0 * 16.0 * (n + m) / kCarryBw;
     }
     double finisher(int longest, long long work) const {
-        const double lat = longest * GPAD_PLAN_TLAT * t_res;
+        const double lat = longest * kTLat * t_res;
         const double thr = (double)work * 1.1 * t_res / num_cus;
         return 2 * t_launch + (lat > thr ? lat : thr);
     }
@@ -1785,10 +1642,10 @@ int panel_plan(const int* iters, int batch, int n, int m, int N, int check_every
 
 size_t panel_work_bytes(int m, int batch) {
     // idx ping-pong [2][batch] | phase counts [kPanelMaxPhases] | finisher queue counters
-    // [kPanelMaxPhases] | duo mailbox: header [4], entries [kMboxSlots][4] | carried w, u
+    // [kPanelMaxPhases] | carried w, u
     // [batch][m] each | per-panel survivor lists: seg_idx [batch + 32], seg_cnt [batch / 16 + 2]
     // (list_survivors)
-    return sizeof(int) * (2 * (size_t)batch + 2 * kPanelMaxPhases + 4 + 4 * (size_t)kMboxSlots) +
+    return sizeof(int) * (2 * (size_t)batch + 2 * kPanelMaxPhases) +
            2 * sizeof(float) * (size_t)batch * m +
            sizeof(int) * ((size_t)batch + 32 + (size_t)batch / 16 + 2);
 }
@@ -1949,10 +1806,6 @@ static void launch_panel_kernel(const SolveArgs<float>& a, int grid, hipStream_t
                 else hipLaunchKernelGGL((gpad_panel2_kernel<T, 0, true>), dim3(grid), dim3(1024), 0, s, a);
                 return;
             }
-            if (a.dflow) {  // the opt-in dataflow boundaries (runtime chain shape)
-                hipLaunchKernelGGL((gpad_panel2_kernel<T, 0, false, true>), dim3(grid), dim3(1024), 0, s, a);
-                return;
-            }
             if (full && kq1 == 1) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 1>), dim3(grid), dim3(1024), 0, s, a); return; }
             if (full && kq1 == 2) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 2>), dim3(grid), dim3(1024), 0, s, a); return; }
             if (full && kq1 == 3) { hipLaunchKernelGGL((gpad_panel2_kernel<T, 3>), dim3(grid), dim3(1024), 0, s, a); return; }
@@ -1973,7 +1826,6 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     int grid = panels < resident ? panels : resident;
     const Tuning tn = a.tune ? *a.tune : Tuning{};
     if (tn.panel_max_grid > 0 && tn.panel_max_grid < grid) grid = tn.panel_max_grid;  // grid-stride panels
-    a.dflow = T == 13 ? tn.panel_dataflow : 0;  // (instantiated for the C3 / C4 tiling only)
     const bool phased = a.tol > 0.0 && a.pwork != nullptr && tn.phased;
     a.fin_thresh = phased ? panel_fin_thresh(a.n, a.m, a.num_cus, &tn) : 0;
     if (!phased) {  // fixed N (or no workspace): one phase, nothing carried
@@ -1988,8 +1840,7 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     int* idx1 = idx0 + a.batch;
     int* counts = idx1 + a.batch;
     int* qctrs = counts + kPanelMaxPhases;
-    int* mbox = qctrs + kPanelMaxPhases;  // (header zeroed with the counters; entries tagged by mgen)
-    float* wc = reinterpret_cast<float*>(mbox + 4 + 4 * kMboxSlots);
+    float* wc = reinterpret_cast<float*>(qctrs + kPanelMaxPhases);
     a.wc = wc;
     a.uc = wc + (size_t)a.batch * a.m;
     // survivors listed per panel, densified at each boundary by phase_compact_kernel (one idx
@@ -1998,21 +1849,19 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     a.seg_cnt = a.seg_idx + a.batch + 32;
     a.idx_out = nullptr;
     a.count_out = nullptr;
-    // the phase counters and queue counters; with the mailbox its header and entries too (one memset)
-    hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * (2 * kPanelMaxPhases + 4 + (tn.duo_mailbox ? 4 * kMboxSlots : 0)), s);
+    // the phase counters and the finisher's queue counters (one memset)
+    hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * 2 * kPanelMaxPhases, s);
     if (e != hipSuccess) return e;
-    if (tn.duo_mailbox) {
-        // entries zeroed with the counters above; the tag (a quiet-NaN bit pattern, per launch) and
-        // -tag (a cancelled entry) are never 0
-        static std::atomic<unsigned> gen{0};
-        a.mbox = mbox;
-        a.mgen = (int)(0x7FC00001u + gen.fetch_add(1) % 0x3FFFFEu);
-    }
     // phase length: a multiple of the test period (phases end right after a test); default
     // four tests, doubling after 10 phases so a long tail costs O(log N) launches (a phase with
     // no survivors left costs one empty launch, ~5 us)
     const int len = panel_phase_len(a.check_every, &tn);
     const PanelPlan* plan = (a.plan && a.plan->nph > 0 && a.plan->N == a.N) ? a.plan : nullptr;
+    if (a.used) {
+        a.used->nph = 0;
+        a.used->N = a.N;
+        a.used->cost_us = plan ? plan->cost_us : 0.0;
+    }
     const int fin_default = a.fin_thresh;
     int fin_prev = 0;  // the previous phase's finisher threshold
     int v0 = 0;
@@ -2037,6 +1886,11 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
             if (e != hipSuccess) return e;
         }
         fin_prev = a.fin_thresh;
+        if (a.used && ph < kPanelMaxPhases) {  // (diagnostics: gpad_last_phases)
+            a.used->ends[ph] = v1;
+            a.used->fins[ph] = ph ? a.fin_thresh : 0;
+            a.used->nph = ph + 1;
+        }
         if (ph && a.fin_thresh) {  // few survivors left: the duo finisher takes them, runs to N --
             // two instances per CU in ping-pong, fed from the survivor list
             a.qctr = qctrs + ph;

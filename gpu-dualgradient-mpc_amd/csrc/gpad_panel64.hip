@@ -30,6 +30,8 @@
 // order, the oracle sequentially (the same values to ~1e-16 relative).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <cmath>
 
 #include "gpad_internal.h"
@@ -611,31 +613,41 @@ hipError_t launch_pack_panel64(const double* src, int rows, int cols, double sca
     return hipGetLastError();
 }
 
-// Workgroups per CU the kernel's registers and LDS allow (hipOccupancy..., cached per
-// instantiation): a persistent grid of num_cus x that, so small tile counts fill the CU with
-// several panels (num_cus workgroups of T waves left T <= 4 at 1-4 waves per CU).
-template <int T, bool RELAY>
+// Workgroups per CU the kernel's registers and LDS allow (hipOccupancy...): a persistent grid of
+// num_cus x that, so small tile counts fill the CU with several panels (num_cus
+// workgroups of T waves left T <= 4 at 1-4 waves per CU).  Cached per instantiation and per device
+// (the group API drives several devices from one process; concurrent host threads may race on a
+// slot, but every writer stores the same value, atomically).
+constexpr int kP64OccDevices = 64;
+template <int T, bool RELAY, bool REFILL>
 int p64_per_cu() {
-    static int occ = 0;
-    if (!occ) {
-        int o = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, gpad_panel64_kernel<T, RELAY, true>, RELAY ? 1024 : 64 * T,
-                                                         0) != hipSuccess ||
-            o < 1)
-            o = 1;
-        occ = o;
+    static std::atomic<int> occ[kP64OccDevices];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    const bool cached = dev >= 0 && dev < kP64OccDevices;
+    if (cached) {
+        const int o = occ[dev].load(std::memory_order_relaxed);
+        if (o) return o;
     }
-    return occ;
+    int o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, gpad_panel64_kernel<T, RELAY, REFILL>, RELAY ? 1024 : 64 * T,
+                                                     0) != hipSuccess ||
+        o < 1)
+        o = 1;
+    if (cached) occ[dev].store(o, std::memory_order_relaxed);
+    return o;
 }
 
 template <int T, bool RELAY>
 hipError_t launch_p64(const SolveArgs<double>& a, hipStream_t s) {
     const int panels = (a.batch + 15) / 16;
-    const int cap = a.num_cus * p64_per_cu<T, RELAY>();
-    const int grid = panels < cap ? panels : cap;
     const int K = a.check_every > 0 ? a.check_every : 1;
-    // refills need a counter, a tolerance, N on a test event, and more panels than workgroups
-    const bool refill = a.qctr && a.tol > 0.0 && a.N % K == 0 && panels > grid && !(a.tune && a.tune->p64_no_refill);
+    // refills need a counter, a tolerance, N on a test event, and more panels than workgroups (the
+    // grid of the refill instantiation decides; its occupancy is then that of the kernel launched)
+    const int cap_r = a.num_cus * p64_per_cu<T, RELAY, true>();
+    const bool refill = a.qctr && a.tol > 0.0 && a.N % K == 0 && panels > cap_r && !(a.tune && a.tune->p64_no_refill);
+    const int cap = refill ? cap_r : a.num_cus * p64_per_cu<T, RELAY, false>();
+    const int grid = panels < cap ? panels : cap;
     if (refill) {
         hipError_t e = hipMemsetAsync(a.qctr, 0, sizeof(int), s);
         if (e != hipSuccess) return e;

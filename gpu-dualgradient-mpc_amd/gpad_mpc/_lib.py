@@ -12,7 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libgpad.so")
 
-VERSION_MAJOR, VERSION_MINOR = 0, 4  # include/gpad.h GPAD_VERSION_*: the layouts this binding declares
+VERSION_MAJOR, VERSION_MINOR = 0, 5  # include/gpad.h GPAD_VERSION_*: the layouts this binding declares
 GPAD_OK = 0
 ERR_INVALID, ERR_HIP, ERR_NOMEM, ERR_UNSUPPORTED, ERR_NOT_SETUP, ERR_NO_DEVICE = -1, -2, -3, -4, -5, -6
 ERR_DEVICE = -7  # a kernel reported a device-side failure (include/gpad.h)
@@ -38,7 +38,8 @@ EXPORTS = [
     "gpad_accumulate_iterations", "gpad_set_option",
     "gpad_group_create", "gpad_group_destroy", "gpad_group_transport", "gpad_group_setup", "gpad_group_run",
     "gpad_solve_sharded", "gpad_device_count", "gpad_group_set_stream",
-    "gpad_setup_hessian", "gpad_release_cached", "gpad_phase_counts",
+    "gpad_setup_hessian", "gpad_release_cached", "gpad_phase_counts", "gpad_last_phases",
+    "gpad_group_rccl_library",
 ]
 GROUP_RCCL, GROUP_PEER = 1, 2
 
@@ -50,19 +51,17 @@ OPT_FLAT_WAVES, OPT_FLAT_A_LDS = 11, 12
 OPT_DEBUG_DROP_HANDOFF = 16  # test-only fault injection
 OPT_P64_RELAY = 18  # f64 panels: 16-wave relay layout at T = 9, 13 (default 1)
 OPT_P64_REFILL = 19  # f64 panels: refill finished columns from the batch (default 1)
-OPT_PANEL_DATAFLOW = 20  # f32 panels: dataflow GEMM boundaries, bits 1 one-panel, 2 pairs, 4 tile order
-OPT_DUO_MAILBOX = 21  # finisher: drained workgroups hand a live instance to idle ones (default 0)
-OPT_RETIRED = (5, 13, 14, 15, 17)  # finisher kind, solo finisher workgroups, plan finisher cost (0.3);
-# condensed panels (0.4, with the condensed operator); 17: the opt-in pair layouts measured in round 4
-# and left out of the product (W32, TailPair)
+OPT_RETIRED = (5, 13, 14, 15, 17, 20, 21)  # finisher kind, solo finisher workgroups, plan finisher cost
+# (0.3); condensed panels (0.4, with the condensed operator); 17: the opt-in pair layouts measured in
+# round 4 and left out of the product (W32, TailPair); 20, 21: the panel dataflow boundaries and the
+# finisher mailbox measured in round 5 and removed in 0.5
 OPTIONS = {"phase_len": OPT_PHASE_LEN, "finish_thresh": OPT_FINISH_THRESH, "plan": OPT_PLAN,
            "phased": OPT_PHASED, "lpt": OPT_LPT,
            "panel_max_grid": OPT_PANEL_MAX_GRID, "duo_max_grid": OPT_DUO_MAX_GRID,
            "flat_panel_min": OPT_FLAT_PANEL_MIN, "flat_panels": OPT_FLAT_PANELS,
            "flat_waves": OPT_FLAT_WAVES, "flat_a_lds": OPT_FLAT_A_LDS,
            "debug_drop_handoff": OPT_DEBUG_DROP_HANDOFF, "p64_relay": OPT_P64_RELAY,
-           "p64_refill": OPT_P64_REFILL, "panel_dataflow": OPT_PANEL_DATAFLOW,
-           "duo_mailbox": OPT_DUO_MAILBOX}
+           "p64_refill": OPT_P64_REFILL}
 
 FILE_ROWMAJOR, FILE_FLIPPED, FILE_FLAT = 0, 1, 2
 
@@ -201,6 +200,12 @@ def load(path: str | None = None) -> C.CDLL:
         getattr(L, name).restype = i
     L.gpad_phase_counts.argtypes = [vp, ip, i]
     L.gpad_phase_counts.restype = i
+    if hasattr(L, "gpad_group_rccl_library"):  # (0.5)
+        L.gpad_group_rccl_library.argtypes = [C.c_char_p, i]
+        L.gpad_group_rccl_library.restype = i
+    if hasattr(L, "gpad_last_phases"):  # (0.5)
+        L.gpad_last_phases.argtypes = [vp, ip, ip, ip, i, ip]
+        L.gpad_last_phases.restype = i
     if hasattr(L, "gpad_release_cached"):
         L.gpad_release_cached.argtypes = []
         L.gpad_release_cached.restype = None

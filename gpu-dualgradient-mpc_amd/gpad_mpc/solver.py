@@ -68,6 +68,24 @@ class GpadSolver:
         self._device = device
         self.dims = None
 
+    def last_phases(self) -> dict:
+        """The phases the last phased panel solve launched (include/gpad.h gpad_last_phases): ends,
+        finisher thresholds, survivors after each phase, whether the shape's plan prior was followed,
+        and the finisher takeover (the first phase whose input the finisher took, its start
+        iteration; None when the panels ran the whole solve)."""
+        cap = 64
+        ends, fins, counts = (C.c_int * cap)(), (C.c_int * cap)(), (C.c_int * cap)()
+        prior = C.c_int(0)
+        n = self.lib.gpad_last_phases(self.h, ends, fins, counts, cap, C.byref(prior))
+        check(min(n, 0), "gpad_last_phases")
+        e, f, c = list(ends[:n]), list(fins[:n]), list(counts[:n])
+        take = None
+        for ph in range(1, n):
+            if f[ph] > 0 and c[ph - 1] <= f[ph]:
+                take = dict(phase=ph, iteration=e[ph - 1], survivors=c[ph - 1])
+                break
+        return dict(ends=e, fins=f, counts=c, prior=bool(prior.value), takeover=take)
+
     @staticmethod
     def _torch_device_ready() -> bool:
         try:

@@ -26,10 +26,11 @@ extern "C" {
 #endif
 
 #define GPAD_VERSION_MAJOR 0
-#define GPAD_VERSION_MINOR 4 /* 0.3: gpad_stats_t gained tol_floor / flags, gpad_dims_t an explicit reserved
+#define GPAD_VERSION_MINOR 5 /* 0.3: gpad_stats_t gained tol_floor / flags, gpad_dims_t an explicit reserved
                               * word (layouts changed: rebuild callers against this header);
                               * 0.4: the condensed operator (kernel 5, option 14) removed, the device
-                              * error word sticky until reported; layouts as in 0.3 */
+                              * error word sticky until reported; layouts as in 0.3;
+                              * 0.5: options 20, 21 removed; layouts as in 0.3 */
 
 /* status codes */
 #define GPAD_OK 0
@@ -288,6 +289,14 @@ int gpad_phase_plan(gpad_handle_t h, int* ends, int* fins, int cap, double* cost
  * (synchronises the handle's stream).  Returns the number written, 0 when the last run was not a
  * phased panel solve. */
 int gpad_phase_counts(gpad_handle_t h, int* counts, int cap);
+/* Diagnostics: the phases the last phased panel solve of this handle actually launched -- ends[ph]
+ * (iterations), fins[ph] (the finisher threshold at the start of phase ph: the finisher takes phase
+ * ph's list when counts[ph - 1] <= fins[ph]; 0 = none) and counts[ph] (survivors after phase ph, as
+ * gpad_phase_counts) -- for up to cap phases (any array may be NULL; counts synchronises the stream);
+ * *prior (may be NULL) = 1 when the solve followed the shape's plan prior (a handle without a plan
+ * of its own: gpad_run).  Returns the number of phases written, 0 when the last run was not a phased
+ * panel solve. */
+int gpad_last_phases(gpad_handle_t h, int* ends, int* fins, int* counts, int cap, int* prior);
 /* The planner itself on given iteration counts (host only, no device work; for tests/tools). */
 int gpad_plan_phases(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus,
                      int* ends, int* fins, int cap, double* cost_us);
@@ -321,6 +330,14 @@ typedef struct gpad_group_s* gpad_group_t;
 int gpad_group_create(gpad_group_t* g, int ndev, const int* devices);
 int gpad_group_destroy(gpad_group_t g);
 int gpad_group_transport(gpad_group_t g); /* GPAD_GROUP_RCCL or GPAD_GROUP_PEER */
+/* Integration / test hook: groups created after this call (gpad_group_create, gpad_solve_sharded)
+ * take their RCCL entry points (ncclCommInitAll, ncclCommDestroy, ncclGroupStart / End, ncclSend,
+ * ncclRecv, ncclBroadcast, ncclGetErrorString) from the shared library at `path` (NULL: the default
+ * librccl).  force_rccl != 0: they use the RCCL transport even when a device is listed twice (for a
+ * library that accepts it -- real RCCL refuses duplicate devices, so the group creation then fails).
+ * Returns GPAD_OK, or GPAD_ERR_UNSUPPORTED when the library or one of the symbols cannot be loaded;
+ * such groups then use the peer copies.  Existing groups keep the library they were created with. */
+int gpad_group_rccl_library(const char* path, int force_rccl);
 /* Device memory: the stream of devices[0] on which the caller produces / consumes the buffers it
  * passes (NULL, the default: the null stream).  Setup and run first make every device stream of
  * the group wait for the work queued on it so far; runs are synchronous, so the results are
@@ -378,8 +395,10 @@ int gpad_schedule(int N, int kind, double* theta, double* beta);
                                     * panels: from 4 panels per CU), 2: always, 0: one launch       */
 /* 5 (finisher kind), 13 (solo finisher workgroups), 15 (plan finisher cost): retired in 0.3 after
  * measuring no gain; 14 (condensed panels): removed with the condensed operator in
- * 0.4; 17: the round-4 pair layouts (W32, TailPair) measured slower and left out of 0.4; setting
- * them returns GPAD_ERR_INVALID                                                                  */
+ * 0.4; 17: the round-4 pair layouts (W32, TailPair) measured slower and left out of 0.4; 20 (panel
+ * dataflow GEMM boundaries, 2-4 % slower) and 21 (finisher slot hand-off mailbox, even at the step
+ * level): built and measured in round 5, removed in 0.5; setting any of them
+ * returns GPAD_ERR_INVALID                                                                       */
 #define GPAD_OPT_LPT 6             /* 1: longest-predicted-first finisher queue (default)          */
 #define GPAD_OPT_PANEL_MAX_GRID 7  /* cap on the panel grid, workgroups (0 = none, default)        */
 #define GPAD_OPT_DUO_MAX_GRID 8    /* cap on the finisher grid (0 = none, default)                 */
@@ -398,14 +417,6 @@ int gpad_schedule(int N, int kind, double* theta, double* beta);
 #define GPAD_OPT_P64_REFILL 19     /* 1: f64 panel solves with tol > 0, N a multiple of check_every and
                                     * more panels than workgroups refill a finished column with the
                                     * next instance (default); 0: each panel runs to its slowest column */
-#define GPAD_OPT_PANEL_DATAFLOW 20 /* f32 panels, n, m in (192, 208]: bits 1 / 2 let the one-panel /
-                                    * pair layout's chains start on the other GEMM's row tiles as they
-                                    * are written instead of after a barrier (bit-identical results);
-                                    * bit 4: one-panel row tiles dealt oldest wave first */
-#define GPAD_OPT_DUO_MAILBOX 21    /* 1: once its queue is drained, a finisher workgroup with two live
-                                    * instances hands one, at its iteration boundary, to a workgroup
-                                    * with none (bit-identical results; n, m in (192, 200], the C3 / C4
-                                    * rows); 0 (default): never */
 int gpad_set_option(gpad_handle_t h, int option, int value);
 
 /* Synchronise the handle's stream (for callers using device memory + async runs). */

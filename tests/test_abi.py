@@ -132,7 +132,7 @@ def test_binding_checks_library_version():
         def gpad_version(self):
             return self.v
     _lib._check_version(Fake(f"gpad-mi355x 0.{minor} (gfx950)".encode()))
-    for bad in (b"gpad-mi355x 0.3 (gfx950)", b"garbage"):
+    for bad in (b"gpad-mi355x 0.4 (gfx950)", b"garbage"):
         with pytest.raises(ImportError):
             _lib._check_version(Fake(bad))
 
@@ -197,3 +197,21 @@ def test_python_option_names_match_the_header():
         assert hdr.get(name) == num, name
     live = {k: v for k, v in hdr.items() if v not in _lib.OPT_RETIRED}
     assert set(live) <= set(_lib.OPTIONS), set(live) - set(_lib.OPTIONS)
+
+
+def test_rccl_library_override_cpu():
+    """gpad_group_rccl_library (the test / integration hook of the group transport) on the CPU: an
+    unloadable library is reported as GPAD_ERR_UNSUPPORTED with a message that groups fall back to
+    peer copies; the tests' stub (tests/rccl_stub, every RCCL entry point libgpad binds) loads; the
+    default is restored.  No device is touched."""
+    from gpad_mpc import _lib
+    lib = _lib.load()
+    stub = os.path.join(ROOT, "tests", "rccl_stub", "librccl_stub.so")
+    if not os.path.exists(stub):
+        subprocess.run(["make", "-s", "-C", os.path.dirname(stub)], check=True, timeout=120)
+    try:
+        assert lib.gpad_group_rccl_library(b"/nonexistent/librccl_missing.so", 1) == _lib.ERR_UNSUPPORTED
+        assert b"peer copies" in lib.gpad_last_error()
+        assert lib.gpad_group_rccl_library(stub.encode(), 1) == _lib.GPAD_OK
+    finally:
+        lib.gpad_group_rccl_library(None, 0)

@@ -156,3 +156,58 @@ def test_c_app_one_shot_bitexact(gpu, oracle):
     np.testing.assert_array_equal(y, yo)
     assert lines["iterations"][0] == "100"
     print("gpad_solve one-shot latency (us/call, battery 3x4, 100 iterations):", lines["solve_us"][0])
+
+
+def test_fresh_handle_follows_shape_prior(gpu, oracle):
+    """a handle with no plan of its own plans its first phased solve from the
+    shape's prior -- the last plan any handle of the process made for the same (n, m, batch, K, N)
+    (csrc/gpad_host.cpp plan_for).  Handle A solves batch 1 (its plan then becomes the prior); a new
+    handle B solves batch 2 following that prior: the same phases and survivor counts as A solving
+    batch 2 with its own plan (made from the same counts), bit-identical results.  Then the north-star
+    gpad_solve, from a freshly created cached handle, equals the oracle on batch 3."""
+    import torch
+
+    import bench
+    import gpad_mpc
+    n = m = 200
+    B, N, tol = 2048, 5000, 1e-4
+    ML, G, L, M1, g1 = bench.make_shard(n, m, B, 0)
+    (M2, g2), (M3, g3) = bench.make_stream(n, m, B, 2, 0)
+    f = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(gpu)  # noqa: E731
+    L32 = float(np.float32(L))
+    dML, dG = f(ML), f(G)
+
+    def solve(s, M, g):
+        z = torch.zeros(B, n, device=gpu)
+        y = torch.zeros(B, m, device=gpu)
+        it = np.zeros(B, np.int32)
+        s.run(z, y, f(M), f(g), N, tol, iters=it)
+        return z.cpu().numpy(), y.cpu().numpy(), it, s.last_phases()
+
+    with gpad_mpc.GpadSolver(0) as a, gpad_mpc.GpadSolver(0) as b:
+        for s in (a, b):
+            s.setup(dML, dG, L32, n=n, m=m, batch=B, shared=True, check_every=10)
+        solve(a, M1, g1)
+        zb, yb, itb, pb = solve(b, M2, g2)
+        za, ya, ita, pa2 = solve(a, M2, g2)
+    assert pb["prior"] and not pa2["prior"]
+    assert pb["ends"] == pa2["ends"] and pb["fins"] == pa2["fins"] and pb["counts"] == pa2["counts"]
+    assert len(pb["ends"]) <= 6, pb  # planned: a few phases, not the default 40-iteration run-up
+    np.testing.assert_array_equal(itb, ita)
+    np.testing.assert_array_equal(zb, za)
+    np.testing.assert_array_equal(yb, ya)
+    # gpad_solve: its cached handle is new after gpad_release_cached, so it follows the prior
+    from gpad_mpc import _lib
+    _lib.load().gpad_release_cached()
+    M3f, g3f = np.ascontiguousarray(M3, np.float32), np.ascontiguousarray(g3, np.float32)
+    MLf, Gf = np.ascontiguousarray(ML, np.float32), np.ascontiguousarray(G, np.float32)
+    Z = np.zeros((B, n), np.float32)
+    Y = np.zeros((B, m), np.float32)
+    it3 = np.zeros(B, np.int32)
+    st = c_solve(Z, Y, MLf, M3f, Gf, g3f, N, np.float32(L), tol, batch=B, iters=it3)
+    assert st.converged == B
+    for k in (0, 1, B // 2, B - 1, int(np.argmax(it3))):
+        zo, yo, ito, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), MLf, M3f[k], Gf, g3f[k], N, np.float32(L), tol)
+        assert it3[k] == ito, k
+        np.testing.assert_array_equal(Z[k], zo)
+        np.testing.assert_array_equal(Y[k], yo)

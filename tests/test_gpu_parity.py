@@ -204,81 +204,6 @@ def test_panel_phased_compaction_bitexact(gpu, oracle, grid, phase, fin, tol, N,
         assert_bitexact(y[b], yo, f"instance {b} y")
 
 
-@pytest.mark.parametrize("dflow", [3, 7])
-@pytest.mark.parametrize("grid,phase,fin", [(3, 20, 24), (0, 10, 0), (1, 0, None)])
-@pytest.mark.parametrize("tol,N", [(1e-4, 3000), (0.0, 57)])
-@pytest.mark.parametrize("nm,B", [((150, 130), 40), ((131, 256), 37), ((200, 200), 120), ((193, 207), 101),
-                                  ((207, 194), 70), ((140, 135), 90), ((170, 176), 80)])
-def test_panel_dataflow_bitexact(gpu, oracle, dflow, grid, phase, fin, tol, N, nm, B):
-    """GPAD_OPT_PANEL_DATAFLOW (gpad_panel.hip DfWait, instantiated for T = 13: (200, 200),
-    (193, 207), (207, 194); the other shapes check that the option leaves them alone): the chains
-    of both layouts start on the other GEMM's row tiles as their owners post them, without the
-    barrier between the GEMMs (bit 4: the one-panel tiles dealt oldest wave first).  Pairs (grid
-    3), one panel per workgroup (grid 0 at these batches), the relay and hand-off, phased
-    compaction with warm starts: every instance equals its own oracle solve, count included."""
-    from gpad_mpc import problems
-    opts = dict(panel_max_grid=grid, phase_len=phase, finish_thresh=-1 if fin is None else fin,
-                panel_dataflow=dflow)
-    n, m = nm
-    qp = problems.synthetic_qp(n, m, batch=B, seed=8)
-    ML, G = qp.ML.astype(np.float32), qp.G.astype(np.float32)
-    M, g = qp.M.astype(np.float32), qp.g.astype(np.float32)
-    L = np.float32(qp.L)
-    rng = np.random.default_rng(1)
-    z0 = (0.1 * rng.normal(size=(B, n))).astype(np.float32)
-    z, y, st, iters = run_gpu(ML, M, G, g, L, N, tol=tol, kernel="panel", z0=z0, opts=opts)
-    assert st["kernel"] == "panel"
-    for b in range(B):
-        zo, yo, it, _ = oracle.solve_f32(z0[b], np.zeros(m), ML, M[b], G, g[b], N, L, tol)
-        assert iters[b] == it, b
-        assert_bitexact(z[b], zo, f"instance {b} z")
-        assert_bitexact(y[b], yo, f"instance {b} y")
-
-
-@pytest.mark.parametrize("B", [4096, 8192])
-def test_panel_dataflow_c3_c4_batches(gpu, oracle, B):
-    """The C3 (4096: one panel per CU) and C4-shard (8192: pairs) batches to eps with dataflow on
-    equal the barrier schedule bit for bit (z, y, every count); instances spot-checked against
-    the oracle."""
-    import bench
-    n = m = 200
-    ML, G, L, M, g = bench.make_shard(n, m, B, 0)
-    f = lambda a: np.ascontiguousarray(np.asarray(a, np.float32))  # noqa: E731
-    ML, G, M, g, L = f(ML), f(G), f(M), f(g), np.float32(L)
-    z0, y0, st0, it0 = run_gpu(ML, M, G, g, L, 5000, tol=1e-4, kernel="panel", opts=dict(panel_dataflow=0))
-    z1, y1, st1, it1 = run_gpu(ML, M, G, g, L, 5000, tol=1e-4, kernel="panel", opts=dict(panel_dataflow=7))
-    assert np.array_equal(it0, it1)
-    assert_bitexact(z1, z0, "z")
-    assert_bitexact(y1, y0, "y")
-    for b in (0, 1, B // 2 + 3, B - 1):
-        zo, yo, it, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), ML, M[b], G, g[b], 5000, L, 1e-4)
-        assert it1[b] == it, b
-        assert_bitexact(z1[b], zo, f"instance {b} z")
-        assert_bitexact(y1[b], yo, f"instance {b} y")
-
-
-@pytest.mark.parametrize("B", [4096, 8192])
-def test_duo_mailbox_c3_c4_batches(gpu, oracle, B):
-    """GPAD_OPT_DUO_MAILBOX on the C3 / C4-shard batches to eps (the planned phases, the duo finisher
-    from ~270-290 with hundreds of workgroups): z, y and every count equal the solve without it;
-    instances spot-checked against the oracle."""
-    import bench
-    n = m = 200
-    ML, G, L, M, g = bench.make_shard(n, m, B, 0)
-    f = lambda a: np.ascontiguousarray(np.asarray(a, np.float32))  # noqa: E731
-    ML, G, M, g, L = f(ML), f(G), f(M), f(g), np.float32(L)
-    z0, y0, _, it0 = run_gpu(ML, M, G, g, L, 5000, tol=1e-4, kernel="panel", opts=dict(duo_mailbox=0))
-    z1, y1, _, it1 = run_gpu(ML, M, G, g, L, 5000, tol=1e-4, kernel="panel", opts=dict(duo_mailbox=1))
-    assert np.array_equal(it0, it1)
-    assert_bitexact(z1, z0, "z")
-    assert_bitexact(y1, y0, "y")
-    for b in (0, int(np.argmax(it1)), B - 1):
-        zo, yo, it, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), ML, M[b], G, g[b], 5000, L, 1e-4)
-        assert it1[b] == it, b
-        assert_bitexact(z1[b], zo, f"instance {b} z")
-        assert_bitexact(y1[b], yo, f"instance {b} y")
-
-
 @pytest.mark.parametrize("tol,N", [(1e-4, 2000), (0.0, 37)])
 @pytest.mark.parametrize("nm,B", [((200, 900), 40), ((300, 300), 20), ((257, 130), 33), ((520, 600), 17), ((1000, 300), 9)])
 @pytest.mark.parametrize("grid,phase", [(0, 0), (2, 20)])
@@ -304,19 +229,16 @@ def test_bigpanel_bitexact(gpu, oracle, tol, N, nm, B, grid, phase):
         assert_bitexact(y[b], yo, f"instance {b} y")
 
 
-@pytest.mark.parametrize("mailbox", [0, 1])
 @pytest.mark.parametrize("grid", [1, 3, 5, 0])
 @pytest.mark.parametrize("nm,B,z0s", [((200, 200), 120, 0.0), ((40, 180), 200, 0.1), ((131, 64), 97, 0.1)])
-def test_finisher_queue_bitexact(gpu, oracle, grid, nm, B, z0s, mailbox):
+def test_finisher_queue_bitexact(gpu, oracle, grid, nm, B, z0s):
     """The tail of a phased panel solve on the duo finisher (two instances per workgroup in
     ping-pong, slots refilled from the survivor list through a device counter; grid capped to 1, 3
     or 5 workgroups to force many claims).  The finisher takes over after the first 10-iteration
     phase, so nearly the whole solve runs there; every instance must match its own oracle solve,
-    iteration count included.  mailbox = 1 (GPAD_OPT_DUO_MAILBOX, instantiated for the 200 x 200
-    rows): once the queue is drained, a workgroup with two live slots hands one to a workgroup with
-    none (grids 3 and 5)."""
+    iteration count included."""
     from gpad_mpc import problems
-    opts = dict(phase_len=10, finish_thresh=100000, duo_max_grid=grid, duo_mailbox=mailbox)
+    opts = dict(phase_len=10, finish_thresh=100000, duo_max_grid=grid)
     n, m = nm
     qp = problems.synthetic_qp(n, m, batch=B, seed=12)
     ML, G = qp.ML.astype(np.float32), qp.G.astype(np.float32)

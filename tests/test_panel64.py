@@ -20,7 +20,7 @@ from test_value import value_problem
 pytestmark = pytest.mark.gpu
 
 
-def _run(ML, G, L, M, g, N, tol, *, kernel, H=None, tol_gap=0.0, K=10, dev=True, opts=None):
+def _run(ML, G, L, M, g, N, tol, *, kernel, H=None, tol_gap=0.0, K=10, dev=True, opts=None, z0=None, y0=None):
     import torch
 
     import gpad_mpc
@@ -28,8 +28,8 @@ def _run(ML, G, L, M, g, N, tol, *, kernel, H=None, tol_gap=0.0, K=10, dev=True,
     B, n = M.shape
     m = g.shape[1]
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float64)).cuda()  # noqa: E731
-    z = torch.zeros(B, n, dtype=torch.float64, device="cuda")
-    y = torch.zeros(B, m, dtype=torch.float64, device="cuda")
+    z = torch.zeros(B, n, dtype=torch.float64, device="cuda") if z0 is None else t(z0)
+    y = torch.zeros(B, m, dtype=torch.float64, device="cuda") if y0 is None else t(y0)
     it = np.zeros(B, np.int32)
     codes = np.full(B, -1, np.int32)
     kern = {"panel": _lib.KERNEL_PANEL, "stream": _lib.KERNEL_STREAM, "auto": _lib.KERNEL_AUTO}[kernel]
@@ -175,6 +175,35 @@ def test_panel64_refill_bitexact(gpu, K):
     for x, y_, w in zip(a[:4], b[:4], c[:4]):
         np.testing.assert_array_equal(x, y_)
         np.testing.assert_array_equal(x, w)
+
+
+@pytest.mark.parametrize("hessian", [True, False])
+def test_panel64_refill_warm_start(gpu, oracle, hessian):
+    """Column refills from a non-zero warm start: every instance starts from its own
+    z_{-1} != 0 and y_0 >= 0, so a refilled column seeds u = G_L z_{-1} with the GEMM over the new
+    columns while the other columns' state sits in the operand tile, and w_0 = y_0.  4608 instances
+    (more panels than workgroups): bit-identical to the run without refills and to the f64 stream
+    kernel (z, y, counts, codes), and a sample equal to the fp64 oracle's warm-started solve."""
+    B, tol = 4608, 1e-6
+    H, ML, M, G, g, L = (np.asarray(a) for a in value_problem(200, 200, 7, 1.0, batch=B)[:6])
+    rng = np.random.default_rng(11)
+    z0 = 0.05 * rng.normal(size=(B, 200))
+    y0 = 0.01 * np.abs(rng.normal(size=(B, 200)))
+    Hb = H if hessian else None
+    a = _run(ML, G, L, M, g, 20000, tol, kernel="panel", H=Hb, tol_gap=tol, z0=z0, y0=y0)
+    b = _run(ML, G, L, M, g, 20000, tol, kernel="panel", H=Hb, tol_gap=tol, z0=z0, y0=y0, opts={"p64_refill": 0})
+    c = _run(ML, G, L, M, g, 20000, tol, kernel="stream", H=Hb, tol_gap=tol, z0=z0, y0=y0)
+    assert a[4]["kernel"] == "panel" and a[4]["converged"] == B
+    for x, y_, w in zip(a[:4], b[:4], c[:4]):
+        np.testing.assert_array_equal(x, y_)
+        np.testing.assert_array_equal(x, w)
+    for i in (0, B // 2 + 1, B - 1, int(np.argmax(a[2]))):
+        if hessian:
+            zo, yo, ito, co = oracle.solve_value_f64(z0[i], y0[i], ML, M[i], G, g[i], H, 20000, L, tol, tol_gap=tol)
+        else:
+            zo, yo, ito, co = oracle.solve_f64(z0[i], y0[i], ML, M[i], G, g[i], 20000, L, tol, tol_gap=tol)
+        assert (a[2][i], a[3][i]) == (ito, co), i
+        np.testing.assert_allclose(a[0][i], zo, rtol=1e-12, atol=1e-14)
 
 
 def test_panel64_refill_max_iterations(gpu):

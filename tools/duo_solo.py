@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "gpu-dualgradient-mpc_amd"))
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-import tune_env  # noqa: E402,F401  (GPAD_* env -> handle options, e.g. GPAD_DUO_MAILBOX=0)
+import tune_env  # noqa: E402,F401  (GPAD_* env -> handle options)
 
 
 def stamps(two=False):

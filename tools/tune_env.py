@@ -23,8 +23,6 @@ _MAP = {  # env name -> (option, value transform)
     "GPAD_FLAT_PANELS": ("flat_panels", int),
     "GPAD_FLAT_WAVES": ("flat_waves", int),
     "GPAD_FLAT_NO_ALDS": ("flat_a_lds", lambda v: 0),
-    "GPAD_PANEL_DATAFLOW": ("panel_dataflow", int),
-    "GPAD_DUO_MAILBOX": ("duo_mailbox", int),
 }
 
 
