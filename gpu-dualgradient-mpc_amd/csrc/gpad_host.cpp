@@ -133,6 +133,13 @@ struct gpad_handle_s {
     int frag64_tiles = 0;
     DevBuf hfrag64;      // ... and H's, bound by gpad_setup_hessian (value branches on the f64 panels)
     DevBuf q64;          // f64 panels: the refill queue counter (one int, zeroed per launch)
+    // f64 panels with refills: the start order of the next solve -- the previous solve's instances by
+    // its counts, longest first (SolveArgs::order; GPAD_OPT_LPT), rebuilt whenever counts arrive
+    DevBuf p64_order;
+    std::vector<int> p64_order_host;
+    int p64_order_batch = 0;
+    bool p64_order_dirty = false;
+    bool last_p64 = false;  // the last run was an f64 panel solve with a tolerance (its counts order the next)
     bool hfrag64_ok = false;
     int frag_tiles = 0;
     DevBuf theta, beta;
@@ -165,6 +172,7 @@ struct gpad_handle_s {
     hipEvent_t plan_ev = nullptr;
     bool plan_pending = false;
     int plan_pending_N = 0, plan_pending_batch = 0;
+    bool plan_pending_p64 = false;      // ... the pending counts are an f64 panel solve's (build_p64_order)
     // plant binding (gpad_setup_plant): affine state maps and dynamics, device copies
     int nx = 0, nu = 0;
     bool plant_ready = false, plant_dyn = false;
@@ -290,6 +298,7 @@ int gpad_destroy(gpad_handle_t h) {
     h->frag64.release();
     h->hfrag64.release();
     h->q64.release();
+    h->p64_order.release();
     h->frag.release();
     h->stage.release();
     h->theta.release();
@@ -410,6 +419,7 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
     h->frag64_ok = false;
     h->hfrag64_ok = false;
     h->plan.nph = 0;
+    h->p64_order_batch = 0;  // (a new problem: the previous counts order nothing)
     h->flat_vpred = 0;
     h->plan_pending = false;
     h->last_phased = false;
@@ -543,6 +553,7 @@ int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* d, int n_u, const float*
     h->shadow_ok = false;
     h->hess_ok = false;
     h->plan.nph = 0;
+    h->p64_order_batch = 0;  // (a new problem: the previous counts order nothing)
     h->flat_vpred = 0;
     h->plan_pending = false;
     h->last_phased = false;
@@ -686,6 +697,21 @@ static void update_plan(gpad_handle_t h, const int* counts, int batch, int N) {
     }
 }
 
+// f64 panels: the next solve starts its instances longest-predicted-first, so
+// the column refills pair long instances with short ones (greedy list scheduling over the columns)
+// instead of in batch order -- each column's two-or-more instances then end together.  Predicted =
+// the previous solve's counts on the same batch size (an MPC stream's statistics, or the same batch
+// re-solved); ties keep batch order (stable).  Only the schedule changes: every instance runs the same
+// arithmetic in any column (bit-identical results, tests/test_panel64.py).
+static void build_p64_order(gpad_handle_t h, const int* counts, int batch) {
+    h->p64_order_host.resize(batch);
+    for (int b = 0; b < batch; ++b) h->p64_order_host[b] = b;
+    std::stable_sort(h->p64_order_host.begin(), h->p64_order_host.end(),
+                     [&](int x, int y) { return counts[x] > counts[y]; });
+    h->p64_order_batch = batch;
+    h->p64_order_dirty = true;
+}
+
 // Counters are laid out [steps][iters[batch] | conv[batch]].
 static int collect_stats(gpad_handle_t h, gpad_stats_t* st) {
     const int batch = h->last_batch;
@@ -714,6 +740,10 @@ static int collect_stats(gpad_handle_t h, gpad_stats_t* st) {
     if (h->last_phased && h->last_steps == 1) {
         update_plan(h, h->h_counts.data(), batch, h->last_N);
         h->plan_pending = false;  // these counts are at least as recent as any copy in flight
+    }
+    if (h->last_p64 && h->last_steps == 1) {
+        build_p64_order(h, h->h_counts.data(), batch);
+        h->plan_pending = false;
     }
     st->kernel = h->last_kernel;
     float ms = 0.0f;
@@ -879,6 +909,7 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
     int kernel = d.kernel;
     const bool prev_phased = h->last_phased;  // the previous launch's counts are still in `iters`
     h->last_phased = false;  // set again below when this launch is a phased panel solve
+    h->last_p64 = false;
     h->last_N = N;
     hipError_t e = hipSuccess;
     bool ok = false;
@@ -899,8 +930,18 @@ static int launch_solve(gpad_handle_t h, T* dz, T* dy, const T* dM, const T* dg,
             a.qctr = static_cast<int*>(h->q64.p);
             a.hfrag64 = (a.Hq && h->hfrag64_ok) ? h->hfrag64.p : nullptr;
             a.Hq = nullptr;
+            if (tol > 0.0 && h->tune.lpt && h->p64_order_batch == batch && (int)h->p64_order_host.size() == batch) {
+                if (h->p64_order_dirty) {
+                    if (int ro = h->p64_order.ensure(sizeof(int) * (size_t)batch)) return ro;
+                    HIP_TRY(hipMemcpyAsync(h->p64_order.p, h->p64_order_host.data(), sizeof(int) * (size_t)batch,
+                                           hipMemcpyHostToDevice, h->stream));
+                    h->p64_order_dirty = false;
+                }
+                a.order = static_cast<const int*>(h->p64_order.p);
+            }
             e = gpad::launch_panel64(a, h->stream);
             if (e != hipSuccess) return fail(GPAD_ERR_HIP, hip_detail("f64 panel", e));
+            h->last_p64 = tol > 0.0;
             *kernel_out = GPAD_KERNEL_PANEL;
             return finish(GPAD_OK);
         }
@@ -1020,7 +1061,10 @@ static int run_typed(gpad_handle_t h, T* z, T* y, const T* M, const T* g, int N,
     const double margin = sizeof(T) == sizeof(float) ? gpad::ViolMargin<float>::value : gpad::ViolMargin<double>::value;
     if ((rc = reset_status(h, tol, margin * h->L * (scaled_vec ? 1.0 : 1.0 / h->L)))) return rc;
     if (h->plan_pending && hipEventQuery(h->plan_ev) == hipSuccess) {  // a previous solve's counts landed
-        if (h->plan_pending_batch == batch) update_plan(h, h->plan_pin, batch, h->plan_pending_N);
+        if (h->plan_pending_batch == batch) {
+            if (h->plan_pending_p64) build_p64_order(h, h->plan_pin, batch);
+            else update_plan(h, h->plan_pin, batch, h->plan_pending_N);
+        }
         h->plan_pending = false;
     }
     HIP_TRY(hipEventRecord(h->ev0, h->stream));
@@ -1031,7 +1075,8 @@ static int run_typed(gpad_handle_t h, T* z, T* y, const T* M, const T* g, int N,
     h->last_kernel = kernel;
     h->last_batch = batch;
     h->last_steps = 1;
-    if (!st && h->last_phased && h->tune.plan) {  // asynchronous run: counts to the host behind it
+    if (!st && ((h->last_phased && h->tune.plan) || (h->last_p64 && h->tune.lpt))) {  // asynchronous run: counts
+        // to the host behind it
         const size_t want = sizeof(int) * (size_t)batch;
         if (h->plan_pin_cap < want) {
             if (h->plan_pending) {  // the previous run's copy into the old buffer must land first
@@ -1050,6 +1095,7 @@ static int run_typed(gpad_handle_t h, T* z, T* y, const T* M, const T* g, int N,
         h->plan_pending = true;
         h->plan_pending_N = N;
         h->plan_pending_batch = batch;
+        h->plan_pending_p64 = h->last_p64;
     }
     if (st) {
         if (d.memory == GPAD_MEM_HOST) {

@@ -108,6 +108,8 @@ struct SolveArgs {
                            // previous solve (or null); orders the finisher's queue longest first
     int n_u;               // flat battery path: cells (n = n_u * horizon), see gpad_flat.hip
     int flat_staged;       // flat path: matrices staged in LDS (set by launch_flat)
+    const int* order;      // f64 panels with column refills: instances in start order (the previous
+                           // solve's counts, longest first: LPT over the columns), or null (0..batch-1)
     const struct PanelPlan* plan;  // panel phases: host-side plan from the previous solve (or null)
     struct PanelPlan* used;        // panel phases: host-side record of the phases launched (or null)
     const Tuning* tune;    // host-side tuning options (never null on a launch from gpad_host.cpp)

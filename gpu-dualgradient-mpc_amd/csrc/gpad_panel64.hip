@@ -312,8 +312,11 @@ __global__ __launch_bounds__(RELAY ? 1024 : 64 * T) void gpad_panel64_kernel(Sol
 
     // (REFILL: one pass -- the panels past the first grid are dealt column by column through the queue)
     for (int p = blockIdx.x; p < panels && (!REFILL || p == (int)blockIdx.x); p += gridDim.x) {
-        int inst = 16 * p + c;
-        bool active = inst < a.batch;
+        // REFILL with a.order: the k-th instance started is order[k] (longest predicted first, so the
+        // refills pair long first instances with short later ones: list scheduling over the columns)
+        const int k0 = 16 * p + c;
+        bool active = k0 < a.batch;
+        int inst = (REFILL && a.order && active) ? a.order[k0] : k0;
         // register r <-> row 16t + 4r + j of the column's instance
         double z[4], y[4], u[4], pd[4];
         // a column's starting state (every column at a panel's start; REFILL: the refilled ones)
@@ -567,7 +570,7 @@ __global__ __launch_bounds__(RELAY ? 1024 : 64 * T) void gpad_panel64_kernel(Sol
                     base = __shfl(base, 0, 64);
                     const int rank = (int)__popcll(needm & ((1ull << lane) - 1ull));
                     const int k = 16 * (int)gridDim.x + base + rank;
-                    newinst[lane] = active ? -2 : (k < a.batch ? k : -1);
+                    newinst[lane] = active ? -2 : (k < a.batch ? (a.order ? a.order[k] : k) : -1);
                 }
                 __syncthreads();
                 const int nk = newinst[c];

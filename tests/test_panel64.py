@@ -220,3 +220,43 @@ def test_panel64_refill_max_iterations(gpu):
     for x, y_ in zip(a[:4], b[:4]):
         np.testing.assert_array_equal(x, y_)
     assert (a[3] == 0).any() and (a[2] <= 120).all()
+
+
+@pytest.mark.parametrize("hessian", [True, False])
+def test_panel64_lpt_order_bitexact(gpu, hessian):
+    """an f64 panel solve with column refills starts its instances longest-
+    predicted-first (the handle's previous counts, GPAD_OPT_LPT) so each column's instances end
+    together.  Three solves of one batch on one handle (the second and third follow the first's /
+    second's counts; a warm start on the third) equal, bit for bit, the same solves with lpt = 0 and
+    the f64 stream kernel -- z, y, counts and codes."""
+    import torch
+
+    import gpad_mpc
+    from gpad_mpc import _lib
+    B, tol = 4608, 1e-6
+    H, ML, M, G, g, L = (np.asarray(a) for a in value_problem(200, 200, 7, 1.0, batch=B)[:6])
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float64)).cuda()  # noqa: E731
+    rng = np.random.default_rng(3)
+    starts = [(np.zeros((B, 200)), np.zeros((B, 200)))] * 2 + [(0.02 * rng.normal(size=(B, 200)),
+                                                                0.01 * np.abs(rng.normal(size=(B, 200))))]
+    res = {}
+    for name, kern, opts in (("lpt", _lib.KERNEL_PANEL, {}), ("plain", _lib.KERNEL_PANEL, {"lpt": 0}),
+                             ("stream", _lib.KERNEL_STREAM, {})):
+        out = []
+        with gpad_mpc.GpadSolver(0) as s:
+            s.setup(t(ML), t(G), float(L), n=200, m=200, batch=B, check_every=10, kernel=kern, tol_gap=tol)
+            if hessian:
+                s.setup_hessian(t(H))
+            s.set_options(**opts)
+            for z0, y0 in starts:
+                z, y = t(z0), t(y0)
+                it = np.zeros(B, np.int32)
+                codes = np.full(B, -1, np.int32)
+                st = s.run(z, y, t(M), t(g), 20000, tol, iters=it, codes=codes)
+                assert st["converged"] == B
+                out.append((z.cpu().numpy(), y.cpu().numpy(), it, codes))
+        res[name] = out
+    for k in range(len(starts)):
+        for x, y_, w in zip(res["lpt"][k], res["plain"][k], res["stream"][k]):
+            np.testing.assert_array_equal(x, y_)
+            np.testing.assert_array_equal(x, w)
