@@ -1,5 +1,6 @@
 """A/B of the f64 panel layouts (csrc/gpad_panel64.hip) on bench.py's f64 value leg: 8192 C4-shaped
-value problems, H bound, e_g = e_V = 1e-6; options interleaved over rounds on one handle each.
+value problems, H bound, e_g = e_V = 1e-6; options interleaved over rounds on one handle each
+(relay+refill+lpt: refills in longest-predicted-first order from the handle's previous counts, r06).
 
   python tools/p64_ab.py [--rounds 3] [--batch 8192] [--small]
 --small adds the ADVICE r04 small-shape check: n = 40, m = 53 at 4096 instances (f64, no H, eps
@@ -23,6 +24,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--batch", type=int, default=8192)
     ap.add_argument("--small", action="store_true")
+    ap.add_argument("--only", nargs="*", default=None, help="variant names to run")
     args = ap.parse_args()
     import torch
 
@@ -37,8 +39,11 @@ def main():
     dH, dML, dG, dM, dg = f64(H), f64(ML), f64(G), f64(M), f64(g)
     z = torch.zeros(B, n, dtype=torch.float64, device=dev)
     y = torch.zeros(B, m, dtype=torch.float64, device=dev)
-    variants = {"relay+refill": {"p64_relay": 1, "p64_refill": 1}, "relay": {"p64_relay": 1, "p64_refill": 0},
-                "tiles": {"p64_relay": 0, "p64_refill": 0}}
+    variants = {"relay+refill+lpt": {"p64_relay": 1, "p64_refill": 1, "lpt": 1},
+                "relay+refill": {"p64_relay": 1, "p64_refill": 1, "lpt": 0},
+                "relay": {"p64_relay": 1, "p64_refill": 0}, "tiles": {"p64_relay": 0, "p64_refill": 0}}
+    if args.only:
+        variants = {k: v for k, v in variants.items() if k in args.only}
     solvers = {}
     for name, opts in variants.items():
         s = gpad_mpc.GpadSolver(0)
