@@ -96,6 +96,32 @@ def parse(args):
             print(f"survivors past iteration {v:>4}: {(it > v).sum()}")
 
 
+def solves(args):
+    """One line per solve of the trace: every launch's kernel (short name) and duration, in order --
+    to line up with the run step's per-rep survivor counts (which solves are slow, in which phase)."""
+    files = glob.glob(os.path.join(args.dir, "**", "*kernel_trace.csv"), recursive=True)
+    if not files:
+        sys.exit(f"no kernel_trace.csv under {args.dir}")
+    with open(files[0]) as f:
+        rows = sorted(csv.DictReader(f), key=lambda r: int(r["Start_Timestamp"]))
+    gpad = [r for r in rows if "gpad" in r["Kernel_Name"] and "pack" not in r["Kernel_Name"]
+            and "accumulate" not in r["Kernel_Name"]]
+    out, cur = [], []
+    for r in gpad:
+        if cur and int(r["Start_Timestamp"]) - int(cur[-1]["End_Timestamp"]) > 200_000:
+            out.append(cur)
+            cur = []
+        cur.append(r)
+    out.append(cur)
+    short = lambda k: ("panel" if "panel2" in k else "duo" if "duo" in k else "cmp" if "compact" in k  # noqa: E731
+                       else k.split("(")[0][-12:])
+    for i, sv in enumerate(out):
+        span = (int(sv[-1]["End_Timestamp"]) - int(sv[0]["Start_Timestamp"])) / 1e3
+        seq = " ".join(f"{short(r['Kernel_Name'])}:{(int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3:.1f}"
+                       for r in sv)
+        print(f"solve {i}: span {span:8.1f} us | {seq}")
+
+
 def stats(args):
     """Per-kernel durations over every solve of the trace, and the solve spans (A/B of a phase)."""
     files = glob.glob(os.path.join(args.dir, "**", "*kernel_trace.csv"), recursive=True)
@@ -136,11 +162,13 @@ def main():
     b = sub.add_parser("parse")
     b.add_argument("dir")
     b.add_argument("--iters", default="gpurun_out/tl_iters.npy")
+    d = sub.add_parser("solves")
+    d.add_argument("dir")
     c = sub.add_parser("stats")
     c.add_argument("dir")
     c.add_argument("--label", default="")
     args = ap.parse_args()
-    {"run": run, "parse": parse, "stats": stats}[args.cmd](args)
+    {"run": run, "parse": parse, "stats": stats, "solves": solves}[args.cmd](args)
 
 
 if __name__ == "__main__":
