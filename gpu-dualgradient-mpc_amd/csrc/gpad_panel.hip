@@ -1491,15 +1491,16 @@ int panel_fin_thresh(int n, int m, int num_cus, const Tuning* t) {
 //                      panels share the CU's four SIMDs
 //   phase overhead   = 2 launches (finisher + panel, 5 us each) + one seed iteration
 //                      + carried z, y, w, u (16 (n + m) bytes per survivor at 5 TB/s)
-//   finisher         = max(L t_lat, W 1.1 t_res / CUs) + 2 launches,  t_res = 0.0021 (n + m) + 0.38,
-//                      t_lat = 1.4 t_res (two workgroups per CU), L the longest remaining solve,
-//                      W the remaining instance-iterations.
+//   finisher         = 1.56 t_res L + 0.70 t_res W / CUs + 2 launches,  t_res = 0.0021 (n + m) + 0.38,
+//                      L the longest remaining solve, W the remaining instance-iterations (r06 refit:
+//                      latency and work add, see PlanModel::finisher).
 namespace {
 struct PlanModel {
     int T, n, m, num_cus, grid;
     bool handoff;  // gpad_panel2_kernel's hand-off shapes (Handoff)
     bool relay;    // ... and its one-panel relay (T = 9, 13)
-    static constexpr double kTLat = 1.4;        // finisher latency factor over t_res (two per CU)
+    static constexpr double kFinLat = 1.56;     // finisher: us per remaining iteration of the longest, / t_res
+    static constexpr double kFinWork = 0.70;    // finisher: us per instance-iteration per CU, / t_res
     static constexpr double kCarryBw = 5e6;     // carried state, bytes per us
     double t_chain, t_res, t_launch = 5.0;
     double iter_time(long long panels) const {
@@ -1531,9 +1532,14 @@ struct PlanModel {
         return 2 * t_launch + (v1 - v0 + 1) * it + (double)s0 * 16.0 * (n + m) / kCarryBw;
     }
     double finisher(int longest, long long work) const {
-        const double lat = longest * kTLat * t_res;
-        const double thr = (double)work * 1.1 * t_res / num_cus;
-        return 2 * t_launch + (lat > thr ? lat : thr);
+        // r06 refit on fresh-input C4 solves (profiles/r06_plan_refit.txt): with the queue in no
+        // useful order (fresh inputs: the previous solve's counts do not rank this one's instances)
+        // the longest survivor waits behind part of its CU's queue, so its latency and the CU's
+        // share of the work ADD -- the duo took 341-370 us from iteration 280 (L = 110, W/CU = 181)
+        // and 236-262 us from 290 (L = 90-100, W/CU = 105), where max(latency, throughput) of the
+        // previous constants priced 242 / 171 us and steered ~30 % of the solves to the costlier
+        // earlier takeover (+47 us per solve, profiles/r06_solve_spread.txt)
+        return 2 * t_launch + kFinLat * t_res * longest + kFinWork * t_res * (double)work / num_cus;
     }
 };
 }  // namespace
