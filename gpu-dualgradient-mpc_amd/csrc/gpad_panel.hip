@@ -774,6 +774,11 @@ struct HoSlots {
     int in, out;  // LDS hand-off slots taken / given (-1: none)
 };
 
+// The results-out and park sites launder the column's instance index and the lane through an empty
+// asm before forming its row pointers and offsets (r06): otherwise the compiler hoists the six per-panel 64-bit row pointers
+// (z, y, wc, uc ... of each panel) out of the solve loop, and at 128 VGPRs the double waves spilled them
+// -- 240 B of scratch per lane whose dirty lines were written back to HBM, ~39 MB per phase-1 launch at
+// C4 (profiles/r06_write_probe.txt: a fixed-N launch that stores only z*, y* (13 MB) wrote 52 MB).
 // This lane's four rows 16t + 4r + j (r = 0..3) of one instance's vector (r05).  vec: one 16-B load
 // of rows 16t + 4j .. +3 per lane (the 16 columns x 64 contiguous bytes of a wave's tile, a quarter
 // of the requests of four 4-B loads per lane), transposed through 1 KiB of LDS the wave owns (its
@@ -962,15 +967,17 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
 #pragma unroll
             for (int q = 0; q < Q; ++q) {  // one round trip per panel (a double wave: two)
                 float zl[4], gpl[4], yl[4], gl[4], wl[4], ul[4];
+                int ln = lane;
+                asm volatile("" : "+v"(ln));  // (offsets formed per item, not kept across the item loop)
                 const size_t b = (size_t)inst[q];
                 float* const st = reinterpret_cast<float*>(&L.Zh[p0 + q][64 * t]);
-                rows4(a.z + b * n, t, n, vec, st, lane, zl);
-                rows4(a.gP + b * a.ld_gP, t, n, vec, st, lane, gpl);
-                rows4(a.y + b * m, t, m, vec, st, lane, yl);
-                rows4(a.g + b * a.ld_g, t, m, vec, st, lane, gl);
+                rows4(a.z + b * n, t, n, vec, st, ln, zl);
+                rows4(a.gP + b * a.ld_gP, t, n, vec, st, ln, gpl);
+                rows4(a.y + b * m, t, m, vec, st, ln, yl);
+                rows4(a.g + b * a.ld_g, t, m, vec, st, ln, gl);
                 if (!fresh) {
-                    rows4(a.wc + b * m, t, m, vec, st, lane, wl);
-                    if (use_tol) rows4(a.uc + b * m, t, m, vec, st, lane, ul);
+                    rows4(a.wc + b * m, t, m, vec, st, ln, wl);
+                    if (use_tol) rows4(a.uc + b * m, t, m, vec, st, ln, ul);
                     else ul[0] = ul[1] = ul[2] = ul[3] = 0.0f;
                 }
                 const int pq = p0 + q;
@@ -1313,11 +1320,13 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 }
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {  // (Zh's block is free again: the rows4 transpose)
-                    const size_t b = (size_t)inst[q];
+                    int iq = inst[q], ln = lane;
+                    asm volatile("" : "+v"(iq), "+v"(ln));  // (no hoisted row pointers / offsets: rows4 note)
+                    const size_t b = (size_t)iq;
                     float* const st = reinterpret_cast<float*>(&L.Zh[p0 + q][64 * t]);
                     const bool zw = cd[q] != 2 || zh_out;  // (B)'s zhat already out before (A)'s GEMM
-                    rows4_store(a.z + b * n, t, n, vec_io, st, lane, zo[q], out[q] && zw);
-                    rows4_store(a.y + b * m, t, m, vec_io, st, lane, y[q], out[q]);
+                    rows4_store(a.z + b * n, t, n, vec_io, st, ln, zo[q], out[q] && zw);
+                    rows4_store(a.y + b * m, t, m, vec_io, st, ln, y[q], out[q]);
                     if (out[q]) {
                         if (t == 0 && j == 0) {
                             a.iters[inst[q]] = v;
@@ -1352,12 +1361,14 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 }
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
-                    const size_t b = (size_t)inst[q];
+                    int iq = inst[q], ln = lane;
+                    asm volatile("" : "+v"(iq), "+v"(ln));  // (no hoisted row pointers / offsets: rows4 note)
+                    const size_t b = (size_t)iq;
                     float* const st = reinterpret_cast<float*>(&L.Zh[p0 + q][64 * t]);
-                    rows4_store(a.z + b * n, t, n, vec_io, st, lane, z[q], pk[q]);
-                    rows4_store(a.y + b * m, t, m, vec_io, st, lane, y[q], pk[q]);
-                    rows4_store(a.wc + b * m, t, m, vec_io, st, lane, wv[q], pk[q]);
-                    if (use_tol) rows4_store(a.uc + b * m, t, m, vec_io, st, lane, u[q], pk[q]);
+                    rows4_store(a.z + b * n, t, n, vec_io, st, ln, z[q], pk[q]);
+                    rows4_store(a.y + b * m, t, m, vec_io, st, ln, y[q], pk[q]);
+                    rows4_store(a.wc + b * m, t, m, vec_io, st, ln, wv[q], pk[q]);
+                    if (use_tol) rows4_store(a.uc + b * m, t, m, vec_io, st, ln, u[q], pk[q]);
                 }
                 if (t == 0) {  // the tile-0 owner of each panel lists its survivors
 #pragma unroll
