@@ -1329,8 +1329,8 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                     rows4_store(a.y + b * m, t, m, vec_io, st, ln, y[q], out[q]);
                     if (out[q]) {
                         if (t == 0 && j == 0) {
-                            a.iters[inst[q]] = v;
-                            a.conv[inst[q]] = cd[q];
+                            a.iters[iq] = v;
+                            a.conv[iq] = cd[q];
                         }
                         act[q] = false;
                     }
@@ -1372,7 +1372,11 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 }
                 if (t == 0) {  // the tile-0 owner of each panel lists its survivors
 #pragma unroll
-                    for (int q = 0; q < Q; ++q) list_survivors(a, pair ? 2 * it + p0 + q : it, pk[q], inst[q], lane, j);
+                    for (int q = 0; q < Q; ++q) {
+                        int iq = inst[q], ln = lane;
+                        asm volatile("" : "+v"(iq), "+v"(ln));
+                        list_survivors(a, pair ? 2 * it + p0 + q : it, pk[q], iq, ln, ln >> 4);
+                    }
                 }
             }
         }
