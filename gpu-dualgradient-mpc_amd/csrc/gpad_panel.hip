@@ -779,32 +779,41 @@ struct HoSlots {
 // (z, y, wc, uc ... of each panel) out of the solve loop, and at 128 VGPRs the double waves spilled them
 // -- 240 B of scratch per lane whose dirty lines were written back to HBM, ~39 MB per phase-1 launch at
 // C4 (profiles/r06_write_probe.txt: a fixed-N launch that stores only z*, y* (13 MB) wrote 52 MB).
-// This lane's four rows 16t + 4r + j (r = 0..3) of one instance's vector (r05).  vec: one 16-B load
-// of rows 16t + 4j .. +3 per lane (the 16 columns x 64 contiguous bytes of a wave's tile, a quarter
-// of the requests of four 4-B loads per lane), transposed through 1 KiB of LDS the wave owns (its
-// (panel, tile) block of Zh, free until the first GEMM's epilogue): column c's 16 floats with the
-// 16-B chunks XOR-swizzled by c >> 2, so the four reads are conflict-free.  The tile's rows past
-// `rows` read the last four rows (the caller zeroes them).  Else four 4-B loads at clamped rows.
-__device__ __forceinline__ void rows4(const float* base, int t, int rows, bool vec, float* st, int lane,
-                                      float (&out)[4]) {
+// This lane's four rows 16t + 4r + j (r = 0..3) of one instance's vector.  vec (16-B aligned rows):
+// rows4_dma, one global_load_lds_dwordx4 per lane (the 16 columns x 64 contiguous bytes of a wave's
+// tile, a quarter of the requests of four 4-B loads per lane) into 1 KiB of LDS the wave owns, then
+// rows4_rd.  The DMA lands lane-linearly: lane l carries column c' = l >> 2's rows 16t + 4j' .. +3,
+// j' = (l & 3) ^ ((c' >> 2) & 3), so the block holds column c's 16 floats with the 16-B chunks
+// XOR-swizzled by c >> 2 and the four reads are conflict-free.  colbase is column c''s instance
+// row 0; the tile's rows past `rows` read the last four rows (the caller zeroes them).  r05 loaded
+// into VGPRs and transposed through the block, which serialised the operands' loads behind each
+// other's LDS waits; r06 stages by DMA, every operand of every panel in flight at once and no VGPRs
+// held meanwhile (batching the VGPR loads instead spilled: 45-69 VGPRs in the pair kernels).
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+__device__ __forceinline__ void rows4_dma(const float* colbase, int t, int rows, int lane, float4* blk) {
+    const int cc = lane >> 2;
+    const int jj = (lane & 3) ^ ((cc >> 2) & 3);
+    const int r0 = 16 * t + 4 * jj;
+    const int rr = r0 + 3 < rows ? r0 : rows - 4;
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)(colbase + rr), (lds_void_t*)blk, 16, 0, 0);
+}
+
+__device__ __forceinline__ void rows4_rd(const float4* blk, int lane, float (&out)[4]) {
+    const float* st = reinterpret_cast<const float*>(blk);
     const int j = lane >> 4, c = lane & 15, sw = (c >> 2) & 3;
-    if (vec) {
-        const int r0 = 16 * t + 4 * j;
-        const int rr = r0 + 3 < rows ? r0 : rows - 4;
-        const float4 v = *reinterpret_cast<const float4*>(base + rr);
-        *reinterpret_cast<float4*>(st + 16 * c + 4 * (j ^ sw)) = v;
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-        for (int r = 0; r < 4; ++r) out[r] = st[16 * c + 4 * (r ^ sw) + j];
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the next use of the block writes it)
-    } else {
+    for (int r = 0; r < 4; ++r) out[r] = st[16 * c + 4 * (r ^ sw) + j];
+}
+
+// the scalar path (rows not 16-B aligned): four 4-B loads at clamped rows
+__device__ __forceinline__ void rows4(const float* base, int t, int rows, int lane, float (&out)[4]) {
+    const int j = lane >> 4;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int i = 16 * t + 4 * r + j;
-            out[r] = base[i < rows ? i : rows - 1];
-        }
+    for (int r = 0; r < 4; ++r) {
+        const int i = 16 * t + 4 * r + j;
+        out[r] = base[i < rows ? i : rows - 1];
     }
 }
 
@@ -964,23 +973,46 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
         if constexpr (NU > 0) {
             const float beta0 = a.beta[0];
             const bool vec = vec_io;
+            // vec (r06): the operands arrive by LDS-DMA (rows4_dma), every panel's in flight at once:
+            // z, gP, y, g into the wave's (panel, tile) blocks of Zh, Gp, Wl, Pd, then (carried
+            // phases) wc, uc into those of Zh, Wl once the first four are read.  The final Gp / Pd /
+            // Wl / Zh rows are stored after the reads of the same blocks (LDS is in order per wave).
+            // Before: each operand's load waited behind the previous one's LDS transpose, four to
+            // six round trips to memory per panel (profiles/r05_phase_stamps_vecio_*.txt: 14-30
+            // kcycles to the first barrier).
+            if (vec) {
 #pragma unroll
-            for (int q = 0; q < Q; ++q) {  // one round trip per panel (a double wave: two)
-                float zl[4], gpl[4], yl[4], gl[4], wl[4], ul[4];
-                int ln = lane;
-                asm volatile("" : "+v"(ln));  // (offsets formed per item, not kept across the item loop)
-                const size_t b = (size_t)inst[q];
-                float* const st = reinterpret_cast<float*>(&L.Zh[p0 + q][64 * t]);
-                rows4(a.z + b * n, t, n, vec, st, ln, zl);
-                rows4(a.gP + b * a.ld_gP, t, n, vec, st, ln, gpl);
-                rows4(a.y + b * m, t, m, vec, st, ln, yl);
-                rows4(a.g + b * a.ld_g, t, m, vec, st, ln, gl);
-                if (!fresh) {
-                    rows4(a.wc + b * m, t, m, vec, st, ln, wl);
-                    if (use_tol) rows4(a.uc + b * m, t, m, vec, st, ln, ul);
-                    else ul[0] = ul[1] = ul[2] = ul[3] = 0.0f;
+                for (int q = 0; q < Q; ++q) {
+                    int ln = lane;
+                    asm volatile("" : "+v"(ln));  // (offsets formed per item, not kept across the item loop)
+                    const size_t bc = (size_t)__shfl(inst[q], ln >> 2);
+                    const int pq = p0 + q;
+                    rows4_dma(a.z + bc * n, t, n, ln, &L.Zh[pq][64 * t]);
+                    rows4_dma(a.gP + bc * a.ld_gP, t, n, ln, &L.Gp[pq][64 * t]);
+                    rows4_dma(a.y + bc * m, t, m, ln, &L.Wl[pq][64 * t]);
+                    rows4_dma(a.g + bc * a.ld_g, t, m, ln, &L.Pd[pq][64 * t]);
                 }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+            }
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                float zl[4], gpl[4], yl[4], gl[4];
+                int ln = lane;
+                asm volatile("" : "+v"(ln));
+                const size_t b = (size_t)inst[q];
                 const int pq = p0 + q;
+                if (vec) {
+                    rows4_rd(&L.Zh[pq][64 * t], ln, zl);
+                    rows4_rd(&L.Gp[pq][64 * t], ln, gpl);
+                    rows4_rd(&L.Wl[pq][64 * t], ln, yl);
+                    rows4_rd(&L.Pd[pq][64 * t], ln, gl);
+                } else {
+                    rows4(a.z + b * n, t, n, ln, zl);
+                    rows4(a.gP + b * a.ld_gP, t, n, ln, gpl);
+                    rows4(a.y + b * m, t, m, ln, yl);
+                    rows4(a.g + b * a.ld_g, t, m, ln, gl);
+                }
                 float gp[4], pd[4], wv[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -992,18 +1024,50 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                     const float gr = okm ? gl[r] : 0.0f;
                     pd[r] = (float)(a.gscale * (double)gr);
                     gmx = absmax_nan(gmx, gr);
-                    if (fresh) {  // w_0 = y_0 + beta_0 (y_0 - y_{-1}), y_{-1} = y_0
-                        wv[r] = __builtin_fmaf(beta0, y[q][r] - y[q][r], y[q][r]);
-                        u[q][r] = 0.0f;
-                    } else {
-                        wv[r] = okm ? wl[r] : 0.0f;
-                        u[q][r] = okm ? ul[r] : 0.0f;
-                    }
+                    // w_0 = y_0 + beta_0 (y_0 - y_{-1}), y_{-1} = y_0 (fresh; carried: wc below)
+                    wv[r] = __builtin_fmaf(beta0, y[q][r] - y[q][r], y[q][r]);
+                    u[q][r] = 0.0f;
                 }
                 L.Gp[pq][slot] = make_float4(gp[0], gp[1], gp[2], gp[3]);
                 L.Pd[pq][slot] = make_float4(pd[0], pd[1], pd[2], pd[3]);
-                L.Wl[pq][slot] = make_float4(wv[0], wv[1], wv[2], wv[3]);
-                if (fresh && use_tol) L.Zh[pq][slot] = make_float4(z[q][0], z[q][1], z[q][2], z[q][3]);
+                if (fresh) {
+                    L.Wl[pq][slot] = make_float4(wv[0], wv[1], wv[2], wv[3]);
+                    if (use_tol) L.Zh[pq][slot] = make_float4(z[q][0], z[q][1], z[q][2], z[q][3]);
+                } else if (vec) {  // round two: wc, uc into the blocks just read
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    const size_t bc = (size_t)__shfl(inst[q], ln >> 2);
+                    rows4_dma(a.wc + bc * m, t, m, ln, &L.Zh[pq][64 * t]);
+                    if (use_tol) rows4_dma(a.uc + bc * m, t, m, ln, &L.Wl[pq][64 * t]);
+                }
+            }
+            if (!fresh) {
+                if (vec) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __builtin_amdgcn_wave_barrier();
+                }
+#pragma unroll
+                for (int q = 0; q < Q; ++q) {
+                    float wl[4], ul[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+                    int ln = lane;
+                    asm volatile("" : "+v"(ln));
+                    const size_t b = (size_t)inst[q];
+                    const int pq = p0 + q;
+                    if (vec) {
+                        rows4_rd(&L.Zh[pq][64 * t], ln, wl);
+                        if (use_tol) rows4_rd(&L.Wl[pq][64 * t], ln, ul);
+                    } else {
+                        rows4(a.wc + b * m, t, m, ln, wl);
+                        if (use_tol) rows4(a.uc + b * m, t, m, ln, ul);
+                    }
+                    float wv[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const bool okm = act[q] && 16 * t + 4 * r + j < m;
+                        wv[r] = okm ? wl[r] : 0.0f;
+                        u[q][r] = okm ? ul[r] : 0.0f;
+                    }
+                    L.Wl[pq][slot] = make_float4(wv[0], wv[1], wv[2], wv[3]);
+                }
             }
         }
 #ifdef GPAD_STAMP
