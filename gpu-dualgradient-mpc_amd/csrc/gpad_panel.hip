@@ -1747,16 +1747,22 @@ size_t panel_work_bytes(int m, int batch) {
 // inside a bin is arbitrary; results never depend on the order, only the schedule does.
 constexpr int kSortMax = 8192;
 constexpr int kSortBins = 4096;
-__device__ __forceinline__ int block_scan_1024(int* part, int tid, int v) {  // exclusive scan, 1024 threads
-    part[tid] = v;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        const int x = tid >= off ? part[tid - off] : 0;
-        __syncthreads();
-        part[tid] += x;
-        __syncthreads();
+// exclusive scan over 1024 threads: an inclusive scan inside each wave (six shuffles), then the 16
+// wave totals through LDS -- two barriers (r06; the LDS Hillis-Steele scan before it took twenty)
+__device__ __forceinline__ int block_scan_1024(int* part, int tid, int v) {
+    const int lane = tid & 63, w = tid >> 6;
+    int x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off);
+        if (lane >= off) x += y;
     }
-    return part[tid] - v;
+    if (lane == 63) part[w] = x;
+    __syncthreads();
+    int wb = 0;
+    for (int i = 0; i < w; ++i) wb += part[i];
+    __syncthreads();  // (the caller's next scan rewrites part)
+    return wb + x - v;
 }
 
 constexpr int kCompactMaxPanels = 8192;  // per-panel bases in LDS up to here (131072 instances)

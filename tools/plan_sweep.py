@@ -61,7 +61,7 @@ def main():
     if args.one:
         one(args.reps, args.fresh)
         return
-    settings = [{}, {"GPAD_FINISHER": "resident"}, {"GPAD_NO_LPT": "1"}, {"GPAD_FINISH_SOLO": "256"}]
+    settings = [{}, {"GPAD_NO_LPT": "1"}]
     for ph in (20, 40, 80, 260):
         for fin in (512, 1024, 2048, 4096):
             settings.append({"GPAD_PANEL_NOPLAN": "1", "GPAD_PANEL_PHASE": str(ph), "GPAD_FINISH_THRESH": str(fin)})
