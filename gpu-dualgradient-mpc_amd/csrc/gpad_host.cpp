@@ -193,9 +193,9 @@ static int reset_status(gpad_handle_t h, double tol, double floor_scale) {
     const bool fresh = h->status.p == nullptr;
     int rc = h->status.ensure(sizeof(RunStatus));
     if (rc) return rc;
+    // the error word once (fetch_status clears it behind each read); the |g| slots are stored by
+    // the run's first writer (SolveArgs::gmax_part), so a solve enqueues no memset here
     if (fresh) HIP_TRY(hipMemsetAsync(h->status.p, 0, sizeof(RunStatus), h->stream));
-    else HIP_TRY(hipMemsetAsync((char*)h->status.p + offsetof(RunStatus, part), 0,
-                                sizeof(RunStatus) - offsetof(RunStatus, part), h->stream));
     h->last_tol = tol;
     h->last_floor_scale = floor_scale;
     h->failed_run = false;

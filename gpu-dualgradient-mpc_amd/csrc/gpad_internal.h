@@ -99,7 +99,11 @@ struct SolveArgs {
     int* seg_idx;          // [16 panel + rank] their instances; phase_compact_kernel densifies
     double* gmax_part;     // [kAbsmaxMaxBlocks] per-workgroup max |g| of the run (the certification
                            // floor; null: not wanted): the panel pairs fold it into their loads,
-                           // every other path runs launch_absmax
+                           // every other path runs launch_absmax.  Not zeroed before the run: its
+                           // first writer (the panel pairs' launch at v_begin == 0, or absmax) stores
+                           // its slots and zeroes the rest; later phase launches max into them
+    int* zero_w;           // panel pairs: words workgroup 0 zeroes at the launch's start (a phased
+    int zero_n;            // solve's phase and queue counters, read by later launches only), or null
     float* wc;             // carried w  [batch][m]
     float* uc;             // carried u = G_L z [batch][m]
     int fin_thresh;        // survivors <= this: the resident finisher takes them (0: none)
@@ -225,9 +229,8 @@ hipError_t launch_precompute(int n, int m, int nf, const double* H, long long sH
                              int count, hipStream_t s);
 hipError_t launch_apply_inv(int n, int batch, const double* Hinv, const double* f, double* gP, hipStream_t s);
 hipError_t launch_accumulate_iters(const int* iters, long long count, long long* acc, hipStream_t s);
-// part[b] = max(part[b], max |g_i| over workgroup b's share), b < absmax_blocks(count): per-
-// workgroup maxima, no atomics (the host reduces them when it reads the stats; zero part before the
-// first call)
+// part[b] = max |g_i| over workgroup b's share, b < absmax_blocks(count), the remaining slots zeroed:
+// per-workgroup maxima, no atomics (the host reduces them when it reads the stats)
 constexpr int kAbsmaxMaxBlocks = 1024;
 // gpad_release_cached: this thread's gpad_solve_sharded group (gpad_group.cpp)
 void release_sharded_cache();

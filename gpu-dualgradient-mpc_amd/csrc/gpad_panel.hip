@@ -1489,6 +1489,12 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
         L.hdrop = DROP && blockIdx.x == 0;  // tests: workgroup 0 drops one post
     }
     if (threadIdx.x < 16) L.gred[threadIdx.x] = 0.0f;
+    if (blockIdx.x == 0) {  // (r06: instead of memset dispatches before the solve)
+        if (a.zero_w)
+            for (int i = threadIdx.x; i < a.zero_n; i += blockDim.x) a.zero_w[i] = 0;
+        if (a.gmax_part && a.v_begin == 0)  // the slots no workgroup of this launch writes
+            for (int i = gridDim.x + threadIdx.x; i < kAbsmaxMaxBlocks; i += blockDim.x) a.gmax_part[i] = 0.0;
+    }
     __syncthreads();
     if constexpr (Handoff<T>::on) {
         using H = Handoff<T>;
@@ -1526,7 +1532,8 @@ __global__ __launch_bounds__(1024) void gpad_panel2_kernel(SolveArgs<float> a) {
         if (a.gmax_part && threadIdx.x == 0) {  // the run's max |g|: this workgroup's slot
             float g = 0.0f;
             for (int i = 0; i < 16; ++i) g = absmax_nan(g, L.gred[i]);
-            a.gmax_part[blockIdx.x] = absmax_nan(a.gmax_part[blockIdx.x], (double)g);
+            // the run's first launch stores (gmax_part note, gpad_internal.h), later phases max in
+            a.gmax_part[blockIdx.x] = a.v_begin == 0 ? (double)g : absmax_nan(a.gmax_part[blockIdx.x], (double)g);
         }
     }
 }
@@ -1940,9 +1947,15 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
     a.seg_cnt = a.seg_idx + a.batch + 32;
     a.idx_out = nullptr;
     a.count_out = nullptr;
-    // the phase counters and the finisher's queue counters (one memset)
-    hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * 2 * kPanelMaxPhases, s);
-    if (e != hipSuccess) return e;
+    // the phase counters and the finisher's queue counters: zeroed by the first launch's workgroup 0
+    // (panel pairs), else one memset
+    hipError_t e = hipSuccess;
+    if constexpr (T > 8) {
+        a.zero_w = counts;
+        a.zero_n = 2 * kPanelMaxPhases;
+    } else if ((e = hipMemsetAsync(counts, 0, sizeof(int) * 2 * kPanelMaxPhases, s)) != hipSuccess) {
+        return e;
+    }
     // phase length: a multiple of the test period (phases end right after a test); default
     // four tests, doubling after 10 phases so a long tail costs O(log N) launches (a phase with
     // no survivors left costs one empty launch, ~5 us)
@@ -1991,6 +2004,7 @@ static hipError_t launch_panel_t(SolveArgs<float> a, hipStream_t s) {
         }
         launch_panel_kernel<T>(a, grid, s);
         if ((e = hipGetLastError()) != hipSuccess) return e;
+        a.zero_w = nullptr;
         v0 = v1;
     }
     return hipSuccess;

@@ -128,7 +128,7 @@ hipError_t launch_accumulate_iters(const int* iters, long long count, long long*
     return hipGetLastError();
 }
 
-// part[b] = max(part[b], max |g_i| of workgroup b) (the certification floor, include/gpad.h
+// part[b] = max |g_i| of workgroup b, the other slots zeroed (the certification floor, include/gpad.h
 // gpad_run): up to 1024 workgroups of 256 threads, 16 elements per thread and pass with the loads of
 // a pass issued together (one pass at the C4 shard), each workgroup reducing through LDS into its
 // own slot.  No atomics: hundreds of same-address atomics serialise at L2 (~30 us per solve
@@ -151,10 +151,12 @@ __global__ __launch_bounds__(256) void absmax_kernel(const T* __restrict__ g, lo
     for (int o = 32; o > 0; o >>= 1) mx = absmax_nan(mx, __shfl_xor(mx, o, 64));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0) {  // (the run's only writer of part: SolveArgs::gmax_part)
         mx = absmax_nan(absmax_nan(red[0], red[1]), absmax_nan(red[2], red[3]));
-        part[blockIdx.x] = absmax_nan(part[blockIdx.x], mx);
+        part[blockIdx.x] = mx;
     }
+    if (blockIdx.x == 0)
+        for (int i = gridDim.x + threadIdx.x; i < kAbsmaxMaxBlocks; i += blockDim.x) part[i] = 0.0;
 }
 
 template <typename T>

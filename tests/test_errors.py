@@ -153,6 +153,25 @@ def test_tol_below_certification_floor_is_flagged(gpu, dtype):
         assert st["tol_floor"] == 0.0 and not st["below_tol_floor"]
 
 
+def test_tol_floor_is_the_current_runs(gpu):
+    """The per-workgroup max |g| slots are not zeroed before a run: its first writer (the panel
+    pairs' first launch, or the absmax kernel) stores them and zeroes the rest.  On one handle, a
+    run with a large |g| followed by smaller ones -- a phased panel solve, then a smaller grid on
+    the absmax path -- must report each run's own floor, never a stale slot."""
+    import gpad_mpc
+    margin = 2.0 ** -20
+    with gpad_mpc.GpadSolver(0) as s:
+        for batch, scale in [(4400, 100.0), (4400, 1.0), (8, 1.0), (4400, 0.5), (8, 3.0)]:
+            ML, G, L, M, g = _shard(batch)
+            g = (g * np.float32(scale)).astype(np.float32)
+            s.setup(ML, G, L, n=200, m=200, batch=batch)
+            z = np.zeros((batch, 200), np.float32)
+            y = np.zeros((batch, 200), np.float32)
+            st = s.run(z, y, M, g, 300, 1e-4)
+            floor = margin * float(np.abs(g.astype(np.float64)).max())
+            assert st["tol_floor"] == pytest.approx(floor, rel=1e-6), (batch, scale, st["tol_floor"], floor)
+
+
 def test_dims_reserved_must_be_zero(gpu):
     import ctypes as C
 
