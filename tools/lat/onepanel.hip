@@ -13,6 +13,12 @@
 //   mode 7: mode 2 + tile 12 as a 3-piece relay on the oldest waves of SIMDs 0-2
 //   mode 8: mode 2 + tile 12 as a 2-piece relay, [0,7) on SIMD 0 then [7,13) on SIMD 1 (oldest waves)
 //   mode 9: mode 2 + tile 12 whole on SIMD 0's oldest wave (no relay: 4 chains there)
+//   mode 10: mode 2 + tile 12 as a LAGGED 4-piece relay (r06): in phase p the oldest waves of SIMDs
+//           0, 1 run pieces [0,3), [3,6) of chain p while those of SIMDs 2, 3 run pieces [6,9), [9,13)
+//           of chain p-1 (the hand-off 1 -> 2 crosses the barrier): a chain's result is due a phase
+//           later, so the phase's sequential path is two pieces, not four
+//   mode 11: mode 1 (singles 3/SIMD) + the lagged relay of mode 10
+//   mode 12: mode 10 without the pieces' raised priority; mode 13: mode 3 without it
 // (relay pieces read their A blocks from registers loaded before the phase's barrier)
 // Bound (modes 1-6): 3 chains x 52 MFMAs x 32 cycles = 4992 cycles per SIMD per phase (modes 3, 4, 6
 // add 13 relay MFMAs per SIMD: 5408).
@@ -88,6 +94,19 @@ template <int MODE>
 __device__ Role role_of(int w) {
     const int s = w & 3, age = w >> 2;  // age 0 = oldest on its SIMD
     const bool relay = MODE == 3 || MODE == 4 || MODE == 6;
+    if (MODE == 13) {
+        if (age == 0) return Role{3, s, 0};
+        if (age == 1) return Role{1, 8 + s, 0};
+        if (age == 2) return Role{2, 2 * s, 2 * s + 1};
+        return Role{0, 0, 0};
+    }
+    if (MODE == 10 || MODE == 11 || MODE == 12) {
+        if (age == 0) return Role{6, s, 0};
+        if (MODE == 11) return Role{1, 3 * s + age - 1, 0};
+        if (age == 1) return Role{1, 8 + s, 0};
+        if (age == 2) return Role{2, 2 * s, 2 * s + 1};
+        return Role{0, 0, 0};
+    }
     if (MODE == 7) {  // double + single per SIMD, 3-piece relay on the oldest waves of SIMDs 0-2
         if (age == 0) return s < 3 ? Role{4, s, 0} : Role{0, 0, 0};
         if (age == 1) return Role{1, 8 + s, 0};
@@ -120,19 +139,19 @@ __device__ Role role_of(int w) {
 template <int MODE>
 __global__ __launch_bounds__(1024) void phases(float* out, const float4* amat) {
     __shared__ float4 bl[T * 64];
-    __shared__ float4 hand[3][64];
-    __shared__ int hflag[3];
+    __shared__ float4 hand[4][64];
+    __shared__ int hflag[4];
     __shared__ float sink[16][64];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int i = threadIdx.x; i < T * 64; i += blockDim.x) bl[i] = make_float4(1e-3f, 2e-3f, 3e-3f, 4e-3f);
-    if (threadIdx.x < 3) hflag[threadIdx.x] = 0;
+    if (threadIdx.x < 4) hflag[threadIdx.x] = 0;
     __syncthreads();
     const Role r = role_of<MODE>(__builtin_amdgcn_readfirstlane(w));
     // relay pieces: their A blocks, loaded before the barrier that precedes each phase
     float4 pre[5];
     auto load_pre = [&]() {
-        if (r.kind == 3 || r.kind == 4) {
-            const int kb0 = r.kind == 3 ? 3 * r.t0 : 4 * r.t0;
+        if (r.kind == 3 || r.kind == 4 || r.kind == 6) {
+            const int kb0 = r.kind == 4 ? 4 * r.t0 : 3 * r.t0;
 #pragma unroll
             for (int i = 0; i < 5; ++i) pre[i] = amat[(size_t)((kb0 + i < T ? kb0 + i : T - 1) * T + 12) * 64 + lane];
         }
@@ -163,6 +182,31 @@ __global__ __launch_bounds__(1024) void phases(float* out, const float4* amat) {
                 __hip_atomic_store(&hflag[0], p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 c0 = f4{0, 0, 0, 0};
             }
+        } else if (r.kind == 6) {  // lagged relay: pieces 0, 1 of chain p, pieces 2, 3 of chain p - 1
+            const int c = r.t0 < 2 ? p : p - 1;  // the chain this piece works on
+            if (c >= 0) {
+                // slots: 0 (piece 0 -> 1), 1 + (c & 1) (1 -> 2, across the barrier), 3 (2 -> 3)
+                const int in = r.t0 == 1 ? 0 : (r.t0 == 2 ? 1 + (c & 1) : 3);
+                if (r.t0 > 0) {
+                    while (__hip_atomic_load(&hflag[in], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != c + 1)
+                        __builtin_amdgcn_s_sleep(1);
+                    const float4 h = hand[in][lane];
+                    c0 = f4{h.x, h.y, h.z, h.w};
+                }
+                if (MODE != 12) __builtin_amdgcn_s_setprio(3);
+                if (r.t0 == 0) piece<0, 3>(pre, bl, lane, c0);
+                if (r.t0 == 1) piece<3, 6>(pre, bl, lane, c0);
+                if (r.t0 == 2) piece<6, 9>(pre, bl, lane, c0);
+                if (r.t0 == 3) piece<9, T>(pre, bl, lane, c0);
+                __builtin_amdgcn_s_setprio(0);
+                if (r.t0 < 3) {
+                    const int out = r.t0 == 0 ? 0 : (r.t0 == 1 ? 1 + (c & 1) : 3);
+                    hand[out][lane] = make_float4(c0.x, c0.y, c0.z, c0.w);
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    __hip_atomic_store(&hflag[out], c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    c0 = f4{0, 0, 0, 0};
+                }
+            }
         } else if (r.kind == 3 || r.kind == 4) {  // tile 12 relayed: 4 pieces [0,3) [3,6) [6,9) [9,13)
             // (kind 3) or 3 pieces [0,4) [4,8) [8,13) (kind 4) on the oldest waves, A loaded ahead
             const int last = r.kind == 3 ? 3 : 2;
@@ -172,7 +216,7 @@ __global__ __launch_bounds__(1024) void phases(float* out, const float4* amat) {
                 const float4 h = hand[r.t0 - 1][lane];
                 c0 = f4{h.x, h.y, h.z, h.w};
             }
-            __builtin_amdgcn_s_setprio(3);
+            if (MODE != 13) __builtin_amdgcn_s_setprio(3);
             if (r.kind == 3) {
                 if (r.t0 == 0) piece<0, 3>(pre, bl, lane, c0);
                 if (r.t0 == 1) piece<3, 6>(pre, bl, lane, c0);
@@ -216,10 +260,12 @@ int main() {
                            "double+single/SIMD, single older (tile 12 skipped)", "mode 2 + 4-piece relay of tile 12",
                            "singles 3/SIMD + 4-piece relay", "double+single, double older (no tile 12)",
                            "mode 5 + 4-piece relay", "double+single + 3-piece relay (SIMDs 0-2)",
-                           "double+single + 2-piece relay [0,7) S0 -> [7,13) S1", "double+single + tile 12 whole on S0"};
+                           "double+single + 2-piece relay [0,7) S0 -> [7,13) S1", "double+single + tile 12 whole on S0",
+                           "double+single + LAGGED 4-piece relay", "singles 3/SIMD + LAGGED 4-piece relay",
+                           "mode 10, pieces at normal priority", "mode 3, pieces at normal priority"};
     float ms = 0;
     for (int rep = 0; rep < 3; ++rep)
-        for (int mode = 0; mode < 10; ++mode) {
+        for (int mode = 0; mode < 14; ++mode) {
             for (int k = 0; k < 2; ++k) {
                 hipEventRecord(e0);
                 switch (mode) {
@@ -233,6 +279,10 @@ int main() {
                     case 7: hipLaunchKernelGGL((phases<7>), dim3(cus), dim3(1024), 0, 0, out, amat); break;
                     case 8: hipLaunchKernelGGL((phases<8>), dim3(cus), dim3(1024), 0, 0, out, amat); break;
                     case 9: hipLaunchKernelGGL((phases<9>), dim3(cus), dim3(1024), 0, 0, out, amat); break;
+                    case 10: hipLaunchKernelGGL((phases<10>), dim3(cus), dim3(1024), 0, 0, out, amat); break;
+                    case 11: hipLaunchKernelGGL((phases<11>), dim3(cus), dim3(1024), 0, 0, out, amat); break;
+                    case 12: hipLaunchKernelGGL((phases<12>), dim3(cus), dim3(1024), 0, 0, out, amat); break;
+                    case 13: hipLaunchKernelGGL((phases<13>), dim3(cus), dim3(1024), 0, 0, out, amat); break;
                 }
                 hipEventRecord(e1);
                 hipEventSynchronize(e1);

@@ -1,7 +1,9 @@
 """Phase schedule sweep for the C4 shard (GPU box): solve time of the planned schedule vs
 unplanned uniform phases x finisher thresholds, one subprocess per setting.
 
-  python3 tools/plan_sweep.py [--reps 6]
+  python3 tools/plan_sweep.py [--reps 6] [--batch 8192] [--fresh] [--takeover]
+--takeover: the planned schedule vs one panel phase to iteration T, then the finisher (T = 230..310;
+C3's shape of schedule at 4096 instances).
 Prints one JSON line per setting: best / median solve ms over the reps (after two warm-up solves).
 """
 from __future__ import annotations
@@ -15,7 +17,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def one(reps, fresh=False):
+def one(reps, fresh=False, B=8192):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "gpu-dualgradient-mpc_amd"))
     import numpy as np
@@ -26,7 +28,7 @@ def one(reps, fresh=False):
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import tune_env  # noqa: F401  (legacy GPAD_* env -> gpad_set_option)
     dev = torch.device("cuda:0")
-    n, m, B = 200, 200, 8192
+    n, m = 200, 200
     ML, G, L, M, g = bench.make_shard(n, m, B, 0)
     f32 = lambda a: torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)  # noqa: E731
     dML, dG, dM, dg = f32(ML), f32(G), f32(M), f32(g)
@@ -57,18 +59,25 @@ def main():
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--one", action="store_true")
     ap.add_argument("--fresh", action="store_true")
+    ap.add_argument("--batch", type=int, default=8192)
+    ap.add_argument("--takeover", action="store_true")
     args = ap.parse_args()
     if args.one:
-        one(args.reps, args.fresh)
+        one(args.reps, args.fresh, args.batch)
         return
     settings = [{}, {"GPAD_NO_LPT": "1"}]
-    for ph in (20, 40, 80, 260):
-        for fin in (512, 1024, 2048, 4096):
-            settings.append({"GPAD_PANEL_NOPLAN": "1", "GPAD_PANEL_PHASE": str(ph), "GPAD_FINISH_THRESH": str(fin)})
+    if args.takeover:
+        for ph in range(230, 320, 10):
+            settings.append({"GPAD_PANEL_NOPLAN": "1", "GPAD_PANEL_PHASE": str(ph), "GPAD_FINISH_THRESH": str(args.batch)})
+    else:
+        for ph in (20, 40, 80, 260):
+            for fin in (512, 1024, 2048, 4096):
+                settings.append({"GPAD_PANEL_NOPLAN": "1", "GPAD_PANEL_PHASE": str(ph), "GPAD_FINISH_THRESH": str(fin)})
     for st in settings:
         env = {k: v for k, v in os.environ.items() if not k.startswith("GPAD_")}
         env.update(st)
-        cmd = [sys.executable, __file__, "--one", "--reps", str(args.reps)] + (["--fresh"] if args.fresh else [])
+        cmd = [sys.executable, __file__, "--one", "--reps", str(args.reps), "--batch", str(args.batch)] + \
+            (["--fresh"] if args.fresh else [])
         subprocess.run(cmd, env=env, check=True)
 
 
