@@ -19,6 +19,10 @@
 //           later, so the phase's sequential path is two pieces, not four
 //   mode 11: mode 1 (singles 3/SIMD) + the lagged relay of mode 10
 //   mode 12: mode 10 without the pieces' raised priority; mode 13: mode 3 without it
+//   mode 14: mode 2 + rows 192..199 on the VALU, lagged: the oldest waves of SIMDs 0, 1 each run 100
+//           fmaf steps of two interleaved chains per lane per phase (128 outputs x 200 steps over
+//           two phases), operands from LDS (A broadcast, B per lane)
+//   mode 15: mode 2 + the same work on the oldest wave of every SIMD: 100 steps of one chain per lane
 // (relay pieces read their A blocks from registers loaded before the phase's barrier)
 // Bound (modes 1-6): 3 chains x 52 MFMAs x 32 cycles = 4992 cycles per SIMD per phase (modes 3, 4, 6
 // add 13 relay MFMAs per SIMD: 5408).
@@ -94,6 +98,12 @@ template <int MODE>
 __device__ Role role_of(int w) {
     const int s = w & 3, age = w >> 2;  // age 0 = oldest on its SIMD
     const bool relay = MODE == 3 || MODE == 4 || MODE == 6;
+    if (MODE == 14 || MODE == 15) {
+        if (age == 0) return (MODE == 15 || s < 2) ? Role{7, s, 0} : Role{0, 0, 0};
+        if (age == 1) return Role{1, 8 + s, 0};
+        if (age == 2) return Role{2, 2 * s, 2 * s + 1};
+        return Role{0, 0, 0};
+    }
     if (MODE == 13) {
         if (age == 0) return Role{3, s, 0};
         if (age == 1) return Role{1, 8 + s, 0};
@@ -142,9 +152,11 @@ __global__ __launch_bounds__(1024) void phases(float* out, const float4* amat) {
     __shared__ float4 hand[4][64];
     __shared__ int hflag[4];
     __shared__ float sink[16][64];
+    __shared__ float4 arow[2][64];  // remainder rows' A values (broadcast reads)
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int i = threadIdx.x; i < T * 64; i += blockDim.x) bl[i] = make_float4(1e-3f, 2e-3f, 3e-3f, 4e-3f);
     if (threadIdx.x < 4) hflag[threadIdx.x] = 0;
+    if (threadIdx.x < 128) arow[threadIdx.x >> 6][threadIdx.x & 63] = make_float4(1e-3f, -2e-3f, 3e-3f, -4e-3f);
     __syncthreads();
     const Role r = role_of<MODE>(__builtin_amdgcn_readfirstlane(w));
     // relay pieces: their A blocks, loaded before the barrier that precedes each phase
@@ -182,6 +194,24 @@ __global__ __launch_bounds__(1024) void phases(float* out, const float4* amat) {
                 __hip_atomic_store(&hflag[0], p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 c0 = f4{0, 0, 0, 0};
             }
+        } else if (r.kind == 7) {  // VALU remainder: 100 steps per phase, 2 chains (mode 14) or 1 (15)
+            float x0 = c0.x, x1 = c0.y;
+#pragma unroll 5
+            for (int k4 = 0; k4 < 25; ++k4) {
+                const float4 a0 = arow[0][k4], b0 = bl[k4 * 64 + lane];
+                x0 = __builtin_fmaf(a0.x, b0.x, x0);
+                x0 = __builtin_fmaf(a0.y, b0.y, x0);
+                x0 = __builtin_fmaf(a0.z, b0.z, x0);
+                x0 = __builtin_fmaf(a0.w, b0.w, x0);
+                if (MODE == 14) {
+                    const float4 a1 = arow[1][k4], b1 = bl[(k4 + 25) * 64 + lane];
+                    x1 = __builtin_fmaf(a1.x, b1.x, x1);
+                    x1 = __builtin_fmaf(a1.y, b1.y, x1);
+                    x1 = __builtin_fmaf(a1.z, b1.z, x1);
+                    x1 = __builtin_fmaf(a1.w, b1.w, x1);
+                }
+            }
+            c0 = f4{x0, x1, 0.0f, 0.0f};
         } else if (r.kind == 6) {  // lagged relay: pieces 0, 1 of chain p, pieces 2, 3 of chain p - 1
             const int c = r.t0 < 2 ? p : p - 1;  // the chain this piece works on
             if (c >= 0) {
@@ -262,10 +292,11 @@ int main() {
                            "mode 5 + 4-piece relay", "double+single + 3-piece relay (SIMDs 0-2)",
                            "double+single + 2-piece relay [0,7) S0 -> [7,13) S1", "double+single + tile 12 whole on S0",
                            "double+single + LAGGED 4-piece relay", "singles 3/SIMD + LAGGED 4-piece relay",
-                           "mode 10, pieces at normal priority", "mode 3, pieces at normal priority"};
+                           "mode 10, pieces at normal priority", "mode 3, pieces at normal priority",
+                           "mode 2 + VALU rows 192..199, 2 waves x 2 chains", "mode 2 + VALU rows 192..199, 4 waves x 1 chain"};
     float ms = 0;
     for (int rep = 0; rep < 3; ++rep)
-        for (int mode = 0; mode < 14; ++mode) {
+        for (int mode = 0; mode < 16; ++mode) {
             for (int k = 0; k < 2; ++k) {
                 hipEventRecord(e0);
                 switch (mode) {
@@ -283,6 +314,8 @@ int main() {
                     case 11: hipLaunchKernelGGL((phases<11>), dim3(cus), dim3(1024), 0, 0, out, amat); break;
                     case 12: hipLaunchKernelGGL((phases<12>), dim3(cus), dim3(1024), 0, 0, out, amat); break;
                     case 13: hipLaunchKernelGGL((phases<13>), dim3(cus), dim3(1024), 0, 0, out, amat); break;
+                    case 14: hipLaunchKernelGGL((phases<14>), dim3(cus), dim3(1024), 0, 0, out, amat); break;
+                    case 15: hipLaunchKernelGGL((phases<15>), dim3(cus), dim3(1024), 0, 0, out, amat); break;
                 }
                 hipEventRecord(e1);
                 hipEventSynchronize(e1);
