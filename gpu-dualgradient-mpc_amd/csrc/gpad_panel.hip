@@ -1785,25 +1785,43 @@ __global__ __launch_bounds__(1024) void phase_compact_kernel(const int* __restri
     __shared__ int pcnt[kCompactMaxPanels];
     __shared__ int total_l;
     const int tid = threadIdx.x;
+    // the thread -> panel runs from the batch's panel count, so the per-panel counts load together
+    // with count_prev (one round trip, not two); panels past the previous phase's count as 0
+    const int pmax = (batch + 15) / 16;
+    const int per = (pmax + 1023) / 1024;
+    const int p0 = tid * per < pmax ? tid * per : pmax, p1 = p0 + per < pmax ? p0 + per : pmax;
+    constexpr int kPer = 8;  // counts held in registers per thread (pmax <= 8192 panels)
+    int cl[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) cl[u] = (per <= kPer && p0 + u < p1) ? seg_cnt[p0 + u] : 0;
     const int prev = count_prev ? *count_prev : batch;
     if (count_prev && prev <= fin_prev) {  // the finisher took the previous list: nothing was listed
         if (tid == 0) *count_out = 0;
         return;
     }
     const int panels = (prev + 15) / 16;
-    const int per = (panels + 1023) / 1024;
-    const int p0 = tid * per < panels ? tid * per : panels, p1 = p0 + per < panels ? p0 + per : panels;
     const bool lds_bases = panels <= kCompactMaxPanels;
+    const int q1 = p1 < panels ? p1 : panels;  // this thread's panels of the previous phase: [p0, q1)
     int sum = 0;
-    for (int p = p0; p < p1; ++p) {
-        const int c = seg_cnt[p];
-        if (lds_bases) pcnt[p] = c;
-        sum += c;
+    if (per <= kPer) {
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            if (p0 + u < q1) {
+                if (lds_bases) pcnt[p0 + u] = cl[u];
+                sum += cl[u];
+            }
+        }
+    } else {
+        for (int p = p0; p < q1; ++p) {
+            const int c = seg_cnt[p];
+            if (lds_bases) pcnt[p] = c;
+            sum += c;
+        }
     }
     int base = block_scan_1024(part, tid, sum);
     if (tid == 1023) total_l = base + sum;
     if (lds_bases) {
-        for (int p = p0; p < p1; ++p) {
+        for (int p = p0; p < q1; ++p) {
             const int c = pcnt[p];
             pbase[p] = c ? base : -1;
             base += c;
@@ -1835,7 +1853,7 @@ __global__ __launch_bounds__(1024) void phase_compact_kernel(const int* __restri
                 if (at[u] >= 0) dst[at[u]] = v[u];
         }
     } else {
-        for (int p = p0; p < p1; ++p) {
+        for (int p = p0; p < q1; ++p) {
             const int c = seg_cnt[p];
             for (int r = 0; r < c; ++r) dst[base + r] = seg_idx[16 * p + r];
             base += c;
