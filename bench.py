@@ -806,7 +806,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    # untimed: the shader clock ramps over the first ~10 solves after an idle box (3.0 -> 3.2 ms per
+    # fresh-input C4 solve, profiles/r06_timeline_fresh_solves.txt); the timed steps are steady state
+    ap.add_argument("--warmup", type=int, default=12)
     ap.add_argument("--batch", type=int, default=8192, help="instances per GPU")
     ap.add_argument("--horizon", type=int, default=50)
     ap.add_argument("--nu", type=int, default=4)
