@@ -195,10 +195,11 @@ def test_panel_phased_compaction_bitexact(gpu, oracle, grid, phase, fin, tol, N,
     L = np.float32(qp.L)
     rng = np.random.default_rng(1)
     z0 = (0.1 * rng.normal(size=(B, n))).astype(np.float32)  # warm starts: exercises the u seed
-    z, y, st, iters = run_gpu(ML, M, G, g, L, N, tol=tol, kernel="panel", z0=z0, opts=opts)
+    y0 = np.abs(0.1 * rng.normal(size=(B, m))).astype(np.float32)  # and every state load per instance
+    z, y, st, iters = run_gpu(ML, M, G, g, L, N, tol=tol, kernel="panel", z0=z0, y0=y0, opts=opts)
     assert st["kernel"] == "panel"
     for b in range(B):
-        zo, yo, it, _ = oracle.solve_f32(z0[b], np.zeros(m), ML, M[b], G, g[b], N, L, tol)
+        zo, yo, it, _ = oracle.solve_f32(z0[b], y0[b], ML, M[b], G, g[b], N, L, tol)
         assert iters[b] == it, b
         assert_bitexact(z[b], zo, f"instance {b} z")
         assert_bitexact(y[b], yo, f"instance {b} y")
