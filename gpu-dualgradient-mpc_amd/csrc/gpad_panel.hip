@@ -817,15 +817,10 @@ __device__ __forceinline__ void rows4(const float* base, int t, int rows, int la
     }
 }
 
-// The waves of a workgroup are co-resident, so a post always arrives unless the layout logic is
-// broken; the wait is still bounded (2^20 sleeps, ~30 ms) so that such a bug cannot hang the GPU,
-// and an expired wait is recorded (L.herr) and ORed into the run's error word when the workgroup
-// exits (gpad_panel2_kernel): the host then fails the run with GPAD_ERR_DEVICE instead of
-// returning the stale accumulator's results as GPAD_OK.  Nothing of this sits on the hand-off's
-// own path: the record is made only after the bound expired.
-// The reverse of rows4: this lane's rows 16t + 4r + j to an instance's vector, on lanes whose `on`
-// holds (uniform over a column's four lanes); vec: through the same LDS block into one 16-B store per
-// lane of rows 16t + 4j .. +3 (every lane takes part in the transpose; rows past `rows` not stored).
+// The reverse of the loads above: this lane's rows 16t + 4r + j to an instance's vector, on lanes
+// whose `on` holds (uniform over a column's four lanes); vec: transposed through the wave's LDS block
+// into one 16-B store per lane of rows 16t + 4j .. +3 (every lane takes part in the transpose; rows
+// past `rows` not stored).
 __device__ __forceinline__ void rows4_store(float* base, int t, int rows, bool vec, float* st, int lane,
                                             const float (&v)[4], bool on) {
     const int j = lane >> 4, c = lane & 15, sw = (c >> 2) & 3;
@@ -848,6 +843,12 @@ __device__ __forceinline__ void rows4_store(float* base, int t, int rows, bool v
     }
 }
 
+// The waves of a workgroup are co-resident, so a post always arrives unless the layout logic is
+// broken; the wait is still bounded (2^20 sleeps, ~30 ms) so that such a bug cannot hang the GPU,
+// and an expired wait is recorded (L.herr) and ORed into the run's error word when the workgroup
+// exits (gpad_panel2_kernel): the host then fails the run with GPAD_ERR_DEVICE instead of
+// returning the stale accumulator's results as GPAD_OK.  Nothing of this sits on the hand-off's
+// own path: the record is made only after the bound expired.
 template <int T>
 __device__ __forceinline__ f32x4 handoff_wait(Panel2Lds<T>& L, int slot, int gen, int lane) {
     for (int s = 0;; ++s) {
