@@ -540,3 +540,42 @@ def test_separate_gap_tolerance_bitexact(gpu, oracle, kernel, tol, tol_gap):
         assert iters[b] == it, b
         assert_bitexact(z[b], zo, f"{b} z")
         assert_bitexact(y[b], yo, f"{b} y")
+
+
+def test_panel_phased_beyond_lds_compaction_bitexact(gpu, oracle):
+    """A phased solve whose first boundary lists more panels than the compaction keeps in LDS
+    (> kCompactMaxPanels = 8192, i.e. > 131072 instances; > 8 panels per compaction thread): the
+    global-memory compaction path.  Two solves on one handle (default schedule, then planned);
+    a sample of instances, the ragged last panel included, must match the oracle exactly, counts
+    included, and every instance must converge."""
+    import gpad_mpc
+    from gpad_mpc import problems
+    n = m = 136  # T = 9 panel pairs
+    B = 140003
+    base = problems.synthetic_qp(n, m, batch=1, seed=21)
+    ML, G = base.ML.astype(np.float32), base.G.astype(np.float32)
+    L = np.float32(base.L)
+    rng = np.random.default_rng(22)
+    Hinv = np.linalg.inv(base.H)
+    M = (rng.normal(0.0, 1.0, size=(B, n)) @ Hinv.T).astype(np.float32)
+    zf = rng.uniform(-0.5, 0.5, size=(B, n))
+    g = (zf @ base.G.T + rng.uniform(0.1, 1.0, size=(B, m))).astype(np.float32)
+    sample = np.unique(np.concatenate([rng.choice(B, 40, replace=False), np.arange(B - 8, B)]))
+    import torch
+    dev = torch.device("cuda:0")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    dM, dg = t(M), t(g)
+    with gpad_mpc.GpadSolver(0) as s:
+        s.setup(t(ML), t(G), float(L), n=n, m=m, batch=B)
+        for _ in range(2):
+            z = torch.zeros(B, n, device=dev)
+            y = torch.zeros(B, m, device=dev)
+            iters = np.zeros(B, np.int32)
+            st = s.run(z, y, dM, dg, 3000, 1e-4, iters=iters)
+            assert st["kernel"] == "panel" and st["converged"] == B, st
+            zh, yh = z.cpu().numpy(), y.cpu().numpy()
+            for b in sample:
+                zo, yo, it, _ = oracle.solve_f32(np.zeros(n), np.zeros(m), ML, M[b], G, g[b], 3000, L, 1e-4)
+                assert iters[b] == it, b
+                assert_bitexact(zh[b], zo, f"instance {b} z")
+                assert_bitexact(yh[b], yo, f"instance {b} y")
