@@ -82,20 +82,21 @@ __device__ __forceinline__ void duo_refill(const SolveArgs<float>& a, const DuoC
     s.x0 = s.x1 = s.x2 = 0.0f;
     const bool has = p < c.count;
     if (has) {
-        const size_t b = (size_t)__builtin_amdgcn_readfirstlane(a.idx_in ? a.idx_in[p] : p);
+        KernArgs& A = kargs();  // (kargs: no argument kept live across the loop)
+        const size_t b = (size_t)__builtin_amdgcn_readfirstlane(A.idx_in ? A.idx_in[p] : p);
         const int o4 = 4 * c.row;
         if (c.isA) {
             if (c.live) {
-                s.x0 = row_ld(a.z, b, c.n, o4);
-                gp_l[c.row] = row_ld(a.gP, b, a.ld_gP, o4);
+                s.x0 = row_ld(A.z, b, c.n, o4);
+                gp_l[c.row] = row_ld(A.gP, b, A.ld_gP, o4);
                 if (c.fresh && c.use_tol) z_l[c.row] = s.x0;
             }
         } else if (c.live) {
-            const float yv = row_ld(a.y, b, c.m, o4);
+            const float yv = row_ld(A.y, b, c.m, o4);
             s.x0 = yv;
-            pd_l[c.row] = (float)(a.gscale * (double)row_ld(a.g, b, a.ld_g, o4));
-            s.x1 = c.fresh ? __builtin_fmaf(a.beta[0], yv - yv, yv) : row_ld(a.wc, b, c.m, o4);
-            if (c.use_tol && !c.fresh) s.x2 = row_ld(a.uc, b, c.m, o4);
+            pd_l[c.row] = (float)(A.gscale * (double)row_ld(A.g, b, A.ld_g, o4));
+            s.x1 = c.fresh ? __builtin_fmaf(A.beta[0], yv - yv, yv) : row_ld(A.wc, b, c.m, o4);
+            if (c.use_tol && !c.fresh) s.x2 = row_ld(A.uc, b, c.m, o4);
             w_l[c.row] = s.x1;
         }
     }
@@ -231,14 +232,15 @@ __device__ __forceinline__ void duo_post_b(const SolveArgs<float>& a, const DuoC
         done = check_code(st1, verified);
     }
     if (done || v >= c.N) {
-        const size_t b = (size_t)__builtin_amdgcn_readfirstlane(a.idx_in ? a.idx_in[sb.pos] : sb.pos);
+        KernArgs& A = kargs();  // (kargs: no argument kept live across the loop)
+        const size_t b = (size_t)__builtin_amdgcn_readfirstlane(A.idx_in ? A.idx_in[sb.pos] : sb.pos);
         if (c.live) {
-            if (c.isA) row_st(a.z, b, c.n, 4 * c.row, done == 2 ? sb.x1 : sb.x0);  // (B) certifies zhat
-            else row_st(a.y, b, c.m, 4 * c.row, sb.x0);
+            if (c.isA) row_st(A.z, b, c.n, 4 * c.row, done == 2 ? sb.x1 : sb.x0);  // (B) certifies zhat
+            else row_st(A.y, b, c.m, 4 * c.row, sb.x0);
         }
         if (c.tid == 0) {
-            a.iters[b] = v;
-            a.conv[b] = done;
+            A.iters[b] = v;
+            A.conv[b] = done;
         }
         duo_claim<KB, K>(a, c, sb, claim_b, wb_l, gpb_l, pdb_l, z_l, r);
     }

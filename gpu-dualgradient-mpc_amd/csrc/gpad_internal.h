@@ -154,7 +154,20 @@ bool panel_folds_gmax(int n, int m);
 // panels appending to one counter serialise at L2, ~25 us per boundary at 512 panels measured).
 // Without it (flat panels) the survivors are appended through a.count_out.  Every
 // panel of a phase calls it, parked or not, so no slot keeps a stale count.
-__device__ __forceinline__ void list_survivors(const SolveArgs<float>& a, int P, bool park, int inst, int lane,
+// A kernel's SolveArgs read afresh from its kernarg segment -- only in kernels whose one argument is
+// a SolveArgs<float> (gpad_panel2_kernel, gpad_duo_kernel).  The pointer passes an empty asm, so the
+// fields loaded through it at a rare site (refills, results out, park, survivor lists, a panel's
+// state loads) are not kept live in SGPRs across the solve loop: loaded once at the top, the dozen
+// row-array pointers spilled to VGPR lanes and were reloaded (v_readlane) around every step.
+typedef const __attribute__((address_space(4))) SolveArgs<float> KernArgs;
+__device__ __forceinline__ KernArgs& kargs() {
+    KernArgs* p = (KernArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *p;
+}
+
+template <class Args>
+__device__ __forceinline__ void list_survivors(const Args& a, int P, bool park, int inst, int lane,
                                                int j) {
     const unsigned long long lv = __ballot(park && j == 0);
     const int rank = (int)__popcll(lv & ((1ull << lane) - 1ull));

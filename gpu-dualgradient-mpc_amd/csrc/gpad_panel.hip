@@ -969,10 +969,12 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
             if constexpr (NU == 0) continue;
             const int k = 16 * (pair ? 2 * it + p0 + q : it) + c;
             act[q] = k < count;
-            inst[q] = a.idx_in ? a.idx_in[act[q] ? k : 0] : (act[q] ? k : 0);
+            KernArgs& A = kargs();
+            inst[q] = A.idx_in ? A.idx_in[act[q] ? k : 0] : (act[q] ? k : 0);
         }
         if constexpr (NU > 0) {
-            const float beta0 = a.beta[0];
+            KernArgs& A = kargs();  // (gpad_internal.h: the row pointers are not kept across the loop)
+            const float beta0 = A.beta[0];
             const bool vec = vec_io;
             // vec (r06): the operands arrive by LDS-DMA (rows4_dma), every panel's in flight at once:
             // z, gP, y, g into the wave's (panel, tile) blocks of Zh, Gp, Wl, Pd, then (carried
@@ -988,10 +990,10 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                     asm volatile("" : "+v"(ln));  // (offsets formed per item, not kept across the item loop)
                     const size_t bc = (size_t)__shfl(inst[q], ln >> 2);
                     const int pq = p0 + q;
-                    rows4_dma(a.z + bc * n, t, n, ln, &L.Zh[pq][64 * t]);
-                    rows4_dma(a.gP + bc * a.ld_gP, t, n, ln, &L.Gp[pq][64 * t]);
-                    rows4_dma(a.y + bc * m, t, m, ln, &L.Wl[pq][64 * t]);
-                    rows4_dma(a.g + bc * a.ld_g, t, m, ln, &L.Pd[pq][64 * t]);
+                    rows4_dma(A.z + bc * n, t, n, ln, &L.Zh[pq][64 * t]);
+                    rows4_dma(A.gP + bc * A.ld_gP, t, n, ln, &L.Gp[pq][64 * t]);
+                    rows4_dma(A.y + bc * m, t, m, ln, &L.Wl[pq][64 * t]);
+                    rows4_dma(A.g + bc * A.ld_g, t, m, ln, &L.Pd[pq][64 * t]);
                 }
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __builtin_amdgcn_wave_barrier();
@@ -1009,10 +1011,10 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                     rows4_rd(&L.Wl[pq][64 * t], ln, yl);
                     rows4_rd(&L.Pd[pq][64 * t], ln, gl);
                 } else {
-                    rows4(a.z + b * n, t, n, ln, zl);
-                    rows4(a.gP + b * a.ld_gP, t, n, ln, gpl);
-                    rows4(a.y + b * m, t, m, ln, yl);
-                    rows4(a.g + b * a.ld_g, t, m, ln, gl);
+                    rows4(A.z + b * n, t, n, ln, zl);
+                    rows4(A.gP + b * A.ld_gP, t, n, ln, gpl);
+                    rows4(A.y + b * m, t, m, ln, yl);
+                    rows4(A.g + b * A.ld_g, t, m, ln, gl);
                 }
                 float gp[4], pd[4], wv[4];
 #pragma unroll
@@ -1023,7 +1025,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                     gp[r] = okn ? gpl[r] : 0.0f;
                     y[q][r] = okm ? yl[r] : 0.0f;
                     const float gr = okm ? gl[r] : 0.0f;
-                    pd[r] = (float)(a.gscale * (double)gr);
+                    pd[r] = (float)(A.gscale * (double)gr);
                     gmx = absmax_nan(gmx, gr);
                     // w_0 = y_0 + beta_0 (y_0 - y_{-1}), y_{-1} = y_0 (fresh; carried: wc below)
                     wv[r] = __builtin_fmaf(beta0, y[q][r] - y[q][r], y[q][r]);
@@ -1037,8 +1039,8 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 } else if (vec) {  // round two: wc, uc into the blocks just read
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                     const size_t bc = (size_t)__shfl(inst[q], ln >> 2);
-                    rows4_dma(a.wc + bc * m, t, m, ln, &L.Zh[pq][64 * t]);
-                    if (use_tol) rows4_dma(a.uc + bc * m, t, m, ln, &L.Wl[pq][64 * t]);
+                    rows4_dma(A.wc + bc * m, t, m, ln, &L.Zh[pq][64 * t]);
+                    if (use_tol) rows4_dma(A.uc + bc * m, t, m, ln, &L.Wl[pq][64 * t]);
                 }
             }
             if (!fresh) {
@@ -1057,8 +1059,8 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                         rows4_rd(&L.Zh[pq][64 * t], ln, wl);
                         if (use_tol) rows4_rd(&L.Wl[pq][64 * t], ln, ul);
                     } else {
-                        rows4(a.wc + b * m, t, m, ln, wl);
-                        if (use_tol) rows4(a.uc + b * m, t, m, ln, ul);
+                        rows4(A.wc + b * m, t, m, ln, wl);
+                        if (use_tol) rows4(A.uc + b * m, t, m, ln, ul);
                     }
                     float wv[4];
 #pragma unroll
@@ -1390,12 +1392,13 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                     const size_t b = (size_t)iq;
                     float* const st = reinterpret_cast<float*>(&L.Zh[p0 + q][64 * t]);
                     const bool zw = cd[q] != 2 || zh_out;  // (B)'s zhat already out before (A)'s GEMM
-                    rows4_store(a.z + b * n, t, n, vec_io, st, ln, zo[q], out[q] && zw);
-                    rows4_store(a.y + b * m, t, m, vec_io, st, ln, y[q], out[q]);
+                    KernArgs& A = kargs();
+                    rows4_store(A.z + b * n, t, n, vec_io, st, ln, zo[q], out[q] && zw);
+                    rows4_store(A.y + b * m, t, m, vec_io, st, ln, y[q], out[q]);
                     if (out[q]) {
                         if (t == 0 && j == 0) {
-                            a.iters[iq] = v;
-                            a.conv[iq] = cd[q];
+                            A.iters[iq] = v;
+                            A.conv[iq] = cd[q];
                         }
                         act[q] = false;
                     }
@@ -1430,17 +1433,18 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                     asm volatile("" : "+v"(iq), "+v"(ln));  // (no hoisted row pointers / offsets: rows4 note)
                     const size_t b = (size_t)iq;
                     float* const st = reinterpret_cast<float*>(&L.Zh[p0 + q][64 * t]);
-                    rows4_store(a.z + b * n, t, n, vec_io, st, ln, z[q], pk[q]);
-                    rows4_store(a.y + b * m, t, m, vec_io, st, ln, y[q], pk[q]);
-                    rows4_store(a.wc + b * m, t, m, vec_io, st, ln, wv[q], pk[q]);
-                    if (use_tol) rows4_store(a.uc + b * m, t, m, vec_io, st, ln, u[q], pk[q]);
+                    KernArgs& A = kargs();
+                    rows4_store(A.z + b * n, t, n, vec_io, st, ln, z[q], pk[q]);
+                    rows4_store(A.y + b * m, t, m, vec_io, st, ln, y[q], pk[q]);
+                    rows4_store(A.wc + b * m, t, m, vec_io, st, ln, wv[q], pk[q]);
+                    if (use_tol) rows4_store(A.uc + b * m, t, m, vec_io, st, ln, u[q], pk[q]);
                 }
                 if (t == 0) {  // the tile-0 owner of each panel lists its survivors
 #pragma unroll
                     for (int q = 0; q < Q; ++q) {
                         int iq = inst[q], ln = lane;
                         asm volatile("" : "+v"(iq), "+v"(ln));
-                        list_survivors(a, pair ? 2 * it + p0 + q : it, pk[q], iq, ln, ln >> 4);
+                        list_survivors(kargs(), pair ? 2 * it + p0 + q : it, pk[q], iq, ln, ln >> 4);
                     }
                 }
             }
