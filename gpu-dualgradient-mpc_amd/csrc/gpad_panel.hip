@@ -1306,10 +1306,24 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                 float4 red;
                 double gq;
                 panel2_reduce<T>(L.slots, lane, red, gq);
+                // the pair layout re-reads the test's doubles here (kargs) rather than keeping them
+                // in SGPRs across the loop: fewer spilled SGPRs reloaded in its loop (the one-panel
+                // roles keep them: re-reading moved their spills to scratch)
+                double tL, ttol, ttg;
+                if constexpr (KQ > 0) {
+                    KernArgs& A = kargs();
+                    tL = A.L;
+                    ttol = A.tol;
+                    ttg = A.tol_gap;
+                } else {
+                    tL = a.L;
+                    ttol = a.tol;
+                    ttg = a.tol_gap;
+                }
                 if (lane < 32 && ((live >> lane) & 1u))
-                    st1 = ((double)red.x * a.L <= a.tol ? 1 : 0) |
-                          ((viol_ok((double)red.y, (double)red.z, a.L, a.tol, ViolMargin<float>::value) &&
-                            (red.w >= 0.0f) && (gq * a.L <= a.tol_gap)) ? 2 : 0);
+                    st1 = ((double)red.x * tL <= ttol ? 1 : 0) |
+                          ((viol_ok((double)red.y, (double)red.z, tL, ttol, ViolMargin<float>::value) &&
+                            (red.w >= 0.0f) && (gq * tL <= ttg)) ? 2 : 0);
                 const unsigned mA = (unsigned)__ballot(st1 & 1);
                 m2 = (unsigned)__ballot(st1 & 2);
                 GPAD_PSTAMP_END(7);
@@ -1361,7 +1375,7 @@ __device__ __forceinline__ void panel2_run(const SolveArgs<float>& a, Panel2Lds<
                     double vgap;
                     panel2_reduce<T>(L.slots, lane, vred, vgap);
                     if (lane < 32 && ((mA >> lane) & 1u))
-                        ver = viol_ok((double)vred.x, (double)vred.z, a.L, a.tol, ViolMargin<float>::value);
+                        ver = viol_ok((double)vred.x, (double)vred.z, tL, ttol, ViolMargin<float>::value);
                     m1 = (unsigned)__ballot(ver);
                     m2 &= ~m1;
                 }
