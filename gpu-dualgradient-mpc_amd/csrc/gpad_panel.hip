@@ -676,14 +676,17 @@ __device__ __forceinline__ void panel2_reduce(const PanelSlot2 (&S)[2][T], int l
     gap = 0.0;
 #pragma unroll
     for (int s2 = 0; s2 < H; ++s2) {
-        if (lo + s2 < hi) {
-            const float4 e = S[pp][lo + s2].f[cc];
-            f.x = fmaxf(f.x, e.x);
-            f.y = fmaxf(f.y, e.y);
-            f.z = fmaxf(f.z, e.z);
-            f.w = fminf(f.w, e.w);
-            gap += S[pp][lo + s2].gap[cc];
-        }
+        // every step but the last is in range on both halves (2H - 2 <= T - 1): no per-lane branch,
+        // whose exec masks the compiler kept in spilled SGPRs; the last step selects
+        const bool ok = s2 < H - 1 || lo + s2 < hi;
+        const int si = ok ? lo + s2 : lo;
+        const float4 e = S[pp][si].f[cc];
+        const double gv = S[pp][si].gap[cc];
+        f.x = ok ? fmaxf(f.x, e.x) : f.x;
+        f.y = ok ? fmaxf(f.y, e.y) : f.y;
+        f.z = ok ? fmaxf(f.z, e.z) : f.z;
+        f.w = ok ? fminf(f.w, e.w) : f.w;
+        gap = ok ? gap + gv : gap;
     }
     f.x = bfly<32>(f.x, OpMax{});  // (gfx950 v_permlane32_swap, gpad_chain.h)
     f.y = bfly<32>(f.y, OpMax{});
