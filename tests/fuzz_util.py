@@ -1,0 +1,150 @@
+"""Randomised parity cases: the HIP path through the C-ABI against the oracle on random shapes,
+batch sizes, kernels, modes, test periods, warm starts, schedule options and repeated solves on
+one handle (the planner then follows the previous solve's counts).  Bar: z*, y* and per-instance
+iteration counts bit-identical to oracle/gpad_oracle.c (which restates seq_functions.cpp:45-87
+and acceldualgrad.m's Algorithm 1).
+
+Used by tests/test_fuzz.py (a fixed seed, a few cases per run) and tools/fuzz_parity.py (many
+seeds, on the GPU box).  Test infrastructure only: the oracle is the checker here."""
+from __future__ import annotations
+
+import numpy as np
+
+SPECIAL = [1, 2, 15, 16, 17, 63, 64, 65, 127, 128, 129, 191, 192, 193, 199, 200, 201, 207, 208, 209, 240, 256]
+BATCHES = [1, 2, 3, 15, 16, 17, 31, 33, 100, 257, 1000, 1025, 2049, 4097, 8191]
+
+
+def draw_case(rng: np.random.Generator) -> dict:
+    """One random configuration (plain dict, JSON-printable)."""
+    def dim():
+        return int(rng.choice(SPECIAL)) if rng.random() < 0.5 else int(rng.integers(1, 261))
+    n, m = dim(), dim()
+    big = max(n, m) <= 208
+    batch = int(rng.choice([b for b in BATCHES if big or b <= 1025]))
+    shared = bool(batch == 1 or rng.random() < 0.85 or batch > 64)
+    kernels = ["auto", "auto", "panel", "stream"] + (["resident"] if max(n, m) <= 208 else [])
+    kernel = str(rng.choice(kernels))
+    if kernel == "panel" and not shared:
+        kernel = "auto"
+    tol_mode = bool(rng.random() < 0.6)
+    cfg = dict(n=n, m=m, batch=batch, shared=shared, kernel=kernel, seed=int(rng.integers(1 << 30)),
+               warm=bool(rng.random() < 0.3), device=bool(rng.random() < 0.5),
+               solves=int(rng.integers(1, 4)), check_every=int(rng.choice([1, 2, 5, 10, 10, 10, 16])))
+    if tol_mode:
+        cfg.update(N=2000, tol=float(rng.choice([1e-2, 1e-3, 1e-4, 1e-4])))
+    else:
+        cfg.update(N=int(rng.integers(1, 151)), tol=0.0)
+    opts = {}
+    if rng.random() < 0.3:
+        opts["phase_len"] = int(rng.choice([10, 20, 40, 100]))
+    if rng.random() < 0.2:
+        opts["finish_thresh"] = int(rng.choice([0, 64, 512, 100000]))
+    if rng.random() < 0.15:
+        opts["duo_max_grid"] = int(rng.choice([1, 3, 17]))
+    if rng.random() < 0.1:
+        opts["lpt"] = 0
+    cfg["opts"] = opts
+    # fp64 (the reference MATLAB precision): shared matrices, the stream kernel or the f64 panels
+    cfg["f64"] = bool(shared and rng.random() < 0.2)
+    if cfg["f64"] and (kernel == "resident" or (kernel == "panel" and (not tol_mode or max(n, m) > 256))):
+        cfg["kernel"] = "auto"
+    return cfg
+
+
+def _problem(cfg: dict):
+    """The case's matrices and the q/b of every solve: shared matrices draw batch x solves
+    instances at once (fresh q/b per solve on the same plant); per-instance matrices repeat."""
+    from gpad_mpc import problems
+    B, n, m, S = cfg["batch"], cfg["n"], cfg["m"], cfg["solves"]
+    nb = B * S if cfg["shared"] else B
+    qp = problems.synthetic_qp(n, m, batch=nb, seed=cfg["seed"], shared=cfg["shared"])
+    dt = np.float64 if cfg.get("f64") else np.float32
+    f = lambda a: np.ascontiguousarray(np.asarray(a, np.float64).astype(dt))  # noqa: E731
+    return f(qp.ML), f(qp.G), f(qp.M).reshape(nb, n), f(qp.g).reshape(nb, m), dt(qp.L)
+
+
+def run_case(cfg: dict, oracle, sample: int = 24, threads: int = 8) -> dict:
+    """Solve cfg["solves"] fresh batches on one handle; check a sample of every batch's instances
+    (first, last and random ones) bit for bit -- fp64 cases: counts equal to the fp64 oracle and
+    z*, y* within 1e-11 norm-relative (acceldualgrad.m's elementwise order differs from the
+    fp32 path's in the last bit).  Returns {"ok": bool, "checked": k, "why": ...}."""
+    import torch
+
+    import gpad_mpc
+    from gpad_mpc import _lib
+    B, n, m = cfg["batch"], cfg["n"], cfg["m"]
+    kc = {"auto": _lib.KERNEL_AUTO, "stream": _lib.KERNEL_STREAM, "resident": _lib.KERNEL_RESIDENT,
+          "panel": _lib.KERNEL_PANEL}[cfg["kernel"]]
+    rng = np.random.default_rng(cfg["seed"])
+    dev = torch.device("cuda:0")
+    checked, kernels = 0, []
+    ML, G, Mall, gall, Lk = _problem(cfg)
+    with gpad_mpc.GpadSolver(0) as s:
+        put = (lambda a: torch.from_numpy(a).to(dev)) if cfg["device"] else (lambda a: a)  # noqa: E731
+        s.setup(put(ML), put(G), float(Lk), n=n, m=m, batch=B, shared=cfg["shared"], kernel=kc,
+                check_every=cfg["check_every"])
+        s.set_options(**cfg["opts"])
+        for k in range(cfg["solves"]):
+            o = k * B if cfg["shared"] else 0
+            M, g = np.ascontiguousarray(Mall[o:o + B]), np.ascontiguousarray(gall[o:o + B])
+            if cfg["warm"]:
+                z0 = rng.uniform(-0.5, 0.5, (B, n)).astype(ML.dtype)
+                y0 = np.maximum(rng.normal(0.0, 0.3, (B, m)), 0.0).astype(ML.dtype)
+            else:
+                z0 = np.zeros((B, n), ML.dtype)
+                y0 = np.zeros((B, m), ML.dtype)
+            iters = np.zeros(B, np.int32)
+            if cfg["device"]:
+                zt, yt = torch.from_numpy(z0.copy()).to(dev), torch.from_numpy(y0.copy()).to(dev)
+                st = s.run(zt, yt, put(M), put(g), cfg["N"], cfg["tol"], iters=iters)
+                z, y = zt.cpu().numpy(), yt.cpu().numpy()
+            else:
+                z, y = z0.copy(), y0.copy()
+                st = s.run(z, y, M, g, cfg["N"], cfg["tol"], iters=iters)
+            kernels.append(st["kernel"])
+            pick = sorted(set([0, B - 1] + [int(i) for i in rng.integers(0, B, min(sample, B))]))
+            if cfg.get("f64"):
+                Zo, Yo, Io = [], [], []
+                for b in pick:
+                    zo, yo, it, _ = oracle.solve_f64(z0[b], y0[b], ML, M[b], G, g[b], cfg["N"], float(Lk),
+                                                     cfg["tol"], cfg["check_every"])
+                    Zo.append(zo)
+                    Yo.append(yo)
+                    Io.append(it)
+                Zo, Yo, Io = np.array(Zo), np.array(Yo), np.array(Io)
+            elif cfg["shared"]:
+                O = oracle
+                MGneg, GL, _ = O.scale(ML, G, g[0], Lk)
+                PD = O.scale_vec(g[pick], Lk)
+                Zo, Yo, Io, _ = O.solve_batch_f32(z0[pick], y0[pick], MGneg, M[pick], GL, PD, cfg["N"], Lk,
+                                                  cfg["tol"], cfg["check_every"], shared=True, threads=threads)
+            else:
+                Zo, Yo, Io = [], [], []
+                for b in pick:
+                    zo, yo, it, _ = oracle.solve_f32(z0[b], y0[b], ML[b], M[b], G[b], g[b], cfg["N"], Lk,
+                                                     cfg["tol"], cfg["check_every"])
+                    Zo.append(zo)
+                    Yo.append(yo)
+                    Io.append(it)
+                Zo, Yo, Io = np.array(Zo), np.array(Yo), np.array(Io)
+            for j, b in enumerate(pick):
+                exp_it = int(Io[j]) if cfg["tol"] > 0 else cfg["N"]
+                if cfg["tol"] > 0 and int(iters[b]) != exp_it:
+                    return dict(ok=False, checked=checked, kernels=kernels,
+                                why=f"solve {k} instance {b}: {int(iters[b])} iterations, oracle {exp_it}")
+                for what, a, o in (("z", z[b], Zo[j]), ("y", y[b], Yo[j])):
+                    if cfg.get("f64"):
+                        e = np.linalg.norm(a - o) / max(np.linalg.norm(o), 1e-300)
+                        if e > 1e-11:
+                            return dict(ok=False, checked=checked, kernels=kernels,
+                                        why=f"solve {k} instance {b} {what}: f64 norm-relative {e:.3g}")
+                        continue
+                    if not np.array_equal(a, o):
+                        d = np.abs(a.astype(np.float64) - o.astype(np.float64))
+                        return dict(ok=False, checked=checked, kernels=kernels,
+                                    why=f"solve {k} instance {b} {what}: {int((d > 0).sum())} of {a.size} differ, "
+                                        f"max {d.max():.3g} (kernel {st['kernel']})")
+                checked += 1
+            if cfg["tol"] > 0 and st["total_iterations"] != int(iters.sum()):
+                return dict(ok=False, checked=checked, kernels=kernels, why="total_iterations != sum of counts")
+    return dict(ok=True, checked=checked, kernels=kernels)

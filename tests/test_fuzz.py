@@ -1,0 +1,36 @@
+"""Randomised parity (tests/fuzz_util.py): random shapes, batch sizes, kernels, fixed-N and
+Algorithm-1 modes, test periods, warm starts, schedule options, host / device memory and
+repeated solves on one handle, each checked bit for bit (z*, y*, iteration counts) against the
+oracle on a sample of instances.  A fixed seed here; tools/fuzz_parity.py runs many more."""
+from __future__ import annotations
+
+import json
+
+import numpy as np
+import pytest
+
+import fuzz_util
+
+SEED = 20261018
+CASES = 12
+
+
+def test_fuzz_cases_are_deterministic_and_valid():
+    a = [fuzz_util.draw_case(np.random.default_rng(SEED + i)) for i in range(50)]
+    b = [fuzz_util.draw_case(np.random.default_rng(SEED + i)) for i in range(50)]
+    assert json.dumps(a) == json.dumps(b)
+    for c in a:
+        assert 1 <= c["n"] <= 260 and 1 <= c["m"] <= 260 and c["batch"] >= 1
+        assert c["kernel"] != "resident" or max(c["n"], c["m"]) <= 208
+        assert c["kernel"] != "panel" or c["shared"]
+        assert (c["tol"] > 0) == (c["N"] == 2000)
+        assert not c["f64"] or (c["shared"] and c["kernel"] != "resident")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("i", range(CASES))
+def test_fuzz_parity(gpu, oracle, i):
+    cfg = fuzz_util.draw_case(np.random.default_rng(SEED + i))
+    r = fuzz_util.run_case(cfg, oracle)
+    assert r["ok"], f"{json.dumps(cfg)}: {r['why']}"
+    assert r["checked"] >= min(cfg["batch"], 2) * cfg["solves"]

@@ -1,0 +1,44 @@
+"""Randomised parity campaign on the GPU box (tests/fuzz_util.py): R random configurations
+from seed S, each solved through the C-ABI and checked bit for bit against the oracle on a
+sample of instances; one JSON line per case, a summary line last.
+  python3 tools/fuzz_parity.py [--seed S] [--cases R] [--sample K] [--budget-s T]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "gpu-dualgradient-mpc_amd"), os.path.join(ROOT, "oracle"),
+          os.path.join(ROOT, "tests")):
+    sys.path.insert(0, p)
+import fuzz_util  # noqa: E402
+import pyoracle  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--seed", type=int, default=1)
+ap.add_argument("--cases", type=int, default=200)
+ap.add_argument("--sample", type=int, default=24)
+ap.add_argument("--budget-s", type=float, default=400.0)
+args = ap.parse_args()
+if not os.path.exists(pyoracle.LIB):
+    pyoracle.build(ref=False)
+O = pyoracle.Oracle()
+t0, fails, done, checked = time.time(), 0, 0, 0
+for i in range(args.cases):
+    if time.time() - t0 > args.budget_s:
+        break
+    cfg = fuzz_util.draw_case(np.random.default_rng(args.seed + i))
+    t = time.time()
+    try:
+        r = fuzz_util.run_case(cfg, O, sample=args.sample, threads=16)
+    except Exception as e:  # a library error is a finding too
+        r = dict(ok=False, checked=0, why=f"{type(e).__name__}: {e}")
+    done += 1
+    checked += r["checked"]
+    fails += not r["ok"]
+    print(json.dumps(dict(case=i, s=round(time.time() - t, 2), cfg=cfg, **r)), flush=True)
+print(json.dumps(dict(summary=True, seed=args.seed, cases=done, failed=fails, instances_checked=checked,
+                      seconds=round(time.time() - t0, 1))), flush=True)
