@@ -124,6 +124,14 @@ def load(path: str | None = None) -> C.CDLL:
     if not os.path.exists(path):
         raise ImportError(f"libgpad.so not built at {path}: run `make -C gpu-dualgradient-mpc_amd` "
                           "(or __graft_entry__.build()); there is no CPU fallback")
+    # One HIP runtime per process.  PyTorch-ROCm ships its own libamdhip64 / libhsa-runtime64: with
+    # torch loaded first, libgpad's libamdhip64.so.7 dependency binds to torch's copy; with libgpad
+    # loaded first (it links /opt/rocm's), a later `import torch` maps a second HIP + HSA runtime pair
+    # and torch then sees no GPU ("No HIP GPUs are available", found by tools/fuzz_parity.py).
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # plain-C / numpy callers: /opt/rocm's runtime
+        pass
     L = C.CDLL(path)
     tolerant = os.environ.get("GPAD_LIB_TOLERANT") == "1"
     if tolerant:  # A/B runs may load an older build: bind what it exports

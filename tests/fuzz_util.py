@@ -1,6 +1,6 @@
 """Randomised parity cases: the HIP path through the C-ABI against the oracle on random shapes,
-batch sizes, kernels, modes, test periods, warm starts, schedule options and repeated solves on
-one handle (the planner then follows the previous solve's counts).  Bar: z*, y* and per-instance
+batch sizes, kernels, modes, test periods, warm starts, schedule options, the multi-device group
+API (shards over a repeated device) and repeated solves on one handle (the planner then follows the previous solve's counts).  Bar: z*, y* and per-instance
 iteration counts bit-identical to oracle/gpad_oracle.c (which restates seq_functions.cpp:45-87
 and acceldualgrad.m's Algorithm 1).
 
@@ -46,6 +46,8 @@ def draw_case(rng: np.random.Generator) -> dict:
     cfg["opts"] = opts
     # fp64 (the reference MATLAB precision): shared matrices, the stream kernel or the f64 panels
     cfg["f64"] = bool(shared and rng.random() < 0.2)
+    # the multi-device group API over repeated device 0 (peer-copy shards): 2 or 3 shards
+    cfg["group"] = int(rng.choice([0, 0, 0, 0, 0, 0, 2, 3])) if batch >= 2 else 0
     if cfg["f64"] and (kernel == "resident" or (kernel == "panel" and (not tol_mode or max(n, m) > 256))):
         cfg["kernel"] = "auto"
     return cfg
@@ -79,11 +81,13 @@ def run_case(cfg: dict, oracle, sample: int = 24, threads: int = 8) -> dict:
     dev = torch.device("cuda:0")
     checked, kernels = 0, []
     ML, G, Mall, gall, Lk = _problem(cfg)
-    with gpad_mpc.GpadSolver(0) as s:
+    grp = cfg.get("group", 0)
+    with (gpad_mpc.GpadGroup([0] * grp) if grp else gpad_mpc.GpadSolver(0)) as s:
         put = (lambda a: torch.from_numpy(a).to(dev)) if cfg["device"] else (lambda a: a)  # noqa: E731
         s.setup(put(ML), put(G), float(Lk), n=n, m=m, batch=B, shared=cfg["shared"], kernel=kc,
                 check_every=cfg["check_every"])
-        s.set_options(**cfg["opts"])
+        if not grp:  # (a group takes its shards' defaults)
+            s.set_options(**cfg["opts"])
         for k in range(cfg["solves"]):
             o = k * B if cfg["shared"] else 0
             M, g = np.ascontiguousarray(Mall[o:o + B]), np.ascontiguousarray(gall[o:o + B])
@@ -101,7 +105,7 @@ def run_case(cfg: dict, oracle, sample: int = 24, threads: int = 8) -> dict:
             else:
                 z, y = z0.copy(), y0.copy()
                 st = s.run(z, y, M, g, cfg["N"], cfg["tol"], iters=iters)
-            kernels.append(st["kernel"])
+            kernels.append(st.get("kernel", "group") if not grp else f"group{grp}")
             pick = sorted(set([0, B - 1] + [int(i) for i in rng.integers(0, B, min(sample, B))]))
             if cfg.get("f64"):
                 Zo, Yo, Io = [], [], []

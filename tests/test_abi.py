@@ -215,3 +215,19 @@ def test_rccl_library_override_cpu():
         assert lib.gpad_group_rccl_library(stub.encode(), 1) == _lib.GPAD_OK
     finally:
         lib.gpad_group_rccl_library(None, 0)
+
+
+def test_one_hip_runtime_whatever_the_import_order():
+    """Loading libgpad before `import torch` must not map a second HIP / HSA runtime pair (torch then
+    finds no GPU): _lib.load() brings torch's runtime in first, so libgpad binds to it."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from gpad_mpc import _lib\n_lib.load()\nimport torch\n"
+            "maps = open('/proc/self/maps').read().splitlines()\n"
+            "libs = sorted(set(l.split()[-1] for l in maps if 'libamdhip64' in l or 'libhsa-runtime64' in l))\n"
+            "print(len([x for x in libs if 'amdhip64' in x]), len([x for x in libs if 'hsa-runtime64' in x]))\n"
+            % PKG)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.split() == ["1", "1"], out.stdout

@@ -1,7 +1,7 @@
 """Randomised parity campaign on the GPU box (tests/fuzz_util.py): R random configurations
 from seed S, each solved through the C-ABI and checked bit for bit against the oracle on a
 sample of instances; one JSON line per case, a summary line last.
-  python3 tools/fuzz_parity.py [--seed S] [--cases R] [--sample K] [--budget-s T]"""
+  python3 tools/fuzz_parity.py [--seed S] [--cases R] [--sample K] [--budget-s T] [--rccl-stub]"""
 import argparse
 import json
 import os
@@ -22,7 +22,13 @@ ap.add_argument("--seed", type=int, default=1)
 ap.add_argument("--cases", type=int, default=200)
 ap.add_argument("--sample", type=int, default=24)
 ap.add_argument("--budget-s", type=float, default=400.0)
+ap.add_argument("--rccl-stub", action="store_true",
+                help="group cases through the RCCL transport (tests/rccl_stub, one GPU standing in for each rank)")
 args = ap.parse_args()
+if args.rccl_stub:
+    from gpad_mpc import _lib
+    so = os.path.join(ROOT, "tests", "rccl_stub", "librccl_stub.so")
+    _lib.check(_lib.load().gpad_group_rccl_library(so.encode(), 1), "gpad_group_rccl_library")
 if not os.path.exists(pyoracle.LIB):
     pyoracle.build(ref=False)
 O = pyoracle.Oracle()
@@ -40,5 +46,5 @@ for i in range(args.cases):
     checked += r["checked"]
     fails += not r["ok"]
     print(json.dumps(dict(case=i, s=round(time.time() - t, 2), cfg=cfg, **r)), flush=True)
-print(json.dumps(dict(summary=True, seed=args.seed, cases=done, failed=fails, instances_checked=checked,
+print(json.dumps(dict(summary=True, seed=args.seed, rccl_stub=args.rccl_stub, cases=done, failed=fails, instances_checked=checked,
                       seconds=round(time.time() - t0, 1))), flush=True)
