@@ -143,7 +143,7 @@ def run_case(cfg: dict, oracle, sample: int = 24, threads: int = 8) -> dict:
                             return dict(ok=False, checked=checked, kernels=kernels,
                                         why=f"solve {k} instance {b} {what}: f64 norm-relative {e:.3g}")
                         continue
-                    if not np.array_equal(a, o):
+                    if not np.array_equal(a, o, equal_nan=True):  # (infeasible draws diverge to NaN in both)
                         d = np.abs(a.astype(np.float64) - o.astype(np.float64))
                         return dict(ok=False, checked=checked, kernels=kernels,
                                     why=f"solve {k} instance {b} {what}: {int((d > 0).sum())} of {a.size} differ, "
@@ -151,4 +151,92 @@ def run_case(cfg: dict, oracle, sample: int = 24, threads: int = 8) -> dict:
                 checked += 1
             if cfg["tol"] > 0 and st["total_iterations"] != int(iters.sum()):
                 return dict(ok=False, checked=checked, kernels=kernels, why="total_iterations != sum of counts")
+    return dict(ok=True, checked=checked, kernels=kernels)
+
+
+def draw_flat_case(rng: np.random.Generator) -> dict:
+    """A random flat battery case (gpad_setup_flat; seq_functions.cpp:5-43's data): n_u cells over
+    a horizon N (n = n_u N, m = 4 n_u N + 2N), a scenario batch on one plant."""
+    n_u = int(rng.choice([1, 2, 3, 4, 4, 5, 8, 16]))
+    Nh = int(rng.integers(1, 61 if n_u <= 8 else 13))
+    batch = int(rng.choice([1, 2, 5, 16, 17, 49, 100, 257, 1025, 4097]))
+    cfg = dict(flat=True, n_u=n_u, Nh=Nh, batch=batch, seed=int(rng.integers(1 << 30)),
+               kernel=str(rng.choice(["auto", "auto", "panel", "stream"])), warm=bool(rng.random() < 0.3),
+               device=bool(rng.random() < 0.5), solves=int(rng.integers(1, 3)),
+               check_every=int(rng.choice([1, 5, 10, 10])))
+    if rng.random() < 0.6:
+        cfg.update(N=3000, tol=float(rng.choice([1e-3, 1e-4])))
+    else:
+        cfg.update(N=int(rng.integers(1, 121)), tol=0.0)
+    opts = {}
+    if rng.random() < 0.3:
+        opts["flat_panels"] = int(rng.choice([1, 2, 3, 4]))
+    elif rng.random() < 0.15:
+        opts["flat_waves"] = 8
+    if rng.random() < 0.3:
+        opts["phased"] = int(rng.choice([0, 2]))
+    if rng.random() < 0.3:
+        opts["phase_len"] = int(rng.choice([10, 20, 30]))
+    cfg["opts"] = opts
+    return cfg
+
+
+def run_flat_case(cfg: dict, oracle, sample: int = 16) -> dict:
+    """Flat battery solves on one handle (fresh initial states per solve) against the oracle's flat
+    solve (orc_solve_flat_f32) on a sample of instances: z*, y*, counts bit for bit."""
+    import torch
+
+    import gpad_mpc
+    from gpad_mpc import _lib, problems
+    n_u, Nh, B, S = cfg["n_u"], cfg["Nh"], cfg["batch"], cfg["solves"]
+    kc = {"auto": _lib.KERNEL_AUTO, "stream": _lib.KERNEL_STREAM, "panel": _lib.KERNEL_PANEL}[cfg["kernel"]]
+    rng = np.random.default_rng(cfg["seed"])
+    qp = problems.battery_scenarios(n_u, Nh, B * S, seed=cfg["seed"])
+    MGf, GLf, L = problems.flatten_battery(qp, n_u, Nh)
+    f32 = lambda a: np.ascontiguousarray(np.asarray(a, np.float64).astype(np.float32))  # noqa: E731
+    L32 = np.float32(L)
+    MGf32, GLf32 = f32(MGf), f32(GLf)
+    GPall = f32(qp.M).reshape(B * S, -1)
+    PDall = np.ascontiguousarray(oracle.scale_vec(f32(qp.g).reshape(B * S, -1), L32))
+    n, m = GPall.shape[1], PDall.shape[1]
+    dev = torch.device("cuda:0")
+    put = (lambda a: torch.from_numpy(a).to(dev)) if cfg["device"] else (lambda a: a)  # noqa: E731
+    checked, kernels = 0, []
+    with gpad_mpc.GpadSolver(0) as s:
+        s.setup_flat(put(MGf32), put(GLf32), float(L32), n_u=n_u, batch=B, kernel=kc,
+                     check_every=cfg["check_every"])
+        s.set_options(**cfg["opts"])
+        for k in range(S):
+            GP = np.ascontiguousarray(GPall[k * B:(k + 1) * B])
+            PD = np.ascontiguousarray(PDall[k * B:(k + 1) * B])
+            if cfg["warm"]:
+                z0 = rng.uniform(-0.5, 0.5, (B, n)).astype(np.float32)
+                y0 = np.maximum(rng.normal(0.0, 0.3, (B, m)), 0.0).astype(np.float32)
+            else:
+                z0 = np.zeros((B, n), np.float32)
+                y0 = np.zeros((B, m), np.float32)
+            iters = np.zeros(B, np.int32)
+            if cfg["device"]:
+                zt, yt = torch.from_numpy(z0.copy()).to(dev), torch.from_numpy(y0.copy()).to(dev)
+                st = s.run(zt, yt, put(GP), put(PD), cfg["N"], cfg["tol"], scaled=True, iters=iters)
+                z, y = zt.cpu().numpy(), yt.cpu().numpy()
+            else:
+                z, y = z0.copy(), y0.copy()
+                st = s.run(z, y, GP, PD, cfg["N"], cfg["tol"], scaled=True, iters=iters)
+            kernels.append(st["kernel"])
+            pick = sorted(set([0, B - 1] + [int(i) for i in rng.integers(0, B, min(sample, B))]))
+            for b in pick:
+                zo, yo, it, _ = oracle.solve_flat_f32(z0[b], y0[b], MGf32, GP[b], GLf32, PD[b], n_u, cfg["N"], L32,
+                                                      cfg["tol"], cfg["check_every"])
+                exp_it = int(it) if cfg["tol"] > 0 else cfg["N"]
+                if cfg["tol"] > 0 and int(iters[b]) != exp_it:
+                    return dict(ok=False, checked=checked, kernels=kernels,
+                                why=f"flat solve {k} instance {b}: {int(iters[b])} iterations, oracle {exp_it}")
+                for what, a, o in (("z", z[b], zo), ("y", y[b], yo)):
+                    if not np.array_equal(a, o, equal_nan=True):  # (infeasible draws diverge to NaN in both)
+                        d = np.abs(a.astype(np.float64) - o.astype(np.float64))
+                        return dict(ok=False, checked=checked, kernels=kernels,
+                                    why=f"flat solve {k} instance {b} {what}: {int((d > 0).sum())} of {a.size} "
+                                        f"differ, max {d.max():.3g} (kernel {st['kernel']})")
+                checked += 1
     return dict(ok=True, checked=checked, kernels=kernels)

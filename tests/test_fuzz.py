@@ -34,3 +34,20 @@ def test_fuzz_parity(gpu, oracle, i):
     r = fuzz_util.run_case(cfg, oracle)
     assert r["ok"], f"{json.dumps(cfg)}: {r['why']}"
     assert r["checked"] >= min(cfg["batch"], 2) * cfg["solves"]
+
+
+FLAT_CASES = 6
+
+
+def test_flat_fuzz_cases_are_valid():
+    for i in range(50):
+        c = fuzz_util.draw_flat_case(np.random.default_rng(SEED + i))
+        assert 1 <= c["n_u"] <= 16 and 1 <= c["Nh"] <= 60 and c["kernel"] in ("auto", "panel", "stream")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("i", range(FLAT_CASES))
+def test_flat_fuzz_parity(gpu, oracle, i):
+    cfg = fuzz_util.draw_flat_case(np.random.default_rng(SEED + 100 + i))
+    r = fuzz_util.run_flat_case(cfg, oracle)
+    assert r["ok"], f"{json.dumps(cfg)}: {r['why']}"
