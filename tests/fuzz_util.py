@@ -240,3 +240,88 @@ def run_flat_case(cfg: dict, oracle, sample: int = 16) -> dict:
                                         f"differ, max {d.max():.3g} (kernel {st['kernel']})")
                 checked += 1
     return dict(ok=True, checked=checked, kernels=kernels)
+
+
+def draw_value_case(rng: np.random.Generator) -> dict:
+    """Algorithm 1 with the value-function branches (gpad_setup_hessian; acceldualgrad.m:73,76):
+    the feasible point shifted away from 0 so both branches occur; f32 on the stream kernel, f64 on
+    the stream kernel or the f64 panels."""
+    f64 = bool(rng.random() < 0.5)
+    n = int(rng.choice([1, 2, 8, 16, 17, 20, 40, 64, 65, 100, 129, 200, 208, 256]))
+    m = int(rng.choice([1, 3, 16, 33, 40, 64, 100, 127, 200, 256]))
+    batch = int(rng.choice([1, 2, 16, 17, 64, 257, 1025, 4097]))
+    kernel = str(rng.choice(["auto", "stream"] + (["panel"] if f64 and max(n, m) <= 256 else [])))
+    tol = float(rng.choice([1e-2, 1e-3, 1e-4]))
+    return dict(value=True, f64=f64, n=n, m=m, batch=batch, kernel=kernel, seed=int(rng.integers(1 << 30)),
+                shift=float(rng.choice([0.0, 1.0, 3.0])), tol=tol,
+                tol_gap=float(tol * rng.choice([1.0, 10.0])), check_every=int(rng.choice([1, 5, 10])),
+                N=int(rng.choice([3000, 20000 if f64 else 5000])), device=bool(rng.random() < 0.5))
+
+
+def _value_problem(cfg: dict):
+    """H = R'R + I, G ~ N(0, 1/n), b = G z_f + U(0.1, 1) with z_f ~ U(shift, shift + 1), q ~ N(0, 0.1),
+    shared H, G; per-instance q, b (tests/test_value.py's generator, restated)."""
+    n, m, B = cfg["n"], cfg["m"], cfg["batch"]
+    rng = np.random.default_rng(cfg["seed"])
+    R = rng.normal(0, 1 / np.sqrt(n), (n, n))
+    H = R.T @ R + np.eye(n)
+    G = rng.normal(0, 1 / np.sqrt(n), (m, n))
+    Hi = np.linalg.inv(H)
+    ML = Hi @ G.T
+    L = float(np.linalg.norm(G @ ML, "fro"))
+    zf = rng.uniform(cfg["shift"], cfg["shift"] + 1, (B, n))
+    Q = rng.normal(0, 0.1, (B, n))
+    g = zf @ G.T + rng.uniform(0.1, 1.0, (B, m))
+    dt = np.float64 if cfg["f64"] else np.float32
+    c = lambda a: np.ascontiguousarray(np.asarray(a, np.float64).astype(dt))  # noqa: E731
+    return c(H), c(ML), c(Q @ Hi.T), c(G), c(g), (float(L) if cfg["f64"] else np.float32(L))
+
+
+def run_value_case(cfg: dict, oracle, sample: int = 16) -> dict:
+    """Counts and termination codes equal to the oracle's value-branch solve on a sample of
+    instances; z*, y* bit-identical (f32) or within 1e-11 norm-relative (f64)."""
+    import torch
+
+    import gpad_mpc
+    from gpad_mpc import _lib
+    n, m, B = cfg["n"], cfg["m"], cfg["batch"]
+    kc = {"auto": _lib.KERNEL_AUTO, "stream": _lib.KERNEL_STREAM, "panel": _lib.KERNEL_PANEL}[cfg["kernel"]]
+    H, ML, M, G, g, L = _value_problem(cfg)
+    dev = torch.device("cuda:0")
+    put = (lambda a: torch.from_numpy(a).to(dev)) if cfg["device"] else (lambda a: a)  # noqa: E731
+    z0 = np.zeros((B, n), ML.dtype)
+    y0 = np.zeros((B, m), ML.dtype)
+    iters = np.zeros(B, np.int32)
+    codes = np.full(B, -1, np.int32)
+    with gpad_mpc.GpadSolver(0) as s:
+        s.setup(put(ML), put(G), float(L), n=n, m=m, batch=B, kernel=kc, check_every=cfg["check_every"],
+                tol_gap=cfg["tol_gap"])
+        s.setup_hessian(put(H))
+        if cfg["device"]:
+            zt, yt = put(z0.copy()), put(y0.copy())
+            st = s.run(zt, yt, put(M), put(g), cfg["N"], cfg["tol"], iters=iters, codes=codes)
+            z, y = zt.cpu().numpy(), yt.cpu().numpy()
+        else:
+            z, y = z0.copy(), y0.copy()
+            st = s.run(z, y, M, g, cfg["N"], cfg["tol"], iters=iters, codes=codes)
+    rng = np.random.default_rng(cfg["seed"] + 1)
+    pick = sorted(set([0, B - 1] + [int(i) for i in rng.integers(0, B, min(sample, B))]))
+    solve = oracle.solve_value_f64 if cfg["f64"] else oracle.solve_value_f32
+    checked = 0
+    for b in pick:
+        zo, yo, ito, co = solve(z0[b], y0[b], ML, M[b], G, g[b], H, cfg["N"], L, cfg["tol"],
+                                check_every=cfg["check_every"], tol_gap=cfg["tol_gap"])
+        if (int(iters[b]), int(codes[b])) != (int(ito), int(co)):
+            return dict(ok=False, checked=checked, kernels=[st["kernel"]],
+                        why=f"instance {b}: (iterations, code) {(int(iters[b]), int(codes[b]))}, oracle {(ito, co)}")
+        for what, a, o in (("z", z[b], zo), ("y", y[b], yo)):
+            if cfg["f64"]:
+                e = np.linalg.norm(a - o) / max(np.linalg.norm(o), 1e-300)
+                bad = e > 1e-11
+            else:
+                bad = not np.array_equal(a, o, equal_nan=True)
+            if bad:
+                return dict(ok=False, checked=checked, kernels=[st["kernel"]],
+                            why=f"instance {b} {what} differs (kernel {st['kernel']})")
+        checked += 1
+    return dict(ok=True, checked=checked, kernels=[st["kernel"]], codes=sorted(set(int(c) for c in codes)))

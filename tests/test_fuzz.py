@@ -51,3 +51,14 @@ def test_flat_fuzz_parity(gpu, oracle, i):
     cfg = fuzz_util.draw_flat_case(np.random.default_rng(SEED + 100 + i))
     r = fuzz_util.run_flat_case(cfg, oracle)
     assert r["ok"], f"{json.dumps(cfg)}: {r['why']}"
+
+
+VALUE_CASES = 6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("i", range(VALUE_CASES))
+def test_value_fuzz_parity(gpu, oracle, i):
+    cfg = fuzz_util.draw_value_case(np.random.default_rng(SEED + 200 + i))
+    r = fuzz_util.run_value_case(cfg, oracle)
+    assert r["ok"], f"{json.dumps(cfg)}: {r['why']}"

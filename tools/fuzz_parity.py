@@ -23,6 +23,7 @@ ap.add_argument("--cases", type=int, default=200)
 ap.add_argument("--sample", type=int, default=24)
 ap.add_argument("--budget-s", type=float, default=400.0)
 ap.add_argument("--flat", type=float, default=0.25, help="share of flat battery cases")
+ap.add_argument("--value", type=float, default=0.0, help="share of value-branch (H bound) cases")
 ap.add_argument("--rccl-stub", action="store_true",
                 help="group cases through the RCCL transport (tests/rccl_stub, one GPU standing in for each rank)")
 args = ap.parse_args()
@@ -38,12 +39,18 @@ for i in range(args.cases):
     if time.time() - t0 > args.budget_s:
         break
     rng = np.random.default_rng(args.seed + i)
-    flat = rng.random() < args.flat
-    cfg = fuzz_util.draw_flat_case(rng) if flat else fuzz_util.draw_case(rng)
+    u = rng.random()
+    kind = "flat" if u < args.flat else ("value" if u < args.flat + args.value else "full")
+    cfg = {"flat": fuzz_util.draw_flat_case, "value": fuzz_util.draw_value_case,
+           "full": fuzz_util.draw_case}[kind](rng)
     t = time.time()
     try:
-        r = (fuzz_util.run_flat_case(cfg, O, sample=min(args.sample, 16)) if flat
-             else fuzz_util.run_case(cfg, O, sample=args.sample, threads=16))
+        if kind == "flat":
+            r = fuzz_util.run_flat_case(cfg, O, sample=min(args.sample, 16))
+        elif kind == "value":
+            r = fuzz_util.run_value_case(cfg, O, sample=min(args.sample, 16))
+        else:
+            r = fuzz_util.run_case(cfg, O, sample=args.sample, threads=16)
     except Exception as e:  # a library error is a finding too
         r = dict(ok=False, checked=0, why=f"{type(e).__name__}: {e}")
     done += 1
