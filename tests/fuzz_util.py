@@ -48,6 +48,11 @@ def draw_case(rng: np.random.Generator) -> dict:
     cfg["f64"] = bool(shared and rng.random() < 0.2)
     # the multi-device group API over repeated device 0 (peer-copy shards): 2 or 3 shards
     cfg["group"] = int(rng.choice([0, 0, 0, 0, 0, 0, 2, 3])) if batch >= 2 else 0
+    # the north-star one-shot gpad_solve (one cached handle per thread, reused across cases: the
+    # cache compares contents, shapes and options); one solve, default options
+    cfg["oneshot"] = bool(not cfg["group"] and rng.random() < 0.2)
+    if cfg["oneshot"]:
+        cfg["solves"], cfg["opts"] = 1, {}
     if cfg["f64"] and (kernel == "resident" or (kernel == "panel" and (not tol_mode or max(n, m) > 256))):
         cfg["kernel"] = "auto"
     return cfg
@@ -82,6 +87,8 @@ def run_case(cfg: dict, oracle, sample: int = 24, threads: int = 8) -> dict:
     checked, kernels = 0, []
     ML, G, Mall, gall, Lk = _problem(cfg)
     grp = cfg.get("group", 0)
+    if cfg.get("oneshot"):
+        return _run_oneshot(cfg, oracle, ML, G, Mall, gall, Lk, kc, sample)
     with (gpad_mpc.GpadGroup([0] * grp) if grp else gpad_mpc.GpadSolver(0)) as s:
         put = (lambda a: torch.from_numpy(a).to(dev)) if cfg["device"] else (lambda a: a)  # noqa: E731
         s.setup(put(ML), put(G), float(Lk), n=n, m=m, batch=B, shared=cfg["shared"], kernel=kc,
@@ -325,3 +332,112 @@ def run_value_case(cfg: dict, oracle, sample: int = 16) -> dict:
                             why=f"instance {b} {what} differs (kernel {st['kernel']})")
         checked += 1
     return dict(ok=True, checked=checked, kernels=[st["kernel"]], codes=sorted(set(int(c) for c in codes)))
+
+
+def draw_loop_case(rng: np.random.Generator) -> dict:
+    """The closed-loop MPC runner (gpad_closed_loop, gpad.m:79-95): a battery plant of n_u cells over
+    a horizon N, a batch of packs from random states, several receding-horizon steps."""
+    n_u = int(rng.integers(1, 5))
+    Nh = int(rng.integers(2, 13))
+    tol_mode = bool(rng.random() < 0.5)
+    kernels = ["auto", "auto", "panel", "stream"] + (["resident"] if 4 * n_u * Nh + 2 * Nh <= 208 else [])
+    return dict(loop=True, n_u=n_u, Nh=Nh, batch=int(rng.choice([1, 3, 17, 64, 300, 1100, 4100])),
+                steps=int(rng.integers(1, 11)), N=(2000 if tol_mode else int(rng.integers(1, 121))),
+                tol=(float(rng.choice([1e-3, 1e-4])) if tol_mode else 0.0), warm=bool(rng.random() < 0.5),
+                kernel=str(rng.choice(kernels)), device=bool(rng.random() < 0.5), seed=int(rng.integers(1 << 30)))
+
+
+def run_loop_case(cfg: dict, oracle, sample: int = 6) -> dict:
+    """Every trajectory value, final state, z*, y* and per-step count of a sample of packs bit for
+    bit against the oracle's closed loop (orc_closed_loop_f32)."""
+    import torch
+
+    import gpad_mpc
+    from gpad_mpc import _lib, problems
+    n_u, B, S = cfg["n_u"], cfg["batch"], cfg["steps"]
+    qp, pl = problems.battery_plant(n_u, cfg["Nh"])
+    f32 = lambda a: np.ascontiguousarray(np.asarray(a, np.float64).astype(np.float32))  # noqa: E731
+    kc = {"auto": _lib.KERNEL_AUTO, "stream": _lib.KERNEL_STREAM, "panel": _lib.KERNEL_PANEL,
+          "resident": _lib.KERNEL_RESIDENT}[cfg["kernel"]]
+    dev = torch.device("cuda:0")
+    put = (lambda a: torch.from_numpy(f32(a)).to(dev)) if cfg["device"] else f32  # noqa: E731
+    rng = np.random.default_rng(cfg["seed"])
+    X0 = (rng.random((B, n_u)) - 0.5).astype(np.float32)
+    L = np.float32(qp.L)
+    with gpad_mpc.GpadSolver(0) as s:
+        s.setup(put(qp.ML), put(qp.G), float(L), n=qp.n, m=qp.m, batch=B, shared=True, kernel=kc)
+        s.setup_plant(put(pl.PM), put(pl.Pg), g0=put(pl.g0), A=put(pl.A), B=put(pl.B))
+        IT = np.zeros(S * B, np.int32)
+        if cfg["device"]:
+            X, Z, Y = put(X0), torch.zeros(B, qp.n, device=dev), torch.zeros(B, qp.m, device=dev)
+            XS, US = torch.zeros(S, B, n_u, device=dev), torch.zeros(S, B, n_u, device=dev)
+            st = s.closed_loop(X, Z, Y, S, cfg["N"], cfg["tol"], warm=cfg["warm"], xs=XS, us=US, iters=IT)
+            X, Z, Y, XS, US = (a.cpu().numpy() for a in (X, Z, Y, XS, US))
+        else:
+            X, Z, Y = X0.copy(), np.zeros((B, qp.n), np.float32), np.zeros((B, qp.m), np.float32)
+            XS, US = np.zeros((S, B, n_u), np.float32), np.zeros((S, B, n_u), np.float32)
+            st = s.closed_loop(X, Z, Y, S, cfg["N"], cfg["tol"], warm=cfg["warm"], xs=XS, us=US, iters=IT)
+    IT = IT.reshape(S, B)
+    MGneg, GL, _ = oracle.scale(f32(qp.ML), f32(qp.G), f32(qp.g), L)
+    pick = sorted(set([0, B - 1] + [int(i) for i in rng.integers(0, B, min(sample, B))]))
+    for b in pick:
+        x, z, y, xs, us, its = oracle.closed_loop_f32(X0[b], MGneg, GL, L, pl.PM, pl.Pg, pl.A, pl.B, S, cfg["N"],
+                                                      cfg["tol"], g0=pl.g0, warm=cfg["warm"])
+        for what, a, o in (("xs", XS[:, b], xs), ("us", US[:, b], us), ("x", X[b], x), ("z", Z[b], z),
+                           ("y", Y[b], y), ("iters", IT[:, b], its)):
+            if not np.array_equal(a, o, equal_nan=True):
+                return dict(ok=False, checked=0, kernels=[st["kernel"]], why=f"pack {b}: {what} differs")
+    if st["total_iterations"] != int(IT.sum()):
+        return dict(ok=False, checked=0, kernels=[st["kernel"]], why="total_iterations != sum of counts")
+    return dict(ok=True, checked=len(pick), kernels=[st["kernel"]])
+
+
+def _run_oneshot(cfg, oracle, ML, G, M, g, L, kc, sample):
+    """gpad_solve(z0, y0, ML, M, G, g, N, L, tol, dims, stats) through ctypes (include/gpad.h), host
+    pointers for numpy, device pointers for torch tensors."""
+    import ctypes as C
+
+    import torch
+
+    from gpad_mpc import _lib
+    lib = _lib.load()
+    B, n, m = cfg["batch"], cfg["n"], cfg["m"]
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(cfg["seed"] + 5)
+    if cfg["warm"]:
+        z0 = rng.uniform(-0.5, 0.5, (B, n)).astype(ML.dtype)
+        y0 = np.maximum(rng.normal(0.0, 0.3, (B, m)), 0.0).astype(ML.dtype)
+    else:
+        z0, y0 = np.zeros((B, n), ML.dtype), np.zeros((B, m), ML.dtype)
+    mem = int(cfg["device"])
+    # (copies: gpad_solve writes z*, y* over its z0, y0 and the oracle needs the starting point)
+    t = (lambda a: torch.from_numpy(np.array(a, copy=True)).to(dev)) if mem else (lambda a: np.array(a, copy=True))  # noqa: E731
+    args = [t(a) for a in (z0, y0, ML, M, G, g)]
+    ptr = (lambda a: C.c_void_p(a.data_ptr())) if mem else (lambda a: C.c_void_p(a.ctypes.data))  # noqa: E731
+    d = _lib.Dims(n=n, m=m, batch=B, shared=int(cfg["shared"]), dtype=int(ML.dtype == np.float64), memory=mem,
+                  schedule=_lib.SCHEDULE_MATLAB, check_every=cfg["check_every"], kernel=kc)
+    st = _lib.Stats()
+    iters = np.zeros(B, np.int32)
+    st.iters = iters.ctypes.data_as(C.POINTER(C.c_int))
+    _lib.check(lib.gpad_solve(*[ptr(a) for a in args], int(cfg["N"]), float(L), float(cfg["tol"]), C.byref(d),
+                              C.byref(st)), "gpad_solve")
+    z, y = (a.cpu().numpy() if mem else a for a in args[:2])
+    pick = sorted(set([0, B - 1] + [int(i) for i in rng.integers(0, B, min(sample, B))]))
+    for b in pick:
+        if cfg.get("f64"):
+            zo, yo, it, _ = oracle.solve_f64(z0[b], y0[b], ML, M[b], G, g[b], cfg["N"], float(L), cfg["tol"],
+                                             cfg["check_every"])
+        else:
+            ml, gg = (ML, G) if cfg["shared"] else (ML[b], G[b])
+            zo, yo, it, _ = oracle.solve_f32(z0[b], y0[b], ml, M[b], gg, g[b], cfg["N"], L, cfg["tol"],
+                                             cfg["check_every"])
+        if cfg["tol"] > 0 and int(iters[b]) != int(it):
+            return dict(ok=False, checked=0, kernels=["oneshot"], why=f"gpad_solve instance {b}: count {iters[b]} vs {it}")
+        for what, a, o in (("z", z[b], zo), ("y", y[b], yo)):
+            if cfg.get("f64"):
+                bad = np.linalg.norm(a - o) / max(np.linalg.norm(o), 1e-300) > 1e-11
+            else:
+                bad = not np.array_equal(a, o, equal_nan=True)
+            if bad:
+                return dict(ok=False, checked=0, kernels=["oneshot"], why=f"gpad_solve instance {b} {what} differs")
+    return dict(ok=True, checked=len(pick), kernels=["oneshot"])

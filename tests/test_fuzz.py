@@ -62,3 +62,14 @@ def test_value_fuzz_parity(gpu, oracle, i):
     cfg = fuzz_util.draw_value_case(np.random.default_rng(SEED + 200 + i))
     r = fuzz_util.run_value_case(cfg, oracle)
     assert r["ok"], f"{json.dumps(cfg)}: {r['why']}"
+
+
+LOOP_CASES = 4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("i", range(LOOP_CASES))
+def test_closed_loop_fuzz_parity(gpu, oracle, i):
+    cfg = fuzz_util.draw_loop_case(np.random.default_rng(SEED + 300 + i))
+    r = fuzz_util.run_loop_case(cfg, oracle)
+    assert r["ok"], f"{json.dumps(cfg)}: {r['why']}"

@@ -24,6 +24,7 @@ ap.add_argument("--sample", type=int, default=24)
 ap.add_argument("--budget-s", type=float, default=400.0)
 ap.add_argument("--flat", type=float, default=0.25, help="share of flat battery cases")
 ap.add_argument("--value", type=float, default=0.0, help="share of value-branch (H bound) cases")
+ap.add_argument("--loop", type=float, default=0.0, help="share of closed-loop (gpad_closed_loop) cases")
 ap.add_argument("--rccl-stub", action="store_true",
                 help="group cases through the RCCL transport (tests/rccl_stub, one GPU standing in for each rank)")
 args = ap.parse_args()
@@ -40,13 +41,16 @@ for i in range(args.cases):
         break
     rng = np.random.default_rng(args.seed + i)
     u = rng.random()
-    kind = "flat" if u < args.flat else ("value" if u < args.flat + args.value else "full")
+    edges = np.cumsum([args.flat, args.value, args.loop])
+    kind = "flat" if u < edges[0] else "value" if u < edges[1] else "loop" if u < edges[2] else "full"
     cfg = {"flat": fuzz_util.draw_flat_case, "value": fuzz_util.draw_value_case,
-           "full": fuzz_util.draw_case}[kind](rng)
+           "loop": fuzz_util.draw_loop_case, "full": fuzz_util.draw_case}[kind](rng)
     t = time.time()
     try:
         if kind == "flat":
             r = fuzz_util.run_flat_case(cfg, O, sample=min(args.sample, 16))
+        elif kind == "loop":
+            r = fuzz_util.run_loop_case(cfg, O)
         elif kind == "value":
             r = fuzz_util.run_value_case(cfg, O, sample=min(args.sample, 16))
         else:
