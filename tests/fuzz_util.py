@@ -113,7 +113,9 @@ def run_case(cfg: dict, oracle, sample: int = 24, threads: int = 8) -> dict:
                 z, y = z0.copy(), y0.copy()
                 st = s.run(z, y, M, g, cfg["N"], cfg["tol"], iters=iters)
             kernels.append(st.get("kernel", "group") if not grp else f"group{grp}")
-            pick = sorted(set([0, B - 1] + [int(i) for i in rng.integers(0, B, min(sample, B))]))
+            # first, last, random, and the four longest (the finisher's tail) instances
+            longest = [int(i) for i in np.argsort(iters)[-4:]] if cfg["tol"] > 0 else []
+            pick = sorted(set([0, B - 1] + longest + [int(i) for i in rng.integers(0, B, min(sample, B))]))
             if cfg.get("f64"):
                 Zo, Yo, Io = [], [], []
                 for b in pick:
@@ -441,3 +443,21 @@ def _run_oneshot(cfg, oracle, ML, G, M, g, L, kc, sample):
             if bad:
                 return dict(ok=False, checked=0, kernels=["oneshot"], why=f"gpad_solve instance {b} {what} differs")
     return dict(ok=True, checked=len(pick), kernels=["oneshot"])
+
+
+def draw_heavy_case(rng: np.random.Generator) -> dict:
+    """C3 / C4-shaped phased solves (shared 200 x 200-ish matrices, thousands of instances to eps, the
+    planner over 2-3 fresh solves, the duo finisher's tail) with random schedule options."""
+    n = int(rng.choice([200, 200, int(rng.integers(150, 209))]))
+    m = int(rng.choice([200, 200, int(rng.integers(150, 209))]))
+    opts = {}
+    for name, choices, p in (("phase_len", [10, 20, 40, 60], 0.3), ("finish_thresh", [0, 256, 512, 2048], 0.3),
+                             ("duo_max_grid", [1, 7, 64, 255], 0.2), ("panel_max_grid", [1, 3, 64, 200], 0.2),
+                             ("lpt", [0], 0.15), ("plan", [0], 0.15), ("phased", [0], 0.1)):
+        if rng.random() < p:
+            opts[name] = int(rng.choice(choices))
+    return dict(n=n, m=m, batch=int(rng.choice([4096, 4100, 8192, 8197, 12000, 16384])), shared=True,
+                kernel=str(rng.choice(["auto", "auto", "panel"])), seed=int(rng.integers(1 << 30)),
+                warm=bool(rng.random() < 0.2), device=bool(rng.random() < 0.7), solves=int(rng.integers(2, 4)),
+                check_every=int(rng.choice([10, 10, 5, 20])), N=5000, tol=float(rng.choice([1e-4, 1e-4, 1e-3])),
+                opts=opts, f64=False, group=0, oneshot=False, heavy=True)

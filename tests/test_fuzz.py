@@ -73,3 +73,16 @@ def test_closed_loop_fuzz_parity(gpu, oracle, i):
     cfg = fuzz_util.draw_loop_case(np.random.default_rng(SEED + 300 + i))
     r = fuzz_util.run_loop_case(cfg, oracle)
     assert r["ok"], f"{json.dumps(cfg)}: {r['why']}"
+
+
+HEAVY_CASES = 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("i", range(HEAVY_CASES))
+def test_heavy_fuzz_parity(gpu, oracle, i):
+    """C3 / C4-shaped phased solves (planner, compaction, duo finisher) with random schedule options;
+    the four longest instances of every solve are among those checked."""
+    cfg = fuzz_util.draw_heavy_case(np.random.default_rng(SEED + 400 + i))
+    r = fuzz_util.run_case(cfg, oracle)
+    assert r["ok"], f"{json.dumps(cfg)}: {r['why']}"

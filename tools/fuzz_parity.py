@@ -25,6 +25,7 @@ ap.add_argument("--budget-s", type=float, default=400.0)
 ap.add_argument("--flat", type=float, default=0.25, help="share of flat battery cases")
 ap.add_argument("--value", type=float, default=0.0, help="share of value-branch (H bound) cases")
 ap.add_argument("--loop", type=float, default=0.0, help="share of closed-loop (gpad_closed_loop) cases")
+ap.add_argument("--heavy", type=float, default=0.0, help="share of C3/C4-shaped phased solves")
 ap.add_argument("--rccl-stub", action="store_true",
                 help="group cases through the RCCL transport (tests/rccl_stub, one GPU standing in for each rank)")
 args = ap.parse_args()
@@ -41,10 +42,11 @@ for i in range(args.cases):
         break
     rng = np.random.default_rng(args.seed + i)
     u = rng.random()
-    edges = np.cumsum([args.flat, args.value, args.loop])
-    kind = "flat" if u < edges[0] else "value" if u < edges[1] else "loop" if u < edges[2] else "full"
-    cfg = {"flat": fuzz_util.draw_flat_case, "value": fuzz_util.draw_value_case,
-           "loop": fuzz_util.draw_loop_case, "full": fuzz_util.draw_case}[kind](rng)
+    edges = np.cumsum([args.flat, args.value, args.loop, args.heavy])
+    kind = ("flat" if u < edges[0] else "value" if u < edges[1] else "loop" if u < edges[2] else
+            "heavy" if u < edges[3] else "full")
+    cfg = {"flat": fuzz_util.draw_flat_case, "value": fuzz_util.draw_value_case, "loop": fuzz_util.draw_loop_case,
+           "heavy": fuzz_util.draw_heavy_case, "full": fuzz_util.draw_case}[kind](rng)
     t = time.time()
     try:
         if kind == "flat":
