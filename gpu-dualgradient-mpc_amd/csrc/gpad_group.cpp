@@ -241,243 +241,257 @@ int sync_all(gpad_group_s* g) {
 extern "C" {
 
 int gpad_group_create(gpad_group_t* out, int ndev, const int* devices) {
-    if (!out || ndev <= 0 || !devices) return gfail(GPAD_ERR_INVALID, "gpad_group_create: bad arguments");
-    *out = nullptr;
-    int visible = 0;
-    if (hipGetDeviceCount(&visible) != hipSuccess || visible <= 0)
-        return gfail(GPAD_ERR_NO_DEVICE, "gpad_group_create: no HIP device visible");
-    for (int d = 0; d < ndev; ++d)
-        if (devices[d] < 0 || devices[d] >= visible)
-            return gfail(GPAD_ERR_INVALID, "gpad_group_create: bad device index");
-    auto* g = new gpad_group_s;
-    g->ndev = ndev;
-    g->dev.assign(devices, devices + ndev);
-    g->h.assign(ndev, nullptr);
-    g->st.assign(ndev, nullptr);
-    g->ev.assign(ndev, nullptr);
-    g->vec.assign(ndev, nullptr);
-    g->vec_bytes.assign(ndev, 0);
-    g->mat.assign(ndev, nullptr);
-    g->mat_bytes.assign(ndev, 0);
-    for (int d = 0; d < ndev; ++d) {
-        int rc;
-        if (hipSetDevice(g->dev[d]) != hipSuccess || hipStreamCreateWithFlags(&g->st[d], hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&g->ev[d], hipEventDisableTiming) != hipSuccess) {
-            release(g);
-            return gfail(GPAD_ERR_HIP, "gpad_group_create: stream/event creation failed");
+    return gpad::abi_guard("gpad_group_create", [&]() -> int {
+        if (!out || ndev <= 0 || !devices) return gfail(GPAD_ERR_INVALID, "gpad_group_create: bad arguments");
+        *out = nullptr;
+        int visible = 0;
+        if (hipGetDeviceCount(&visible) != hipSuccess || visible <= 0)
+            return gfail(GPAD_ERR_NO_DEVICE, "gpad_group_create: no HIP device visible");
+        for (int d = 0; d < ndev; ++d)
+            if (devices[d] < 0 || devices[d] >= visible)
+                return gfail(GPAD_ERR_INVALID, "gpad_group_create: bad device index");
+        auto* g = new gpad_group_s;
+        g->ndev = ndev;
+        g->dev.assign(devices, devices + ndev);
+        g->h.assign(ndev, nullptr);
+        g->st.assign(ndev, nullptr);
+        g->ev.assign(ndev, nullptr);
+        g->vec.assign(ndev, nullptr);
+        g->vec_bytes.assign(ndev, 0);
+        g->mat.assign(ndev, nullptr);
+        g->mat_bytes.assign(ndev, 0);
+        for (int d = 0; d < ndev; ++d) {
+            int rc;
+            if (hipSetDevice(g->dev[d]) != hipSuccess || hipStreamCreateWithFlags(&g->st[d], hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&g->ev[d], hipEventDisableTiming) != hipSuccess) {
+                release(g);
+                return gfail(GPAD_ERR_HIP, "gpad_group_create: stream/event creation failed");
+            }
+            if ((rc = gpad_create(&g->h[d], g->dev[d], g->st[d]))) {
+                release(g);
+                return rc;
+            }
         }
-        if ((rc = gpad_create(&g->h[d], g->dev[d], g->st[d]))) {
+        if (hipSetDevice(g->dev[0]) != hipSuccess ||
+            hipEventCreateWithFlags(&g->caller_ev, hipEventDisableTiming) != hipSuccess) {
             release(g);
-            return rc;
+            return gfail(GPAD_ERR_HIP, "gpad_group_create: event creation failed");
         }
-    }
-    if (hipSetDevice(g->dev[0]) != hipSuccess ||
-        hipEventCreateWithFlags(&g->caller_ev, hipEventDisableTiming) != hipSuccess) {
-        release(g);
-        return gfail(GPAD_ERR_HIP, "gpad_group_create: event creation failed");
-    }
-    std::vector<int> sorted(g->dev);
-    std::sort(sorted.begin(), sorted.end());
-    const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
-    g->r = current_rccl();
-    if ((distinct || g->r->force) && g->r->ok) {  // one RCCL clique, rank d on devices[d]
-        g->comm.assign(ndev, nullptr);
-        const ncclResult_t r = g->r->CommInitAll(g->comm.data(), ndev, g->dev.data());
-        if (r != ncclSuccess) {
-            g->comm.clear();
-            release(g);
-            return gfail(GPAD_ERR_HIP, std::string("ncclCommInitAll: ") + g->r->GetErrorString(r));
+        std::vector<int> sorted(g->dev);
+        std::sort(sorted.begin(), sorted.end());
+        const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+        g->r = current_rccl();
+        if ((distinct || g->r->force) && g->r->ok) {  // one RCCL clique, rank d on devices[d]
+            g->comm.assign(ndev, nullptr);
+            const ncclResult_t r = g->r->CommInitAll(g->comm.data(), ndev, g->dev.data());
+            if (r != ncclSuccess) {
+                g->comm.clear();
+                release(g);
+                return gfail(GPAD_ERR_HIP, std::string("ncclCommInitAll: ") + g->r->GetErrorString(r));
+            }
         }
-    }
-    *out = g;
-    return GPAD_OK;
+        *out = g;
+        return GPAD_OK;
+    });
 }
 
 int gpad_group_destroy(gpad_group_t g) {
-    if (!g) return GPAD_OK;
-    return release(g);
+    return gpad::abi_guard("gpad_group_destroy", [&]() -> int {
+        if (!g) return GPAD_OK;
+        return release(g);
+    });
 }
 
 int gpad_group_rccl_library(const char* path, int force_rccl) {
-    auto r = load_rccl(path ? std::string(path) : std::string(), force_rccl != 0);
-    {
-        std::lock_guard<std::mutex> lk(g_rccl_mu);
-        g_rccl = r;
-        ++g_rccl_gen;
-    }
-    if (!r->ok)
-        return gfail(GPAD_ERR_UNSUPPORTED, std::string("gpad_group_rccl_library: cannot load the RCCL entry points from ") +
-                                               (path ? path : "librccl") + " (groups use peer copies)");
-    return GPAD_OK;
+    return gpad::abi_guard("gpad_group_rccl_library", [&]() -> int {
+        auto r = load_rccl(path ? std::string(path) : std::string(), force_rccl != 0);
+        {
+            std::lock_guard<std::mutex> lk(g_rccl_mu);
+            g_rccl = r;
+            ++g_rccl_gen;
+        }
+        if (!r->ok)
+            return gfail(GPAD_ERR_UNSUPPORTED, std::string("gpad_group_rccl_library: cannot load the RCCL entry points from ") +
+                                                   (path ? path : "librccl") + " (groups use peer copies)");
+        return GPAD_OK;
+    });
 }
 
 int gpad_group_transport(gpad_group_t g) {
-    if (!g) return gfail(GPAD_ERR_INVALID, "gpad_group_transport: null group");
-    return g->comm.empty() ? GPAD_GROUP_PEER : GPAD_GROUP_RCCL;
+    return gpad::abi_guard("gpad_group_transport", [&]() -> int {
+        if (!g) return gfail(GPAD_ERR_INVALID, "gpad_group_transport: null group");
+        return g->comm.empty() ? GPAD_GROUP_PEER : GPAD_GROUP_RCCL;
+    });
 }
 
 int gpad_group_set_stream(gpad_group_t g, void* hip_stream) {
-    if (!g) return gfail(GPAD_ERR_INVALID, "gpad_group_set_stream: null group");
-    g->caller = static_cast<hipStream_t>(hip_stream);
-    return GPAD_OK;
+    return gpad::abi_guard("gpad_group_set_stream", [&]() -> int {
+        if (!g) return gfail(GPAD_ERR_INVALID, "gpad_group_set_stream: null group");
+        g->caller = static_cast<hipStream_t>(hip_stream);
+        return GPAD_OK;
+    });
 }
 
 int gpad_group_setup(gpad_group_t g, const gpad_dims_t* dims, const void* ML, const void* G, double L) {
-    if (!g || !dims || !ML || !G) return gfail(GPAD_ERR_INVALID, "gpad_group_setup: bad arguments");
-    if (dims->batch < 1 || dims->n <= 0 || dims->m <= 0)
-        return gfail(GPAD_ERR_INVALID, "gpad_group_setup: dims: n, m, batch must be positive");
-    g->ready = false;
-    const int nd = g->ndev, B = dims->batch;
-    g->start.assign(nd, 0);
-    g->count.assign(nd, 0);
-    for (int d = 0, s = 0; d < nd; ++d) {  // contiguous shards, larger first
-        g->count[d] = B / nd + (d < B % nd ? 1 : 0);
-        g->start[d] = s;
-        s += g->count[d];
-    }
-    const bool host = dims->memory == GPAD_MEM_HOST;
-    const size_t es = esz(dims->dtype), nm = (size_t)dims->n * dims->m * es;
-    std::vector<Move> mv;
-    std::vector<const void*> mlp(nd), gp(nd);
-    int rc;
-    if (!host && (rc = order_after_caller(g))) return rc;
-    for (int d = 0; d < nd; ++d) {
-        const int c = std::max(g->count[d], 1);
-        const size_t per = dims->shared ? nm : nm * (size_t)c;  // each of ML and G
-        const size_t off = dims->shared ? 0 : nm * (size_t)g->start[d];
-        if (g->count[d] == 0 && !dims->shared) {  // more devices than instances: an idle shard
-            if ((rc = ensure(g, g->mat, g->mat_bytes, d, 2 * per))) return rc;
-            G_HIP(hipSetDevice(g->dev[d]));
-            G_HIP(hipMemsetAsync(g->mat[d], 0, 2 * per, g->st[d]));
-            mlp[d] = g->mat[d];
-            gp[d] = (char*)g->mat[d] + per;
-            continue;
+    return gpad::abi_guard("gpad_group_setup", [&]() -> int {
+        if (!g || !dims || !ML || !G) return gfail(GPAD_ERR_INVALID, "gpad_group_setup: bad arguments");
+        if (dims->batch < 1 || dims->n <= 0 || dims->m <= 0)
+            return gfail(GPAD_ERR_INVALID, "gpad_group_setup: dims: n, m, batch must be positive");
+        g->ready = false;
+        const int nd = g->ndev, B = dims->batch;
+        g->start.assign(nd, 0);
+        g->count.assign(nd, 0);
+        for (int d = 0, s = 0; d < nd; ++d) {  // contiguous shards, larger first
+            g->count[d] = B / nd + (d < B % nd ? 1 : 0);
+            g->start[d] = s;
+            s += g->count[d];
         }
-        if (!host && d == 0) {  // the root's shard reads the caller's buffers in place
-            mlp[d] = (const char*)ML + off;
-            gp[d] = (const char*)G + off;
-            continue;
-        }
-        if ((rc = ensure(g, g->mat, g->mat_bytes, d, 2 * per))) return rc;
-        void* dml = g->mat[d];
-        void* dg = (char*)g->mat[d] + per;
-        mlp[d] = dml;
-        gp[d] = dg;
-        if (host) {
-            G_HIP(hipSetDevice(g->dev[d]));
-            G_HIP(hipMemcpyAsync(dml, (const char*)ML + off, per, hipMemcpyHostToDevice, g->st[d]));
-            G_HIP(hipMemcpyAsync(dg, (const char*)G + off, per, hipMemcpyHostToDevice, g->st[d]));
-        } else if (!dims->shared || g->comm.empty()) {
-            mv.push_back({d, dml, (const char*)ML + off, per});
-            mv.push_back({d, dg, (const char*)G + off, per});
-        }
-    }
-    if (!host && dims->shared && !g->comm.empty() && nd > 1) {  // shared matrices: one broadcast each
-        G_NCCL(GroupStart());
+        const bool host = dims->memory == GPAD_MEM_HOST;
+        const size_t es = esz(dims->dtype), nm = (size_t)dims->n * dims->m * es;
+        std::vector<Move> mv;
+        std::vector<const void*> mlp(nd), gp(nd);
+        int rc;
+        if (!host && (rc = order_after_caller(g))) return rc;
         for (int d = 0; d < nd; ++d) {
-            G_NCCL(Broadcast(d == 0 ? ML : nullptr, const_cast<void*>(mlp[d]), nm, ncclChar, 0, g->comm[d], g->st[d]));
-            G_NCCL(Broadcast(d == 0 ? G : nullptr, const_cast<void*>(gp[d]), nm, ncclChar, 0, g->comm[d], g->st[d]));
+            const int c = std::max(g->count[d], 1);
+            const size_t per = dims->shared ? nm : nm * (size_t)c;  // each of ML and G
+            const size_t off = dims->shared ? 0 : nm * (size_t)g->start[d];
+            if (g->count[d] == 0 && !dims->shared) {  // more devices than instances: an idle shard
+                if ((rc = ensure(g, g->mat, g->mat_bytes, d, 2 * per))) return rc;
+                G_HIP(hipSetDevice(g->dev[d]));
+                G_HIP(hipMemsetAsync(g->mat[d], 0, 2 * per, g->st[d]));
+                mlp[d] = g->mat[d];
+                gp[d] = (char*)g->mat[d] + per;
+                continue;
+            }
+            if (!host && d == 0) {  // the root's shard reads the caller's buffers in place
+                mlp[d] = (const char*)ML + off;
+                gp[d] = (const char*)G + off;
+                continue;
+            }
+            if ((rc = ensure(g, g->mat, g->mat_bytes, d, 2 * per))) return rc;
+            void* dml = g->mat[d];
+            void* dg = (char*)g->mat[d] + per;
+            mlp[d] = dml;
+            gp[d] = dg;
+            if (host) {
+                G_HIP(hipSetDevice(g->dev[d]));
+                G_HIP(hipMemcpyAsync(dml, (const char*)ML + off, per, hipMemcpyHostToDevice, g->st[d]));
+                G_HIP(hipMemcpyAsync(dg, (const char*)G + off, per, hipMemcpyHostToDevice, g->st[d]));
+            } else if (!dims->shared || g->comm.empty()) {
+                mv.push_back({d, dml, (const char*)ML + off, per});
+                mv.push_back({d, dg, (const char*)G + off, per});
+            }
         }
-        G_NCCL(GroupEnd());
-    }
-    if ((rc = scatter(g, mv))) return rc;
-    for (int d = 0; d < nd; ++d) {  // pack on every device (each handle orders on its stream)
-        gpad_dims_t dd = *dims;
-        dd.batch = std::max(g->count[d], 1);
-        dd.memory = GPAD_MEM_DEVICE;
-        if ((rc = gpad_setup(g->h[d], &dd, mlp[d], gp[d], L))) return rc;
-    }
-    if ((rc = sync_all(g))) return rc;
-    g->dims = *dims;
-    g->L = L;
-    g->ready = true;
-    return GPAD_OK;
+        if (!host && dims->shared && !g->comm.empty() && nd > 1) {  // shared matrices: one broadcast each
+            G_NCCL(GroupStart());
+            for (int d = 0; d < nd; ++d) {
+                G_NCCL(Broadcast(d == 0 ? ML : nullptr, const_cast<void*>(mlp[d]), nm, ncclChar, 0, g->comm[d], g->st[d]));
+                G_NCCL(Broadcast(d == 0 ? G : nullptr, const_cast<void*>(gp[d]), nm, ncclChar, 0, g->comm[d], g->st[d]));
+            }
+            G_NCCL(GroupEnd());
+        }
+        if ((rc = scatter(g, mv))) return rc;
+        for (int d = 0; d < nd; ++d) {  // pack on every device (each handle orders on its stream)
+            gpad_dims_t dd = *dims;
+            dd.batch = std::max(g->count[d], 1);
+            dd.memory = GPAD_MEM_DEVICE;
+            if ((rc = gpad_setup(g->h[d], &dd, mlp[d], gp[d], L))) return rc;
+        }
+        if ((rc = sync_all(g))) return rc;
+        g->dims = *dims;
+        g->L = L;
+        g->ready = true;
+        return GPAD_OK;
+    });
 }
 
 int gpad_group_run(gpad_group_t g, void* z0, void* y0, const void* M, const void* gv, int N, double tol,
                    gpad_stats_t* st) {
-    if (!g) return gfail(GPAD_ERR_INVALID, "gpad_group_run: null group");
-    if (!g->ready) return gfail(GPAD_ERR_NOT_SETUP, "gpad_group_run: call gpad_group_setup first");
-    if (!z0 || !y0 || !M || !gv) return gfail(GPAD_ERR_INVALID, "gpad_group_run: null vector");
-    const gpad_dims_t& D = g->dims;
-    const bool host = D.memory == GPAD_MEM_HOST;
-    const size_t es = esz(D.dtype), nb = (size_t)D.n * es, mb = (size_t)D.m * es;
-    const int nd = g->ndev;
-    std::vector<char*> Mp(nd), gp(nd), zp(nd), yp(nd);
-    std::vector<Move> in, out;
-    int rc;
-    if (!host && (rc = order_after_caller(g))) return rc;
-    for (int d = 0; d < nd; ++d) {
-        const size_t c = (size_t)g->count[d], s0 = (size_t)g->start[d];
-        if (!host && d == 0) {  // root shard in place
-            Mp[d] = (char*)M;
-            gp[d] = (char*)gv;
-            zp[d] = (char*)z0;
-            yp[d] = (char*)y0;
-            continue;
-        }
-        if ((rc = ensure(g, g->vec, g->vec_bytes, d, std::max<size_t>(1, 2 * c * (nb + mb))))) return rc;
-        Mp[d] = (char*)g->vec[d];
-        gp[d] = Mp[d] + c * nb;
-        zp[d] = gp[d] + c * mb;
-        yp[d] = zp[d] + c * nb;
-        if (c == 0) continue;
-        if (host) {
-            G_HIP(hipSetDevice(g->dev[d]));
-            G_HIP(hipMemcpyAsync(Mp[d], (const char*)M + s0 * nb, c * nb, hipMemcpyHostToDevice, g->st[d]));
-            G_HIP(hipMemcpyAsync(gp[d], (const char*)gv + s0 * mb, c * mb, hipMemcpyHostToDevice, g->st[d]));
-            G_HIP(hipMemcpyAsync(zp[d], (const char*)z0 + s0 * nb, c * nb, hipMemcpyHostToDevice, g->st[d]));
-            G_HIP(hipMemcpyAsync(yp[d], (const char*)y0 + s0 * mb, c * mb, hipMemcpyHostToDevice, g->st[d]));
-        } else {
-            in.push_back({d, Mp[d], (const char*)M + s0 * nb, c * nb});
-            in.push_back({d, gp[d], (const char*)gv + s0 * mb, c * mb});
-            in.push_back({d, zp[d], (const char*)z0 + s0 * nb, c * nb});
-            in.push_back({d, yp[d], (const char*)y0 + s0 * mb, c * mb});
-            out.push_back({d, (char*)z0 + s0 * nb, zp[d], c * nb});
-            out.push_back({d, (char*)y0 + s0 * mb, yp[d], c * mb});
-        }
-    }
-    if ((rc = scatter(g, in))) return rc;
-    for (int d = 0; d < nd; ++d) {  // every shard's solve, asynchronous on its device's stream
-        if (g->count[d] == 0) continue;
-        if ((rc = gpad_run(g->h[d], zp[d], yp[d], Mp[d], gp[d], N, tol, nullptr))) return rc;
-    }
-    if ((rc = gather(g, out))) return rc;
-    if (host) {
+    return gpad::abi_guard("gpad_group_run", [&]() -> int {
+        if (!g) return gfail(GPAD_ERR_INVALID, "gpad_group_run: null group");
+        if (!g->ready) return gfail(GPAD_ERR_NOT_SETUP, "gpad_group_run: call gpad_group_setup first");
+        if (!z0 || !y0 || !M || !gv) return gfail(GPAD_ERR_INVALID, "gpad_group_run: null vector");
+        const gpad_dims_t& D = g->dims;
+        const bool host = D.memory == GPAD_MEM_HOST;
+        const size_t es = esz(D.dtype), nb = (size_t)D.n * es, mb = (size_t)D.m * es;
+        const int nd = g->ndev;
+        std::vector<char*> Mp(nd), gp(nd), zp(nd), yp(nd);
+        std::vector<Move> in, out;
+        int rc;
+        if (!host && (rc = order_after_caller(g))) return rc;
         for (int d = 0; d < nd; ++d) {
             const size_t c = (size_t)g->count[d], s0 = (size_t)g->start[d];
+            if (!host && d == 0) {  // root shard in place
+                Mp[d] = (char*)M;
+                gp[d] = (char*)gv;
+                zp[d] = (char*)z0;
+                yp[d] = (char*)y0;
+                continue;
+            }
+            if ((rc = ensure(g, g->vec, g->vec_bytes, d, std::max<size_t>(1, 2 * c * (nb + mb))))) return rc;
+            Mp[d] = (char*)g->vec[d];
+            gp[d] = Mp[d] + c * nb;
+            zp[d] = gp[d] + c * mb;
+            yp[d] = zp[d] + c * nb;
             if (c == 0) continue;
-            G_HIP(hipSetDevice(g->dev[d]));
-            G_HIP(hipMemcpyAsync((char*)z0 + s0 * nb, zp[d], c * nb, hipMemcpyDeviceToHost, g->st[d]));
-            G_HIP(hipMemcpyAsync((char*)y0 + s0 * mb, yp[d], c * mb, hipMemcpyDeviceToHost, g->st[d]));
+            if (host) {
+                G_HIP(hipSetDevice(g->dev[d]));
+                G_HIP(hipMemcpyAsync(Mp[d], (const char*)M + s0 * nb, c * nb, hipMemcpyHostToDevice, g->st[d]));
+                G_HIP(hipMemcpyAsync(gp[d], (const char*)gv + s0 * mb, c * mb, hipMemcpyHostToDevice, g->st[d]));
+                G_HIP(hipMemcpyAsync(zp[d], (const char*)z0 + s0 * nb, c * nb, hipMemcpyHostToDevice, g->st[d]));
+                G_HIP(hipMemcpyAsync(yp[d], (const char*)y0 + s0 * mb, c * mb, hipMemcpyHostToDevice, g->st[d]));
+            } else {
+                in.push_back({d, Mp[d], (const char*)M + s0 * nb, c * nb});
+                in.push_back({d, gp[d], (const char*)gv + s0 * mb, c * mb});
+                in.push_back({d, zp[d], (const char*)z0 + s0 * nb, c * nb});
+                in.push_back({d, yp[d], (const char*)y0 + s0 * mb, c * mb});
+                out.push_back({d, (char*)z0 + s0 * nb, zp[d], c * nb});
+                out.push_back({d, (char*)y0 + s0 * mb, yp[d], c * mb});
+            }
         }
-    }
-    if ((rc = sync_all(g))) return rc;
-    for (int d = 0; d < nd; ++d)  // device-side failures of any shard fail the run (GPAD_ERR_DEVICE)
-        if (g->count[d] > 0 && (rc = gpad_sync(g->h[d]))) return rc;
-    if (st) {  // per-shard counters (host copies), aggregated; st->iters [batch] in global order
-        gpad_stats_t tot{};
-        for (int d = 0; d < nd; ++d) {
+        if ((rc = scatter(g, in))) return rc;
+        for (int d = 0; d < nd; ++d) {  // every shard's solve, asynchronous on its device's stream
             if (g->count[d] == 0) continue;
-            gpad_stats_t sd{};
-            sd.iters = st->iters ? st->iters + g->start[d] : nullptr;
-            sd.codes = st->codes ? st->codes + g->start[d] : nullptr;
-            if ((rc = gpad_last_stats(g->h[d], &sd))) return rc;
-            tot.iterations = std::max(tot.iterations, sd.iterations);
-            tot.converged += sd.converged;
-            tot.total_iterations += sd.total_iterations;
-            tot.kernel = sd.kernel;
-            tot.kernel_ms = std::max(tot.kernel_ms, sd.kernel_ms);
-            tot.tol_floor = std::max(tot.tol_floor, sd.tol_floor);
-            tot.flags |= sd.flags;
+            if ((rc = gpad_run(g->h[d], zp[d], yp[d], Mp[d], gp[d], N, tol, nullptr))) return rc;
         }
-        int* keep = st->iters;
-        int* keep_codes = st->codes;
-        *st = tot;
-        st->iters = keep;
-        st->codes = keep_codes;
-    }
-    return GPAD_OK;
+        if ((rc = gather(g, out))) return rc;
+        if (host) {
+            for (int d = 0; d < nd; ++d) {
+                const size_t c = (size_t)g->count[d], s0 = (size_t)g->start[d];
+                if (c == 0) continue;
+                G_HIP(hipSetDevice(g->dev[d]));
+                G_HIP(hipMemcpyAsync((char*)z0 + s0 * nb, zp[d], c * nb, hipMemcpyDeviceToHost, g->st[d]));
+                G_HIP(hipMemcpyAsync((char*)y0 + s0 * mb, yp[d], c * mb, hipMemcpyDeviceToHost, g->st[d]));
+            }
+        }
+        if ((rc = sync_all(g))) return rc;
+        for (int d = 0; d < nd; ++d)  // device-side failures of any shard fail the run (GPAD_ERR_DEVICE)
+            if (g->count[d] > 0 && (rc = gpad_sync(g->h[d]))) return rc;
+        if (st) {  // per-shard counters (host copies), aggregated; st->iters [batch] in global order
+            gpad_stats_t tot{};
+            for (int d = 0; d < nd; ++d) {
+                if (g->count[d] == 0) continue;
+                gpad_stats_t sd{};
+                sd.iters = st->iters ? st->iters + g->start[d] : nullptr;
+                sd.codes = st->codes ? st->codes + g->start[d] : nullptr;
+                if ((rc = gpad_last_stats(g->h[d], &sd))) return rc;
+                tot.iterations = std::max(tot.iterations, sd.iterations);
+                tot.converged += sd.converged;
+                tot.total_iterations += sd.total_iterations;
+                tot.kernel = sd.kernel;
+                tot.kernel_ms = std::max(tot.kernel_ms, sd.kernel_ms);
+                tot.tol_floor = std::max(tot.tol_floor, sd.tol_floor);
+                tot.flags |= sd.flags;
+            }
+            int* keep = st->iters;
+            int* keep_codes = st->codes;
+            *st = tot;
+            st->iters = keep;
+            st->codes = keep_codes;
+        }
+        return GPAD_OK;
+    });
 }
 
 }  // extern "C"
@@ -505,22 +519,24 @@ extern "C" {
 int gpad_solve_sharded(int ndev, const int* devices, void* z0, void* y0, const void* ML, const void* M,
                        const void* G, const void* g, int N, double L, double tol, const gpad_dims_t* dims,
                        gpad_stats_t* st) {
-    ShardCache& cache = t_shard_cache;
-    if (ndev <= 0 || !devices) return gfail(GPAD_ERR_INVALID, "gpad_solve_sharded: bad device list");
-    std::vector<int> want(devices, devices + ndev);
-    unsigned gen = 0;
-    (void)current_rccl(&gen);
-    if (!cache.grp || cache.devs != want || cache.rccl_gen != gen) {
-        if (cache.grp) gpad_group_destroy(cache.grp);
-        cache.grp = nullptr;
-        int rc = gpad_group_create(&cache.grp, ndev, devices);
+    return gpad::abi_guard("gpad_solve_sharded", [&]() -> int {
+        ShardCache& cache = t_shard_cache;
+        if (ndev <= 0 || !devices) return gfail(GPAD_ERR_INVALID, "gpad_solve_sharded: bad device list");
+        std::vector<int> want(devices, devices + ndev);
+        unsigned gen = 0;
+        (void)current_rccl(&gen);
+        if (!cache.grp || cache.devs != want || cache.rccl_gen != gen) {
+            if (cache.grp) gpad_group_destroy(cache.grp);
+            cache.grp = nullptr;
+            int rc = gpad_group_create(&cache.grp, ndev, devices);
+            if (rc) return rc;
+            cache.devs = want;
+            cache.rccl_gen = gen;
+        }
+        int rc = gpad_group_setup(cache.grp, dims, ML, G, L);
         if (rc) return rc;
-        cache.devs = want;
-        cache.rccl_gen = gen;
-    }
-    int rc = gpad_group_setup(cache.grp, dims, ML, G, L);
-    if (rc) return rc;
-    return gpad_group_run(cache.grp, z0, y0, M, g, N, tol, st);
+        return gpad_group_run(cache.grp, z0, y0, M, g, N, tol, st);
+    });
 }
 
 }  // extern "C"

@@ -240,10 +240,12 @@ extern "C" {
 const char* gpad_version(void) { return "gpad-mi355x 0.5 (gfx950)"; }
 
 int gpad_device_count(void) {
-    int count = 0;
-    const hipError_t e = hipGetDeviceCount(&count);
-    if (e != hipSuccess) return fail(GPAD_ERR_NO_DEVICE, hip_detail("gpad_device_count: hipGetDeviceCount", e));
-    return count;
+    return gpad::abi_guard("gpad_device_count", [&]() -> int {
+        int count = 0;
+        const hipError_t e = hipGetDeviceCount(&count);
+        if (e != hipSuccess) return fail(GPAD_ERR_NO_DEVICE, hip_detail("gpad_device_count: hipGetDeviceCount", e));
+        return count;
+    });
 }
 
 const char* gpad_strerror(int status) {
@@ -263,128 +265,140 @@ const char* gpad_strerror(int status) {
 const char* gpad_last_error(void) { return g_last_error.c_str(); }
 
 int gpad_create(gpad_handle_t* out, int device, void* stream) {
-    if (!out) return fail(GPAD_ERR_INVALID, "gpad_create: null handle pointer");
-    *out = nullptr;
-    int count = 0;
-    const hipError_t e = hipGetDeviceCount(&count);
-    if (e != hipSuccess) return fail(GPAD_ERR_NO_DEVICE, hip_detail("gpad_create: hipGetDeviceCount", e));
-    if (count <= 0) return fail(GPAD_ERR_NO_DEVICE, "gpad_create: hipGetDeviceCount reported 0 devices");
-    if (device < 0 || device >= count)
-        return fail(GPAD_ERR_INVALID, "gpad_create: bad device index " + std::to_string(device) + " (" +
-                                          std::to_string(count) + " visible)");
-    HIP_TRY(hipSetDevice(device));
-    auto h = std::make_unique<gpad_handle_s>();
-    h->device = device;
-    h->stream = static_cast<hipStream_t>(stream);  // NULL = the device's default (null) stream
-    {
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
-            h->num_cus = prop.multiProcessorCount;
-    }
-    HIP_TRY(hipEventCreate(&h->ev0));
-    HIP_TRY(hipEventCreate(&h->ev1));
-    *out = h.release();
-    return GPAD_OK;
+    return gpad::abi_guard("gpad_create", [&]() -> int {
+        if (!out) return fail(GPAD_ERR_INVALID, "gpad_create: null handle pointer");
+        *out = nullptr;
+        int count = 0;
+        const hipError_t e = hipGetDeviceCount(&count);
+        if (e != hipSuccess) return fail(GPAD_ERR_NO_DEVICE, hip_detail("gpad_create: hipGetDeviceCount", e));
+        if (count <= 0) return fail(GPAD_ERR_NO_DEVICE, "gpad_create: hipGetDeviceCount reported 0 devices");
+        if (device < 0 || device >= count)
+            return fail(GPAD_ERR_INVALID, "gpad_create: bad device index " + std::to_string(device) + " (" +
+                                              std::to_string(count) + " visible)");
+        HIP_TRY(hipSetDevice(device));
+        auto h = std::make_unique<gpad_handle_s>();
+        h->device = device;
+        h->stream = static_cast<hipStream_t>(stream);  // NULL = the device's default (null) stream
+        {
+            hipDeviceProp_t prop;
+            if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+                h->num_cus = prop.multiProcessorCount;
+        }
+        HIP_TRY(hipEventCreate(&h->ev0));
+        HIP_TRY(hipEventCreate(&h->ev1));
+        *out = h.release();
+        return GPAD_OK;
+    });
 }
 
 int gpad_destroy(gpad_handle_t h) {
-    if (!h) return GPAD_OK;
-    (void)hipSetDevice(h->device);
-    (void)hipStreamSynchronize(h->stream);
-    h->MGt.release();
-    h->GLt.release();
-    h->GLx.release();
-    h->Hq.release();
-    h->frag64.release();
-    h->hfrag64.release();
-    h->q64.release();
-    h->p64_order.release();
-    h->frag.release();
-    h->stage.release();
-    h->theta.release();
-    h->beta.release();
-    h->work.release();
-    h->counters.release();
-    h->pwork.release();
-    h->status.release();
-    h->plant.release();
-    h->state.release();
-    if (h->ev0) (void)hipEventDestroy(h->ev0);
-    if (h->ev1) (void)hipEventDestroy(h->ev1);
-    if (h->plan_ev) (void)hipEventDestroy(h->plan_ev);
-    if (h->plan_pin) (void)hipHostFree(h->plan_pin);
-    delete h;
-    return GPAD_OK;
+    return gpad::abi_guard("gpad_destroy", [&]() -> int {
+        if (!h) return GPAD_OK;
+        (void)hipSetDevice(h->device);
+        (void)hipStreamSynchronize(h->stream);
+        h->MGt.release();
+        h->GLt.release();
+        h->GLx.release();
+        h->Hq.release();
+        h->frag64.release();
+        h->hfrag64.release();
+        h->q64.release();
+        h->p64_order.release();
+        h->frag.release();
+        h->stage.release();
+        h->theta.release();
+        h->beta.release();
+        h->work.release();
+        h->counters.release();
+        h->pwork.release();
+        h->status.release();
+        h->plant.release();
+        h->state.release();
+        if (h->ev0) (void)hipEventDestroy(h->ev0);
+        if (h->ev1) (void)hipEventDestroy(h->ev1);
+        if (h->plan_ev) (void)hipEventDestroy(h->plan_ev);
+        if (h->plan_pin) (void)hipHostFree(h->plan_pin);
+        delete h;
+        return GPAD_OK;
+    });
 }
 
 int gpad_set_stream(gpad_handle_t h, void* stream) {
-    if (!h) return fail(GPAD_ERR_INVALID, "gpad_set_stream: null handle");
-    HIP_TRY(hipSetDevice(h->device));
-    HIP_TRY(hipStreamSynchronize(h->stream));  // work queued on the old stream completes first
-    h->stream = static_cast<hipStream_t>(stream);
-    return GPAD_OK;
+    return gpad::abi_guard("gpad_set_stream", [&]() -> int {
+        if (!h) return fail(GPAD_ERR_INVALID, "gpad_set_stream: null handle");
+        HIP_TRY(hipSetDevice(h->device));
+        HIP_TRY(hipStreamSynchronize(h->stream));  // work queued on the old stream completes first
+        h->stream = static_cast<hipStream_t>(stream);
+        return GPAD_OK;
+    });
 }
 
 int gpad_set_option(gpad_handle_t h, int option, int value) {
-    if (!h) return fail(GPAD_ERR_INVALID, "gpad_set_option: null handle");
-    gpad::Tuning& t = h->tune;
-    const gpad::Tuning def{};
-    auto set = [&](int& field, int lo, int hi, int dflt) -> int {
-        if (value == GPAD_OPT_DEFAULT) {
-            field = dflt;
+    return gpad::abi_guard("gpad_set_option", [&]() -> int {
+        if (!h) return fail(GPAD_ERR_INVALID, "gpad_set_option: null handle");
+        gpad::Tuning& t = h->tune;
+        const gpad::Tuning def{};
+        auto set = [&](int& field, int lo, int hi, int dflt) -> int {
+            if (value == GPAD_OPT_DEFAULT) {
+                field = dflt;
+                return GPAD_OK;
+            }
+            if (value < lo || value > hi) return fail(GPAD_ERR_INVALID, "gpad_set_option: value out of range");
+            field = value;
             return GPAD_OK;
+        };
+        const int big = 1 << 30;
+        switch (option) {
+            case GPAD_OPT_PHASE_LEN: return set(t.phase_len, 0, big, def.phase_len);
+            case GPAD_OPT_FINISH_THRESH: return set(t.finish_thresh, 0, big, def.finish_thresh);
+            case GPAD_OPT_PLAN: h->plan.nph = 0; h->plan_key = 0; return set(t.plan, 0, 1, def.plan);
+            case GPAD_OPT_PHASED: return set(t.phased, 0, 2, def.phased);
+            case GPAD_OPT_LPT: return set(t.lpt, 0, 1, def.lpt);
+            case GPAD_OPT_PANEL_MAX_GRID: return set(t.panel_max_grid, 0, big, def.panel_max_grid);
+            case GPAD_OPT_DUO_MAX_GRID: return set(t.duo_max_grid, 0, big, def.duo_max_grid);
+            case GPAD_OPT_FLAT_PANEL_MIN: return set(t.flat_panel_min, 0, big, def.flat_panel_min);
+            case GPAD_OPT_FLAT_PANELS: return set(t.flat_panels, 0, 4, def.flat_panels);
+            case GPAD_OPT_FLAT_WAVES:
+                if (value != GPAD_OPT_DEFAULT && value != 0 && value != 8 && value != 16)
+                    return fail(GPAD_ERR_INVALID, "gpad_set_option: flat waves must be 0, 8 or 16");
+                return set(t.flat_waves, 0, 16, def.flat_waves);
+            case GPAD_OPT_FLAT_A_LDS: return set(t.flat_a_lds, 0, 1, def.flat_a_lds);
+            case GPAD_OPT_DEBUG_DROP_HANDOFF: return set(t.debug_drop_handoff, 0, 1, def.debug_drop_handoff);
+            case GPAD_OPT_P64_REFILL: {
+                int on = 1 - t.p64_no_refill;
+                const int rc = set(on, 0, 1, 1);
+                t.p64_no_refill = 1 - on;
+                return rc;
+            }
+            case GPAD_OPT_P64_RELAY: {
+                int on = 1 - t.p64_no_relay;
+                const int rc = set(on, 0, 1, 1);
+                t.p64_no_relay = 1 - on;
+                return rc;
+            }
+            default: return fail(GPAD_ERR_INVALID, "gpad_set_option: unknown option");
         }
-        if (value < lo || value > hi) return fail(GPAD_ERR_INVALID, "gpad_set_option: value out of range");
-        field = value;
-        return GPAD_OK;
-    };
-    const int big = 1 << 30;
-    switch (option) {
-        case GPAD_OPT_PHASE_LEN: return set(t.phase_len, 0, big, def.phase_len);
-        case GPAD_OPT_FINISH_THRESH: return set(t.finish_thresh, 0, big, def.finish_thresh);
-        case GPAD_OPT_PLAN: h->plan.nph = 0; h->plan_key = 0; return set(t.plan, 0, 1, def.plan);
-        case GPAD_OPT_PHASED: return set(t.phased, 0, 2, def.phased);
-        case GPAD_OPT_LPT: return set(t.lpt, 0, 1, def.lpt);
-        case GPAD_OPT_PANEL_MAX_GRID: return set(t.panel_max_grid, 0, big, def.panel_max_grid);
-        case GPAD_OPT_DUO_MAX_GRID: return set(t.duo_max_grid, 0, big, def.duo_max_grid);
-        case GPAD_OPT_FLAT_PANEL_MIN: return set(t.flat_panel_min, 0, big, def.flat_panel_min);
-        case GPAD_OPT_FLAT_PANELS: return set(t.flat_panels, 0, 4, def.flat_panels);
-        case GPAD_OPT_FLAT_WAVES:
-            if (value != GPAD_OPT_DEFAULT && value != 0 && value != 8 && value != 16)
-                return fail(GPAD_ERR_INVALID, "gpad_set_option: flat waves must be 0, 8 or 16");
-            return set(t.flat_waves, 0, 16, def.flat_waves);
-        case GPAD_OPT_FLAT_A_LDS: return set(t.flat_a_lds, 0, 1, def.flat_a_lds);
-        case GPAD_OPT_DEBUG_DROP_HANDOFF: return set(t.debug_drop_handoff, 0, 1, def.debug_drop_handoff);
-        case GPAD_OPT_P64_REFILL: {
-            int on = 1 - t.p64_no_refill;
-            const int rc = set(on, 0, 1, 1);
-            t.p64_no_refill = 1 - on;
-            return rc;
-        }
-        case GPAD_OPT_P64_RELAY: {
-            int on = 1 - t.p64_no_relay;
-            const int rc = set(on, 0, 1, 1);
-            t.p64_no_relay = 1 - on;
-            return rc;
-        }
-        default: return fail(GPAD_ERR_INVALID, "gpad_set_option: unknown option");
-    }
+    });
 }
 
 int gpad_sync(gpad_handle_t h) {
-    if (!h) return fail(GPAD_ERR_INVALID, "gpad_sync: null handle");
-    HIP_TRY(hipSetDevice(h->device));
-    RunStatus& rs = h->h_status;
-    int rc = fetch_status(h, &rs);
-    if (rc) return rc;
-    HIP_TRY(hipStreamSynchronize(h->stream));
-    return status_error(h, rs);
+    return gpad::abi_guard("gpad_sync", [&]() -> int {
+        if (!h) return fail(GPAD_ERR_INVALID, "gpad_sync: null handle");
+        HIP_TRY(hipSetDevice(h->device));
+        RunStatus& rs = h->h_status;
+        int rc = fetch_status(h, &rs);
+        if (rc) return rc;
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        return status_error(h, rs);
+    });
 }
 
 int gpad_schedule(int N, int kind, double* theta, double* beta) {
-    if (N < 0 || !theta || !beta) return fail(GPAD_ERR_INVALID, "gpad_schedule: bad arguments");
-    host_schedule(N, kind, theta, beta);
-    return GPAD_OK;
+    return gpad::abi_guard("gpad_schedule", [&]() -> int {
+        if (N < 0 || !theta || !beta) return fail(GPAD_ERR_INVALID, "gpad_schedule: bad arguments");
+        host_schedule(N, kind, theta, beta);
+        return GPAD_OK;
+    });
 }
 
 static int validate_dims(const gpad_dims_t* d) {
@@ -491,114 +505,122 @@ static int setup_impl(gpad_handle_t h, const gpad_dims_t* d, const void* A, cons
 }
 
 int gpad_setup(gpad_handle_t h, const gpad_dims_t* d, const void* ML, const void* G, double L) {
-    return setup_impl(h, d, ML, G, L, false);
+    return gpad::abi_guard("gpad_setup", [&]() -> int {
+        return setup_impl(h, d, ML, G, L, false);
+    });
 }
 
 int gpad_setup_scaled(gpad_handle_t h, const gpad_dims_t* d, const void* MGneg, const void* GL,
                       double L) {
-    return setup_impl(h, d, MGneg, GL, L, true);
+    return gpad::abi_guard("gpad_setup_scaled", [&]() -> int {
+        return setup_impl(h, d, MGneg, GL, L, true);
+    });
 }
 
 int gpad_setup_hessian(gpad_handle_t h, const void* H) {
-    if (!h) return fail(GPAD_ERR_INVALID, "gpad_setup_hessian: null handle");
-    if (!h->ready) return fail(GPAD_ERR_NOT_SETUP, "gpad_setup_hessian: call gpad_setup first");
-    if (h->flat) return fail(GPAD_ERR_UNSUPPORTED, "gpad_setup_hessian: not on the flat battery path");
-    h->hess_ok = false;
-    h->hfrag64_ok = false;
-    if (!H) return GPAD_OK;
-    HIP_TRY(hipSetDevice(h->device));
-    const gpad_dims_t& d = h->dims;
-    const int n = d.n, nmats = d.shared ? 1 : d.batch;
-    const size_t es = esize(d.dtype), raw = (size_t)n * n * nmats * es;
-    int rc;
-    if ((rc = h->Hq.ensure(es * (size_t)n * h->ldn * nmats))) return rc;
-    const void* dH = H;
-    DevBuf stage;
-    if (d.memory == GPAD_MEM_HOST) {
-        if ((rc = stage.ensure(raw))) return rc;
-        HIP_TRY(hipMemcpyAsync(stage.p, H, raw, hipMemcpyHostToDevice, h->stream));
-        dH = stage.p;
-    }
-    const long long in_stride = d.shared ? 0 : (long long)n * n, out_stride = (long long)n * h->ldn;
-    if (d.dtype == GPAD_DTYPE_F32)
-        HIP_TRY(gpad::launch_pack_kmajor<float>((const float*)dH, (float*)h->Hq.p, n, n, h->ldn, 1.0, nmats, in_stride,
-                                                out_stride, h->stream));
-    else
-        HIP_TRY(gpad::launch_pack_kmajor<double>((const double*)dH, (double*)h->Hq.p, n, n, h->ldn, 1.0, nmats,
-                                                 in_stride, out_stride, h->stream));
-    if (h->frag64_ok) {  // shared f64: H for the f64 panels' value branches
-        if ((rc = h->hfrag64.ensure(gpad::panel64_frag_bytes(n, d.m)))) return rc;
-        HIP_TRY(gpad::launch_pack_panel64((const double*)dH, n, n, 1.0, h->frag64_tiles, h->hfrag64.p, h->stream));
-        h->hfrag64_ok = true;
-    }
-    HIP_TRY(hipStreamSynchronize(h->stream));
-    h->hess_ok = true;
-    return GPAD_OK;
+    return gpad::abi_guard("gpad_setup_hessian", [&]() -> int {
+        if (!h) return fail(GPAD_ERR_INVALID, "gpad_setup_hessian: null handle");
+        if (!h->ready) return fail(GPAD_ERR_NOT_SETUP, "gpad_setup_hessian: call gpad_setup first");
+        if (h->flat) return fail(GPAD_ERR_UNSUPPORTED, "gpad_setup_hessian: not on the flat battery path");
+        h->hess_ok = false;
+        h->hfrag64_ok = false;
+        if (!H) return GPAD_OK;
+        HIP_TRY(hipSetDevice(h->device));
+        const gpad_dims_t& d = h->dims;
+        const int n = d.n, nmats = d.shared ? 1 : d.batch;
+        const size_t es = esize(d.dtype), raw = (size_t)n * n * nmats * es;
+        int rc;
+        if ((rc = h->Hq.ensure(es * (size_t)n * h->ldn * nmats))) return rc;
+        const void* dH = H;
+        DevBuf stage;
+        if (d.memory == GPAD_MEM_HOST) {
+            if ((rc = stage.ensure(raw))) return rc;
+            HIP_TRY(hipMemcpyAsync(stage.p, H, raw, hipMemcpyHostToDevice, h->stream));
+            dH = stage.p;
+        }
+        const long long in_stride = d.shared ? 0 : (long long)n * n, out_stride = (long long)n * h->ldn;
+        if (d.dtype == GPAD_DTYPE_F32)
+            HIP_TRY(gpad::launch_pack_kmajor<float>((const float*)dH, (float*)h->Hq.p, n, n, h->ldn, 1.0, nmats, in_stride,
+                                                    out_stride, h->stream));
+        else
+            HIP_TRY(gpad::launch_pack_kmajor<double>((const double*)dH, (double*)h->Hq.p, n, n, h->ldn, 1.0, nmats,
+                                                     in_stride, out_stride, h->stream));
+        if (h->frag64_ok) {  // shared f64: H for the f64 panels' value branches
+            if ((rc = h->hfrag64.ensure(gpad::panel64_frag_bytes(n, d.m)))) return rc;
+            HIP_TRY(gpad::launch_pack_panel64((const double*)dH, n, n, 1.0, h->frag64_tiles, h->hfrag64.p, h->stream));
+            h->hfrag64_ok = true;
+        }
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        h->hess_ok = true;
+        return GPAD_OK;
+    });
 }
 
 int gpad_setup_flat(gpad_handle_t h, const gpad_dims_t* d, int n_u, const float* MGf, const float* GLf,
                     double L) {
-    if (!h) return fail(GPAD_ERR_INVALID, "gpad_setup_flat: null handle");
-    int rc = validate_dims(d);
-    if (rc) return rc;
-    if (!MGf || !GLf) return fail(GPAD_ERR_INVALID, "gpad_setup_flat: null matrix");
-    if (!(L > 0.0) || !std::isfinite(L)) return fail(GPAD_ERR_INVALID, "gpad_setup_flat: L must be > 0");
-    if (d->dtype != GPAD_DTYPE_F32 || !d->shared)
-        return fail(GPAD_ERR_UNSUPPORTED, "gpad_setup_flat: f32 and shared matrices only");
-    if (n_u <= 0 || d->n % n_u != 0 || d->m < 4 * d->n)
-        return fail(GPAD_ERR_INVALID, "gpad_setup_flat: need n = n_u*N and m >= 4 n_u N");
-    HIP_TRY(hipSetDevice(h->device));
-    h->ready = false;
-    h->flat = false;
-    h->shadow_ok = false;
-    h->hess_ok = false;
-    h->plan.nph = 0;
-    h->p64_order_batch = 0;  // (a new problem: the previous counts order nothing)
-    h->flat_vpred = 0;
-    h->plan_pending = false;
-    h->last_phased = false;
-    h->dims = *d;
-    if (h->dims.check_every <= 0) h->dims.check_every = 10;
-    h->L = L;
-    h->scaled = true;
-    const int Nh = d->n / n_u, m = d->m;
-    const size_t bytes = sizeof(float) * (size_t)Nh * m;
-    h->ldn = round4(d->n);
-    h->ldm = round4(m);
-    if ((rc = h->MGt.ensure(bytes)) || (rc = h->GLt.ensure(bytes))) return rc;
-    const void* dG = GLf;
-    if (d->memory == GPAD_MEM_HOST) {
-        if ((rc = h->stage.ensure(bytes))) return rc;
-        HIP_TRY(hipMemcpyAsync(h->MGt.p, MGf, bytes, hipMemcpyHostToDevice, h->stream));
-        HIP_TRY(hipMemcpyAsync(h->stage.p, GLf, bytes, hipMemcpyHostToDevice, h->stream));
-        dG = h->stage.p;
-    } else {
-        HIP_TRY(hipMemcpyAsync(h->MGt.p, MGf, bytes, hipMemcpyDeviceToDevice, h->stream));
-    }
-    HIP_TRY(gpad::launch_transpose_flat((const float*)dG, (float*)h->GLt.p, m, Nh, h->stream));
-    h->GLx.release();
-    if (gpad::flat_resident_supported(d->n, m, n_u)) {
-        if ((rc = h->GLx.ensure(sizeof(float) * (size_t)d->n * h->ldm))) return rc;
-        HIP_TRY(gpad::launch_expand_flat_gl((const float*)dG, (float*)h->GLx.p, Nh, n_u, m, h->ldm,
-                                            h->stream));
-    }
-    h->frag_ok = false;
-    h->frag_tiles = 0;
-    {  // MFMA panels over the flat data (gpad_flatpanel.hip)
-        const size_t fb = gpad::flatpanel_frag_bytes(d->n, m, n_u);
-        if (fb) {
-            if ((rc = h->frag.ensure(fb))) return rc;
-            HIP_TRY(gpad::launch_pack_flatpanel((const float*)h->MGt.p, (const float*)h->GLt.p, d->n, m, n_u,
-                                                h->frag.p, h->stream));
-            h->frag_ok = true;
+    return gpad::abi_guard("gpad_setup_flat", [&]() -> int {
+        if (!h) return fail(GPAD_ERR_INVALID, "gpad_setup_flat: null handle");
+        int rc = validate_dims(d);
+        if (rc) return rc;
+        if (!MGf || !GLf) return fail(GPAD_ERR_INVALID, "gpad_setup_flat: null matrix");
+        if (!(L > 0.0) || !std::isfinite(L)) return fail(GPAD_ERR_INVALID, "gpad_setup_flat: L must be > 0");
+        if (d->dtype != GPAD_DTYPE_F32 || !d->shared)
+            return fail(GPAD_ERR_UNSUPPORTED, "gpad_setup_flat: f32 and shared matrices only");
+        if (n_u <= 0 || d->n % n_u != 0 || d->m < 4 * d->n)
+            return fail(GPAD_ERR_INVALID, "gpad_setup_flat: need n = n_u*N and m >= 4 n_u N");
+        HIP_TRY(hipSetDevice(h->device));
+        h->ready = false;
+        h->flat = false;
+        h->shadow_ok = false;
+        h->hess_ok = false;
+        h->plan.nph = 0;
+        h->p64_order_batch = 0;  // (a new problem: the previous counts order nothing)
+        h->flat_vpred = 0;
+        h->plan_pending = false;
+        h->last_phased = false;
+        h->dims = *d;
+        if (h->dims.check_every <= 0) h->dims.check_every = 10;
+        h->L = L;
+        h->scaled = true;
+        const int Nh = d->n / n_u, m = d->m;
+        const size_t bytes = sizeof(float) * (size_t)Nh * m;
+        h->ldn = round4(d->n);
+        h->ldm = round4(m);
+        if ((rc = h->MGt.ensure(bytes)) || (rc = h->GLt.ensure(bytes))) return rc;
+        const void* dG = GLf;
+        if (d->memory == GPAD_MEM_HOST) {
+            if ((rc = h->stage.ensure(bytes))) return rc;
+            HIP_TRY(hipMemcpyAsync(h->MGt.p, MGf, bytes, hipMemcpyHostToDevice, h->stream));
+            HIP_TRY(hipMemcpyAsync(h->stage.p, GLf, bytes, hipMemcpyHostToDevice, h->stream));
+            dG = h->stage.p;
+        } else {
+            HIP_TRY(hipMemcpyAsync(h->MGt.p, MGf, bytes, hipMemcpyDeviceToDevice, h->stream));
         }
-    }
-    HIP_TRY(hipStreamSynchronize(h->stream));
-    if (d->memory == GPAD_MEM_HOST && !h->keep_stage) h->stage.release();
-    h->n_u = n_u;
-    h->flat = true;
-    h->ready = true;
-    return GPAD_OK;
+        HIP_TRY(gpad::launch_transpose_flat((const float*)dG, (float*)h->GLt.p, m, Nh, h->stream));
+        h->GLx.release();
+        if (gpad::flat_resident_supported(d->n, m, n_u)) {
+            if ((rc = h->GLx.ensure(sizeof(float) * (size_t)d->n * h->ldm))) return rc;
+            HIP_TRY(gpad::launch_expand_flat_gl((const float*)dG, (float*)h->GLx.p, Nh, n_u, m, h->ldm,
+                                                h->stream));
+        }
+        h->frag_ok = false;
+        h->frag_tiles = 0;
+        {  // MFMA panels over the flat data (gpad_flatpanel.hip)
+            const size_t fb = gpad::flatpanel_frag_bytes(d->n, m, n_u);
+            if (fb) {
+                if ((rc = h->frag.ensure(fb))) return rc;
+                HIP_TRY(gpad::launch_pack_flatpanel((const float*)h->MGt.p, (const float*)h->GLt.p, d->n, m, n_u,
+                                                    h->frag.p, h->stream));
+                h->frag_ok = true;
+            }
+        }
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        if (d->memory == GPAD_MEM_HOST && !h->keep_stage) h->stage.release();
+        h->n_u = n_u;
+        h->flat = true;
+        h->ready = true;
+        return GPAD_OK;
+    });
 }
 
 static int ensure_schedule(gpad_handle_t h, int N, const void* theta_in, const void* beta_in) {
@@ -757,61 +779,71 @@ static int collect_stats(gpad_handle_t h, gpad_stats_t* st) {
 }
 
 int gpad_accumulate_iterations(gpad_handle_t h, long long* acc) {
-    if (!h || !acc) return fail(GPAD_ERR_INVALID, "gpad_accumulate_iterations: null argument");
-    if (h->last_batch <= 0) return fail(GPAD_ERR_NOT_SETUP, "gpad_accumulate_iterations: no run yet");
-    HIP_TRY(hipSetDevice(h->device));
-    // counters: [steps][iters[batch] | conv[batch]]; each solve's iteration block in turn
-    for (int t = 0; t < h->last_steps; ++t)
-        HIP_TRY(gpad::launch_accumulate_iters((const int*)h->counters.p + (size_t)2 * h->last_batch * t,
-                                              h->last_batch, acc, h->stream));
-    return GPAD_OK;
+    return gpad::abi_guard("gpad_accumulate_iterations", [&]() -> int {
+        if (!h || !acc) return fail(GPAD_ERR_INVALID, "gpad_accumulate_iterations: null argument");
+        if (h->last_batch <= 0) return fail(GPAD_ERR_NOT_SETUP, "gpad_accumulate_iterations: no run yet");
+        HIP_TRY(hipSetDevice(h->device));
+        // counters: [steps][iters[batch] | conv[batch]]; each solve's iteration block in turn
+        for (int t = 0; t < h->last_steps; ++t)
+            HIP_TRY(gpad::launch_accumulate_iters((const int*)h->counters.p + (size_t)2 * h->last_batch * t,
+                                                  h->last_batch, acc, h->stream));
+        return GPAD_OK;
+    });
 }
 
 int gpad_last_stats(gpad_handle_t h, gpad_stats_t* st) {
-    if (!h || !st) return fail(GPAD_ERR_INVALID, "gpad_last_stats: null argument");
-    if (h->last_batch <= 0) return fail(GPAD_ERR_NOT_SETUP, "gpad_last_stats: no run yet");
-    HIP_TRY(hipSetDevice(h->device));
-    return collect_stats(h, st);
+    return gpad::abi_guard("gpad_last_stats", [&]() -> int {
+        if (!h || !st) return fail(GPAD_ERR_INVALID, "gpad_last_stats: null argument");
+        if (h->last_batch <= 0) return fail(GPAD_ERR_NOT_SETUP, "gpad_last_stats: no run yet");
+        HIP_TRY(hipSetDevice(h->device));
+        return collect_stats(h, st);
+    });
 }
 
 int gpad_phase_plan(gpad_handle_t h, int* ends, int* fins, int cap, double* cost_us) {
-    if (!h) return fail(GPAD_ERR_INVALID, "gpad_phase_plan: null handle");
-    const int n = h->plan.nph;
-    for (int i = 0; i < n && i < cap; ++i) {
-        if (ends) ends[i] = h->plan.ends[i];
-        if (fins) fins[i] = h->plan.fins[i];
-    }
-    if (cost_us) *cost_us = h->plan.cost_us;
-    return n;
+    return gpad::abi_guard("gpad_phase_plan", [&]() -> int {
+        if (!h) return fail(GPAD_ERR_INVALID, "gpad_phase_plan: null handle");
+        const int n = h->plan.nph;
+        for (int i = 0; i < n && i < cap; ++i) {
+            if (ends) ends[i] = h->plan.ends[i];
+            if (fins) fins[i] = h->plan.fins[i];
+        }
+        if (cost_us) *cost_us = h->plan.cost_us;
+        return n;
+    });
 }
 
 int gpad_last_phases(gpad_handle_t h, int* ends, int* fins, int* counts, int cap, int* prior) {
-    if (!h || cap < 0) return fail(GPAD_ERR_INVALID, "gpad_last_phases: bad argument");
-    if (prior) *prior = h->last_prior ? 1 : 0;
-    if (!h->last_phased || !h->pwork.p || h->flat) return 0;
-    const int k = std::min(cap, h->last_phases.nph);
-    for (int i = 0; i < k; ++i) {
-        if (ends) ends[i] = h->last_phases.ends[i];
-        if (fins) fins[i] = h->last_phases.fins[i];
-    }
-    if (counts && k > 0) {
-        HIP_TRY(hipSetDevice(h->device));
-        const int* dev = reinterpret_cast<const int*>(h->pwork.p) + 2 * (size_t)h->last_batch;  // panel_work_bytes
-        HIP_TRY(hipMemcpyAsync(counts, dev, sizeof(int) * (size_t)k, hipMemcpyDeviceToHost, h->stream));
-        HIP_TRY(hipStreamSynchronize(h->stream));
-    }
-    return k;
+    return gpad::abi_guard("gpad_last_phases", [&]() -> int {
+        if (!h || cap < 0) return fail(GPAD_ERR_INVALID, "gpad_last_phases: bad argument");
+        if (prior) *prior = h->last_prior ? 1 : 0;
+        if (!h->last_phased || !h->pwork.p || h->flat) return 0;
+        const int k = std::min(cap, h->last_phases.nph);
+        for (int i = 0; i < k; ++i) {
+            if (ends) ends[i] = h->last_phases.ends[i];
+            if (fins) fins[i] = h->last_phases.fins[i];
+        }
+        if (counts && k > 0) {
+            HIP_TRY(hipSetDevice(h->device));
+            const int* dev = reinterpret_cast<const int*>(h->pwork.p) + 2 * (size_t)h->last_batch;  // panel_work_bytes
+            HIP_TRY(hipMemcpyAsync(counts, dev, sizeof(int) * (size_t)k, hipMemcpyDeviceToHost, h->stream));
+            HIP_TRY(hipStreamSynchronize(h->stream));
+        }
+        return k;
+    });
 }
 
 int gpad_phase_counts(gpad_handle_t h, int* counts, int cap) {
-    if (!h || !counts || cap < 0) return fail(GPAD_ERR_INVALID, "gpad_phase_counts: bad argument");
-    if (!h->last_phased || !h->pwork.p) return 0;
-    HIP_TRY(hipSetDevice(h->device));
-    const int k = cap < gpad::kPanelMaxPhases ? cap : gpad::kPanelMaxPhases;
-    const int* dev = reinterpret_cast<const int*>(h->pwork.p) + 2 * (size_t)h->last_batch;  // panel_work_bytes
-    HIP_TRY(hipMemcpyAsync(counts, dev, sizeof(int) * (size_t)k, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
-    return k;
+    return gpad::abi_guard("gpad_phase_counts", [&]() -> int {
+        if (!h || !counts || cap < 0) return fail(GPAD_ERR_INVALID, "gpad_phase_counts: bad argument");
+        if (!h->last_phased || !h->pwork.p) return 0;
+        HIP_TRY(hipSetDevice(h->device));
+        const int k = cap < gpad::kPanelMaxPhases ? cap : gpad::kPanelMaxPhases;
+        const int* dev = reinterpret_cast<const int*>(h->pwork.p) + 2 * (size_t)h->last_batch;  // panel_work_bytes
+        HIP_TRY(hipMemcpyAsync(counts, dev, sizeof(int) * (size_t)k, hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        return k;
+    });
 }
 
 #ifdef GPAD_STAMP
@@ -823,32 +855,40 @@ hipError_t read_duo_stamps(unsigned long long* out, size_t bytes);  // gpad_duo.
 }
 extern "C" {
 int gpad_debug_res_stamps(unsigned long long* out, size_t bytes) {
-    HIP_TRY(gpad::read_res_stamps(out, bytes));
-    return GPAD_OK;
+    return gpad::abi_guard("gpad_debug_res_stamps", [&]() -> int {
+        HIP_TRY(gpad::read_res_stamps(out, bytes));
+        return GPAD_OK;
+    });
 }
 int gpad_debug_duo_stamps(unsigned long long* out, size_t bytes) {
-    HIP_TRY(gpad::read_duo_stamps(out, bytes));
-    return GPAD_OK;
+    return gpad::abi_guard("gpad_debug_duo_stamps", [&]() -> int {
+        HIP_TRY(gpad::read_duo_stamps(out, bytes));
+        return GPAD_OK;
+    });
 }
 // diagnostic builds only (not declared in gpad.h): the phase-anatomy stamps of the last panel-pair run
 int gpad_debug_stamps(unsigned long long* out, size_t bytes) {
-    HIP_TRY(gpad::read_stamps(out, bytes));
-    return GPAD_OK;
+    return gpad::abi_guard("gpad_debug_stamps", [&]() -> int {
+        HIP_TRY(gpad::read_stamps(out, bytes));
+        return GPAD_OK;
+    });
 }
 #endif
 
 int gpad_plan_phases(const int* iters, int batch, int n, int m, int N, int check_every, int num_cus,
                      int* ends, int* fins, int cap, double* cost_us) {
-    if (!iters || batch <= 0 || n <= 0 || m <= 0 || N <= 0 || num_cus <= 0)
-        return fail(GPAD_ERR_INVALID, "gpad_plan_phases: bad argument");
-    gpad::PanelPlan p;
-    gpad::panel_plan(iters, batch, n, m, N, check_every, num_cus, nullptr, &p);
-    for (int i = 0; i < p.nph && i < cap; ++i) {
-        if (ends) ends[i] = p.ends[i];
-        if (fins) fins[i] = p.fins[i];
-    }
-    if (cost_us) *cost_us = p.cost_us;
-    return p.nph;
+    return gpad::abi_guard("gpad_plan_phases", [&]() -> int {
+        if (!iters || batch <= 0 || n <= 0 || m <= 0 || N <= 0 || num_cus <= 0)
+            return fail(GPAD_ERR_INVALID, "gpad_plan_phases: bad argument");
+        gpad::PanelPlan p;
+        gpad::panel_plan(iters, batch, n, m, N, check_every, num_cus, nullptr, &p);
+        for (int i = 0; i < p.nph && i < cap; ++i) {
+            if (ends) ends[i] = p.ends[i];
+            if (fins) fins[i] = p.fins[i];
+        }
+        if (cost_us) *cost_us = p.cost_us;
+        return p.nph;
+    });
 }
 
 }  // extern "C"
@@ -1132,12 +1172,16 @@ static int run_impl(gpad_handle_t h, void* z0, void* y0, const void* M, const vo
 
 int gpad_run(gpad_handle_t h, void* z0, void* y0, const void* M, const void* g, int N, double tol,
              gpad_stats_t* st) {
-    return run_impl(h, z0, y0, M, g, N, tol, nullptr, nullptr, false, st);
+    return gpad::abi_guard("gpad_run", [&]() -> int {
+        return run_impl(h, z0, y0, M, g, N, tol, nullptr, nullptr, false, st);
+    });
 }
 
 int gpad_run_scaled(gpad_handle_t h, void* z0, void* y0, const void* gP, const void* pD, int N,
                     double tol, const void* theta, const void* beta, gpad_stats_t* st) {
-    return run_impl(h, z0, y0, gP, pD, N, tol, theta, beta, true, st);
+    return gpad::abi_guard("gpad_run_scaled", [&]() -> int {
+        return run_impl(h, z0, y0, gP, pD, N, tol, theta, beta, true, st);
+    });
 }
 
 // field by field: a stack-built dims may carry different padding bytes on every call
@@ -1170,45 +1214,47 @@ void gpad_release_cached(void) {
 
 int gpad_solve(void* z0, void* y0, const void* ML, const void* M, const void* G, const void* g, int N,
                double L, double tol, const gpad_dims_t* dims, gpad_stats_t* st) {
-    // One handle per thread and device, kept between calls: a per-MPC-step caller (gpad.m:90)
-    // pays the handle, the workspaces and -- when the host matrices are unchanged -- the H2D
-    // copy and repack of ML/G once, not per call.  gpad_release_cached() frees it.
-    SolveCache& cache = t_solve_cache;
-    int rc = validate_dims(dims);
-    if (rc) return rc;
-    if (!ML || !G) return fail(GPAD_ERR_INVALID, "gpad_solve: null matrix");
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev));
-    if (!cache.h || cache.device != dev) {
-        if (cache.h) gpad_destroy(cache.h);
-        cache.h = nullptr;
-        if ((rc = gpad_create(&cache.h, dev, nullptr))) return rc;
-        cache.device = dev;
-        cache.h->keep_stage = true;
-    }
-    gpad_handle_t h = cache.h;
-    // host matrices: reuse the bound problem when (dims, L, ML, G) equal the last call's; the
-    // comparison is the full contents (a caller may rewrite its buffers in place).  Device
-    // matrices are always repacked (two stream-ordered pack kernels, no copy).
-    const bool host = dims->memory == GPAD_MEM_HOST;
-    const size_t bytes = (size_t)dims->n * dims->m * esize(dims->dtype) * (dims->shared ? 1 : dims->batch);
-    bool same = false;
-    if (host && h->ready && h->shadow_ok && L == h->shadow_L && same_dims(h->shadow_dims, *dims) &&
-        h->shadow.size() == 2 * bytes)
-        same = std::memcmp(h->shadow.data(), ML, bytes) == 0 && std::memcmp(h->shadow.data() + bytes, G, bytes) == 0;
-    if (!same) {
-        if ((rc = gpad_setup(h, dims, ML, G, L))) return rc;
-        if (host) {
-            h->shadow.resize(2 * bytes);
-            std::memcpy(h->shadow.data(), ML, bytes);
-            std::memcpy(h->shadow.data() + bytes, G, bytes);
-            h->shadow_dims = *dims;
-            h->shadow_L = L;
-            h->shadow_ok = true;
+    return gpad::abi_guard("gpad_solve", [&]() -> int {
+        // One handle per thread and device, kept between calls: a per-MPC-step caller (gpad.m:90)
+        // pays the handle, the workspaces and -- when the host matrices are unchanged -- the H2D
+        // copy and repack of ML/G once, not per call.  gpad_release_cached() frees it.
+        SolveCache& cache = t_solve_cache;
+        int rc = validate_dims(dims);
+        if (rc) return rc;
+        if (!ML || !G) return fail(GPAD_ERR_INVALID, "gpad_solve: null matrix");
+        int dev = 0;
+        HIP_TRY(hipGetDevice(&dev));
+        if (!cache.h || cache.device != dev) {
+            if (cache.h) gpad_destroy(cache.h);
+            cache.h = nullptr;
+            if ((rc = gpad_create(&cache.h, dev, nullptr))) return rc;
+            cache.device = dev;
+            cache.h->keep_stage = true;
         }
-    }
-    if ((rc = gpad_run(h, z0, y0, M, g, N, tol, st))) return rc;
-    return gpad_sync(h);
+        gpad_handle_t h = cache.h;
+        // host matrices: reuse the bound problem when (dims, L, ML, G) equal the last call's; the
+        // comparison is the full contents (a caller may rewrite its buffers in place).  Device
+        // matrices are always repacked (two stream-ordered pack kernels, no copy).
+        const bool host = dims->memory == GPAD_MEM_HOST;
+        const size_t bytes = (size_t)dims->n * dims->m * esize(dims->dtype) * (dims->shared ? 1 : dims->batch);
+        bool same = false;
+        if (host && h->ready && h->shadow_ok && L == h->shadow_L && same_dims(h->shadow_dims, *dims) &&
+            h->shadow.size() == 2 * bytes)
+            same = std::memcmp(h->shadow.data(), ML, bytes) == 0 && std::memcmp(h->shadow.data() + bytes, G, bytes) == 0;
+        if (!same) {
+            if ((rc = gpad_setup(h, dims, ML, G, L))) return rc;
+            if (host) {
+                h->shadow.resize(2 * bytes);
+                std::memcpy(h->shadow.data(), ML, bytes);
+                std::memcpy(h->shadow.data() + bytes, G, bytes);
+                h->shadow_dims = *dims;
+                h->shadow_L = L;
+                h->shadow_ok = true;
+            }
+        }
+        if ((rc = gpad_run(h, z0, y0, M, g, N, tol, st))) return rc;
+        return gpad_sync(h);
+    });
 }
 
 // ---- per-state QP data and closed-loop MPC (gpad.m:79-95) --------
@@ -1233,105 +1279,109 @@ PlantOffsets plant_offsets(int n, int m, int nx, int nu) {
 
 extern "C" int gpad_precompute(gpad_handle_t h, int n, int m, int batch, int shared, int memory, const double* H,
                                const double* A, const double* f, double* ML, double* gP, double* L) {
-    if (!h) return fail(GPAD_ERR_INVALID, "gpad_precompute: null handle");
-    if (n <= 0 || m < 0 || batch <= 0 || !H || !A || !ML || !L || (f == nullptr) != (gP == nullptr) ||
-        (memory != GPAD_MEM_HOST && memory != GPAD_MEM_DEVICE))
-        return fail(GPAD_ERR_INVALID, "gpad_precompute: bad arguments");
-    HIP_TRY(hipSetDevice(h->device));
-    const bool host = memory == GPAD_MEM_HOST;
-    const int nmat = shared ? 1 : batch;  // eliminations
-    const size_t nH = (size_t)nmat * n * n, nA = (size_t)nmat * m * n, nML = (size_t)nmat * n * m;
-    const size_t nF = f ? (size_t)batch * n : 0;
-    // shared: one elimination of [H | A' | I] gives ML and inv(H); gP = inv(H) f' per row after
-    const int fchunk = shared ? (f ? n : 0) : (f ? 1 : 0);
-    if (!gpad::precompute_supported(n, m, fchunk))
-        return fail(GPAD_ERR_UNSUPPORTED, "gpad_precompute: 2n + m too large for the LDS pivot row");
-    // device views of the operands (host memory: staged copies)
-    DevBuf stage, work;
-    const double *dH = H, *dA = A, *df = f;
-    double *dML = ML, *dgP = gP, *dL = L;
-    const size_t tot = nH + nA + nF + nML + nF + nmat;
-    int rc;
-    if (host) {
-        if ((rc = stage.ensure(sizeof(double) * tot))) return rc;
-        double* b = (double*)stage.p;
-        double* sH = b;
-        double* sA = sH + nH;
-        double* sf = sA + nA;
-        dML = sf + nF;
-        dgP = f ? dML + nML : nullptr;
-        dL = dML + nML + nF;
-        HIP_TRY(hipMemcpyAsync(sH, H, sizeof(double) * nH, hipMemcpyHostToDevice, h->stream));
-        HIP_TRY(hipMemcpyAsync(sA, A, sizeof(double) * nA, hipMemcpyHostToDevice, h->stream));
-        if (f) HIP_TRY(hipMemcpyAsync(sf, f, sizeof(double) * nF, hipMemcpyHostToDevice, h->stream));
-        dH = sH;
-        dA = sA;
-        df = f ? sf : nullptr;
-    }
-    if (shared) {
-        const size_t wb = gpad::precompute_work_bytes(n, m, fchunk, 1);
-        if ((rc = work.ensure(wb + (f ? sizeof(double) * (size_t)n * n : 0)))) return rc;
-        double* Hinv = f ? (double*)((char*)work.p + wb) : nullptr;
-        HIP_TRY(gpad::launch_precompute(n, m, fchunk, dH, 0, dA, 0, nullptr, 0, (double*)work.p, dML, Hinv, dL, 0, 1,
-                                        h->stream));
-        if (f) HIP_TRY(gpad::launch_apply_inv(n, batch, Hinv, df, dgP, h->stream));
-    } else {
-        const size_t per = gpad::precompute_work_bytes(n, m, fchunk, 1);
-        int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)batch, ((size_t)1 << 30) / per));
-        chunk = std::min(chunk, 4 * h->num_cus);
-        if ((rc = work.ensure(per * chunk))) return rc;
-        for (int b0 = 0; b0 < batch; b0 += chunk) {
-            const int cnt = std::min(chunk, batch - b0);
-            HIP_TRY(gpad::launch_precompute(n, m, fchunk, dH, (long long)n * n, dA, (long long)m * n, df, n,
-                                            (double*)work.p, dML, dgP, dL, b0, cnt, h->stream));
+    return gpad::abi_guard("gpad_precompute", [&]() -> int {
+        if (!h) return fail(GPAD_ERR_INVALID, "gpad_precompute: null handle");
+        if (n <= 0 || m < 0 || batch <= 0 || !H || !A || !ML || !L || (f == nullptr) != (gP == nullptr) ||
+            (memory != GPAD_MEM_HOST && memory != GPAD_MEM_DEVICE))
+            return fail(GPAD_ERR_INVALID, "gpad_precompute: bad arguments");
+        HIP_TRY(hipSetDevice(h->device));
+        const bool host = memory == GPAD_MEM_HOST;
+        const int nmat = shared ? 1 : batch;  // eliminations
+        const size_t nH = (size_t)nmat * n * n, nA = (size_t)nmat * m * n, nML = (size_t)nmat * n * m;
+        const size_t nF = f ? (size_t)batch * n : 0;
+        // shared: one elimination of [H | A' | I] gives ML and inv(H); gP = inv(H) f' per row after
+        const int fchunk = shared ? (f ? n : 0) : (f ? 1 : 0);
+        if (!gpad::precompute_supported(n, m, fchunk))
+            return fail(GPAD_ERR_UNSUPPORTED, "gpad_precompute: 2n + m too large for the LDS pivot row");
+        // device views of the operands (host memory: staged copies)
+        DevBuf stage, work;
+        const double *dH = H, *dA = A, *df = f;
+        double *dML = ML, *dgP = gP, *dL = L;
+        const size_t tot = nH + nA + nF + nML + nF + nmat;
+        int rc;
+        if (host) {
+            if ((rc = stage.ensure(sizeof(double) * tot))) return rc;
+            double* b = (double*)stage.p;
+            double* sH = b;
+            double* sA = sH + nH;
+            double* sf = sA + nA;
+            dML = sf + nF;
+            dgP = f ? dML + nML : nullptr;
+            dL = dML + nML + nF;
+            HIP_TRY(hipMemcpyAsync(sH, H, sizeof(double) * nH, hipMemcpyHostToDevice, h->stream));
+            HIP_TRY(hipMemcpyAsync(sA, A, sizeof(double) * nA, hipMemcpyHostToDevice, h->stream));
+            if (f) HIP_TRY(hipMemcpyAsync(sf, f, sizeof(double) * nF, hipMemcpyHostToDevice, h->stream));
+            dH = sH;
+            dA = sA;
+            df = f ? sf : nullptr;
         }
-    }
-    if (host) {
-        HIP_TRY(hipMemcpyAsync(ML, dML, sizeof(double) * nML, hipMemcpyDeviceToHost, h->stream));
-        if (f) HIP_TRY(hipMemcpyAsync(gP, dgP, sizeof(double) * nF, hipMemcpyDeviceToHost, h->stream));
-        HIP_TRY(hipMemcpyAsync(L, dL, sizeof(double) * nmat, hipMemcpyDeviceToHost, h->stream));
-    }
-    HIP_TRY(hipStreamSynchronize(h->stream));
-    return GPAD_OK;
+        if (shared) {
+            const size_t wb = gpad::precompute_work_bytes(n, m, fchunk, 1);
+            if ((rc = work.ensure(wb + (f ? sizeof(double) * (size_t)n * n : 0)))) return rc;
+            double* Hinv = f ? (double*)((char*)work.p + wb) : nullptr;
+            HIP_TRY(gpad::launch_precompute(n, m, fchunk, dH, 0, dA, 0, nullptr, 0, (double*)work.p, dML, Hinv, dL, 0, 1,
+                                            h->stream));
+            if (f) HIP_TRY(gpad::launch_apply_inv(n, batch, Hinv, df, dgP, h->stream));
+        } else {
+            const size_t per = gpad::precompute_work_bytes(n, m, fchunk, 1);
+            int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)batch, ((size_t)1 << 30) / per));
+            chunk = std::min(chunk, 4 * h->num_cus);
+            if ((rc = work.ensure(per * chunk))) return rc;
+            for (int b0 = 0; b0 < batch; b0 += chunk) {
+                const int cnt = std::min(chunk, batch - b0);
+                HIP_TRY(gpad::launch_precompute(n, m, fchunk, dH, (long long)n * n, dA, (long long)m * n, df, n,
+                                                (double*)work.p, dML, dgP, dL, b0, cnt, h->stream));
+            }
+        }
+        if (host) {
+            HIP_TRY(hipMemcpyAsync(ML, dML, sizeof(double) * nML, hipMemcpyDeviceToHost, h->stream));
+            if (f) HIP_TRY(hipMemcpyAsync(gP, dgP, sizeof(double) * nF, hipMemcpyDeviceToHost, h->stream));
+            HIP_TRY(hipMemcpyAsync(L, dL, sizeof(double) * nmat, hipMemcpyDeviceToHost, h->stream));
+        }
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        return GPAD_OK;
+    });
 }
 
 extern "C" int gpad_setup_plant(gpad_handle_t h, int nx, int nu, const void* PM, const void* M0,
                                 const void* Pg, const void* g0, const void* A, const void* B) {
-    if (!h) return fail(GPAD_ERR_INVALID, "gpad_setup_plant: null handle");
-    if (!h->ready) return fail(GPAD_ERR_NOT_SETUP, "gpad_setup_plant: call gpad_setup first");
-    if (nx <= 0 || nu < 0 || !PM || !Pg) return fail(GPAD_ERR_INVALID, "gpad_setup_plant: bad arguments");
-    if ((A == nullptr) != (B == nullptr) || (A && nu == 0))
-        return fail(GPAD_ERR_INVALID, "gpad_setup_plant: give A and B together (nu >= 1)");
-    if (nu > h->dims.n) return fail(GPAD_ERR_INVALID, "gpad_setup_plant: nu > n");
-    HIP_TRY(hipSetDevice(h->device));
-    const int n = h->dims.n, m = h->dims.m;
-    const size_t es = esize(h->dims.dtype);
-    const PlantOffsets o = plant_offsets(n, m, nx, nu);
-    int rc;
-    if ((rc = h->plant.ensure(es * o.total))) return rc;
-    char* base = (char*)h->plant.p;
-    const hipMemcpyKind kind = h->dims.memory == GPAD_MEM_HOST ? hipMemcpyHostToDevice
-                                                                : hipMemcpyDeviceToDevice;
-    auto put = [&](size_t off, const void* src, size_t elems) -> int {
-        if (!src || elems == 0) return GPAD_OK;
-        HIP_TRY(hipMemcpyAsync(base + es * off, src, es * elems, kind, h->stream));
+    return gpad::abi_guard("gpad_setup_plant", [&]() -> int {
+        if (!h) return fail(GPAD_ERR_INVALID, "gpad_setup_plant: null handle");
+        if (!h->ready) return fail(GPAD_ERR_NOT_SETUP, "gpad_setup_plant: call gpad_setup first");
+        if (nx <= 0 || nu < 0 || !PM || !Pg) return fail(GPAD_ERR_INVALID, "gpad_setup_plant: bad arguments");
+        if ((A == nullptr) != (B == nullptr) || (A && nu == 0))
+            return fail(GPAD_ERR_INVALID, "gpad_setup_plant: give A and B together (nu >= 1)");
+        if (nu > h->dims.n) return fail(GPAD_ERR_INVALID, "gpad_setup_plant: nu > n");
+        HIP_TRY(hipSetDevice(h->device));
+        const int n = h->dims.n, m = h->dims.m;
+        const size_t es = esize(h->dims.dtype);
+        const PlantOffsets o = plant_offsets(n, m, nx, nu);
+        int rc;
+        if ((rc = h->plant.ensure(es * o.total))) return rc;
+        char* base = (char*)h->plant.p;
+        const hipMemcpyKind kind = h->dims.memory == GPAD_MEM_HOST ? hipMemcpyHostToDevice
+                                                                    : hipMemcpyDeviceToDevice;
+        auto put = [&](size_t off, const void* src, size_t elems) -> int {
+            if (!src || elems == 0) return GPAD_OK;
+            HIP_TRY(hipMemcpyAsync(base + es * off, src, es * elems, kind, h->stream));
+            return GPAD_OK;
+        };
+        if ((rc = put(o.PM, PM, (size_t)n * nx)) || (rc = put(o.M0, M0, n)) ||
+            (rc = put(o.Pg, Pg, (size_t)m * nx)) || (rc = put(o.g0, g0, m)) ||
+            (rc = put(o.A, A, (size_t)nx * nx)) || (rc = put(o.B, B, (size_t)nx * nu)))
+            return rc;
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        h->nx = nx;
+        h->nu = nu;
+        h->has_M0 = M0 != nullptr;
+        h->has_g0 = g0 != nullptr;
+        h->plant_dyn = A != nullptr;
+        h->plant_ready = true;
+        h->plant_n = n;
+        h->plant_m = m;
+        h->plant_dtype = h->dims.dtype;
         return GPAD_OK;
-    };
-    if ((rc = put(o.PM, PM, (size_t)n * nx)) || (rc = put(o.M0, M0, n)) ||
-        (rc = put(o.Pg, Pg, (size_t)m * nx)) || (rc = put(o.g0, g0, m)) ||
-        (rc = put(o.A, A, (size_t)nx * nx)) || (rc = put(o.B, B, (size_t)nx * nu)))
-        return rc;
-    HIP_TRY(hipStreamSynchronize(h->stream));
-    h->nx = nx;
-    h->nu = nu;
-    h->has_M0 = M0 != nullptr;
-    h->has_g0 = g0 != nullptr;
-    h->plant_dyn = A != nullptr;
-    h->plant_ready = true;
-    h->plant_n = n;
-    h->plant_m = m;
-    h->plant_dtype = h->dims.dtype;
-    return GPAD_OK;
+    });
 }
 
 template <typename T>
@@ -1437,71 +1487,87 @@ extern "C" {
 
 int gpad_run_state(gpad_handle_t h, const void* x, void* z0, void* y0, int N, double tol,
                    gpad_stats_t* st) {
-    return state_impl(h, const_cast<void*>(x), z0, y0, 0, N, tol, 1, nullptr, nullptr, st,
-                      "gpad_run_state");
+    return gpad::abi_guard("gpad_run_state", [&]() -> int {
+        return state_impl(h, const_cast<void*>(x), z0, y0, 0, N, tol, 1, nullptr, nullptr, st,
+                          "gpad_run_state");
+    });
 }
 
 int gpad_closed_loop(gpad_handle_t h, void* x, void* z, void* y, int steps, int N, double tol, int warm,
                      void* xs, void* us, gpad_stats_t* st) {
-    if (steps == 0) return GPAD_OK;
-    return state_impl(h, x, z, y, steps, N, tol, warm, xs, us, st, "gpad_closed_loop");
+    return gpad::abi_guard("gpad_closed_loop", [&]() -> int {
+        if (steps == 0) return GPAD_OK;
+        return state_impl(h, x, z, y, steps, N, tol, warm, xs, us, st, "gpad_closed_loop");
+    });
 }
 
 // ---- per-step entry points ---------------------------------------------------------------
 int gpad_step1_extrapolate(gpad_handle_t h, const float* y, const float* ym1, float* w, float beta,
                            int m) {
-    if (!h || !y || !ym1 || !w || m < 0) return fail(GPAD_ERR_INVALID, "gpad_step1: bad arguments");
-    if (m == 0) return GPAD_OK;
-    HIP_TRY(hipSetDevice(h->device));
-    HIP_TRY(gpad::launch_step1(y, ym1, w, beta, m, h->stream));
-    return GPAD_OK;
+    return gpad::abi_guard("gpad_step1_extrapolate", [&]() -> int {
+        if (!h || !y || !ym1 || !w || m < 0) return fail(GPAD_ERR_INVALID, "gpad_step1: bad arguments");
+        if (m == 0) return GPAD_OK;
+        HIP_TRY(hipSetDevice(h->device));
+        HIP_TRY(gpad::launch_step1(y, ym1, w, beta, m, h->stream));
+        return GPAD_OK;
+    });
 }
 
 int gpad_step2_primal(gpad_handle_t h, const float* MGneg, const float* w, const float* gP,
                       float* zhat, int n, int m) {
-    if (!h || !MGneg || !w || !gP || !zhat || n <= 0 || m <= 0)
-        return fail(GPAD_ERR_INVALID, "gpad_step2: bad arguments");
-    if ((size_t)m * sizeof(float) > 64 * 1024) return fail(GPAD_ERR_UNSUPPORTED, "gpad_step2: m too large");
-    HIP_TRY(hipSetDevice(h->device));
-    HIP_TRY(gpad::launch_step2(MGneg, w, gP, zhat, n, m, h->stream));
-    return GPAD_OK;
+    return gpad::abi_guard("gpad_step2_primal", [&]() -> int {
+        if (!h || !MGneg || !w || !gP || !zhat || n <= 0 || m <= 0)
+            return fail(GPAD_ERR_INVALID, "gpad_step2: bad arguments");
+        if ((size_t)m * sizeof(float) > 64 * 1024) return fail(GPAD_ERR_UNSUPPORTED, "gpad_step2: m too large");
+        HIP_TRY(hipSetDevice(h->device));
+        HIP_TRY(gpad::launch_step2(MGneg, w, gP, zhat, n, m, h->stream));
+        return GPAD_OK;
+    });
 }
 
 int gpad_step2_primal_flat(gpad_handle_t h, const float* MGf, const float* w, const float* gP,
                            float* zhat, int N, int n_u, int m) {
-    if (!h || !MGf || !w || !gP || !zhat || N <= 0 || n_u <= 0 || m < 4 * n_u * N)
-        return fail(GPAD_ERR_INVALID, "gpad_step2_flat: bad arguments");
-    HIP_TRY(hipSetDevice(h->device));
-    HIP_TRY(gpad::launch_step2_flat(MGf, w, gP, zhat, N, n_u, m, h->stream));
-    return GPAD_OK;
+    return gpad::abi_guard("gpad_step2_primal_flat", [&]() -> int {
+        if (!h || !MGf || !w || !gP || !zhat || N <= 0 || n_u <= 0 || m < 4 * n_u * N)
+            return fail(GPAD_ERR_INVALID, "gpad_step2_flat: bad arguments");
+        HIP_TRY(hipSetDevice(h->device));
+        HIP_TRY(gpad::launch_step2_flat(MGf, w, gP, zhat, N, n_u, m, h->stream));
+        return GPAD_OK;
+    });
 }
 
 int gpad_step4_project_flat(gpad_handle_t h, const float* GLf, float* yp1, const float* w,
                             const float* pD, const float* zhat, int N, int n_u, int m) {
-    if (!h || !GLf || !yp1 || !w || !pD || !zhat || N <= 0 || n_u <= 0 || m < 4 * n_u * N)
-        return fail(GPAD_ERR_INVALID, "gpad_step4_flat: bad arguments");
-    HIP_TRY(hipSetDevice(h->device));
-    HIP_TRY(gpad::launch_step4_flat(GLf, yp1, w, pD, zhat, N, n_u, m, h->stream));
-    return GPAD_OK;
+    return gpad::abi_guard("gpad_step4_project_flat", [&]() -> int {
+        if (!h || !GLf || !yp1 || !w || !pD || !zhat || N <= 0 || n_u <= 0 || m < 4 * n_u * N)
+            return fail(GPAD_ERR_INVALID, "gpad_step4_flat: bad arguments");
+        HIP_TRY(hipSetDevice(h->device));
+        HIP_TRY(gpad::launch_step4_flat(GLf, yp1, w, pD, zhat, N, n_u, m, h->stream));
+        return GPAD_OK;
+    });
 }
 
 int gpad_step3_average(gpad_handle_t h, float theta, const float* zm1, const float* zhat, float* z,
                        int n) {
-    if (!h || !zm1 || !zhat || !z || n < 0) return fail(GPAD_ERR_INVALID, "gpad_step3: bad arguments");
-    if (n == 0) return GPAD_OK;
-    HIP_TRY(hipSetDevice(h->device));
-    HIP_TRY(gpad::launch_step3(theta, zm1, zhat, z, n, h->stream));
-    return GPAD_OK;
+    return gpad::abi_guard("gpad_step3_average", [&]() -> int {
+        if (!h || !zm1 || !zhat || !z || n < 0) return fail(GPAD_ERR_INVALID, "gpad_step3: bad arguments");
+        if (n == 0) return GPAD_OK;
+        HIP_TRY(hipSetDevice(h->device));
+        HIP_TRY(gpad::launch_step3(theta, zm1, zhat, z, n, h->stream));
+        return GPAD_OK;
+    });
 }
 
 int gpad_step4_project(gpad_handle_t h, const float* GL, float* yp1, const float* w,
                        const float* pD, const float* zhat, int n, int m) {
-    if (!h || !GL || !yp1 || !w || !pD || !zhat || n <= 0 || m <= 0)
-        return fail(GPAD_ERR_INVALID, "gpad_step4: bad arguments");
-    if ((size_t)n * sizeof(float) > 64 * 1024) return fail(GPAD_ERR_UNSUPPORTED, "gpad_step4: n too large");
-    HIP_TRY(hipSetDevice(h->device));
-    HIP_TRY(gpad::launch_step4(GL, yp1, w, pD, zhat, n, m, h->stream));
-    return GPAD_OK;
+    return gpad::abi_guard("gpad_step4_project", [&]() -> int {
+        if (!h || !GL || !yp1 || !w || !pD || !zhat || n <= 0 || m <= 0)
+            return fail(GPAD_ERR_INVALID, "gpad_step4: bad arguments");
+        if ((size_t)n * sizeof(float) > 64 * 1024) return fail(GPAD_ERR_UNSUPPORTED, "gpad_step4: n too large");
+        HIP_TRY(hipSetDevice(h->device));
+        HIP_TRY(gpad::launch_step4(GL, yp1, w, pD, zhat, n, m, h->stream));
+        return GPAD_OK;
+    });
 }
 
 }  // extern "C"
