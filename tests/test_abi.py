@@ -231,3 +231,32 @@ def test_one_hip_runtime_whatever_the_import_order():
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
     assert out.stdout.split() == ["1", "1"], out.stdout
+
+
+def test_phase_planner_random_inputs():
+    """gpad_plan_phases on random survival data (any batch, counts incl. 0 and > N, any N, test
+    period, CU count, panel-taken shape): never an error or a crash, and every plan it returns is
+    well formed -- strictly increasing ends closing at N, after a test each, within the slots."""
+    from gpad_mpc.solver import GpadSolver
+    rng = np.random.default_rng(3)
+    for _ in range(400):
+        B = int(rng.choice([1, 2, 15, 16, 17, 255, 1000, 4096, 8193, 70000]))
+        N = int(rng.choice([1, 9, 10, 11, 100, 300, 5000, 20000]))
+        K = int(rng.choice([1, 2, 5, 10, 16, 100]))
+        kind = rng.integers(0, 4)
+        if kind == 0:
+            it = rng.integers(0, N + 50, B)
+        elif kind == 1:
+            it = np.clip(rng.normal(rng.uniform(0, N + 1), rng.uniform(1, 200), B), 0, N)
+        elif kind == 2:
+            it = np.full(B, int(rng.integers(0, N + 1)))
+        else:
+            it = rng.geometric(rng.uniform(0.001, 0.5), B)
+        n, m = int(rng.choice([8, 40, 129, 200, 208, 256])), int(rng.choice([8, 64, 180, 200, 256]))
+        p = GpadSolver.plan_phases(it.astype(np.int32), n, m, N, K, int(rng.choice([1, 8, 256, 304])))
+        e = p["ends"]
+        if not e:
+            continue
+        assert e[-1] == N and all(a < b for a, b in zip(e, e[1:])), (B, N, K, e)
+        assert all(x % K == 0 for x in e[:-1]), (K, e)
+        assert len(e) <= 64 and len(p["fins"]) == len(e)
