@@ -466,3 +466,36 @@ def draw_heavy_case(rng: np.random.Generator) -> dict:
                 warm=bool(rng.random() < 0.2), device=bool(rng.random() < 0.7), solves=int(rng.integers(2, 4)),
                 check_every=int(rng.choice([10, 10, 5, 20])), N=5000, tol=float(rng.choice([1e-4, 1e-4, 1e-3])),
                 opts=opts, f64=False, group=0, oneshot=False, heavy=True)
+
+
+def run_steps_case(seed: int, oracle) -> dict:
+    """The per-step entry points (gpad_step1..4, the kernel_functions.h mirror) on random sizes and
+    values against the oracle's steps 8a-8d (seq_functions.cpp:45-87), bit for bit."""
+    import torch
+
+    import gpad_mpc
+    rng = np.random.default_rng(seed)
+    n = int(rng.choice(SPECIAL + [300, 511, 512, 513, 1000, 1500]))
+    m = int(rng.choice(SPECIAL + [300, 511, 512, 513, 1000, 1500]))
+    dev = torch.device("cuda:0")
+    f = lambda *s: rng.normal(0, 1, s).astype(np.float32)  # noqa: E731
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    MGneg, GL, gP, pD = f(n, m), f(m, n), f(n), f(m)
+    y, ym1, zm1 = np.maximum(f(m), 0), np.maximum(f(m), 0), f(n)
+    beta, theta = float(np.float32(rng.uniform(0, 1))), float(np.float32(rng.uniform(0, 1)))
+    w, zh, z, yp = (torch.empty(m, device=dev), torch.empty(n, device=dev), torch.empty(n, device=dev),
+                    torch.empty(m, device=dev))
+    with gpad_mpc.GpadSolver(0) as s:
+        s.step1(t(y), t(ym1), w, beta)
+        s.step2(t(MGneg), w, t(gP), zh)
+        s.step3(theta, t(zm1), zh, z)
+        s.step4(t(GL), yp, w, t(pD), zh)
+        s.sync()
+    wo = oracle.step1(y, ym1, np.float32(beta))
+    zho = oracle.step2(MGneg, wo, gP)
+    zo = oracle.step3(np.float32(theta), zm1, zho)
+    ypo = oracle.step4(GL, wo, pD, zho)
+    for what, a, o in (("8a", w, wo), ("8b", zh, zho), ("8c", z, zo), ("8d", yp, ypo)):
+        if not np.array_equal(a.cpu().numpy(), o):
+            return dict(ok=False, checked=0, kernels=["steps"], why=f"step {what} differs at n={n} m={m}")
+    return dict(ok=True, checked=1, kernels=["steps"])

@@ -86,3 +86,10 @@ def test_heavy_fuzz_parity(gpu, oracle, i):
     cfg = fuzz_util.draw_heavy_case(np.random.default_rng(SEED + 400 + i))
     r = fuzz_util.run_case(cfg, oracle)
     assert r["ok"], f"{json.dumps(cfg)}: {r['why']}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("i", range(4))
+def test_step_entry_points_fuzz(gpu, oracle, i):
+    r = fuzz_util.run_steps_case(SEED + 500 + i, oracle)
+    assert r["ok"], r["why"]

@@ -26,6 +26,7 @@ ap.add_argument("--flat", type=float, default=0.25, help="share of flat battery 
 ap.add_argument("--value", type=float, default=0.0, help="share of value-branch (H bound) cases")
 ap.add_argument("--loop", type=float, default=0.0, help="share of closed-loop (gpad_closed_loop) cases")
 ap.add_argument("--heavy", type=float, default=0.0, help="share of C3/C4-shaped phased solves")
+ap.add_argument("--steps", type=float, default=0.0, help="share of per-step entry point cases")
 ap.add_argument("--rccl-stub", action="store_true",
                 help="group cases through the RCCL transport (tests/rccl_stub, one GPU standing in for each rank)")
 args = ap.parse_args()
@@ -42,15 +43,18 @@ for i in range(args.cases):
         break
     rng = np.random.default_rng(args.seed + i)
     u = rng.random()
-    edges = np.cumsum([args.flat, args.value, args.loop, args.heavy])
+    edges = np.cumsum([args.flat, args.value, args.loop, args.heavy, args.steps])
     kind = ("flat" if u < edges[0] else "value" if u < edges[1] else "loop" if u < edges[2] else
-            "heavy" if u < edges[3] else "full")
+            "heavy" if u < edges[3] else "steps" if u < edges[4] else "full")
     cfg = {"flat": fuzz_util.draw_flat_case, "value": fuzz_util.draw_value_case, "loop": fuzz_util.draw_loop_case,
-           "heavy": fuzz_util.draw_heavy_case, "full": fuzz_util.draw_case}[kind](rng)
+           "heavy": fuzz_util.draw_heavy_case, "full": fuzz_util.draw_case,
+           "steps": lambda r: {"steps_seed": int(r.integers(1 << 30))}}[kind](rng)
     t = time.time()
     try:
         if kind == "flat":
             r = fuzz_util.run_flat_case(cfg, O, sample=min(args.sample, 16))
+        elif kind == "steps":
+            r = fuzz_util.run_steps_case(cfg["steps_seed"], O)
         elif kind == "loop":
             r = fuzz_util.run_loop_case(cfg, O)
         elif kind == "value":
