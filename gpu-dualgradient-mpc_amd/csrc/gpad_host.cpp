@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/gpad.h"
+#include "gpad_abi.h"
 #include "gpad_internal.h"
 
 namespace {

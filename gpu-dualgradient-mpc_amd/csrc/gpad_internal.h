@@ -5,31 +5,12 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
-#include <exception>
-#include <new>
 #include <string>
 
 namespace gpad {
 
 // gpad_last_error() detail for the calling thread; returns code (gpad_host.cpp)
 int set_last_error(int code, const std::string& msg);
-
-// Every int-returning C-ABI entry point runs its body through abi_guard: no C++ exception (a
-// std::bad_alloc of a host buffer sized from caller dims or a corrupted data file, a
-// std::length_error) crosses the extern "C" boundary -- it becomes GPAD_ERR_NOMEM / GPAD_ERR_INVALID
-// with the reason in gpad_last_error() instead of std::terminate.
-template <class F>
-int abi_guard(const char* where, F&& body) noexcept {
-    try {
-        return body();
-    } catch (const std::bad_alloc&) {
-        return set_last_error(-3 /* GPAD_ERR_NOMEM */, std::string(where) + ": host allocation failed");
-    } catch (const std::exception& e) {
-        return set_last_error(-1 /* GPAD_ERR_INVALID */, std::string(where) + ": " + e.what());
-    } catch (...) {
-        return set_last_error(-1 /* GPAD_ERR_INVALID */, std::string(where) + ": unknown C++ exception");
-    }
-}
 
 // Schedule / launch tuning of a handle (gpad_set_option, include/gpad.h GPAD_OPT_*): for tests,
 // diagnostics and A/B tools.  None of these changes results -- only launch boundaries, grid
